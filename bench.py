@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Benchmark: edges/sec of the wD-MPNN encoder forward (MPNEncoder.forward, mpn.py:66-173) on
+synthetic polymer batches of 64 graphs, depth 3, hidden 300 (BASELINE.json metric), inputs packed
+and resident in HBM before the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+One process per GPU.  Every rank encodes its own disjoint synthetic batches (seed = base + rank):
+the path shards as independent graphs with no data-path collective (weak scaling); the only
+collectives are the barrier and the max-over-ranks of the elapsed time.
+
+Rank 0 prints ONE JSON line (stdout).  Diagnostics go to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'polymer-chemprop_amd'))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from chemprop_amd import TrainArgs, _native, synthetic  # noqa: E402
+from chemprop_amd.featurization import BatchMolGraph, get_atom_fdim, get_bond_fdim  # noqa: E402
+from chemprop_amd.mpn import MPNEncoder  # noqa: E402
+from chemprop_amd.nn_utils import initialize_weights  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_encoder(args, device):
+    torch.manual_seed(0)
+    enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim())
+    initialize_weights(enc)  # model.py:39 semantics: xavier_normal_ weights, zero biases
+    return enc.to(device).eval()
+
+
+def cpu_baseline(args, graph, seconds):
+    """The oracle (op-for-op restatement of the reference forward, oracle/mpn_ref.py) on host cores."""
+    from oracle import mpn_ref
+    enc = make_encoder(args, torch.device('cpu'))
+    p = {n: t.detach() for n, t in enc.named_parameters()}
+    times = []
+    t_end = time.perf_counter() + seconds
+    with torch.no_grad():
+        mpn_ref.encoder_forward(p, graph, args)  # warm-up
+        while len(times) < 5 or time.perf_counter() < t_end:
+            t0 = time.perf_counter()
+            mpn_ref.encoder_forward(p, graph, args)
+            times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {'value': (graph.n_bonds - 1) / med, 'unit': 'edges/s', 'cores': torch.get_num_threads(), 'kind': 'port',
+            'sample': f'{len(times)} forwards of one polymer B={len(graph.a_scope)} batch (E={graph.n_bonds - 1} '
+                      f'directed edges), median {med * 1e3:.2f} ms, torch {torch.__version__} CPU, eval/no_grad'}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--batch', type=int, default=64)
+    ap.add_argument('--depth', type=int, default=3)
+    ap.add_argument('--hidden', type=int, default=300)
+    ap.add_argument('--kind', default='polymer', choices=['polymer', 'qm9', 'zinc'])
+    ap.add_argument('--n-batches', type=int, default=8, help='distinct resident batches cycled per rank')
+    ap.add_argument('--cpu-seconds', type=float, default=12.0)
+    ap.add_argument('--no-cpu', action='store_true')
+    a = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    device = torch.device('cuda', local)
+    args = TrainArgs(hidden_size=a.hidden, depth=a.depth, device=device)
+
+    # inputs: packed + resident in HBM before timing (featurization.py:757-813 equivalent on host)
+    graphs = [BatchMolGraph(synthetic.make_batch(a.kind, a.batch, 1000 + 7919 * rank + i)) for i in range(a.n_batches)]
+    for g in graphs:
+        g.device_graph(device)
+    torch.cuda.synchronize(device)
+    enc = make_encoder(args, device)
+    edges = [g.n_bonds - 1 for g in graphs]
+
+    def step(i, prof=None):
+        enc._prof = prof
+        return enc(graphs[i % len(graphs)])
+
+    def barrier():
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+
+    with torch.no_grad():
+        for i in range(a.warmup):
+            step(i)
+        barrier()
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            step(i)
+        barrier()
+        elapsed = time.perf_counter() - t0
+        my_edges = sum(edges[i % len(edges)] for i in range(a.steps))
+
+        # second pass: HIP events around the dominant launches (message passing gather-GEMM) on the
+        # stream they run on
+        L = _native.lib()
+        pairs = a.steps * max(a.depth - 1, 1)
+        pool = ctypes.c_void_p()
+        _native.check(L.wdmpnn_event_pool_create(pairs, ctypes.byref(pool)), 'event pool')
+        barrier()
+        t1 = time.perf_counter()
+        for i in range(a.steps):
+            step(i, (pool.value, i * (a.depth - 1)))
+        barrier()
+        elapsed_prof = time.perf_counter() - t1
+        enc._prof = None
+        kernel_ms = ctypes.c_float()
+        n_launch = a.steps * (a.depth - 1)
+        if n_launch:
+            _native.check(L.wdmpnn_event_pool_elapsed_ms(pool, 0, n_launch, ctypes.byref(kernel_ms)), 'events')
+        L.wdmpnn_event_pool_destroy(pool)
+
+    t = torch.tensor([elapsed, elapsed_prof], dtype=torch.float64, device=device)
+    e = torch.tensor([my_edges], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(e, op=dist.ReduceOp.SUM)
+    elapsed, elapsed_prof = float(t[0]), float(t[1])
+    total_edges = float(e[0])
+
+    if rank == 0:
+        H = a.hidden
+        E_avg = sum(edges[i % len(edges)] for i in range(a.steps)) / a.steps
+        flops_launch = 2.0 * E_avg * H * H  # algorithmic W_h GEMM flops of one message-passing launch
+        avg_launch_s = (kernel_ms.value / 1e3 / n_launch) if n_launch else float('nan')
+        achieved = flops_launch / avg_launch_s / 1e12 if n_launch else None
+        line = {
+            'metric': 'edges/sec MPN forward, batch=64 polymer graphs, depth=3 hidden=300',
+            'value': total_edges / elapsed,
+            'unit': 'edges/s',
+            'n_gpus': world,
+            'steps': a.steps,
+            'warmup': a.warmup,
+            'ms_per_step': elapsed / a.steps * 1e3,
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'fp32',
+            'data': 'synthetic',
+            'config': {'workload': f'MPNEncoder.forward on synthetic {a.kind} batches of {a.batch} graphs '
+                                   f'(avg E={E_avg:.0f} directed edges), depth={a.depth}, hidden={H}, '
+                                   f'{a.n_batches} resident batches cycled per rank',
+                       'global_batch': a.batch * world, 'depth': a.depth, 'hidden': H,
+                       'parallelism': f'dp{world} (independent graphs, no collective in the forward)'},
+            'roofline': {'bound': 'mfma', 'kernel': 'gemm_kernel<64,64,2,2,NT> message passing (mpn.py:110-124)',
+                         'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                         'frac': achieved / FP32_MFMA_PEAK_TFLOPS if achieved else None, 'traffic': None,
+                         'avg_launch_us': avg_launch_s * 1e6, 'flops_per_launch': flops_launch,
+                         'launches_timed': n_launch},
+        }
+        if not a.no_cpu:
+            cpu = cpu_baseline(TrainArgs(hidden_size=H, depth=a.depth, device=torch.device('cpu')), graphs[0],
+                               a.cpu_seconds)
+            line['cpu_baseline'] = cpu
+        log(f'timed {a.steps} steps: {elapsed * 1e3:.2f} ms ({elapsed / a.steps * 1e6:.1f} us/step); with events '
+            f'{elapsed_prof / a.steps * 1e6:.1f} us/step')
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

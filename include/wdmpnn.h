@@ -1,0 +1,163 @@
+/*
+ * wdmpnn.h — C-ABI of the MI355X-native wD-MPNN encoder (libwdmpnn.so, gfx950).
+ *
+ * Drop-in boundary.  The reference (ayildiri/polymer-chemprop, pure Python/PyTorch) has no FFI for
+ * this path: the hot path is the nn.Module call chain
+ *
+ *     MoleculeModel.forward   chemprop/models/model.py:152-194
+ *       -> MPN.forward        chemprop/models/mpn.py:210-289
+ *         -> MPNEncoder.forward  chemprop/models/mpn.py:66-173        (replaced by wdmpnn_forward)
+ *              index_select_ND   chemprop/nn_utils.py:50-67           (replaced by wdmpnn_index_select_rows
+ *                                                                      and by the CSR gathers inside forward)
+ *              BatchMolGraph     chemprop/features/featurization.py:742-875 (device layout = WdGraph)
+ *         autograd backward of the above (train.py:79 loss.backward)  (replaced by wdmpnn_backward)
+ *
+ * The Python host package (polymer-chemprop_amd/chemprop_amd) keeps the reference's Python API and
+ * binds these entry points with ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - Every pointer in WdGraph / WdParams / WdGrads is a DEVICE pointer owned by the caller (the
+ *    PyTorch caching allocator).  The library never allocates device memory.
+ *  - Row 0 of every atom / bond array is the reference's zero pad row (featurization.py:767-781);
+ *    n_atoms / n_bonds INCLUDE it, exactly like BatchMolGraph.n_atoms / n_bonds.
+ *  - fp32 storage and fp32 arithmetic (MFMA f32 in/out), int32 indices.
+ *  - Return 0 on success, a negative WD_ERR_* code on argument errors, or -(hipError_t) on a HIP
+ *    launch error; wdmpnn_last_error() then holds a message (thread-local).
+ *  - All work is enqueued on `stream` (a hipStream_t; NULL = default stream); no host sync, no
+ *    allocation, re-entrant per stream, no global mutable state besides the thread-local error.
+ */
+#ifndef WDMPNN_H
+#define WDMPNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WDMPNN_ABI_VERSION 1
+
+enum WdActivation {     /* nn_utils.py:70-99 get_activation_function */
+    WD_ACT_RELU = 0, WD_ACT_LEAKY_RELU = 1, WD_ACT_PRELU = 2, WD_ACT_TANH = 3,
+    WD_ACT_SELU = 4, WD_ACT_ELU = 5, WD_ACT_IDENTITY = 6
+};
+
+enum WdAggregation {    /* mpn.py:158-163 */
+    WD_AGG_MEAN = 0, WD_AGG_SUM = 1, WD_AGG_NORM = 2
+};
+
+enum WdError {
+    WD_OK = 0, WD_ERR_ARG = -1000, WD_ERR_SHAPE = -1001, WD_ERR_WORKSPACE = -1002,
+    WD_ERR_UNSUPPORTED = -1003
+};
+
+/* One row-gather list: row r of the gathered operand = sum_{e=ptr[r]}^{ptr[r+1]-1} coef[e] * src[idx[e]]. */
+typedef struct WdCsr {
+    const int32_t *ptr;   /* [rows + 1] */
+    const int32_t *idx;   /* [ptr[rows]] source row ids */
+    const float   *coef;  /* [ptr[rows]] coefficients, NULL = all ones */
+} WdCsr;
+
+/*
+ * Device-resident packed BatchMolGraph (featurization.py:757-813) plus the gather lists derived
+ * from it by the host packer (chemprop_amd/featurization.py, BatchMolGraph.device_graph()).
+ */
+typedef struct WdGraph {
+    int32_t n_atoms;        /* V+1 (incl. pad row 0)                               */
+    int32_t n_bonds;        /* E+1 (incl. pad row 0)                               */
+    int32_t n_mols;         /* B = len(a_scope)                                    */
+    int32_t atom_fdim;      /* Fa: columns of f_atoms actually used                */
+    int32_t bond_fdim;      /* Fb: columns of f_bonds actually used (14 in atom-message mode) */
+    int32_t ld_atoms;       /* row stride of f_atoms (floats)                      */
+    int32_t ld_bonds;       /* row stride of f_bonds (floats)                      */
+    int32_t bond_col0;      /* first used column of f_bonds (Fb_full - 14 in atom-message mode) */
+    const float *f_atoms;   /* [n_atoms, ld_atoms]                                 */
+    const float *f_bonds;   /* [n_bonds, ld_bonds]                                 */
+    const float *w_atoms;   /* [n_atoms]  (featurization.py:778, pad weight 0)     */
+    const int32_t *mol_start;  /* [B] a_scope[i][0]                                */
+    const int32_t *mol_size;   /* [B] a_scope[i][1]                                */
+    const float *degree_of_polym; /* [B]                                           */
+    /* bond-message mode (mpn.py:110-120): X_b = sum_{j in in(b2a[b])} w_j M_j - M_{b2revb[b]} */
+    WdCsr msg_gather;       /* rows = n_bonds (bond mode) or n_atoms (atom mode, a2a + pad-slot term) */
+    WdCsr bond_feat_gather; /* atom mode only: rows = n_atoms, sum of f_bonds tails over a2b (mpn.py:106) */
+    WdCsr atom_gather;      /* rows = n_atoms: final aggregate of mpn.py:126-131 (coef = edge weight) */
+    const int32_t *b2revb;  /* [n_bonds] (undirected: mpn.py:101-102)                */
+    /* transposed lists for the backward pass (gradient of the gathers) */
+    WdCsr msg_gather_t;     /* rows = message rows: dM_j += sum coef * dX_row          */
+    WdCsr bond_feat_gather_t; /* unused by the gradients (inputs need no grad); may be zero */
+    WdCsr atom_gather_t;    /* rows = message rows: dM_j += coef * dA_atom              */
+    /* atom_descriptors == 'descriptor' (mpn.py:136-143) */
+    const float *atom_desc; /* [n_atoms, desc_dim] (row 0 zero pad) or NULL           */
+    int32_t desc_dim;
+    int32_t atom_messages;  /* 1 = atom-message mode (mpn.py:47-53, 93-94, 104-108) */
+} WdGraph;
+
+/* nn.Module parameters of MPNEncoder (mpn.py:17-64); all device pointers, row-major like nn.Linear. */
+typedef struct WdParams {
+    int32_t hidden;         /* H = args.hidden_size                                */
+    const float *W_i;       /* [H, Kin], Kin = bond_fdim (bond mode) or atom_fdim */
+    const float *b_i;       /* [H] or NULL (args.bias)                             */
+    const float *W_h;       /* [H, H] (bond mode) or [H, H + bond_fdim] (atom mode) */
+    const float *b_h;       /* [H] or NULL                                         */
+    const float *W_o;       /* [H, atom_fdim + H]                                  */
+    const float *b_o;       /* [H] (always present, mpn.py:58)                     */
+    const float *W_d;       /* [H+d, H+d] atom_descriptors_layer or NULL          */
+    const float *b_d;       /* [H+d] or NULL                                       */
+    const float *prelu;     /* [1] PReLU slope (device) when activation == PReLU   */
+    const float *zero_vec;  /* [H] cached_zero_vector (mpn.py:44, 148-149)         */
+} WdParams;
+
+typedef struct WdConfig {
+    int32_t depth;          /* args.depth (>= 1)                                   */
+    int32_t undirected;     /* args.undirected                                     */
+    int32_t activation;     /* WdActivation                                        */
+    int32_t aggregation;    /* WdAggregation                                       */
+    float   aggregation_norm;
+    float   dropout;        /* args.dropout; 0 at eval                             */
+    uint64_t seed;          /* dropout RNG stream (counter based, re-derivable in backward) */
+    int32_t save_for_backward; /* 1: keep pre-activations + every message layer in the workspace */
+    int32_t prof_slot;      /* first event pair used when prof_pool != NULL                      */
+    void   *prof_pool;      /* optional WdEventPool: an event pair is recorded around each message-
+                               passing launch (the dominant kernel), pairs prof_slot + t - 1       */
+} WdConfig;
+
+/* Gradients (device, caller-zeroed NOT required: every pointer is fully overwritten). NULL = skip. */
+typedef struct WdGrads {
+    float *W_i, *b_i, *W_h, *b_h, *W_o, *b_o, *W_d, *b_d, *prelu;
+} WdGrads;
+
+int wdmpnn_abi_version(void);
+const char *wdmpnn_last_error(void);
+
+/* Bytes of forward workspace (intermediates kept for backward when save_for_backward). */
+int wdmpnn_workspace_bytes(const WdGraph *g, const WdParams *p, const WdConfig *c, size_t *bytes);
+/* Bytes of scratch for wdmpnn_backward. */
+int wdmpnn_backward_workspace_bytes(const WdGraph *g, const WdParams *p, const WdConfig *c, size_t *bytes);
+
+/* MPNEncoder.forward (mpn.py:66-173): out [n_mols, H (+desc_dim)]. */
+int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c,
+                   void *workspace, size_t workspace_bytes, float *out, void *stream);
+
+/* Gradient of MPNEncoder.forward w.r.t. its parameters, given dout [n_mols, H (+desc_dim)] and the
+ * workspace of a forward run with save_for_backward = 1 and identical g/p/c. */
+int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c,
+                    const void *workspace, size_t workspace_bytes, const float *dout,
+                    void *scratch, size_t scratch_bytes, const WdGrads *grads, void *stream);
+
+/* Measurement hook (bench.py): a pool of hipEvent pairs recorded by wdmpnn_forward around its
+ * dominant launches (see WdConfig.prof_pool).  elapsed_ms synchronises on the events it reads. */
+int wdmpnn_event_pool_create(int32_t n_pairs, void **pool);
+int wdmpnn_event_pool_destroy(void *pool);
+int wdmpnn_event_pool_elapsed_ms(void *pool, int32_t first, int32_t count, float *total_ms);
+
+/* index_select_ND (nn_utils.py:50-67): out[i, :] = src[index[i], :], row_len floats per row.
+ * Indices are int64 like the reference's LongTensor; out-of-range indices are an error checked by
+ * the caller (the kernel clamps nothing and reads src[index]). */
+int wdmpnn_index_select_rows(const float *src, int64_t n_src_rows, int64_t row_len,
+                             const int64_t *index, int64_t n_index, float *out, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WDMPNN_H */

@@ -1,0 +1,118 @@
+"""ctypes binding of libwdmpnn.so (include/wdmpnn.h).
+
+The library is the product: there is no CPU or PyTorch fallback.  If ``libwdmpnn.so`` is missing
+or fails to load, :func:`lib` raises, and every GPU entry point of the package raises with it.
+
+``torch`` is imported before the library is loaded so that the library's ``libamdhip64.so.7``
+dependency resolves (by SONAME) to the HIP runtime torch already loaded: one runtime, one set of
+device pointers and streams.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, Structure, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64, c_void_p
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('WDMPNN_LIB', os.path.join(HERE, 'libwdmpnn.so'))
+
+ACTIVATIONS = {'ReLU': 0, 'LeakyReLU': 1, 'PReLU': 2, 'tanh': 3, 'SELU': 4, 'ELU': 5}
+ACT_IDENTITY = 6
+AGGREGATIONS = {'mean': 0, 'sum': 1, 'norm': 2}
+ABI_VERSION = 1
+
+EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace_bytes',
+                    'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
+                    'wdmpnn_index_select_rows', 'wdmpnn_event_pool_create', 'wdmpnn_event_pool_destroy',
+                    'wdmpnn_event_pool_elapsed_ms')
+
+
+class WdCsr(Structure):
+    _fields_ = [('ptr', c_void_p), ('idx', c_void_p), ('coef', c_void_p)]
+
+
+class WdGraph(Structure):
+    _fields_ = [('n_atoms', c_int32), ('n_bonds', c_int32), ('n_mols', c_int32), ('atom_fdim', c_int32),
+                ('bond_fdim', c_int32), ('ld_atoms', c_int32), ('ld_bonds', c_int32), ('bond_col0', c_int32),
+                ('f_atoms', c_void_p), ('f_bonds', c_void_p), ('w_atoms', c_void_p), ('mol_start', c_void_p),
+                ('mol_size', c_void_p), ('degree_of_polym', c_void_p),
+                ('msg_gather', WdCsr), ('bond_feat_gather', WdCsr), ('atom_gather', WdCsr), ('b2revb', c_void_p),
+                ('msg_gather_t', WdCsr), ('bond_feat_gather_t', WdCsr), ('atom_gather_t', WdCsr),
+                ('atom_desc', c_void_p), ('desc_dim', c_int32), ('atom_messages', c_int32)]
+
+
+class WdParams(Structure):
+    _fields_ = [('hidden', c_int32), ('W_i', c_void_p), ('b_i', c_void_p), ('W_h', c_void_p), ('b_h', c_void_p),
+                ('W_o', c_void_p), ('b_o', c_void_p), ('W_d', c_void_p), ('b_d', c_void_p), ('prelu', c_void_p),
+                ('zero_vec', c_void_p)]
+
+
+class WdConfig(Structure):
+    _fields_ = [('depth', c_int32), ('undirected', c_int32), ('activation', c_int32), ('aggregation', c_int32),
+                ('aggregation_norm', c_float), ('dropout', c_float), ('seed', c_uint64),
+                ('save_for_backward', c_int32), ('prof_slot', c_int32), ('prof_pool', c_void_p)]
+
+
+class WdGrads(Structure):
+    _fields_ = [(n, c_void_p) for n in ('W_i', 'b_i', 'W_h', 'b_h', 'W_o', 'b_o', 'W_d', 'b_d', 'prelu')]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_LIB = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the HIP library; raise if it is missing or has the wrong ABI."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(f'libwdmpnn.so not found at {LIB_PATH}: build it with '
+                          f'`python -c "import __graft_entry__ as g; g.build()"` (no CPU fallback exists)')
+    L = ctypes.CDLL(LIB_PATH)
+    L.wdmpnn_abi_version.restype = c_int
+    L.wdmpnn_last_error.restype = c_char_p
+    L.wdmpnn_workspace_bytes.argtypes = [POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig), POINTER(c_size_t)]
+    L.wdmpnn_backward_workspace_bytes.argtypes = [POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig),
+                                                  POINTER(c_size_t)]
+    L.wdmpnn_forward.argtypes = [POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig), c_void_p, c_size_t,
+                                 c_void_p, c_void_p]
+    L.wdmpnn_backward.argtypes = [POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig), c_void_p, c_size_t,
+                                  c_void_p, c_void_p, c_size_t, POINTER(WdGrads), c_void_p]
+    L.wdmpnn_index_select_rows.argtypes = [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p]
+    L.wdmpnn_event_pool_create.argtypes = [c_int32, POINTER(c_void_p)]
+    L.wdmpnn_event_pool_destroy.argtypes = [c_void_p]
+    L.wdmpnn_event_pool_elapsed_ms.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_float)]
+    for fn in ('wdmpnn_event_pool_create', 'wdmpnn_event_pool_destroy', 'wdmpnn_event_pool_elapsed_ms',
+               'wdmpnn_workspace_bytes', 'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
+               'wdmpnn_index_select_rows'):
+        getattr(L, fn).restype = c_int
+    v = L.wdmpnn_abi_version()
+    if v != ABI_VERSION:
+        raise NativeError(f'libwdmpnn ABI {v} != expected {ABI_VERSION}; rebuild the library')
+    _LIB = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().wdmpnn_last_error().decode(errors='replace')
+        if rc in (-1000, -1001):
+            raise ValueError(f'{what}: {msg}')
+        if rc == -1003:
+            raise NotImplementedError(f'{what}: {msg}')
+        raise NativeError(f'{what} failed ({rc}): {msg}')
+
+
+def ptr(t) -> int:
+    """Device pointer of a tensor (0 for None)."""
+    return 0 if t is None else t.data_ptr()
+
+
+def current_stream(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,240 @@
+"""MPNEncoder / MPN with the reference's constructor, state_dict keys and forward signatures
+(``chemprop/models/mpn.py:14-289``), computed by the HIP library (libwdmpnn.so).
+
+The encoder's whole forward (mpn.py:66-173) is one ``wdmpnn_forward`` call; its gradient is one
+``wdmpnn_backward`` call (autograd.Function below).  Parameters stay ordinary ``nn.Linear`` /
+``nn.Parameter`` objects so optimisers, checkpoints (``encoder.encoder.0.W_i.weight`` ...) and
+``load_checkpoint``'s key remapping (utils.py:114-115) work unchanged.
+"""
+from __future__ import annotations
+
+import ctypes
+from functools import reduce
+from typing import List, Union
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _native
+from .featurization import BatchMolGraph, get_atom_fdim, get_bond_fdim, mol2graph
+from .nn_utils import get_activation_function
+
+
+def _f32(t):
+    if t is None:
+        return None
+    if t.dtype != torch.float32 or not t.is_contiguous():
+        raise TypeError('chemprop_amd expects contiguous float32 parameters')
+    return t
+
+
+class _EncoderFunction(torch.autograd.Function):
+    """Forward = wdmpnn_forward, backward = wdmpnn_backward (parameter gradients only: the graph
+    features are inputs without gradient, as in the reference training loop)."""
+
+    @staticmethod
+    def forward(ctx, enc, gstruct, cfg, hidden_out, device, W_i, b_i, W_h, b_h, W_o, b_o, W_d, b_d, prelu, zero_vec,
+                desc_keepalive):
+        L = _native.lib()
+        p = _native.WdParams()
+        p.hidden = enc.hidden_size
+        p.W_i, p.b_i, p.W_h, p.b_h = map(_native.ptr, (W_i, b_i, W_h, b_h))
+        p.W_o, p.b_o, p.W_d, p.b_d = map(_native.ptr, (W_o, b_o, W_d, b_d))
+        p.prelu, p.zero_vec = _native.ptr(prelu), _native.ptr(zero_vec)
+        nbytes = ctypes.c_size_t()
+        _native.check(L.wdmpnn_workspace_bytes(ctypes.byref(gstruct), ctypes.byref(p), ctypes.byref(cfg),
+                                               ctypes.byref(nbytes)), 'MPNEncoder workspace')
+        ws = torch.empty(max(nbytes.value, 256), dtype=torch.uint8, device=device)
+        out = torch.empty((gstruct.n_mols, hidden_out), dtype=torch.float32, device=device)
+        stream = _native.current_stream(device)
+        _native.check(L.wdmpnn_forward(ctypes.byref(gstruct), ctypes.byref(p), ctypes.byref(cfg), ws.data_ptr(),
+                                       nbytes.value, out.data_ptr(), stream), 'MPNEncoder forward')
+        if cfg.save_for_backward:
+            ctx.save_for_backward(W_i, b_i, W_h, b_h, W_o, b_o, W_d, b_d, prelu, zero_vec)
+            ctx.ws, ctx.ws_bytes, ctx.gstruct, ctx.cfg, ctx.p = ws, nbytes.value, gstruct, cfg, p
+            ctx.keep = desc_keepalive
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        W_i, b_i, W_h, b_h, W_o, b_o, W_d, b_d, prelu, zero_vec = ctx.saved_tensors
+        L = _native.lib()
+        dev = dout.device
+        dout = dout.contiguous()
+        nbytes = ctypes.c_size_t()
+        _native.check(L.wdmpnn_backward_workspace_bytes(ctypes.byref(ctx.gstruct), ctypes.byref(ctx.p),
+                                                        ctypes.byref(ctx.cfg), ctypes.byref(nbytes)),
+                      'MPNEncoder backward workspace')
+        scratch = torch.empty(max(nbytes.value, 256), dtype=torch.uint8, device=dev)
+        want = ctx.needs_input_grad
+        # argument positions: 5 W_i, 6 b_i, 7 W_h, 8 b_h, 9 W_o, 10 b_o, 11 W_d, 12 b_d, 13 prelu
+        grads = {}
+        g = _native.WdGrads()
+        for name, t, pos in (('W_i', W_i, 5), ('b_i', b_i, 6), ('W_h', W_h, 7), ('b_h', b_h, 8), ('W_o', W_o, 9),
+                             ('b_o', b_o, 10), ('W_d', W_d, 11), ('b_d', b_d, 12), ('prelu', prelu, 13)):
+            if name in ('W_h', 'b_h') and ctx.cfg.depth == 1:
+                continue  # unused when depth == 1 (mpn.py:100 loop body never runs): no gradient, like autograd
+            if t is not None and want[pos]:
+                grads[name] = torch.empty_like(t)
+                setattr(g, name, grads[name].data_ptr())
+        _native.check(L.wdmpnn_backward(ctypes.byref(ctx.gstruct), ctypes.byref(ctx.p), ctypes.byref(ctx.cfg),
+                                        ctx.ws.data_ptr(), ctx.ws_bytes, dout.data_ptr(), scratch.data_ptr(),
+                                        nbytes.value, ctypes.byref(g), _native.current_stream(dev)),
+                      'MPNEncoder backward')
+        ctx.ws = None
+        return (None, None, None, None, None, grads.get('W_i'), grads.get('b_i'), grads.get('W_h'), grads.get('b_h'),
+                grads.get('W_o'), grads.get('b_o'), grads.get('W_d'), grads.get('b_d'), grads.get('prelu'), None, None)
+
+
+class MPNEncoder(nn.Module):
+    """mpn.py:14-173.  Same constructor arguments, attributes, parameters and forward signature."""
+
+    def __init__(self, args, atom_fdim: int, bond_fdim: int):
+        super(MPNEncoder, self).__init__()
+        self.atom_fdim = atom_fdim
+        self.bond_fdim = bond_fdim
+        self.atom_messages = args.atom_messages
+        self.hidden_size = args.hidden_size
+        self.bias = args.bias
+        self.depth = args.depth
+        self.dropout = args.dropout
+        self.layers_per_message = 1
+        self.undirected = args.undirected
+        self.device = args.device
+        self.aggregation = args.aggregation
+        self.aggregation_norm = args.aggregation_norm
+        self.activation = args.activation
+
+        self.dropout_layer = nn.Dropout(p=self.dropout)
+        self.act_func = get_activation_function(args.activation)
+        self.cached_zero_vector = nn.Parameter(torch.zeros(self.hidden_size), requires_grad=False)
+        input_dim = self.atom_fdim if self.atom_messages else self.bond_fdim
+        self.W_i = nn.Linear(input_dim, self.hidden_size, bias=self.bias)
+        w_h_input_size = self.hidden_size + self.bond_fdim if self.atom_messages else self.hidden_size
+        self.W_h = nn.Linear(w_h_input_size, self.hidden_size, bias=self.bias)
+        self.W_o = nn.Linear(self.atom_fdim + self.hidden_size, self.hidden_size)
+        if getattr(args, 'atom_descriptors', None) == 'descriptor':
+            self.atom_descriptors_size = args.atom_descriptors_size
+            self.atom_descriptors_layer = nn.Linear(self.hidden_size + self.atom_descriptors_size,
+                                                    self.hidden_size + self.atom_descriptors_size)
+        if self.aggregation not in _native.AGGREGATIONS:
+            raise ValueError(f'Aggregation "{self.aggregation}" not supported.')
+        if self.atom_messages and self.undirected:
+            raise NotImplementedError('undirected=True with atom_messages=True indexes atom messages with bond '
+                                      'indices in the reference (mpn.py:101-102) and is not supported')
+        self._seed_counter = 0
+        self._prof = None  # (event pool, first pair): bench.py measurement hook, see WdConfig.prof_pool
+
+    def _config(self, save: bool) -> _native.WdConfig:
+        c = _native.WdConfig()
+        c.depth = self.depth
+        c.undirected = int(bool(self.undirected))
+        c.activation = _native.ACTIVATIONS[self.activation]
+        c.aggregation = _native.AGGREGATIONS[self.aggregation]
+        c.aggregation_norm = float(self.aggregation_norm)
+        p = float(self.dropout) if self.training else 0.0
+        c.dropout = p
+        if p > 0.0:
+            self._seed_counter += 1
+            c.seed = (int(torch.initial_seed()) * 1000003 + self._seed_counter) & 0xFFFFFFFFFFFFFFFF
+        c.save_for_backward = int(bool(save))
+        if self._prof is not None:
+            c.prof_pool, c.prof_slot = self._prof
+        return c
+
+    def forward(self, mol_graph: BatchMolGraph, atom_descriptors_batch: List[np.ndarray] = None) -> torch.FloatTensor:
+        """mpn.py:66-173 -> [num_molecules, hidden_size (+ atom_descriptors_size)]."""
+        device = self.W_i.weight.device
+        if device.type != 'cuda':
+            raise RuntimeError('chemprop_amd.MPNEncoder runs on the MI355X HIP path only: move the model to a '
+                               'GPU (model.to("cuda"))')
+        dg = mol_graph.device_graph(device, self.atom_messages, self.bond_fdim)
+        gs = _native.WdGraph.from_buffer_copy(dg.struct)
+        fa_expect = self.atom_fdim
+        fb_expect = self.bond_fdim
+        if gs.n_atoms > 1 and gs.atom_fdim != fa_expect:
+            raise ValueError(f'atom feature size {gs.atom_fdim} != encoder atom_fdim {fa_expect}')
+        if gs.n_bonds > 1 and gs.bond_fdim != fb_expect:
+            raise ValueError(f'bond feature size {gs.bond_fdim} != encoder bond_fdim {fb_expect}')
+        gs.atom_fdim, gs.bond_fdim = fa_expect, fb_expect
+        desc = None
+        hidden_out = self.hidden_size
+        if atom_descriptors_batch is not None:  # mpn.py:77-79, 136-143
+            if not hasattr(self, 'atom_descriptors_layer'):
+                raise ValueError('atom descriptors given but the encoder has no atom_descriptors_layer')
+            d = atom_descriptors_batch[0].shape[1]
+            padded = [np.zeros([1, d])] + list(atom_descriptors_batch)
+            desc = torch.from_numpy(np.concatenate(padded, axis=0)).float().to(device).contiguous()
+            if desc.shape[0] != gs.n_atoms:
+                raise ValueError('The number of atoms is different from the length of the extra atom features')
+            if any(n == 0 for _, n in mol_graph.a_scope):
+                raise RuntimeError('stack expects each tensor to be equal size (empty molecule with atom '
+                                   'descriptors, mpn.py:149 vs 171)')
+            gs.atom_desc, gs.desc_dim = desc.data_ptr(), d
+            hidden_out += d
+        act_w = self.act_func.weight if isinstance(self.act_func, nn.PReLU) else None
+        if act_w is not None and act_w.numel() != 1:
+            raise NotImplementedError('PReLU with num_parameters > 1')
+        params = [self.W_i.weight, self.W_i.bias, self.W_h.weight, self.W_h.bias, self.W_o.weight, self.W_o.bias]
+        if desc is not None:
+            params += [self.atom_descriptors_layer.weight, self.atom_descriptors_layer.bias]
+        else:
+            params += [None, None]
+        params += [act_w, self.cached_zero_vector]
+        params = [_f32(t) for t in params]
+        save = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in params)
+        cfg = self._config(save)
+        return _EncoderFunction.apply(self, gs, cfg, hidden_out, device, *params, desc)
+
+
+class MPN(nn.Module):
+    """mpn.py:176-289."""
+
+    def __init__(self, args, atom_fdim: int = None, bond_fdim: int = None):
+        super(MPN, self).__init__()
+        self.atom_fdim = atom_fdim or get_atom_fdim(overwrite_default_atom=args.overwrite_default_atom_features)
+        self.bond_fdim = bond_fdim or get_bond_fdim(overwrite_default_atom=args.overwrite_default_atom_features,
+                                                    overwrite_default_bond=args.overwrite_default_bond_features,
+                                                    atom_messages=args.atom_messages)
+        self.features_only = args.features_only
+        self.use_input_features = args.use_input_features
+        self.device = args.device
+        self.atom_descriptors = args.atom_descriptors
+        self.overwrite_default_atom_features = args.overwrite_default_atom_features
+        self.overwrite_default_bond_features = args.overwrite_default_bond_features
+        if self.features_only:
+            return
+        if args.mpn_shared:
+            self.encoder = nn.ModuleList([MPNEncoder(args, self.atom_fdim, self.bond_fdim)] * args.number_of_molecules)
+        else:
+            self.encoder = nn.ModuleList([MPNEncoder(args, self.atom_fdim, self.bond_fdim)
+                                          for _ in range(args.number_of_molecules)])
+
+    def forward(self, batch, features_batch: List[np.ndarray] = None, atom_descriptors_batch: List[np.ndarray] = None,
+                atom_features_batch: List[np.ndarray] = None,
+                bond_features_batch: List[np.ndarray] = None) -> torch.FloatTensor:
+        if type(batch[0]) != BatchMolGraph:
+            batch = [[mols[i] for mols in batch] for i in range(len(batch[0]))]
+            if self.atom_descriptors == 'feature' and len(batch) > 1:
+                raise NotImplementedError('Atom/bond descriptors are currently only supported with one molecule '
+                                          'per input (i.e., number_of_molecules = 1).')
+            batch = [mol2graph(b) for b in batch]
+        dev = self.encoder[0].W_i.weight.device if not self.features_only else torch.device(self.device)
+        if self.use_input_features:
+            features_batch = torch.from_numpy(np.stack(features_batch)).float().to(dev)
+            if self.features_only:
+                return features_batch
+        if self.atom_descriptors == 'descriptor':
+            if len(batch) > 1:
+                raise NotImplementedError('Atom descriptors are currently only supported with one molecule '
+                                          'per input (i.e., number_of_molecules = 1).')
+            encodings = [enc(ba, atom_descriptors_batch) for enc, ba in zip(self.encoder, batch)]
+        else:
+            encodings = [enc(ba) for enc, ba in zip(self.encoder, batch)]
+        output = reduce(lambda x, y: torch.cat((x, y), dim=1), encodings)
+        if self.use_input_features:
+            if len(features_batch.shape) == 1:
+                features_batch = features_batch.view(1, -1)
+            output = torch.cat([output, features_batch], dim=1)
+        return output
