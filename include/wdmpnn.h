@@ -21,6 +21,10 @@
  *  - Row 0 of every atom / bond array is the reference's zero pad row (featurization.py:767-781);
  *    n_atoms / n_bonds INCLUDE it, exactly like BatchMolGraph.n_atoms / n_bonds.
  *  - fp32 storage and fp32 arithmetic (MFMA f32 in/out), int32 indices.
+ *  - Padding: f_atoms / f_bonds / atom_desc rows are allocated up to a multiple of 64 and their row
+ *    stride covers the feature width rounded up to 32; padding is zero.  (The host packer,
+ *    BatchMolGraph.device_graph, lays them out this way.)  Weights are the unpadded nn.Linear
+ *    tensors; wdmpnn_pack_params builds the padded GEMM operands from them.
  *  - Return 0 on success, a negative WD_ERR_* code on argument errors, or -(hipError_t) on a HIP
  *    launch error; wdmpnn_last_error() then holds a message (thread-local).
  *  - All work is enqueued on `stream` (a hipStream_t; NULL = default stream); no host sync, no
@@ -88,7 +92,7 @@ typedef struct WdGraph {
     WdCsr bond_feat_gather_t; /* unused by the gradients (inputs need no grad); may be zero */
     WdCsr atom_gather_t;    /* rows = message rows: dM_j += coef * dA_atom              */
     /* atom_descriptors == 'descriptor' (mpn.py:136-143) */
-    const float *atom_desc; /* [n_atoms, desc_dim] (row 0 zero pad) or NULL           */
+    const float *atom_desc; /* [n_atoms, round32(desc_dim)] (row 0 zero pad) or NULL */
     int32_t desc_dim;
     int32_t atom_messages;  /* 1 = atom-message mode (mpn.py:47-53, 93-94, 104-108) */
 } WdGraph;
@@ -106,6 +110,9 @@ typedef struct WdParams {
     const float *b_d;       /* [H+d] or NULL                                       */
     const float *prelu;     /* [1] PReLU slope (device) when activation == PReLU   */
     const float *zero_vec;  /* [H] cached_zero_vector (mpn.py:44, 148-149)         */
+    const void  *packed;    /* optional: output of wdmpnn_pack_params for these weights; NULL =
+                               wdmpnn_forward packs into its own workspace (one extra launch)     */
+    size_t packed_bytes;
 } WdParams;
 
 typedef struct WdConfig {
@@ -120,6 +127,8 @@ typedef struct WdConfig {
     int32_t prof_slot;      /* first event pair used when prof_pool != NULL                      */
     void   *prof_pool;      /* optional WdEventPool: an event pair is recorded around each message-
                                passing launch (the dominant kernel), pairs prof_slot + t - 1       */
+    int32_t gemm_variant;   /* 0 = default; 1..4 = tile 64x64|32x64 x prefetch depth 1|2 (tuning) */
+    int32_t reserved;
 } WdConfig;
 
 /* Gradients (device, caller-zeroed NOT required: every pointer is fully overwritten). NULL = skip. */
@@ -129,6 +138,12 @@ typedef struct WdGrads {
 
 int wdmpnn_abi_version(void);
 const char *wdmpnn_last_error(void);
+
+/* Padded / transposed copies of the weights for the GEMMs; depends only on the parameter values and
+ * the encoder dimensions, so callers cache it per parameter version (chemprop_amd does). */
+int wdmpnn_packed_params_bytes(const WdGraph *g, const WdParams *p, const WdConfig *c, size_t *bytes);
+int wdmpnn_pack_params(const WdGraph *g, const WdParams *p, const WdConfig *c, void *packed, size_t bytes,
+                       void *stream);
 
 /* Bytes of forward workspace (intermediates kept for backward when save_for_backward). */
 int wdmpnn_workspace_bytes(const WdGraph *g, const WdParams *p, const WdConfig *c, size_t *bytes);

@@ -53,15 +53,21 @@ def _linear(p: Dict[str, torch.Tensor], name: str, x: torch.Tensor) -> torch.Ten
 
 
 def encoder_forward(p: Dict[str, torch.Tensor], graph, args,
-                    atom_descriptors_batch: Optional[List[np.ndarray]] = None) -> torch.Tensor:
+                    atom_descriptors_batch: Optional[List[np.ndarray]] = None, dtype=None) -> torch.Tensor:
     """mpn.py:66-173 with dropout = 0.  ``p`` keys: W_i.weight, [W_i.bias], W_h.weight, [W_h.bias],
-    W_o.weight, W_o.bias, cached_zero_vector, [act_func.weight], [atom_descriptors_layer.*]."""
+    W_o.weight, W_o.bias, cached_zero_vector, [act_func.weight], [atom_descriptors_layer.*].
+    ``dtype=torch.float64`` evaluates the same op sequence in double precision (conditioning
+    reference for the parity tests); the default keeps the reference's float32."""
     act = lambda x: activation(args.activation, x, p.get('act_func.weight'))  # noqa: E731
     if atom_descriptors_batch is not None:  # mpn.py:77-79
         atom_descriptors_batch = [np.zeros([1, atom_descriptors_batch[0].shape[1]])] + list(atom_descriptors_batch)
         atom_descriptors_batch = torch.from_numpy(np.concatenate(atom_descriptors_batch, axis=0)).float()
+        if dtype is not None:
+            atom_descriptors_batch = atom_descriptors_batch.to(dtype)
     f_atoms, f_bonds, w_atoms, w_bonds, a2b, b2a, b2revb, a_scope, b_scope, degree_of_polym = \
         graph.get_components(atom_messages=args.atom_messages)  # mpn.py:81-82
+    if dtype is not None:
+        f_atoms, f_bonds, w_atoms, w_bonds = (t.to(dtype) for t in (f_atoms, f_bonds, w_atoms, w_bonds))
     if args.atom_messages:
         a2a = graph.get_a2a()  # mpn.py:89-90
         inp = _linear(p, 'W_i', f_atoms)  # mpn.py:93-94

@@ -26,7 +26,7 @@ ABI_VERSION = 1
 EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace_bytes',
                     'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
                     'wdmpnn_index_select_rows', 'wdmpnn_event_pool_create', 'wdmpnn_event_pool_destroy',
-                    'wdmpnn_event_pool_elapsed_ms')
+                    'wdmpnn_event_pool_elapsed_ms', 'wdmpnn_packed_params_bytes', 'wdmpnn_pack_params')
 
 
 class WdCsr(Structure):
@@ -46,13 +46,14 @@ class WdGraph(Structure):
 class WdParams(Structure):
     _fields_ = [('hidden', c_int32), ('W_i', c_void_p), ('b_i', c_void_p), ('W_h', c_void_p), ('b_h', c_void_p),
                 ('W_o', c_void_p), ('b_o', c_void_p), ('W_d', c_void_p), ('b_d', c_void_p), ('prelu', c_void_p),
-                ('zero_vec', c_void_p)]
+                ('zero_vec', c_void_p), ('packed', c_void_p), ('packed_bytes', c_size_t)]
 
 
 class WdConfig(Structure):
     _fields_ = [('depth', c_int32), ('undirected', c_int32), ('activation', c_int32), ('aggregation', c_int32),
                 ('aggregation_norm', c_float), ('dropout', c_float), ('seed', c_uint64),
-                ('save_for_backward', c_int32), ('prof_slot', c_int32), ('prof_pool', c_void_p)]
+                ('save_for_backward', c_int32), ('prof_slot', c_int32), ('prof_pool', c_void_p),
+                ('gemm_variant', c_int32), ('reserved', c_int32)]
 
 
 class WdGrads(Structure):
@@ -85,10 +86,14 @@ def lib() -> ctypes.CDLL:
     L.wdmpnn_backward.argtypes = [POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig), c_void_p, c_size_t,
                                   c_void_p, c_void_p, c_size_t, POINTER(WdGrads), c_void_p]
     L.wdmpnn_index_select_rows.argtypes = [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p]
+    L.wdmpnn_packed_params_bytes.argtypes = [POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig),
+                                             POINTER(c_size_t)]
+    L.wdmpnn_pack_params.argtypes = [POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig), c_void_p, c_size_t,
+                                     c_void_p]
     L.wdmpnn_event_pool_create.argtypes = [c_int32, POINTER(c_void_p)]
     L.wdmpnn_event_pool_destroy.argtypes = [c_void_p]
     L.wdmpnn_event_pool_elapsed_ms.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_float)]
-    for fn in ('wdmpnn_event_pool_create', 'wdmpnn_event_pool_destroy', 'wdmpnn_event_pool_elapsed_ms',
+    for fn in ('wdmpnn_packed_params_bytes', 'wdmpnn_pack_params', 'wdmpnn_event_pool_create', 'wdmpnn_event_pool_destroy', 'wdmpnn_event_pool_elapsed_ms',
                'wdmpnn_workspace_bytes', 'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
                'wdmpnn_index_select_rows'):
         getattr(L, fn).restype = c_int

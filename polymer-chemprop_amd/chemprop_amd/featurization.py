@@ -49,8 +49,8 @@ def set_extra_bond_fdim(extra: int) -> None:
     _PARAMS['EXTRA_BOND_FDIM'] = extra
 
 
-def _round4(x: int) -> int:
-    return (x + 3) & ~3
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
 
 
 class Csr:
@@ -276,11 +276,11 @@ class BatchMolGraph:
             nb_used = bond_fdim if bond_fdim is not None else get_bond_fdim(atom_messages=True)
             fb = fb[:, fb.shape[1] - nb_used:]
         Fa, Fb = fa.shape[1], fb.shape[1]
-        lda, ldb = _round4(Fa), _round4(Fb)
-        fa_p = np.zeros((fa.shape[0], lda), np.float32)
-        fa_p[:, :Fa] = fa
-        fb_p = np.zeros((fb.shape[0], ldb), np.float32)
-        fb_p[:, :Fb] = fb
+        lda, ldb = _round_up(Fa, 32), _round_up(Fb, 32)
+        fa_p = np.zeros((_round_up(fa.shape[0], 64), lda), np.float32)  # rows to the GEMM tile, K to 32
+        fa_p[:fa.shape[0], :Fa] = fa
+        fb_p = np.zeros((_round_up(fb.shape[0], 64), ldb), np.float32)
+        fb_p[:fb.shape[0], :Fb] = fb
         a_start = np.array([s for s, _ in self.a_scope], np.int32)
         a_size = np.array([n for _, n in self.a_scope], np.int32)
         xn = np.array(self.degree_of_polym, np.float32)

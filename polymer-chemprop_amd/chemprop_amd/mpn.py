@@ -34,31 +34,25 @@ class _EncoderFunction(torch.autograd.Function):
     features are inputs without gradient, as in the reference training loop)."""
 
     @staticmethod
-    def forward(ctx, enc, gstruct, cfg, hidden_out, device, W_i, b_i, W_h, b_h, W_o, b_o, W_d, b_d, prelu, zero_vec,
-                desc_keepalive):
+    def forward(ctx, enc, gstruct, cfg, pstruct, keep, hidden_out, device, W_i, b_i, W_h, b_h, W_o, b_o, W_d, b_d,
+                prelu):
         L = _native.lib()
-        p = _native.WdParams()
-        p.hidden = enc.hidden_size
-        p.W_i, p.b_i, p.W_h, p.b_h = map(_native.ptr, (W_i, b_i, W_h, b_h))
-        p.W_o, p.b_o, p.W_d, p.b_d = map(_native.ptr, (W_o, b_o, W_d, b_d))
-        p.prelu, p.zero_vec = _native.ptr(prelu), _native.ptr(zero_vec)
         nbytes = ctypes.c_size_t()
-        _native.check(L.wdmpnn_workspace_bytes(ctypes.byref(gstruct), ctypes.byref(p), ctypes.byref(cfg),
+        _native.check(L.wdmpnn_workspace_bytes(ctypes.byref(gstruct), ctypes.byref(pstruct), ctypes.byref(cfg),
                                                ctypes.byref(nbytes)), 'MPNEncoder workspace')
         ws = torch.empty(max(nbytes.value, 256), dtype=torch.uint8, device=device)
         out = torch.empty((gstruct.n_mols, hidden_out), dtype=torch.float32, device=device)
-        stream = _native.current_stream(device)
-        _native.check(L.wdmpnn_forward(ctypes.byref(gstruct), ctypes.byref(p), ctypes.byref(cfg), ws.data_ptr(),
-                                       nbytes.value, out.data_ptr(), stream), 'MPNEncoder forward')
+        _native.check(L.wdmpnn_forward(ctypes.byref(gstruct), ctypes.byref(pstruct), ctypes.byref(cfg), ws.data_ptr(),
+                                       nbytes.value, out.data_ptr(), _native.current_stream(device)),
+                      'MPNEncoder forward')
         if cfg.save_for_backward:
-            ctx.save_for_backward(W_i, b_i, W_h, b_h, W_o, b_o, W_d, b_d, prelu, zero_vec)
-            ctx.ws, ctx.ws_bytes, ctx.gstruct, ctx.cfg, ctx.p = ws, nbytes.value, gstruct, cfg, p
-            ctx.keep = desc_keepalive
+            ctx.save_for_backward(W_i, b_i, W_h, b_h, W_o, b_o, W_d, b_d, prelu)
+            ctx.ws, ctx.ws_bytes, ctx.gstruct, ctx.cfg, ctx.p, ctx.keep = ws, nbytes.value, gstruct, cfg, pstruct, keep
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        W_i, b_i, W_h, b_h, W_o, b_o, W_d, b_d, prelu, zero_vec = ctx.saved_tensors
+        W_i, b_i, W_h, b_h, W_o, b_o, W_d, b_d, prelu = ctx.saved_tensors
         L = _native.lib()
         dev = dout.device
         dout = dout.contiguous()
@@ -68,23 +62,23 @@ class _EncoderFunction(torch.autograd.Function):
                       'MPNEncoder backward workspace')
         scratch = torch.empty(max(nbytes.value, 256), dtype=torch.uint8, device=dev)
         want = ctx.needs_input_grad
-        # argument positions: 5 W_i, 6 b_i, 7 W_h, 8 b_h, 9 W_o, 10 b_o, 11 W_d, 12 b_d, 13 prelu
         grads = {}
         g = _native.WdGrads()
-        for name, t, pos in (('W_i', W_i, 5), ('b_i', b_i, 6), ('W_h', W_h, 7), ('b_h', b_h, 8), ('W_o', W_o, 9),
-                             ('b_o', b_o, 10), ('W_d', W_d, 11), ('b_d', b_d, 12), ('prelu', prelu, 13)):
+        first = 7  # position of W_i in forward's arguments
+        for k, (name, t) in enumerate((('W_i', W_i), ('b_i', b_i), ('W_h', W_h), ('b_h', b_h), ('W_o', W_o),
+                                       ('b_o', b_o), ('W_d', W_d), ('b_d', b_d), ('prelu', prelu))):
             if name in ('W_h', 'b_h') and ctx.cfg.depth == 1:
                 continue  # unused when depth == 1 (mpn.py:100 loop body never runs): no gradient, like autograd
-            if t is not None and want[pos]:
+            if t is not None and want[first + k]:
                 grads[name] = torch.empty_like(t)
                 setattr(g, name, grads[name].data_ptr())
         _native.check(L.wdmpnn_backward(ctypes.byref(ctx.gstruct), ctypes.byref(ctx.p), ctypes.byref(ctx.cfg),
                                         ctx.ws.data_ptr(), ctx.ws_bytes, dout.data_ptr(), scratch.data_ptr(),
                                         nbytes.value, ctypes.byref(g), _native.current_stream(dev)),
                       'MPNEncoder backward')
-        ctx.ws = None
-        return (None, None, None, None, None, grads.get('W_i'), grads.get('b_i'), grads.get('W_h'), grads.get('b_h'),
-                grads.get('W_o'), grads.get('b_o'), grads.get('W_d'), grads.get('b_d'), grads.get('prelu'), None, None)
+        ctx.ws = ctx.keep = None
+        return (None,) * 7 + tuple(grads.get(n) for n in ('W_i', 'b_i', 'W_h', 'b_h', 'W_o', 'b_o', 'W_d', 'b_d',
+                                                           'prelu'))
 
 
 class MPNEncoder(nn.Module):
@@ -125,6 +119,8 @@ class MPNEncoder(nn.Module):
                                       'indices in the reference (mpn.py:101-102) and is not supported')
         self._seed_counter = 0
         self._prof = None  # (event pool, first pair): bench.py measurement hook, see WdConfig.prof_pool
+        self._pack_cache = None  # (parameter-version key, packed weight buffer)
+        self._gemm_variant = 0  # WdConfig.gemm_variant (tuning knob; 0 = automatic)
 
     def _config(self, save: bool) -> _native.WdConfig:
         c = _native.WdConfig()
@@ -141,6 +137,7 @@ class MPNEncoder(nn.Module):
         c.save_for_backward = int(bool(save))
         if self._prof is not None:
             c.prof_pool, c.prof_slot = self._prof
+        c.gemm_variant = self._gemm_variant
         return c
 
     def forward(self, mol_graph: BatchMolGraph, atom_descriptors_batch: List[np.ndarray] = None) -> torch.FloatTensor:
@@ -164,13 +161,15 @@ class MPNEncoder(nn.Module):
             if not hasattr(self, 'atom_descriptors_layer'):
                 raise ValueError('atom descriptors given but the encoder has no atom_descriptors_layer')
             d = atom_descriptors_batch[0].shape[1]
-            padded = [np.zeros([1, d])] + list(atom_descriptors_batch)
-            desc = torch.from_numpy(np.concatenate(padded, axis=0)).float().to(device).contiguous()
-            if desc.shape[0] != gs.n_atoms:
+            rows = np.concatenate([np.zeros([1, d])] + list(atom_descriptors_batch), axis=0)
+            if rows.shape[0] != gs.n_atoms:
                 raise ValueError('The number of atoms is different from the length of the extra atom features')
             if any(n == 0 for _, n in mol_graph.a_scope):
                 raise RuntimeError('stack expects each tensor to be equal size (empty molecule with atom '
                                    'descriptors, mpn.py:149 vs 171)')
+            padded = np.zeros((-(-rows.shape[0] // 64) * 64, -(-d // 32) * 32), np.float32)
+            padded[:rows.shape[0], :d] = rows
+            desc = torch.from_numpy(padded).to(device)
             gs.atom_desc, gs.desc_dim = desc.data_ptr(), d
             hidden_out += d
         act_w = self.act_func.weight if isinstance(self.act_func, nn.PReLU) else None
@@ -181,11 +180,34 @@ class MPNEncoder(nn.Module):
             params += [self.atom_descriptors_layer.weight, self.atom_descriptors_layer.bias]
         else:
             params += [None, None]
-        params += [act_w, self.cached_zero_vector]
+        params += [act_w]
         params = [_f32(t) for t in params]
         save = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in params)
         cfg = self._config(save)
-        return _EncoderFunction.apply(self, gs, cfg, hidden_out, device, *params, desc)
+        pstruct, packed = self._packed_params(gs, cfg, params, device)
+        return _EncoderFunction.apply(self, gs, cfg, pstruct, (packed, desc), hidden_out, device, *params)
+
+    def _packed_params(self, gs, cfg, params, device):
+        """WdParams + the padded weight copies (wdmpnn_pack_params), cached per parameter version."""
+        p = _native.WdParams()
+        p.hidden = self.hidden_size
+        p.W_i, p.b_i, p.W_h, p.b_h, p.W_o, p.b_o, p.W_d, p.b_d, p.prelu = map(_native.ptr, params)
+        p.zero_vec = _native.ptr(_f32(self.cached_zero_vector))
+        key = (tuple((t.data_ptr(), t._version) if t is not None else None for t in params),
+               gs.atom_fdim, gs.bond_fdim, gs.desc_dim, gs.atom_messages, str(device))
+        cached = self._pack_cache
+        if cached is None or cached[0] != key:
+            L = _native.lib()
+            nbytes = ctypes.c_size_t()
+            _native.check(L.wdmpnn_packed_params_bytes(ctypes.byref(gs), ctypes.byref(p), ctypes.byref(cfg),
+                                                       ctypes.byref(nbytes)), 'pack size')
+            buf = torch.empty(nbytes.value, dtype=torch.uint8, device=device)
+            _native.check(L.wdmpnn_pack_params(ctypes.byref(gs), ctypes.byref(p), ctypes.byref(cfg), buf.data_ptr(),
+                                               nbytes.value, _native.current_stream(device)), 'pack params')
+            cached = self._pack_cache = (key, buf)
+        buf = cached[1]
+        p.packed, p.packed_bytes = buf.data_ptr(), buf.numel()
+        return p, buf
 
 
 class MPN(nn.Module):

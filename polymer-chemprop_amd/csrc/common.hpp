@@ -1,0 +1,78 @@
+// common.hpp — device helpers shared by the wD-MPNN kernels (activations, dropout hash, vector I/O).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wd {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+enum Act : int { ACT_RELU = 0, ACT_LEAKY = 1, ACT_PRELU = 2, ACT_TANH = 3, ACT_SELU = 4, ACT_ELU = 5,
+                 ACT_IDENTITY = 6 };
+
+constexpr float SELU_ALPHA = 1.6732632423543772848170429916717f;
+constexpr float SELU_SCALE = 1.0507009873554804934193349852946f;
+
+// nn_utils.py:70-99 activations (ReLU, LeakyReLU(0.1), PReLU, tanh, SELU, ELU); act(0) == 0 for all,
+// which keeps zero-padded columns zero through every layer.
+__device__ __forceinline__ float act_fwd(int act, float z, float slope) {
+    switch (act) {
+    case ACT_RELU: return z < 0.f ? 0.f : z;
+    case ACT_LEAKY: return z > 0.f ? z : 0.1f * z;
+    case ACT_PRELU: return z > 0.f ? z : slope * z;
+    case ACT_TANH: return tanhf(z);
+    case ACT_SELU: return z > 0.f ? SELU_SCALE * z : SELU_SCALE * (SELU_ALPHA * expm1f(z));
+    case ACT_ELU: return z > 0.f ? z : expm1f(z);
+    default: return z;
+    }
+}
+
+// d act / d z from the pre-activation z (torch's conventions at z == 0: ReLU 0, LeakyReLU/PReLU slope).
+__device__ __forceinline__ float act_grad(int act, float z, float slope) {
+    switch (act) {
+    case ACT_RELU: return z > 0.f ? 1.f : 0.f;
+    case ACT_LEAKY: return z > 0.f ? 1.f : 0.1f;
+    case ACT_PRELU: return z > 0.f ? 1.f : slope;
+    case ACT_TANH: { float t = tanhf(z); return 1.f - t * t; }
+    case ACT_SELU: return z > 0.f ? SELU_SCALE : SELU_SCALE * SELU_ALPHA * expf(z);
+    case ACT_ELU: return z > 0.f ? 1.f : expf(z);
+    default: return 1.f;
+    }
+}
+
+// Counter-based dropout: keep with probability 1-p, scale 1/(1-p).  Re-derived in backward from
+// (seed, layer, row, col), so no mask is stored.
+__device__ __forceinline__ float dropout_scale(uint64_t seed, uint32_t layer, uint32_t row, uint32_t col, float p) {
+    uint64_t x = seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(layer + 1));
+    x ^= ((uint64_t)row << 32) | col;
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    const float u = (float)(uint32_t)(x >> 40) * (1.0f / 16777216.0f);
+    return u >= p ? 1.0f / (1.0f - p) : 0.0f;
+}
+
+__device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+__device__ __forceinline__ void fma4(float4 &acc, float c, const float4 &v) {
+    acc.x = fmaf(c, v.x, acc.x);
+    acc.y = fmaf(c, v.y, acc.y);
+    acc.z = fmaf(c, v.z, acc.z);
+    acc.w = fmaf(c, v.w, acc.w);
+}
+
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+__device__ __forceinline__ void st4(float *p, const float4 &v) { *reinterpret_cast<float4 *>(p) = v; }
+
+// Bijective XCD-aware block -> tile map (cdna_hip_programming.md §5.5 T1): blocks b and b+8 share an
+// XCD under round-robin dispatch, so give each XCD a contiguous range of tiles; tiles of one row
+// block (same A rows, different column blocks) then share that XCD's L2.  Speed only, never
+// correctness.
+__device__ __forceinline__ int xcd_tile(int b, int ntiles) {
+    const int base = ntiles >> 3, rem = ntiles & 7;
+    const int x = b & 7, local = b >> 3;
+    return x * base + (x < rem ? x : rem) + local;
+}
+
+}  // namespace wd

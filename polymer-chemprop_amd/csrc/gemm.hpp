@@ -1,0 +1,341 @@
+// gemm.hpp — fp32 MFMA GEMMs of the wD-MPNN encoder (v_mfma_f32_32x32x2_f32, exact f32 fma chain,
+// 64 FLOP/clk/SIMD = the fp32 dense peak of MI355X).
+//
+// gemm_nt_kernel  C[m][n] = epi( sum_k A(m,k) * B[n][k] )        forward layers + data gradients
+//     A = one or two dense row-major segments laid side by side along k (mpn.py:132's concat without a
+//     copy), B = a packed weight [Np][Kp].  Every buffer is padded (rows to the 64-row tile, columns
+//     and K to the 32-wide chunk, padding zero), so the loads are unconditional float4 and the
+//     segment of a K-chunk is uniform over the workgroup: no per-element branches or waits in the
+//     K loop.
+// gemm_tn_kernel  slab[z][n][j] (+)= sum_{m in split z} dZ[m][n] * X[m][j]   weight gradients
+//     reduction over rows m (thousands of bonds) split across workgroups into slabs that a second
+//     kernel reduces in a fixed order (deterministic, no atomics).
+//
+// Tile: BM x BN per workgroup of WM x WN waves, each wave a (BM/WM) x (BN/WN) block of 32x32 MFMA
+// accumulators; K in chunks of 32 staged through LDS with a one-chunk register prefetch.  At MFMA
+// step s of a chunk, lane l supplies k = 16*(l>>5) + s, so a row-major LDS tile (row stride 36
+// floats, conflict-free for ds_read_b128 and ds_write_b128: checked by brute force over the lane
+// groups of MI355X_MICROARCH.md §LDS) feeds 16 MFMAs with four ds_read_b128 per operand.
+#pragma once
+#include "common.hpp"
+
+namespace wd {
+
+constexpr int BK = 32;
+
+enum EpiKind : int { EPI_ACT = 0, EPI_STORE = 1 };
+
+struct Epi {
+    int kind;
+    const float *bias;     // [N] (EPI_ACT; packed, zero padded)
+    const float *resid;    // [M][ld] or null (mpn.py:123 `input + message`)
+    float *Z;              // pre-activation out or null
+    float *Y;              // output
+    int ld;                // row stride of resid / Z / Y
+    long long slab_stride; // EPI_STORE (tn): Y += blockIdx.y * slab_stride
+    int accumulate;        // EPI_STORE: Y += C
+    int act;
+    const float *slope;    // PReLU slope (device)
+    float p_drop;
+    uint64_t seed;
+    uint32_t layer;
+};
+
+template <int TM, int TN>
+__device__ __forceinline__ void epilogue(const Epi &E, floatx16 (&acc)[TM][TN], int i0, int j0, int h, int l32,
+                                         int M, int N, float *Y) {
+    const float slope = (E.kind == EPI_ACT && E.act == ACT_PRELU) ? E.slope[0] : 0.f;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+            const int j = j0 + b * 32 + l32;
+            if (j >= N) continue;
+            const float bias = (E.kind == EPI_ACT && E.bias) ? E.bias[j] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = i0 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (i >= M) continue;
+                const size_t o = (size_t)i * E.ld + j;
+                const float v = acc[a][b][r];
+                if (E.kind == EPI_ACT) {
+                    float z = v + bias;
+                    if (E.resid) z += E.resid[o];
+                    if (E.Z) E.Z[o] = z;
+                    float y = act_fwd(E.act, z, slope);
+                    if (E.p_drop > 0.f) y *= dropout_scale(E.seed, E.layer, i, j, E.p_drop);
+                    Y[o] = y;
+                } else {
+                    Y[o] = E.accumulate ? Y[o] + v : v;
+                }
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------------------------
+// NT kernel over padded dense operands
+// ---------------------------------------------------------------------------------------------
+struct NtParams {
+    const float *a0; int lda0; int ka0;   // A segment 0: [Mp][lda0], K extent ka0 (multiple of 32)
+    const float *a1; int lda1; int ka1;   // A segment 1 (ka1 = 0: absent)
+    const float *b; int ldb;              // B packed [Np][ldb], ldb >= ka0 + ka1
+    int M, N;                             // valid output rows / cols written (<= padded extents)
+    int tiles_m, tiles_n;
+    Epi epi;
+};
+
+// KC = K-chunk (32 or 64 floats) consumed per LDS stage / barrier: 16 * KC / 32 MFMAs per wave and
+// accumulator between two barriers.  DEPTH = global-load prefetch distance in chunks.  DEPTH 1:
+// chunk k+1 is loaded while chunk k is multiplied.  DEPTH 2: two register sets alternate (loop
+// unrolled by two so every register index is static, §5.4 rule 20) and chunk k+2 is loaded while
+// chunk k is multiplied.  Two LDS stages, one barrier per chunk.  LDS row stride KC + 4 floats
+// (36 or 68: conflict-free for the b128 reads and writes).
+template <int BM, int BN, int WM, int WN, int DEPTH, int KC>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_nt_kernel(NtParams P) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    constexpr int LD = KC + 4;
+    constexpr int Q4 = KC / 4;  // float4 per tile row
+    constexpr int A_V4 = BM * Q4, B_V4 = BN * Q4;
+    constexpr int PA = A_V4 / NT, PB = B_V4 / NT;
+    constexpr int STAGE = (BM + BN) * LD;
+    static_assert(A_V4 % NT == 0 && B_V4 % NT == 0, "tile must divide evenly over threads");
+    __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wi = wave / WN, wj = wave % WN, h = lane >> 5, l32 = lane & 31;
+    const int tile = xcd_tile(blockIdx.x, P.tiles_m * P.tiles_n);
+    const int mt = tile / P.tiles_n, nt = tile % P.tiles_n;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int K = P.ka0 + P.ka1;
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+    const float *pb[PB];
+#pragma unroll
+    for (int p = 0; p < PB; ++p) {
+        const int q = tid + p * NT, r = q / Q4, c = (q % Q4) * 4;
+        pb[p] = P.b + (size_t)(n0 + r) * P.ldb + c;
+    }
+    struct Regs { float4 a[PA], b[PB]; };
+    auto load_chunk = [&](Regs &R, int k0) {
+        const bool seg1 = k0 >= P.ka0;  // workgroup-uniform (segments are KC-aligned)
+        const float *base = seg1 ? P.a1 : P.a0;
+        const int ld = seg1 ? P.lda1 : P.lda0;
+        const int kk = seg1 ? k0 - P.ka0 : k0;
+#pragma unroll
+        for (int p = 0; p < PA; ++p) {
+            const int q = tid + p * NT, r = q / Q4, c = (q % Q4) * 4;
+            R.a[p] = ld4(base + (size_t)(m0 + r) * ld + kk + c);
+        }
+#pragma unroll
+        for (int p = 0; p < PB; ++p) R.b[p] = ld4(pb[p] + k0);
+    };
+    auto store_chunk = [&](const Regs &R, float *st) {
+#pragma unroll
+        for (int p = 0; p < PA; ++p) {
+            const int q = tid + p * NT, r = q / Q4, c = (q % Q4) * 4;
+            st4(st + r * LD + c, R.a[p]);
+        }
+#pragma unroll
+        for (int p = 0; p < PB; ++p) {
+            const int q = tid + p * NT, r = q / Q4, c = (q % Q4) * 4;
+            st4(st + BM * LD + r * LD + c, R.b[p]);
+        }
+    };
+    auto compute = [&](const float *As) {
+        const float *Bs = As + BM * LD;
+#pragma unroll
+        for (int sub = 0; sub < KC / 32; ++sub) {
+            float af[TM][16], bf[TN][16];
+#pragma unroll
+            for (int a = 0; a < TM; ++a) {
+                const float *src = As + (wi * (BM / WM) + a * 32 + l32) * LD + 32 * sub + 16 * h;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 v = ld4(src + 4 * q);
+                    af[a][4 * q] = v.x; af[a][4 * q + 1] = v.y; af[a][4 * q + 2] = v.z; af[a][4 * q + 3] = v.w;
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < TN; ++b) {
+                const float *src = Bs + (wj * (BN / WN) + b * 32 + l32) * LD + 32 * sub + 16 * h;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 v = ld4(src + 4 * q);
+                    bf[b][4 * q] = v.x; bf[b][4 * q + 1] = v.y; bf[b][4 * q + 2] = v.z; bf[b][4 * q + 3] = v.w;
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+#pragma unroll
+                for (int a = 0; a < TM; ++a)
+#pragma unroll
+                    for (int b = 0; b < TN; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
+        }
+    };
+
+    const int nchunks = K / KC;
+    if constexpr (DEPTH == 1) {
+        Regs R;
+        load_chunk(R, 0);
+        store_chunk(R, lds);
+        __syncthreads();
+        for (int kc = 0; kc < nchunks; ++kc) {
+            const bool more = kc + 1 < nchunks;
+            if (more) load_chunk(R, (kc + 1) * KC);
+            compute(lds + (kc & 1) * STAGE);
+            if (more) store_chunk(R, lds + ((kc + 1) & 1) * STAGE);
+            __syncthreads();
+        }
+    } else {
+        Regs R0, R1;
+        load_chunk(R0, 0);
+        if (nchunks > 1) load_chunk(R1, KC);
+        store_chunk(R0, lds);
+        __syncthreads();
+        // step(kc, Rnext, Rfree): Rnext holds chunk kc+1 (in flight), Rfree receives chunk kc+2
+        auto step = [&](int kc, Regs &Rnext, Regs &Rfree) {
+            if (kc + 2 < nchunks) load_chunk(Rfree, (kc + 2) * KC);
+            compute(lds + (kc & 1) * STAGE);
+            if (kc + 1 < nchunks) store_chunk(Rnext, lds + ((kc + 1) & 1) * STAGE);
+            __syncthreads();
+        };
+        int kc = 0;
+        for (; kc + 1 < nchunks; kc += 2) {
+            step(kc, R1, R0);
+            step(kc + 1, R0, R1);
+        }
+        if (kc < nchunks) step(kc, R1, R0);
+    }
+    epilogue<TM, TN>(P.epi, acc, m0 + wi * (BM / WM), n0 + wj * (BN / WN), h, l32, P.M, P.N, P.epi.Y);
+}
+
+// ---------------------------------------------------------------------------------------------
+// TN kernel (weight gradients): both operands k-major (rows = m), masked at the split's row range.
+// ---------------------------------------------------------------------------------------------
+enum SegKind : int { SEG_DENSE = 0, SEG_ONES = 2 };
+
+struct Seg {
+    const float *src;
+    int ld;
+    int K;      // width (padded extent; zeros beyond the real width are fine)
+    int kp0;    // first column in the operand's column space (multiple of 4)
+    int kind;
+};
+
+struct Src {
+    Seg s[3];
+    int nseg;
+    int rows;      // valid rows
+    int cols_p;    // column extent (multiple of 4)
+};
+
+__device__ __forceinline__ float4 seg_load4(const Seg &g, int r, int kk) {
+    if (kk >= g.K) return f4zero();
+    if (g.kind == SEG_ONES) return kk == 0 ? make_float4(1.f, 0.f, 0.f, 0.f) : f4zero();
+    return ld4(g.src + (size_t)r * g.ld + kk);
+}
+
+__device__ __forceinline__ float4 src_load4(const Src &S, int r, int cp, int rlim) {
+    if (r >= rlim || cp >= S.cols_p) return f4zero();
+    int s = 0;
+    if (S.nseg > 1 && cp >= S.s[1].kp0) s = 1;
+    if (S.nseg > 2 && cp >= S.s[2].kp0) s = 2;
+    const Seg &g = s == 0 ? S.s[0] : (s == 1 ? S.s[1] : S.s[2]);
+    return seg_load4(g, r, cp - g.kp0);
+}
+
+struct TnParams {
+    Src A, B;        // A: rows m, cols i (=n);  B: rows m, cols j
+    int M, N;        // output rows (i) / cols (j)
+    int K;           // reduction rows
+    int k_per_split; // multiple of 32
+    int tiles_m, tiles_n;
+    Epi epi;
+};
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(TnParams P) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+    constexpr int A_LD = BM + 4, B_LD = BN + 4;
+    constexpr int A_V4 = BK * BM / 4, B_V4 = BK * BN / 4;
+    constexpr int PA = (A_V4 + NT - 1) / NT, PB = (B_V4 + NT - 1) / NT;
+    __shared__ __attribute__((aligned(16))) float lds[BK * A_LD + BK * B_LD];
+    float *As = lds, *Bs = lds + BK * A_LD;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wi = wave / WN, wj = wave % WN, h = lane >> 5, l32 = lane & 31;
+    const int tile = blockIdx.x;
+    const int mt = tile / P.tiles_n, nt = tile % P.tiles_n;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int kbeg = blockIdx.y * P.k_per_split;
+    const int kend = min(P.K, kbeg + P.k_per_split);
+
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+    float4 ra[PA], rb[PB];
+    auto load_chunk = [&](int k0) {
+#pragma unroll
+        for (int p = 0; p < PA; ++p) {
+            const int q = tid + p * NT;
+            ra[p] = q < A_V4 ? src_load4(P.A, k0 + q / (BM / 4), m0 + (q % (BM / 4)) * 4, kend) : f4zero();
+        }
+#pragma unroll
+        for (int p = 0; p < PB; ++p) {
+            const int q = tid + p * NT;
+            rb[p] = q < B_V4 ? src_load4(P.B, k0 + q / (BN / 4), n0 + (q % (BN / 4)) * 4, kend) : f4zero();
+        }
+    };
+    const int nchunks = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+    if (nchunks > 0) load_chunk(kbeg);
+    for (int kc = 0; kc < nchunks; ++kc) {
+        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < PA; ++p) {
+            const int q = tid + p * NT;
+            if (q < A_V4) st4(As + (q / (BM / 4)) * A_LD + (q % (BM / 4)) * 4, ra[p]);
+        }
+#pragma unroll
+        for (int p = 0; p < PB; ++p) {
+            const int q = tid + p * NT;
+            if (q < B_V4) st4(Bs + (q / (BN / 4)) * B_LD + (q % (BN / 4)) * 4, rb[p]);
+        }
+        __syncthreads();
+        if (kc + 1 < nchunks) load_chunk(kbeg + (kc + 1) * BK);
+        float af[TM][16], bf[TN][16];
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int s = 0; s < 16; ++s) af[a][s] = As[(16 * h + s) * A_LD + wi * (BM / WM) + a * 32 + l32];
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int s = 0; s < 16; ++s) bf[b][s] = Bs[(16 * h + s) * B_LD + wj * (BN / WN) + b * 32 + l32];
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
+    }
+    float *Y = P.epi.Y + (size_t)blockIdx.y * P.epi.slab_stride;
+    epilogue<TM, TN>(P.epi, acc, m0 + wi * (BM / WM), n0 + wj * (BN / WN), h, l32, P.M, P.N, Y);
+}
+
+}  // namespace wd

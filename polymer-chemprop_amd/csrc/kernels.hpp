@@ -1,0 +1,268 @@
+// kernels.hpp — bandwidth-bound kernels of the wD-MPNN encoder: CSR row gathers (the padded
+// index_select_ND + weighted sum of mpn.py:112-131), the molecule readout (mpn.py:145-171), the
+// fused activation/gather backward, weight packing and the deterministic slab reduction.
+#pragma once
+#include "common.hpp"
+
+namespace wd {
+
+// ---------------------------------------------------------------------------------------------
+// Row gather:  out[r][c] = sum_{e in [ptr[r], ptr[r+1])} coef[e] * S(idx[e], c),  c < K,  r < rows
+//   S(j, c) = src[j][c]  or  (src[j][c] + src[rev[j]][c]) / 2 with sym_rev (mpn.py:101-102)
+// Rows [rows, rows_p) are zero filled (padding of the next GEMM's A operand).
+// One lane per (row, 4 columns): a 1,200-B message row is read by 75 consecutive lanes (coalesced
+// float4); the dependent chain is ptr -> idx -> row, hidden by having every row in flight at once.
+// ---------------------------------------------------------------------------------------------
+struct GatherP {
+    const float *src; int ld_src; int K;
+    const int32_t *ptr; const int32_t *idx; const float *coef;
+    const int32_t *sym_rev;
+    float *out; int ld_out;
+    int rows, rows_p;
+};
+
+__global__ __launch_bounds__(256) void gather_rows_kernel(GatherP P) {
+    const int nq = P.K >> 2;  // K multiple of 4
+    const size_t total = (size_t)P.rows_p * nq;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+        const int r = (int)(t / nq), c = (int)(t % nq) * 4;
+        float4 acc = f4zero();
+        if (r < P.rows) {
+            const int e0 = P.ptr[r], e1 = P.ptr[r + 1];
+            for (int e = e0; e < e1; ++e) {
+                const int j = P.idx[e];
+                const float w = P.coef ? P.coef[e] : 1.0f;
+                float4 v = ld4(P.src + (size_t)j * P.ld_src + c);
+                if (P.sym_rev) {
+                    const float4 u = ld4(P.src + (size_t)P.sym_rev[j] * P.ld_src + c);
+                    v.x = (v.x + u.x) / 2.0f; v.y = (v.y + u.y) / 2.0f;
+                    v.z = (v.z + u.z) / 2.0f; v.w = (v.w + u.w) / 2.0f;
+                }
+                fma4(acc, w, v);
+            }
+        }
+        st4(P.out + (size_t)r * P.ld_out + c, acc);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Readout (mpn.py:145-171): out_i = Xn_i * (sum_a w_a h_a) / sum_a w_a  (mean) | sum | / norm.
+// One workgroup per molecule; lanes = (atom slot, float4 column); atom slots reduced through LDS
+// in a fixed order.
+// ---------------------------------------------------------------------------------------------
+struct ReadoutP {
+    const float *h; int ldh; int ncols;
+    const float *w_atoms; const int32_t *mol_start; const int32_t *mol_size; const float *xn;
+    int agg; float norm;
+    const float *zero_vec;
+    float *out;
+};
+
+constexpr int RO_THREADS = 256;
+constexpr int RO_QW = 16;                    // float4 columns per workgroup
+constexpr int RO_SLOTS = RO_THREADS / RO_QW;  // atom slots per workgroup
+
+// grid = (molecules, ceil(ncols / (4 * RO_QW))); lane = (atom slot, float4 column); the 16 slot
+// partial sums are added in slot order (deterministic).
+__global__ __launch_bounds__(RO_THREADS) void readout_kernel(ReadoutP P) {
+    __shared__ float4 part[RO_THREADS];
+    const int i = blockIdx.x;
+    const int a0 = P.mol_start[i], n = P.mol_size[i];
+    const int slot = threadIdx.x / RO_QW, ql = threadIdx.x % RO_QW;
+    const int q = blockIdx.y * RO_QW + ql;
+    float *out = P.out + (size_t)i * P.ncols;
+    if (n == 0) {  // mpn.py:148-149 cached_zero_vector (no Xn factor)
+        if (slot == 0)
+            for (int e = 0; e < 4; ++e)
+                if (4 * q + e < P.ncols) out[4 * q + e] = P.zero_vec[4 * q + e];
+        return;
+    }
+    float4 s = f4zero();
+    if (4 * q < P.ncols)
+        for (int a = slot; a < n; a += RO_SLOTS) fma4(s, P.w_atoms[a0 + a], ld4(P.h + (size_t)(a0 + a) * P.ldh + 4 * q));
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (slot != 0 || 4 * q >= P.ncols) return;
+    float4 t = part[ql];
+    for (int k = 1; k < RO_SLOTS; ++k) {
+        const float4 u = part[k * RO_QW + ql];
+        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    float wsum = 0.f;  // sequential, identical order in every thread
+    for (int a = 0; a < n; ++a) wsum += P.w_atoms[a0 + a];
+    const float x = P.xn[i];
+    const float v[4] = {t.x, t.y, t.z, t.w};
+    for (int e = 0; e < 4; ++e) {
+        const int c = 4 * q + e;
+        if (c >= P.ncols) break;
+        const float m = P.agg == 0 ? v[e] / wsum : (P.agg == 2 ? v[e] / P.norm : v[e]);
+        out[c] = x * m;
+    }
+}
+
+// d readout / d h: dh[a] = dout[i] * Xn_i * w_a * (1/sum w | 1 | 1/norm); rows outside every scope
+// stay 0 (caller memsets).
+__global__ __launch_bounds__(256) void readout_bwd_kernel(ReadoutP P, const float *__restrict__ dout,
+                                                          float *__restrict__ dh) {
+    const int i = blockIdx.x;
+    const int a0 = P.mol_start[i], n = P.mol_size[i];
+    if (n == 0) return;
+    float wsum = 0.f;
+    for (int a = 0; a < n; ++a) wsum += P.w_atoms[a0 + a];
+    const float x = P.xn[i];
+    for (int t = threadIdx.x; t < n * P.ncols; t += blockDim.x) {
+        const int a = t / P.ncols, c = t % P.ncols;
+        const float g = dout[(size_t)i * P.ncols + c] * x;
+        const float gs = P.agg == 0 ? g / wsum : (P.agg == 2 ? g / P.norm : g);
+        dh[(size_t)(a0 + a) * P.ldh + c] = gs * P.w_atoms[a0 + a];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Backward of one activation layer, fused with the gather that produces its incoming gradient:
+//   g   = sum_e coef[e] * G[idx[e]]  (csr) | (G[r] + G[rev[r]]) / 2 (sym) | G[r] (dense)
+//   dz  = g * dropout_scale * act'(z)          (Z == null: dz = g)
+//   dz += add_in[r];  res_out (=|+=) dz;  PReLU partial sum of z * g * scale over z <= 0
+// Rows [rows, rows_p) are written as 0.
+// ---------------------------------------------------------------------------------------------
+struct ActBwd {
+    const float *G; int ldg;
+    const int32_t *ptr; const int32_t *idx; const float *coef;
+    const int32_t *sym_rev;
+    const float *Z; int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;
+    const float *add_in;
+    float *res_out; int res_init;
+    float *out;
+    float *prelu_part;
+    int rows, rows_p, cols, ld;  // cols: padded width (zero columns stay zero)
+};
+
+__global__ __launch_bounds__(256) void act_bwd_kernel(ActBwd P) {
+    __shared__ float red[256];
+    const float slope = (P.Z && P.act == ACT_PRELU) ? P.slope[0] : 0.f;
+    float ppart = 0.f;
+    const size_t total = (size_t)P.rows_p * P.cols;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+        const int r = (int)(t / P.cols), c = (int)(t % P.cols);
+        const size_t o = (size_t)r * P.ld + c;
+        float dz = 0.f;
+        if (r < P.rows) {
+            float g;
+            if (P.ptr) {
+                g = 0.f;
+                for (int e = P.ptr[r]; e < P.ptr[r + 1]; ++e)
+                    g = fmaf(P.coef ? P.coef[e] : 1.f, P.G[(size_t)P.idx[e] * P.ldg + c], g);
+            } else if (P.sym_rev) {
+                g = (P.G[(size_t)r * P.ldg + c] + P.G[(size_t)P.sym_rev[r] * P.ldg + c]) * 0.5f;
+            } else {
+                g = P.G[(size_t)r * P.ldg + c];
+            }
+            dz = g;
+            if (P.Z) {
+                const float z = P.Z[o];
+                const float s = P.p_drop > 0.f ? dropout_scale(P.seed, P.layer, r, c, P.p_drop) : 1.f;
+                dz = g * s * act_grad(P.act, z, slope);
+                if (P.act == ACT_PRELU && !(z > 0.f)) ppart += z * g * s;
+            }
+            if (P.add_in) dz += P.add_in[o];
+        }
+        if (P.res_out) P.res_out[o] = P.res_init ? dz : P.res_out[o] + dz;
+        P.out[o] = dz;
+    }
+    if (P.prelu_part) {
+        red[threadIdx.x] = ppart;
+        __syncthreads();
+        for (int s = 128; s > 0; s >>= 1) {
+            if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) P.prelu_part[blockIdx.x] = red[0];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Weight packing: nn.Linear weights -> zero-padded GEMM operands (and transposes for the data
+// gradients).  dst[r][c], r < rows_p, c < cols_p:
+//   plain:      segment s with dst cols [dc0_s, dc0_s + K_s): src[r][sc0_s + c - dc0_s]  (r < nrows)
+//   transpose:  src[c][sc0_0 + r]  for r < nrows (= K_0 source cols), c < K_0 (source rows)
+// ---------------------------------------------------------------------------------------------
+struct PackJob {
+    float *dst; int rows_p, cols_p;
+    const float *src; int ld_src;
+    int transpose, nrows, nseg;
+    int dc0[2], sc0[2], K[2];
+};
+struct PackJobs { PackJob j[12]; int n; };
+
+__global__ __launch_bounds__(256) void pack_kernel(PackJobs J) {
+    const PackJob &P = J.j[blockIdx.y];
+    const size_t total = (size_t)P.rows_p * P.cols_p;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+        const int r = (int)(t / P.cols_p), c = (int)(t % P.cols_p);
+        float v = 0.f;
+        if (P.src && r < P.nrows) {
+            if (P.transpose) {
+                if (c < P.K[0]) v = P.src[(size_t)c * P.ld_src + P.sc0[0] + r];
+            } else {
+                for (int s = 0; s < P.nseg; ++s)
+                    if (c >= P.dc0[s] && c < P.dc0[s] + P.K[s]) v = P.src[(size_t)r * P.ld_src + P.sc0[s] + c - P.dc0[s]];
+            }
+        }
+        P.dst[t] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Slab reduction of the weight-gradient GEMMs (fixed split order: deterministic).
+//   dW[n][w0_s + kk] = sum_z slab[z][n][c0_s + kk],  db[n] = sum_z slab[z][n][bias_col]
+// ---------------------------------------------------------------------------------------------
+struct SlabReduce {
+    const float *slab; int nsplit; long long slab_stride; int ld_slab;
+    int rows;
+    int nseg; int c0[3], w0[3], K[3];
+    float *dW; int ldw;
+    float *db; int bias_col;
+};
+
+__global__ __launch_bounds__(256) void slab_reduce_kernel(SlabReduce P) {
+    const int n = blockIdx.x;
+    const float *row = P.slab + (size_t)n * P.ld_slab;
+    if (P.dW)
+        for (int s = 0; s < P.nseg; ++s)
+            for (int kk = threadIdx.x; kk < P.K[s]; kk += blockDim.x) {
+                float acc = 0.f;
+                for (int z = 0; z < P.nsplit; ++z) acc += row[(size_t)z * P.slab_stride + P.c0[s] + kk];
+                P.dW[(size_t)n * P.ldw + P.w0[s] + kk] = acc;
+            }
+    if (P.db && threadIdx.x == 0) {
+        float acc = 0.f;
+        for (int z = 0; z < P.nsplit; ++z) acc += row[(size_t)z * P.slab_stride + P.bias_col];
+        P.db[n] = acc;
+    }
+}
+
+__global__ void sum_kernel(const float *__restrict__ x, int n, float *__restrict__ out) {
+    __shared__ float red[256];
+    float s = 0.f;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) s += x[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[0] = red[0];
+}
+
+// nn_utils.py:50-67 index_select_ND on rows.
+__global__ __launch_bounds__(256) void index_select_rows_kernel(const float *__restrict__ src, int64_t row_len,
+                                                                const int64_t *__restrict__ index, int64_t n_index,
+                                                                float *__restrict__ out) {
+    const int64_t total = n_index * row_len;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = t / row_len, c = t % row_len;
+        out[t] = src[index[i] * row_len + c];
+    }
+}
+
+}  // namespace wd

@@ -1,29 +1,32 @@
-// wdmpnn.hip — MI355X (gfx950) wD-MPNN encoder: kernels + C-ABI (include/wdmpnn.h).
+// wdmpnn.hip — MI355X (gfx950) wD-MPNN encoder: C-ABI (include/wdmpnn.h) and launch orchestration.
 //
-// Forward = MPNEncoder.forward (chemprop/models/mpn.py:66-173) as depth+2 (+1 with atom descriptors)
-// launches of one fused gather-GEMM kernel (gemm_gather.hpp) and one readout kernel:
+// Forward = MPNEncoder.forward (chemprop/models/mpn.py:66-173):
 //
-//   L0        M0 = act(f_bonds W_i^T (+b_i))                          mpn.py:92-97
-//   L1..T-1   M_t = act(Z0 + X_t W_h^T (+b_h)),                        mpn.py:100-124
-//             X_t[b] = sum_{j in in(b2a[b])} w_j M_{t-1}[j] - M_{t-1}[b2revb[b]]
-//             (gathered into LDS inside the GEMM; the reverse term is folded into the gather list
-//              as coefficient w_rev - 1, dropped when it is 0)
-//   LT        h = act([f_atoms | sum_{j in in(a)} w_j M_{T-1}[j]] W_o^T + b_o)   mpn.py:126-134
-//   (LT+1     hd = [h | desc] W_d^T + b_d                              mpn.py:136-143)
-//   readout   out_i = Xn_i * sum_a w_a h_a / sum_a w_a  (mean|sum|norm)  mpn.py:145-171
+//   L0        Z0 = f_bonds W_i^T (+b_i);  M0 = act(Z0)                      mpn.py:92-97
+//   t=1..T-1  X_t = gather(M_{t-1})        X_t[b] = sum_{j in in(b2a[b])} w_j M_j - M_{b2revb[b]}
+//                                         (reverse term folded into the list as w_rev - 1)
+//             M_t = act(Z0 + X_t W_h^T (+b_h))                             mpn.py:100-124
+//   LT        A = gather(M_{T-1}) (sum_{j in in(a)} w_j M_j);  h = act([f_atoms | A] W_o^T + b_o)
+//                                                                           mpn.py:126-134
+//  (LT+1      hd = [h | desc] W_d^T + b_d                                   mpn.py:136-143)
+//   readout   out_i = Xn_i * sum_a w_a h_a / sum_a w_a (mean | sum | norm)   mpn.py:145-171
 //
-// Backward = the autograd graph of the same (used by train.py:79) with deterministic, atomics-free
-// kernels: transposed gather lists for the scatter-adds, split-K slabs + ordered reduction for the
-// weight gradients.
+// Buffers are padded: rows to 64 (GEMM row tile), hidden columns to 64, K extents to 32, padding
+// zero; weights are packed once per parameter version (wdmpnn_pack_params) into the same padded
+// shapes (+ transposes for the backward data gradients).  Backward = the autograd graph of the
+// above with deterministic, atomics-free kernels.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <array>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
 
-#include "gemm_gather.hpp"
+#include "gemm.hpp"
+#include "kernels.hpp"
 #include "wdmpnn.h"
 
 using namespace wd;
@@ -42,320 +45,20 @@ int fail(int code, const char *fmt, ...) {
     return code;
 }
 
-#define WD_CHECK_LAUNCH(what)                                                              \
-    do {                                                                                   \
-        hipError_t e_ = hipGetLastError();                                                 \
-        if (e_ != hipSuccess) return fail(-(int)e_, "%s: %s", what, hipGetErrorString(e_)); \
+#define WD_CHECK_LAUNCH(what)                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = hipGetLastError();                                                     \
+        if (e_ != hipSuccess) return fail(-(int)e_, "%s: %s", what, hipGetErrorString(e_));   \
+    } while (0)
+#define WD_TRY(x)             \
+    do {                      \
+        int rc_ = (x);        \
+        if (rc_) return rc_;  \
     } while (0)
 
-inline int round4(int x) { return (x + 3) & ~3; }
+inline int rup(int x, int m) { return (x + m - 1) / m * m; }
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
-
-// ------------------------------------------------------------------------------------------------
-// small kernels
-// ------------------------------------------------------------------------------------------------
-
-// mpn.py:145-171: per-molecule weighted readout.  One workgroup per molecule, columns over lanes.
-__global__ __launch_bounds__(128) void readout_kernel(const float *__restrict__ h, int ldh, int ncols,
-                                                      const float *__restrict__ w_atoms,
-                                                      const int32_t *__restrict__ mol_start,
-                                                      const int32_t *__restrict__ mol_size,
-                                                      const float *__restrict__ xn, int agg, float norm,
-                                                      const float *__restrict__ zero_vec,
-                                                      float *__restrict__ out) {
-    const int i = blockIdx.x;
-    const int a0 = mol_start[i], n = mol_size[i];
-    if (n == 0) {  // mpn.py:148-149 cached_zero_vector (no Xn factor)
-        for (int c = threadIdx.x; c < ncols; c += blockDim.x) out[(size_t)i * ncols + c] = zero_vec[c];
-        return;
-    }
-    float wsum = 0.f;
-    for (int a = 0; a < n; ++a) wsum += w_atoms[a0 + a];
-    const float x = xn[i];
-    for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
-        float s = 0.f;
-        for (int a = 0; a < n; ++a) s += w_atoms[a0 + a] * h[(size_t)(a0 + a) * ldh + c];
-        float v = agg == WD_AGG_MEAN ? s / wsum : (agg == WD_AGG_NORM ? s / norm : s);
-        out[(size_t)i * ncols + c] = x * v;
-    }
-}
-
-// d readout / d h: dh[a] = dout[i] * Xn_i * w_a * (1/sum w | 1 | 1/norm); rows outside every scope
-// stay 0 (caller memsets).
-__global__ __launch_bounds__(128) void readout_bwd_kernel(const float *__restrict__ dout, int ncols,
-                                                          const float *__restrict__ w_atoms,
-                                                          const int32_t *__restrict__ mol_start,
-                                                          const int32_t *__restrict__ mol_size,
-                                                          const float *__restrict__ xn, int agg, float norm,
-                                                          float *__restrict__ dh, int lddh) {
-    const int i = blockIdx.x;
-    const int a0 = mol_start[i], n = mol_size[i];
-    if (n == 0) return;
-    float wsum = 0.f;
-    for (int a = 0; a < n; ++a) wsum += w_atoms[a0 + a];
-    const float x = xn[i];
-    const float scale = agg == WD_AGG_MEAN ? 1.f / wsum : (agg == WD_AGG_NORM ? 1.f / norm : 1.f);
-    for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
-        const float g = dout[(size_t)i * ncols + c] * x;
-        const float gs = agg == WD_AGG_MEAN ? g / wsum : g * scale;
-        for (int a = 0; a < n; ++a) dh[(size_t)(a0 + a) * lddh + c] = gs * w_atoms[a0 + a];
-    }
-}
-
-// mpn.py:101-102: message = (message + message[b2revb]) / 2
-__global__ __launch_bounds__(256) void symmetrize_kernel(const float *__restrict__ m, const int32_t *__restrict__ rev,
-                                                         int rows, int cols, float *__restrict__ out) {
-    const size_t total = (size_t)rows * cols;
-    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
-        const int r = (int)(t / cols), c = (int)(t % cols);
-        out[t] = (m[t] + m[(size_t)rev[r] * cols + c]) / 2.0f;
-    }
-}
-
-// Backward of one activation layer, fused with the gather that produces its incoming gradient:
-//   g   = sum_e coef[e] * G[idx[e]]         (csr) | 0.5*(G[r] + G[rev[r]]) (sym) | G[r] (dense)
-//   dz  = g * dropout_scale * act'(z)        (Z == null: dz = g, gather only)
-//   dz += add_in[r]                           (residual gradient of mpn.py:123 reaching input)
-//   res_out (=|+=) dz                         (accumulate the residual gradient)
-//   prelu partial: sum over z<=0 of z * g * dropout_scale
-struct ActBwd {
-    const float *G; int ldg;
-    const int32_t *ptr; const int32_t *idx; const float *coef;
-    const int32_t *sym_rev;
-    const float *Z; int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;
-    const float *add_in;
-    float *res_out; int res_init;
-    float *out;
-    float *prelu_part;
-    int rows, cols;
-};
-
-__global__ __launch_bounds__(256) void act_bwd_kernel(ActBwd P) {
-    __shared__ float red[256];
-    const float slope = (P.Z && P.act == ACT_PRELU) ? P.slope[0] : 0.f;
-    float ppart = 0.f;
-    const size_t total = (size_t)P.rows * P.cols;
-    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
-        const int r = (int)(t / P.cols), c = (int)(t % P.cols);
-        float g;
-        if (P.ptr) {
-            g = 0.f;
-            for (int e = P.ptr[r]; e < P.ptr[r + 1]; ++e)
-                g = fmaf(P.coef ? P.coef[e] : 1.f, P.G[(size_t)P.idx[e] * P.ldg + c], g);
-        } else if (P.sym_rev) {
-            g = (P.G[(size_t)r * P.ldg + c] + P.G[(size_t)P.sym_rev[r] * P.ldg + c]) * 0.5f;
-        } else {
-            g = P.G[(size_t)r * P.ldg + c];
-        }
-        float dz = g;
-        if (P.Z) {
-            const float z = P.Z[t];
-            const float s = P.p_drop > 0.f ? dropout_scale(P.seed, P.layer, r, c, P.p_drop) : 1.f;
-            dz = g * s * act_grad(P.act, z, slope);
-            if (P.act == ACT_PRELU && !(z > 0.f)) ppart += z * g * s;
-        }
-        if (P.add_in) dz += P.add_in[t];
-        if (P.res_out) P.res_out[t] = P.res_init ? dz : P.res_out[t] + dz;
-        P.out[t] = dz;
-    }
-    if (P.prelu_part) {
-        red[threadIdx.x] = ppart;
-        __syncthreads();
-        for (int s = 128; s > 0; s >>= 1) {
-            if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) P.prelu_part[blockIdx.x] = red[0];
-    }
-}
-
-struct SlabSeg { int kp0, K, wcol, kind; float *dst; };
-struct SlabReduce {
-    const float *slab; int nsplit; long long slab_stride; int ld_slab;
-    int rows;  // output rows (n)
-    SlabSeg s[3]; int nseg;
-    int ldw;
-};
-
-// dW[n][wcol + kk] = sum_z slab[z][n][kp0 + kk]  (fixed split order: deterministic)
-__global__ __launch_bounds__(256) void slab_reduce_kernel(SlabReduce P) {
-    const int n = blockIdx.x;
-    for (int si = 0; si < P.nseg; ++si) {
-        const SlabSeg g = P.s[si];
-        if (!g.dst) continue;
-        for (int kk = threadIdx.x; kk < g.K; kk += blockDim.x) {
-            float acc = 0.f;
-            for (int z = 0; z < P.nsplit; ++z)
-                acc += P.slab[(size_t)z * P.slab_stride + (size_t)n * P.ld_slab + g.kp0 + kk];
-            if (g.kind == SEG_ONES) g.dst[n] = acc;
-            else g.dst[(size_t)n * P.ldw + g.wcol + kk] = acc;
-        }
-    }
-}
-
-__global__ void sum_kernel(const float *__restrict__ x, int n, float *__restrict__ out) {
-    __shared__ float red[256];
-    float s = 0.f;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) s += x[i];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int k = 128; k > 0; k >>= 1) {
-        if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) out[0] = red[0];
-}
-
-// nn_utils.py:50-67 index_select_ND on rows.
-__global__ __launch_bounds__(256) void index_select_rows_kernel(const float *__restrict__ src, int64_t row_len,
-                                                                const int64_t *__restrict__ index, int64_t n_index,
-                                                                float *__restrict__ out) {
-    const int64_t total = n_index * row_len;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = t / row_len, c = t % row_len;
-        out[t] = src[index[i] * row_len + c];
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// host helpers
-// ------------------------------------------------------------------------------------------------
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
-
-Seg seg_dense(const float *src, int ld, int K, int kp0) {
-    Seg s{};
-    s.src = src; s.ld = ld; s.K = K; s.kp0 = kp0; s.kind = SEG_DENSE;
-    s.vec = (ld % 4 == 0) && aligned16(src);
-    return s;
-}
-
-Seg seg_gather(const float *src, int ld, int K, int kp0, const WdCsr &csr) {
-    Seg s = seg_dense(src, ld, K, kp0);
-    s.kind = SEG_GATHER; s.ptr = csr.ptr; s.idx = csr.idx; s.coef = csr.coef;
-    return s;
-}
-
-Seg seg_ones(int kp0) {
-    Seg s{};
-    s.K = 1; s.kp0 = kp0; s.kind = SEG_ONES; s.ld = 1;
-    return s;
-}
-
-Src make_src(int rows, std::initializer_list<Seg> segs) {
-    Src S{};
-    S.rows = rows;
-    S.nseg = 0;
-    int kp = 0;
-    for (const Seg &g : segs) {
-        S.s[S.nseg] = g;
-        S.s[S.nseg].kp0 = kp;
-        kp += round4(g.K);
-        ++S.nseg;
-    }
-    S.cols_p = kp;
-    return S;
-}
-
-// B operand of an NT layer: the weight matrix W[n][wcol + k] laid out with the same padded column
-// segments as the A operand.
-Src weight_src_like(const Src &A, const float *W, int ldw, int nrows, const int *wcol) {
-    Src S{};
-    S.rows = nrows; S.nseg = A.nseg; S.cols_p = A.cols_p;
-    for (int i = 0; i < A.nseg; ++i) S.s[i] = seg_dense(W + wcol[i], ldw, A.s[i].K, A.s[i].kp0);
-    return S;
-}
-
-Epi epi_act(int act, const float *slope, const float *bias, const float *resid, int ld_resid, float *Z, float *Y,
-            int ld, const WdConfig *c, uint32_t layer) {
-    Epi e{};
-    e.kind = EPI_ACT; e.act = act; e.slope = slope; e.bias = bias; e.resid = resid; e.ld_resid = ld_resid;
-    e.Z = Z; e.ld_z = ld; e.Y = Y; e.ld_y = ld;
-    e.p_drop = c->dropout; e.seed = c->seed; e.layer = layer;
-    return e;
-}
-
-Epi epi_store(float *Y, int ld, long long slab_stride, int accumulate) {
-    Epi e{};
-    e.kind = EPI_STORE; e.Y = Y; e.ld_y = ld; e.slab_stride = slab_stride; e.accumulate = accumulate;
-    return e;
-}
-
-constexpr int GBM = 64, GBN = 64, GWM = 2, GWN = 2;
-
-int gemm_nt(const Src &A, const Src &B, int M, int N, const Epi &epi, hipStream_t st) {
-    if (M <= 0 || N <= 0) return 0;
-    GemmParams P{};
-    P.A = A; P.B = B; P.M = M; P.N = N; P.K = A.cols_p; P.k_per_split = ((A.cols_p + BK - 1) / BK) * BK;
-    P.tiles_n = (N + GBN - 1) / GBN;
-    P.epi = epi;
-    dim3 grid(((M + GBM - 1) / GBM) * P.tiles_n, 1);
-    hipLaunchKernelGGL((gemm_kernel<GBM, GBN, GWM, GWN, false, false>), grid, dim3(64 * GWM * GWN), 0, st, P);
-    WD_CHECK_LAUNCH("gemm_nt");
-    return 0;
-}
-
-// C[m][n] = sum_k A[m][k] * W[k][wcol + n]  (A dense rows, B = rows k of W)
-int gemm_nn(const Src &A, const float *W, int ldw, int wcol, int M, int N, int K, const Epi &epi, hipStream_t st) {
-    if (M <= 0 || N <= 0) return 0;
-    GemmParams P{};
-    P.A = A;
-    P.B = make_src(K, {seg_dense(W + wcol, ldw, N, 0)});
-    P.M = M; P.N = N; P.K = K; P.k_per_split = ((K + BK - 1) / BK) * BK;
-    P.tiles_n = (N + GBN - 1) / GBN;
-    P.epi = epi;
-    dim3 grid(((M + GBM - 1) / GBM) * P.tiles_n, 1);
-    hipLaunchKernelGGL((gemm_kernel<GBM, GBN, GWM, GWN, false, true>), grid, dim3(64 * GWM * GWN), 0, st, P);
-    WD_CHECK_LAUNCH("gemm_nn");
-    return 0;
-}
-
-// slab[z][n][j] (+)= sum_{m in split z} dZ[m][n] * X(m, j)
-struct TnPlan { int nsplit; int k_per_split; long long slab_stride; int ld_slab; };
-
-TnPlan tn_plan(int n_out, int cols_p, int m_rows) {
-    TnPlan t{};
-    const int tiles = ((n_out + GBM - 1) / GBM) * ((cols_p + GBN - 1) / GBN);
-    int chunks = (m_rows + BK - 1) / BK;
-    int ns = (1024 + tiles - 1) / tiles;
-    if (ns > chunks) ns = chunks;
-    if (ns < 1) ns = 1;
-    int cps = (chunks + ns - 1) / ns;
-    t.k_per_split = cps * BK;
-    t.nsplit = (m_rows + t.k_per_split - 1) / t.k_per_split;
-    if (t.nsplit < 1) t.nsplit = 1;
-    t.ld_slab = cols_p;
-    t.slab_stride = (long long)n_out * cols_p;
-    return t;
-}
-
-int gemm_tn(const Src &dZ, const Src &X, int n_out, int m_rows, const TnPlan &tp, float *slab, int accumulate,
-            hipStream_t st) {
-    if (n_out <= 0 || m_rows <= 0) return 0;
-    GemmParams P{};
-    P.A = dZ; P.B = X; P.M = n_out; P.N = X.cols_p; P.K = m_rows; P.k_per_split = tp.k_per_split;
-    P.tiles_n = (X.cols_p + GBN - 1) / GBN;
-    P.epi = epi_store(slab, tp.ld_slab, tp.slab_stride, accumulate);
-    dim3 grid(((n_out + GBM - 1) / GBM) * P.tiles_n, tp.nsplit);
-    hipLaunchKernelGGL((gemm_kernel<GBM, GBN, GWM, GWN, true, true>), grid, dim3(64 * GWM * GWN), 0, st, P);
-    WD_CHECK_LAUNCH("gemm_tn");
-    return 0;
-}
-
-int slab_reduce(const TnPlan &tp, const float *slab, int n_out, const Src &X, float *dW, int ldw, const int *wcol,
-                float *db, hipStream_t st) {
-    SlabReduce R{};
-    R.slab = slab; R.nsplit = tp.nsplit; R.slab_stride = tp.slab_stride; R.ld_slab = tp.ld_slab; R.rows = n_out;
-    R.nseg = X.nseg; R.ldw = ldw;
-    for (int i = 0; i < X.nseg; ++i) {
-        R.s[i].kp0 = X.s[i].kp0; R.s[i].K = X.s[i].K; R.s[i].kind = X.s[i].kind;
-        R.s[i].wcol = X.s[i].kind == SEG_ONES ? 0 : wcol[i];
-        R.s[i].dst = X.s[i].kind == SEG_ONES ? db : dW;
-    }
-    if (!dW && !db) return 0;
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3(n_out), dim3(256), 0, st, R);
-    WD_CHECK_LAUNCH("slab_reduce");
-    return 0;
-}
 
 int ew_blocks(size_t total) {
     size_t b = (total + 255) / 256;
@@ -365,10 +68,11 @@ int ew_blocks(size_t total) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// workspace layouts
+// dimensions
 // ------------------------------------------------------------------------------------------------
 struct Dims {
-    int H, T, R, Va, B, Fa, Fb, d, Hout, Kin;
+    int H, Hk, T, R, Rp, Va, Vap, B, Fa, Fak, Fb, Fbk, d, dk, Hd, Hdk, Kin, Kink;
+    int ldx, Ko, Kd;
     bool atom, undirected, save, desc;
 };
 
@@ -381,40 +85,272 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     if (c->aggregation < 0 || c->aggregation > WD_AGG_NORM) return fail(WD_ERR_ARG, "bad aggregation %d", c->aggregation);
     if (c->activation == WD_ACT_PRELU && !p->prelu) return fail(WD_ERR_ARG, "PReLU needs a slope pointer");
     if (!(c->dropout >= 0.f && c->dropout < 1.f)) return fail(WD_ERR_ARG, "dropout must be in [0, 1)");
-    D.H = p->hidden; D.T = c->depth; D.Va = g->n_atoms; D.B = g->n_mols;
+    D.H = p->hidden; D.Hk = rup(D.H, 64); D.T = c->depth;
     D.atom = g->atom_messages != 0; D.undirected = c->undirected != 0; D.save = c->save_for_backward != 0;
-    D.R = D.atom ? g->n_atoms : g->n_bonds;
-    D.Fa = g->atom_fdim; D.Fb = g->bond_fdim;
+    D.Va = g->n_atoms; D.Vap = rup(D.Va, 64); D.B = g->n_mols;
+    D.R = D.atom ? g->n_atoms : g->n_bonds; D.Rp = rup(D.R, 64);
+    D.Fa = g->atom_fdim; D.Fak = rup(D.Fa, 32); D.Fb = g->bond_fdim; D.Fbk = rup(D.Fb, 32);
     D.desc = g->atom_desc != nullptr && g->desc_dim > 0;
-    D.d = D.desc ? g->desc_dim : 0;
-    D.Hout = D.H + D.d;
-    D.Kin = D.atom ? D.Fa : D.Fb;
+    D.d = D.desc ? g->desc_dim : 0; D.dk = rup(D.d, 32);
+    D.Hd = D.H + D.d; D.Hdk = rup(D.Hd, 64);
+    D.Kin = D.atom ? D.Fa : D.Fb; D.Kink = D.atom ? D.Fak : D.Fbk;
+    D.ldx = D.atom ? D.Hk + D.Fbk : D.Hk;
+    D.Ko = D.Fak + D.Hk;
+    D.Kd = D.Hk + D.dk;
     if (D.atom && D.undirected)
         return fail(WD_ERR_UNSUPPORTED, "undirected with atom_messages (the reference indexes atom messages "
                                         "with b2revb, mpn.py:101-102)");
     if (D.desc && (!p->W_d || !p->b_d)) return fail(WD_ERR_ARG, "atom descriptors need W_d and b_d");
     if (!p->W_i || !p->W_h || !p->W_o || !p->b_o || !p->zero_vec) return fail(WD_ERR_ARG, "missing weights");
+    if (g->ld_atoms < D.Fak || g->ld_atoms % 4 || g->ld_bonds < D.Fbk || g->ld_bonds % 4 || g->bond_col0 != 0)
+        return fail(WD_ERR_SHAPE, "f_atoms / f_bonds must be zero padded to 32 columns (ld %d/%d, need %d/%d) "
+                                  "with bond_col0 == 0", g->ld_atoms, g->ld_bonds, D.Fak, D.Fbk);
+    if (!aligned16(g->f_atoms) || !aligned16(g->f_bonds) || (D.desc && !aligned16(g->atom_desc)))
+        return fail(WD_ERR_ARG, "feature arrays must be 16-byte aligned");
     return 0;
 }
 
-struct FwdLayout {
-    std::vector<size_t> Z, M, Ms;
-    size_t Zo = 0, h = 0, Zd = 0, hd = 0, total = 0;
+// ------------------------------------------------------------------------------------------------
+// packed parameters
+// ------------------------------------------------------------------------------------------------
+struct PackLayout {
+    size_t Wi = 0, bi = 0, Wh = 0, bh = 0, Wo = 0, bo = 0, Wd = 0, bd = 0, WhT = 0, WoT = 0, WdT = 0, total = 0;
 };
 
-FwdLayout fwd_layout(const Dims &D) {
-    FwdLayout L;
+PackLayout pack_layout(const Dims &D) {
+    PackLayout L;
     size_t off = 0;
     auto take = [&](size_t floats) { size_t o = off; off = align256(off + floats * 4); return o; };
-    const size_t msg = (size_t)D.R * D.H, atm = (size_t)D.Va * D.H, atd = (size_t)D.Va * D.Hout;
-    const int nZ = D.save ? D.T : 1;
-    for (int t = 0; t < nZ; ++t) L.Z.push_back(take(msg));
-    const int nM = D.save ? D.T : (D.T > 1 ? 2 : 1);
-    for (int t = 0; t < nM; ++t) L.M.push_back(take(msg));
-    if (D.undirected) {
-        const int nS = D.save ? D.T : 1;
-        for (int t = 0; t < nS; ++t) L.Ms.push_back(take(msg));
+    L.Wi = take((size_t)D.Hk * D.Kink);
+    L.bi = take(D.Hk);
+    L.Wh = take((size_t)D.Hk * D.ldx);
+    L.bh = take(D.Hk);
+    L.Wo = take((size_t)D.Hk * D.Ko);
+    L.bo = take(D.Hk);
+    L.WhT = take((size_t)D.Hk * D.Hk);
+    L.WoT = take((size_t)D.Hk * D.Hk);
+    if (D.desc) {
+        L.Wd = take((size_t)D.Hdk * D.Kd);
+        L.bd = take(D.Hdk);
+        L.WdT = take((size_t)D.Hk * D.Hdk);
     }
+    L.total = off;
+    return L;
+}
+
+PackJob job_plain(float *dst, int rows_p, int cols_p, const float *src, int ld, int nrows,
+                  std::initializer_list<std::array<int, 3>> segs) {  // {dst_col0, src_col0, K}
+    PackJob j{};
+    j.dst = dst; j.rows_p = rows_p; j.cols_p = cols_p; j.src = src; j.ld_src = ld; j.nrows = nrows;
+    for (const auto &s : segs) {
+        j.dc0[j.nseg] = s[0]; j.sc0[j.nseg] = s[1]; j.K[j.nseg] = s[2];
+        ++j.nseg;
+    }
+    return j;
+}
+
+PackJob job_transpose(float *dst, int rows_p, int cols_p, const float *src, int ld, int src_col0, int nrows,
+                      int src_rows) {
+    PackJob j{};
+    j.dst = dst; j.rows_p = rows_p; j.cols_p = cols_p; j.src = src; j.ld_src = ld; j.transpose = 1;
+    j.nrows = nrows; j.nseg = 1; j.sc0[0] = src_col0; j.K[0] = src_rows;
+    return j;
+}
+
+int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
+    const PackLayout L = pack_layout(D);
+    auto F = [&](size_t off) { return (float *)(base + off); };
+    const int H = D.H;
+    PackJobs J{};
+    auto add = [&](const PackJob &j) { J.j[J.n++] = j; };
+    add(job_plain(F(L.Wi), D.Hk, D.Kink, p->W_i, D.Kin, H, {{0, 0, D.Kin}}));
+    add(job_plain(F(L.bi), 1, D.Hk, p->b_i, H, 1, {{0, 0, H}}));
+    if (D.atom)
+        add(job_plain(F(L.Wh), D.Hk, D.ldx, p->W_h, H + D.Fb, H, {{0, 0, H}, {D.Hk, H, D.Fb}}));
+    else
+        add(job_plain(F(L.Wh), D.Hk, D.ldx, p->W_h, H, H, {{0, 0, H}}));
+    add(job_plain(F(L.bh), 1, D.Hk, p->b_h, H, 1, {{0, 0, H}}));
+    add(job_plain(F(L.Wo), D.Hk, D.Ko, p->W_o, D.Fa + H, H, {{0, 0, D.Fa}, {D.Fak, D.Fa, H}}));
+    add(job_plain(F(L.bo), 1, D.Hk, p->b_o, H, 1, {{0, 0, H}}));
+    // transposes for dX = dZ W_h[:, :H] and dA = dZo W_o[:, Fa:]
+    add(job_transpose(F(L.WhT), D.Hk, D.Hk, p->W_h, D.atom ? H + D.Fb : H, 0, H, H));
+    add(job_transpose(F(L.WoT), D.Hk, D.Hk, p->W_o, D.Fa + H, D.Fa, H, H));
+    if (D.desc) {
+        add(job_plain(F(L.Wd), D.Hdk, D.Kd, p->W_d, D.Hd, D.Hd, {{0, 0, H}, {D.Hk, H, D.d}}));
+        add(job_plain(F(L.bd), 1, D.Hdk, p->b_d, D.Hd, 1, {{0, 0, D.Hd}}));
+        add(job_transpose(F(L.WdT), D.Hk, D.Hdk, p->W_d, D.Hd, 0, H, D.Hd));
+    }
+    hipLaunchKernelGGL(pack_kernel, dim3(64, J.n), dim3(256), 0, st, J);
+    WD_CHECK_LAUNCH("pack_params");
+    return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
+Epi epi_act(int act, const float *slope, const float *bias, const float *resid, float *Z, float *Y, int ld,
+            const WdConfig *c, uint32_t layer) {
+    Epi e{};
+    e.kind = EPI_ACT; e.act = act; e.slope = slope; e.bias = bias; e.resid = resid; e.Z = Z; e.Y = Y; e.ld = ld;
+    e.p_drop = c->dropout; e.seed = c->seed; e.layer = layer;
+    return e;
+}
+
+Epi epi_store(float *Y, int ld, long long slab_stride = 0, int accumulate = 0) {
+    Epi e{};
+    e.kind = EPI_STORE; e.Y = Y; e.ld = ld; e.slab_stride = slab_stride; e.accumulate = accumulate;
+    return e;
+}
+
+constexpr int NBM = 64, NBN = 64, NWM = 2, NWN = 2;
+
+// C[Mp][Np] = epi([A0 | A1] B^T); A segments [Mp][lda], K extents multiples of 32; B [Np][ldb].
+// Tile 64x64 (4 waves) or 32x64 (2 waves), global-load prefetch depth 1 or 2; WdConfig.gemm_variant
+// selects one for tuning (0 = default, 64x64 depth 2).
+int gemm_nt(const float *a0, int lda0, int ka0, const float *a1, int lda1, int ka1, const float *b, int ldb, int Mp,
+            int Np, const Epi &epi, hipStream_t st, int variant = 0) {
+    if (Mp <= 0 || Np <= 0) return 0;
+    if (Mp % NBM || Np % NBN || ka0 % BK || ka1 % BK || ka0 <= 0 || lda0 % 4 || (ka1 && lda1 % 4) || ldb % 4)
+        return fail(WD_ERR_SHAPE, "gemm_nt: unpadded operand (Mp %d Np %d ka %d/%d)", Mp, Np, ka0, ka1);
+    NtParams P{};
+    P.a0 = a0; P.lda0 = lda0; P.ka0 = ka0; P.a1 = a1; P.lda1 = lda1; P.ka1 = ka1; P.b = b; P.ldb = ldb;
+    P.M = Mp; P.N = Np; P.epi = epi;
+    // variants (tuning): 1 = 64x64 depth 1, 2 = 32x64 depth 1, 3 = 64x64 depth 2, 4 = 32x64 depth 2,
+    // 5 = 64x64 depth 2 with 64-wide K chunks (needs K segments aligned to 64, else falls back to 3)
+    const bool k64 = ka0 % 64 == 0 && ka1 % 64 == 0;
+    if (variant == 0) variant = k64 ? 5 : 3;
+    if (variant == 5 && !k64) variant = 3;
+    const dim3 blk64(64 * NWM * NWN);
+    if (variant == 2 || variant == 4) {
+        P.tiles_m = Mp / 32; P.tiles_n = Np / 64;
+        const dim3 grid(P.tiles_m * P.tiles_n);
+        if (variant == 2) hipLaunchKernelGGL((gemm_nt_kernel<32, 64, 1, 2, 1, 32>), grid, dim3(128), 0, st, P);
+        else hipLaunchKernelGGL((gemm_nt_kernel<32, 64, 1, 2, 2, 32>), grid, dim3(128), 0, st, P);
+    } else {
+        P.tiles_m = Mp / NBM; P.tiles_n = Np / NBN;
+        const dim3 grid(P.tiles_m * P.tiles_n);
+        if (variant == 1) hipLaunchKernelGGL((gemm_nt_kernel<NBM, NBN, NWM, NWN, 1, 32>), grid, blk64, 0, st, P);
+        else if (variant == 5) hipLaunchKernelGGL((gemm_nt_kernel<NBM, NBN, NWM, NWN, 2, 64>), grid, blk64, 0, st, P);
+        else hipLaunchKernelGGL((gemm_nt_kernel<NBM, NBN, NWM, NWN, 2, 32>), grid, blk64, 0, st, P);
+    }
+    WD_CHECK_LAUNCH("gemm_nt");
+    return 0;
+}
+
+Seg seg_dense(const float *src, int ld, int K) {
+    Seg s{};
+    s.src = src; s.ld = ld; s.K = K; s.kind = SEG_DENSE;
+    return s;
+}
+Seg seg_ones() {
+    Seg s{};
+    s.K = 1; s.kind = SEG_ONES;
+    return s;
+}
+Src make_src(int rows, std::initializer_list<Seg> segs) {
+    Src S{};
+    S.rows = rows;
+    int kp = 0;
+    for (const Seg &g : segs) {
+        S.s[S.nseg] = g;
+        S.s[S.nseg].kp0 = kp;
+        kp += rup(g.K, 4);
+        ++S.nseg;
+    }
+    S.cols_p = kp;
+    return S;
+}
+
+struct TnPlan { int nsplit; int k_per_split; long long slab_stride; int ld_slab; };
+
+TnPlan tn_plan(int n_out, int cols_p, int m_rows) {
+    TnPlan t{};
+    const int tiles = ((n_out + NBM - 1) / NBM) * ((cols_p + NBN - 1) / NBN);
+    const int chunks = (m_rows + BK - 1) / BK;
+    int ns = (1024 + tiles - 1) / tiles;
+    if (ns > chunks) ns = chunks;
+    if (ns < 1) ns = 1;
+    const int cps = (chunks + ns - 1) / ns;
+    t.k_per_split = cps * BK;
+    t.nsplit = (m_rows + t.k_per_split - 1) / t.k_per_split;
+    if (t.nsplit < 1) t.nsplit = 1;
+    t.ld_slab = cols_p;
+    t.slab_stride = (long long)n_out * cols_p;
+    return t;
+}
+
+// slab[z][n][j] (+)= sum_{m in split z} dZ[m][n] * X[m][j]
+int gemm_tn(const Src &dZ, const Src &X, int n_out, int m_rows, const TnPlan &tp, float *slab, int accumulate,
+            hipStream_t st) {
+    if (n_out <= 0 || m_rows <= 0) return 0;
+    TnParams P{};
+    P.A = dZ; P.B = X; P.M = n_out; P.N = X.cols_p; P.K = m_rows; P.k_per_split = tp.k_per_split;
+    P.tiles_m = (n_out + NBM - 1) / NBM; P.tiles_n = (X.cols_p + NBN - 1) / NBN;
+    P.epi = epi_store(slab, tp.ld_slab, tp.slab_stride, accumulate);
+    hipLaunchKernelGGL((gemm_tn_kernel<NBM, NBN, NWM, NWN>), dim3(P.tiles_m * P.tiles_n, tp.nsplit),
+                       dim3(64 * NWM * NWN), 0, st, P);
+    WD_CHECK_LAUNCH("gemm_tn");
+    return 0;
+}
+
+// dW[n][w0 + kk] = sum_z slab[z][n][c0 + kk] per mapping {c0, w0, K}; db[n] = slab bias column
+int slab_reduce(const TnPlan &tp, const float *slab, int n_rows, std::initializer_list<std::array<int, 3>> map,
+                float *dW, int ldw, float *db, int bias_col, hipStream_t st) {
+    if (!dW && !db) return 0;
+    SlabReduce R{};
+    R.slab = slab; R.nsplit = tp.nsplit; R.slab_stride = tp.slab_stride; R.ld_slab = tp.ld_slab; R.rows = n_rows;
+    for (const auto &m : map) {
+        R.c0[R.nseg] = m[0]; R.w0[R.nseg] = m[1]; R.K[R.nseg] = m[2];
+        ++R.nseg;
+    }
+    R.dW = dW; R.ldw = ldw; R.db = db; R.bias_col = bias_col;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(n_rows), dim3(256), 0, st, R);
+    WD_CHECK_LAUNCH("slab_reduce");
+    return 0;
+}
+
+int gather(const float *src, int ld_src, int K, const WdCsr &csr, const int32_t *sym_rev, float *out, int ld_out,
+           int rows, int rows_p, hipStream_t st) {
+    if (rows_p <= 0 || K <= 0) return 0;
+    GatherP P{};
+    P.src = src; P.ld_src = ld_src; P.K = K; P.ptr = csr.ptr; P.idx = csr.idx; P.coef = csr.coef;
+    P.sym_rev = sym_rev; P.out = out; P.ld_out = ld_out; P.rows = rows; P.rows_p = rows_p;
+    const size_t total = (size_t)rows_p * (K / 4);
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(ew_blocks(total)), dim3(256), 0, st, P);
+    WD_CHECK_LAUNCH("gather_rows");
+    return 0;
+}
+
+ReadoutP readout_params(const WdGraph *g, const WdParams *p, const WdConfig *c, const float *h, int ldh, int ncols,
+                        float *out) {
+    ReadoutP R{};
+    R.h = h; R.ldh = ldh; R.ncols = ncols; R.w_atoms = g->w_atoms; R.mol_start = g->mol_start;
+    R.mol_size = g->mol_size; R.xn = g->degree_of_polym; R.agg = c->aggregation; R.norm = c->aggregation_norm;
+    R.zero_vec = p->zero_vec; R.out = out;
+    return R;
+}
+
+// ------------------------------------------------------------------------------------------------
+// workspace layouts
+// ------------------------------------------------------------------------------------------------
+struct FwdLayout {
+    std::vector<size_t> Z, M, X;
+    size_t packed = 0, A = 0, Zo = 0, h = 0, Zd = 0, hd = 0, total = 0;
+    bool own_pack = false;
+};
+
+FwdLayout fwd_layout(const Dims &D, bool own_pack) {
+    FwdLayout L;
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off = align256(off + bytes); return o; };
+    const size_t msg = (size_t)D.Rp * D.Hk * 4, atm = (size_t)D.Vap * D.Hk * 4, atd = (size_t)D.Vap * D.Hdk * 4;
+    L.own_pack = own_pack;
+    if (own_pack) L.packed = take(pack_layout(D).total);
+    for (int t = 0; t < (D.save ? D.T : 1); ++t) L.Z.push_back(take(msg));
+    for (int t = 0; t < (D.save ? D.T : (D.T > 1 ? 2 : 1)); ++t) L.M.push_back(take(msg));
+    if (D.T > 1)
+        for (int t = 0; t < (D.save ? D.T - 1 : 1); ++t) L.X.push_back(take((size_t)D.Rp * D.ldx * 4));
+    L.A = take(atm);
     if (D.save) L.Zo = take(atm);
     L.h = take(atm);
     if (D.desc) {
@@ -428,41 +364,28 @@ FwdLayout fwd_layout(const Dims &D) {
 struct BwdLayout {
     size_t dH = 0, dZd = 0, dHo = 0, dZo = 0, dA = 0, dZ0 = 0, dZ1 = 0, dRes = 0, dX = 0, dMs = 0, slab = 0,
            prelu = 0, total = 0;
-    size_t slab_floats = 0, prelu_floats = 0;
+    size_t prelu_floats = 0;
 };
 
-// TN plans of the three weight-gradient GEMMs
-Src x_src_in(const WdGraph *g, const Dims &D) {  // rows of W_i's input
-    return D.atom ? make_src(D.R, {seg_dense(g->f_atoms, g->ld_atoms, D.Fa, 0), seg_ones(0)})
-                  : make_src(D.R, {seg_dense(g->f_bonds + g->bond_col0, g->ld_bonds, D.Fb, 0), seg_ones(0)});
+Src x_in(const WdGraph *g, const Dims &D) {
+    return D.atom ? make_src(D.R, {seg_dense(g->f_atoms, g->ld_atoms, D.Fak), seg_ones()})
+                  : make_src(D.R, {seg_dense(g->f_bonds, g->ld_bonds, D.Fbk), seg_ones()});
 }
-Src x_src_h(const WdGraph *g, const Dims &D, const float *srcM, bool ones) {  // gathered W_h input X_t
-    if (D.atom) {
-        Seg a = seg_gather(srcM, D.H, D.H, 0, g->msg_gather);
-        Seg b = seg_gather(g->f_bonds + g->bond_col0, g->ld_bonds, D.Fb, 0, g->bond_feat_gather);
-        return ones ? make_src(D.R, {a, b, seg_ones(0)}) : make_src(D.R, {a, b});
-    }
-    Seg a = seg_gather(srcM, D.H, D.H, 0, g->msg_gather);
-    return ones ? make_src(D.R, {a, seg_ones(0)}) : make_src(D.R, {a});
+Src x_h(const Dims &D, const float *X) { return make_src(D.R, {seg_dense(X, D.ldx, D.ldx), seg_ones()}); }
+Src x_o(const WdGraph *g, const Dims &D, const float *A) {
+    return make_src(D.Va, {seg_dense(g->f_atoms, g->ld_atoms, D.Fak), seg_dense(A, D.Hk, D.Hk), seg_ones()});
 }
-Src x_src_o(const WdGraph *g, const Dims &D, const float *M_last, bool ones) {  // [f_atoms | A]
-    Seg a = seg_dense(g->f_atoms, g->ld_atoms, D.Fa, 0);
-    Seg b = seg_gather(M_last, D.H, D.H, 0, g->atom_gather);
-    return ones ? make_src(D.Va, {a, b, seg_ones(0)}) : make_src(D.Va, {a, b});
-}
-Src x_src_d(const WdGraph *g, const Dims &D, const float *h, bool ones) {  // [h | desc]
-    Seg a = seg_dense(h, D.H, D.H, 0);
-    Seg b = seg_dense(g->atom_desc, D.d, D.d, 0);
-    return ones ? make_src(D.Va, {a, b, seg_ones(0)}) : make_src(D.Va, {a, b});
+Src x_d(const WdGraph *g, const Dims &D, const float *h) {
+    return make_src(D.Va, {seg_dense(h, D.Hk, D.Hk), seg_dense(g->atom_desc, D.dk, D.dk), seg_ones()});
 }
 
 BwdLayout bwd_layout(const WdGraph *g, const Dims &D) {
     BwdLayout L;
     size_t off = 0;
     auto take = [&](size_t floats) { size_t o = off; off = align256(off + floats * 4); return o; };
-    const size_t msg = (size_t)D.R * D.H, atm = (size_t)D.Va * D.H;
-    L.dH = take((size_t)D.Va * D.Hout);
-    if (D.desc) { L.dZd = take((size_t)D.Va * D.Hout); L.dHo = take(atm); }
+    const size_t msg = (size_t)D.Rp * D.Hk, atm = (size_t)D.Vap * D.Hk, atd = (size_t)D.Vap * D.Hdk;
+    L.dH = take(D.desc ? atd : atm);
+    if (D.desc) { L.dZd = take(atd); L.dHo = take(atm); }
     L.dZo = take(atm);
     L.dA = take(atm);
     L.dZ0 = take(msg);
@@ -473,14 +396,12 @@ BwdLayout bwd_layout(const WdGraph *g, const Dims &D) {
     size_t slab = 0;
     auto upd = [&](int n_out, const Src &X, int m_rows) {
         TnPlan tp = tn_plan(n_out, X.cols_p, m_rows);
-        size_t s = (size_t)tp.nsplit * tp.slab_stride;
-        if (s > slab) slab = s;
+        slab = std::max<size_t>(slab, (size_t)tp.nsplit * (size_t)tp.slab_stride);
     };
-    upd(D.H, x_src_in(g, D), D.R);
-    upd(D.H, x_src_h(g, D, nullptr, true), D.R);
-    upd(D.H, x_src_o(g, D, nullptr, true), D.Va);
-    if (D.desc) upd(D.Hout, x_src_d(g, D, nullptr, true), D.Va);
-    L.slab_floats = slab;
+    upd(D.Hk, x_in(g, D), D.R);
+    upd(D.Hk, x_h(D, nullptr), D.R);
+    upd(D.Hk, x_o(g, D, nullptr), D.Va);
+    if (D.desc) upd(D.Hdk, x_d(g, D, nullptr), D.Va);
     L.slab = take(slab);
     L.prelu_floats = (size_t)(D.T + 2) * 4096;
     L.prelu = take(L.prelu_floats);
@@ -513,19 +434,33 @@ int wdmpnn_abi_version(void) { return WDMPNN_ABI_VERSION; }
 
 const char *wdmpnn_last_error(void) { return g_err.c_str(); }
 
+int wdmpnn_packed_params_bytes(const WdGraph *g, const WdParams *p, const WdConfig *c, size_t *bytes) {
+    Dims D;
+    WD_TRY(get_dims(g, p, c, D));
+    if (!bytes) return fail(WD_ERR_ARG, "null bytes");
+    *bytes = pack_layout(D).total;
+    return 0;
+}
+
+int wdmpnn_pack_params(const WdGraph *g, const WdParams *p, const WdConfig *c, void *packed, size_t bytes,
+                       void *stream) {
+    Dims D;
+    WD_TRY(get_dims(g, p, c, D));
+    if (!packed || bytes < pack_layout(D).total) return fail(WD_ERR_WORKSPACE, "packed buffer too small");
+    return pack_params(D, p, (char *)packed, (hipStream_t)stream);
+}
+
 int wdmpnn_workspace_bytes(const WdGraph *g, const WdParams *p, const WdConfig *c, size_t *bytes) {
     Dims D;
-    int rc = get_dims(g, p, c, D);
-    if (rc) return rc;
+    WD_TRY(get_dims(g, p, c, D));
     if (!bytes) return fail(WD_ERR_ARG, "null bytes");
-    *bytes = fwd_layout(D).total;
+    *bytes = fwd_layout(D, p->packed == nullptr).total;
     return 0;
 }
 
 int wdmpnn_backward_workspace_bytes(const WdGraph *g, const WdParams *p, const WdConfig *c, size_t *bytes) {
     Dims D;
-    int rc = get_dims(g, p, c, D);
-    if (rc) return rc;
+    WD_TRY(get_dims(g, p, c, D));
     if (!bytes) return fail(WD_ERR_ARG, "null bytes");
     *bytes = bwd_layout(g, D).total;
     return 0;
@@ -534,77 +469,69 @@ int wdmpnn_backward_workspace_bytes(const WdGraph *g, const WdParams *p, const W
 int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void *workspace, size_t workspace_bytes,
                    float *out, void *stream) {
     Dims D;
-    int rc = get_dims(g, p, c, D);
-    if (rc) return rc;
-    const FwdLayout L = fwd_layout(D);
+    WD_TRY(get_dims(g, p, c, D));
+    const FwdLayout L = fwd_layout(D, p->packed == nullptr);
     if (!workspace || workspace_bytes < L.total)
         return fail(WD_ERR_WORKSPACE, "workspace too small: need %zu bytes, got %zu", L.total, workspace_bytes);
     if (!out) return fail(WD_ERR_ARG, "null out");
+    const PackLayout PL = pack_layout(D);
+    if (p->packed && p->packed_bytes < PL.total) return fail(WD_ERR_WORKSPACE, "packed params too small");
     hipStream_t st = (hipStream_t)stream;
     char *ws = (char *)workspace;
     auto F = [&](size_t off) { return (float *)(ws + off); };
-    const int H = D.H;
+    if (L.own_pack) WD_TRY(pack_params(D, p, ws + L.packed, st));
+    const char *pk = L.own_pack ? ws + L.packed : (const char *)p->packed;
+    auto W = [&](size_t off) { return (const float *)(pk + off); };
+    const int Hk = D.Hk;
 
     // L0: input layer (mpn.py:92-97)
     {
-        Src A = D.atom ? make_src(D.R, {seg_dense(g->f_atoms, g->ld_atoms, D.Fa, 0)})
-                       : make_src(D.R, {seg_dense(g->f_bonds + g->bond_col0, g->ld_bonds, D.Fb, 0)});
-        const int wcol[1] = {0};
-        Src B = weight_src_like(A, p->W_i, D.Kin, H, wcol);
-        rc = gemm_nt(A, B, D.R, H, epi_act(c->activation, p->prelu, p->b_i, nullptr, 0, F(L.Z[0]), F(L.M[0]), H, c, 0),
-                     st);
-        if (rc) return rc;
+        const float *a = D.atom ? g->f_atoms : g->f_bonds;
+        const int lda = D.atom ? g->ld_atoms : g->ld_bonds;
+        WD_TRY(gemm_nt(a, lda, D.Kink, nullptr, 0, 0, W(PL.Wi), D.Kink, D.Rp, Hk,
+                       epi_act(c->activation, p->prelu, W(PL.bi), nullptr, F(L.Z[0]), F(L.M[0]), Hk, c, 0), st,
+                       c->gemm_variant));
     }
     // L1..T-1: message passing (mpn.py:100-124)
     int cur = 0;
     for (int t = 1; t < D.T; ++t) {
         const int prev = D.save ? t - 1 : cur;
         const int next = D.save ? t : 1 - cur;
-        const float *srcM = F(L.M[prev]);
-        if (D.undirected) {
-            float *ms = F(L.Ms[D.save ? t : 0]);
-            const size_t total = (size_t)D.R * H;
-            hipLaunchKernelGGL(symmetrize_kernel, dim3(ew_blocks(total)), dim3(256), 0, st, srcM, g->b2revb, D.R, H, ms);
-            WD_CHECK_LAUNCH("symmetrize");
-            srcM = ms;
-        }
-        Src A = x_src_h(g, D, srcM, false);
-        const int wcol[2] = {0, H};
-        Src B = weight_src_like(A, p->W_h, D.atom ? H + D.Fb : H, H, wcol);
+        float *Xt = F(L.X[D.save ? t - 1 : 0]);
+        WD_TRY(gather(F(L.M[prev]), Hk, Hk, g->msg_gather, D.undirected ? g->b2revb : nullptr, Xt, D.ldx, D.R, D.Rp,
+                      st));
+        if (D.atom)
+            WD_TRY(gather(g->f_bonds, g->ld_bonds, D.Fbk, g->bond_feat_gather, nullptr, Xt + Hk, D.ldx, D.R, D.Rp, st));
         float *Zt = D.save ? F(L.Z[t]) : nullptr;
-        if ((rc = record_prof(c, t - 1, 0, st))) return rc;
-        rc = gemm_nt(A, B, D.R, H, epi_act(c->activation, p->prelu, p->b_h, F(L.Z[0]), H, Zt, F(L.M[next]), H, c, t),
-                     st);
-        if (rc) return rc;
-        if ((rc = record_prof(c, t - 1, 1, st))) return rc;
+        WD_TRY(record_prof(c, t - 1, 0, st));
+        WD_TRY(gemm_nt(Xt, D.ldx, D.ldx, nullptr, 0, 0, W(PL.Wh), D.ldx, D.Rp, Hk,
+                       epi_act(c->activation, p->prelu, W(PL.bh), F(L.Z[0]), Zt, F(L.M[next]), Hk, c, t), st,
+                       c->gemm_variant));
+        WD_TRY(record_prof(c, t - 1, 1, st));
         cur = next;
     }
     const float *M_last = F(L.M[D.save ? D.T - 1 : cur]);
     // LT: atom hidden states (mpn.py:126-134)
-    {
-        Src A = x_src_o(g, D, M_last, false);
-        const int wcol[2] = {0, D.Fa};
-        Src B = weight_src_like(A, p->W_o, D.Fa + H, H, wcol);
-        float *Zo = D.save ? F(L.Zo) : nullptr;
-        rc = gemm_nt(A, B, D.Va, H, epi_act(c->activation, p->prelu, p->b_o, nullptr, 0, Zo, F(L.h), H, c, D.T), st);
-        if (rc) return rc;
-    }
+    WD_TRY(gather(M_last, Hk, Hk, g->atom_gather, nullptr, F(L.A), Hk, D.Va, D.Vap, st));
+    WD_TRY(gemm_nt(g->f_atoms, g->ld_atoms, D.Fak, F(L.A), Hk, Hk, W(PL.Wo), D.Ko, D.Vap, Hk,
+                   epi_act(c->activation, p->prelu, W(PL.bo), nullptr, D.save ? F(L.Zo) : nullptr, F(L.h), Hk, c,
+                           D.T),
+                   st, c->gemm_variant));
     const float *hfin = F(L.h);
+    int ldfin = Hk;
     // LT+1: atom descriptors layer (mpn.py:136-143): Linear + dropout, no activation
     if (D.desc) {
-        Src A = x_src_d(g, D, F(L.h), false);
-        const int wcol[2] = {0, H};
-        Src B = weight_src_like(A, p->W_d, D.Hout, D.Hout, wcol);
-        float *Zd = D.save ? F(L.Zd) : nullptr;
-        rc = gemm_nt(A, B, D.Va, D.Hout,
-                     epi_act(WD_ACT_IDENTITY, nullptr, p->b_d, nullptr, 0, Zd, F(L.hd), D.Hout, c, D.T + 1), st);
-        if (rc) return rc;
+        WD_TRY(gemm_nt(F(L.h), Hk, Hk, g->atom_desc, D.dk, D.dk, W(PL.Wd), D.Kd, D.Vap, D.Hdk,
+                       epi_act(WD_ACT_IDENTITY, nullptr, W(PL.bd), nullptr, D.save ? F(L.Zd) : nullptr, F(L.hd), D.Hdk,
+                               c, D.T + 1),
+                       st));
         hfin = F(L.hd);
+        ldfin = D.Hdk;
     }
     // readout (mpn.py:145-171)
     if (D.B > 0) {
-        hipLaunchKernelGGL(readout_kernel, dim3(D.B), dim3(128), 0, st, hfin, D.Hout, D.Hout, g->w_atoms, g->mol_start,
-                           g->mol_size, g->degree_of_polym, c->aggregation, c->aggregation_norm, p->zero_vec, out);
+        hipLaunchKernelGGL(readout_kernel, dim3(D.B, (D.Hd + 4 * RO_QW - 1) / (4 * RO_QW)), dim3(RO_THREADS), 0, st,
+                           readout_params(g, p, c, hfin, ldfin, D.Hd, out));
         WD_CHECK_LAUNCH("readout");
     }
     return 0;
@@ -614,21 +541,23 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
                     size_t workspace_bytes, const float *dout, void *scratch, size_t scratch_bytes,
                     const WdGrads *grads, void *stream) {
     Dims D;
-    int rc = get_dims(g, p, c, D);
-    if (rc) return rc;
+    WD_TRY(get_dims(g, p, c, D));
     if (!D.save) return fail(WD_ERR_ARG, "backward needs a forward run with save_for_backward=1");
-    const FwdLayout L = fwd_layout(D);
+    const FwdLayout L = fwd_layout(D, p->packed == nullptr);
     const BwdLayout Bl = bwd_layout(g, D);
     if (!workspace || workspace_bytes < L.total) return fail(WD_ERR_WORKSPACE, "forward workspace too small");
     if (!scratch || scratch_bytes < Bl.total)
         return fail(WD_ERR_WORKSPACE, "backward scratch too small: need %zu bytes, got %zu", Bl.total, scratch_bytes);
     if (!dout || !grads) return fail(WD_ERR_ARG, "null dout/grads");
     hipStream_t st = (hipStream_t)stream;
-    const char *ws = (const char *)workspace;
+    char *ws = (char *)workspace;
     char *sc = (char *)scratch;
     auto F = [&](size_t off) { return (float *)(ws + off); };
     auto S = [&](size_t off) { return (float *)(sc + off); };
-    const int H = D.H;
+    const PackLayout PL = pack_layout(D);
+    const char *pk = L.own_pack ? ws + L.packed : (const char *)p->packed;
+    auto W = [&](size_t off) { return (const float *)(pk + off); };
+    const int H = D.H, Hk = D.Hk;
     const bool prelu = c->activation == WD_ACT_PRELU;
     float *prelu_part = S(Bl.prelu);
     int prelu_used = 0;
@@ -636,114 +565,111 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
         return fail(WD_ERR_ARG, "memset failed");
 
     auto act_bwd = [&](ActBwd P) -> int {
-        const size_t total = (size_t)P.rows * P.cols;
+        const size_t total = (size_t)P.rows_p * P.cols;
         const int nb = ew_blocks(total);
         if (prelu && P.Z) { P.prelu_part = prelu_part + prelu_used; prelu_used += nb; }
         hipLaunchKernelGGL(act_bwd_kernel, dim3(nb), dim3(256), 0, st, P);
         WD_CHECK_LAUNCH("act_bwd");
         return 0;
     };
-    auto base_bwd = [&](const float *Z, uint32_t layer, int act, int rows, int cols, float *out) {
+    auto base_bwd = [&](const float *Z, uint32_t layer, int act, int rows, int rows_p, int cols, float *out) {
         ActBwd P{};
         P.Z = Z; P.act = act; P.slope = p->prelu; P.p_drop = c->dropout; P.seed = c->seed; P.layer = layer;
-        P.rows = rows; P.cols = cols; P.out = out;
+        P.rows = rows; P.rows_p = rows_p; P.cols = cols; P.ld = cols; P.out = out;
         return P;
     };
 
-    // readout backward -> dH [Va, Hout]
+    // readout backward -> dH [Vap][Hk or Hdk]
+    const int ldH = D.desc ? D.Hdk : Hk;
     float *dH = S(Bl.dH);
-    if (hipMemsetAsync(dH, 0, (size_t)D.Va * D.Hout * 4, st) != hipSuccess) return fail(WD_ERR_ARG, "memset failed");
+    if (hipMemsetAsync(dH, 0, (size_t)D.Vap * ldH * 4, st) != hipSuccess) return fail(WD_ERR_ARG, "memset failed");
     if (D.B > 0) {
-        hipLaunchKernelGGL(readout_bwd_kernel, dim3(D.B), dim3(128), 0, st, dout, D.Hout, g->w_atoms, g->mol_start,
-                           g->mol_size, g->degree_of_polym, c->aggregation, c->aggregation_norm, dH, D.Hout);
+        hipLaunchKernelGGL(readout_bwd_kernel, dim3(D.B), dim3(256), 0, st,
+                           readout_params(g, p, c, nullptr, ldH, D.Hd, nullptr), dout, dH);
         WD_CHECK_LAUNCH("readout_bwd");
     }
-    const float *M_last = F(L.M[D.T - 1]);
     const float *dh = dH;
     if (D.desc) {  // hd = Zd * s (identity act)
-        ActBwd P = base_bwd(F(L.Zd), D.T + 1, WD_ACT_IDENTITY, D.Va, D.Hout, S(Bl.dZd));
-        P.G = dH; P.ldg = D.Hout;
-        if ((rc = act_bwd(P))) return rc;
-        Src dZ = make_src(D.Va, {seg_dense(S(Bl.dZd), D.Hout, D.Hout, 0)});
-        Src X = x_src_d(g, D, F(L.h), true);
-        TnPlan tp = tn_plan(D.Hout, X.cols_p, D.Va);
-        if ((rc = gemm_tn(dZ, X, D.Hout, D.Va, tp, S(Bl.slab), 0, st))) return rc;
-        const int wcol[3] = {0, H, 0};
-        if ((rc = slab_reduce(tp, S(Bl.slab), D.Hout, X, grads->W_d, D.Hout, wcol, grads->b_d, st))) return rc;
-        // dh = dZd @ W_d[:, :H]
-        Src A = make_src(D.Va, {seg_dense(S(Bl.dZd), D.Hout, D.Hout, 0)});
-        if ((rc = gemm_nn(A, p->W_d, D.Hout, 0, D.Va, H, D.Hout, epi_store(S(Bl.dHo), H, 0, 0), st))) return rc;
+        ActBwd P = base_bwd(F(L.Zd), D.T + 1, WD_ACT_IDENTITY, D.Va, D.Vap, D.Hdk, S(Bl.dZd));
+        P.G = dH; P.ldg = D.Hdk;
+        WD_TRY(act_bwd(P));
+        Src dZ = make_src(D.Va, {seg_dense(S(Bl.dZd), D.Hdk, D.Hdk)});
+        Src X = x_d(g, D, F(L.h));
+        TnPlan tp = tn_plan(D.Hdk, X.cols_p, D.Va);
+        WD_TRY(gemm_tn(dZ, X, D.Hdk, D.Va, tp, S(Bl.slab), 0, st));
+        WD_TRY(slab_reduce(tp, S(Bl.slab), D.Hd, {{0, 0, H}, {Hk, H, D.d}}, grads->W_d, D.Hd, grads->b_d,
+                           X.s[2].kp0, st));
+        // dh = dZd W_d[:, :H]
+        WD_TRY(gemm_nt(S(Bl.dZd), D.Hdk, D.Hdk, nullptr, 0, 0, W(PL.WdT), D.Hdk, D.Vap, Hk,
+                       epi_store(S(Bl.dHo), Hk), st));
         dh = S(Bl.dHo);
     }
     // W_o layer
     {
-        ActBwd P = base_bwd(F(L.Zo), D.T, c->activation, D.Va, H, S(Bl.dZo));
-        P.G = dh; P.ldg = H;
-        if ((rc = act_bwd(P))) return rc;
-        Src dZ = make_src(D.Va, {seg_dense(S(Bl.dZo), H, H, 0)});
-        Src X = x_src_o(g, D, M_last, true);
-        TnPlan tp = tn_plan(H, X.cols_p, D.Va);
-        if ((rc = gemm_tn(dZ, X, H, D.Va, tp, S(Bl.slab), 0, st))) return rc;
-        const int wcol[3] = {0, D.Fa, 0};
-        if ((rc = slab_reduce(tp, S(Bl.slab), H, X, grads->W_o, D.Fa + H, wcol, grads->b_o, st))) return rc;
-        // dA = dZo @ W_o[:, Fa:]
-        if ((rc = gemm_nn(dZ, p->W_o, D.Fa + H, D.Fa, D.Va, H, H, epi_store(S(Bl.dA), H, 0, 0), st))) return rc;
+        ActBwd P = base_bwd(F(L.Zo), D.T, c->activation, D.Va, D.Vap, Hk, S(Bl.dZo));
+        P.G = dh; P.ldg = Hk;
+        WD_TRY(act_bwd(P));
+        Src dZ = make_src(D.Va, {seg_dense(S(Bl.dZo), Hk, Hk)});
+        Src X = x_o(g, D, F(L.A));
+        TnPlan tp = tn_plan(Hk, X.cols_p, D.Va);
+        WD_TRY(gemm_tn(dZ, X, Hk, D.Va, tp, S(Bl.slab), 0, st));
+        WD_TRY(slab_reduce(tp, S(Bl.slab), H, {{0, 0, D.Fa}, {D.Fak, D.Fa, H}}, grads->W_o, D.Fa + H, grads->b_o,
+                           X.s[2].kp0, st));
+        // dA = dZo W_o[:, Fa:]
+        WD_TRY(gemm_nt(S(Bl.dZo), Hk, Hk, nullptr, 0, 0, W(PL.WoT), Hk, D.Vap, Hk, epi_store(S(Bl.dA), Hk), st));
     }
     // gradient reaching M_{T-1} through the final aggregation, then the message layers
     float *dZbuf[2] = {S(Bl.dZ0), S(Bl.dZ1)};
     int cur = 0;
     {
-        ActBwd P = base_bwd(F(L.Z[D.T - 1]), D.T - 1, c->activation, D.R, H, dZbuf[cur]);
-        P.G = S(Bl.dA); P.ldg = H;
+        ActBwd P = base_bwd(F(L.Z[D.T - 1]), D.T - 1, c->activation, D.R, D.Rp, Hk, dZbuf[cur]);
+        P.G = S(Bl.dA); P.ldg = Hk;
         P.ptr = g->atom_gather_t.ptr; P.idx = g->atom_gather_t.idx; P.coef = g->atom_gather_t.coef;
         if (D.T > 1) { P.res_out = S(Bl.dRes); P.res_init = 1; }
-        if ((rc = act_bwd(P))) return rc;
+        WD_TRY(act_bwd(P));
     }
-    TnPlan tph{};
-    Src Xh0 = x_src_h(g, D, nullptr, true);
-    tph = tn_plan(H, Xh0.cols_p, D.R);
+    const Src Xh0 = x_h(D, nullptr);
+    const TnPlan tph = tn_plan(Hk, Xh0.cols_p, D.R);
     for (int t = D.T - 1; t >= 1; --t) {
         float *dZt = dZbuf[cur];
-        const float *srcM = D.undirected ? F(L.Ms[t]) : F(L.M[t - 1]);
         // dW_h, db_h (+)= dZ_t^T [X_t | 1]
-        Src dZ = make_src(D.R, {seg_dense(dZt, H, H, 0)});
-        Src X = x_src_h(g, D, srcM, true);
-        if ((rc = gemm_tn(dZ, X, H, D.R, tph, S(Bl.slab), t != D.T - 1, st))) return rc;
-        // dX = dZ_t @ W_h[:, :H]
-        const int ldwh = D.atom ? H + D.Fb : H;
-        if ((rc = gemm_nn(dZ, p->W_h, ldwh, 0, D.R, H, H, epi_store(S(Bl.dX), H, 0, 0), st))) return rc;
-        // dM_{t-1} = gather^T(dX) (+ symmetrize), then through act of layer t-1
+        Src dZ = make_src(D.R, {seg_dense(dZt, Hk, Hk)});
+        WD_TRY(gemm_tn(dZ, x_h(D, F(L.X[t - 1])), Hk, D.R, tph, S(Bl.slab), t != D.T - 1, st));
+        // dX = dZ_t W_h[:, :H]
+        WD_TRY(gemm_nt(dZt, Hk, Hk, nullptr, 0, 0, W(PL.WhT), Hk, D.Rp, Hk, epi_store(S(Bl.dX), Hk), st));
+        // dM_{t-1} = gather^T(dX) (+ symmetrize), then through the activation of layer t-1
         const int nxt = 1 - cur;
-        ActBwd P = base_bwd(F(L.Z[t - 1]), t - 1, c->activation, D.R, H, dZbuf[nxt]);
+        ActBwd P = base_bwd(F(L.Z[t - 1]), t - 1, c->activation, D.R, D.Rp, Hk, dZbuf[nxt]);
         if (D.undirected) {
             ActBwd Q{};
-            Q.G = S(Bl.dX); Q.ldg = H;
+            Q.G = S(Bl.dX); Q.ldg = Hk;
             Q.ptr = g->msg_gather_t.ptr; Q.idx = g->msg_gather_t.idx; Q.coef = g->msg_gather_t.coef;
-            Q.rows = D.R; Q.cols = H; Q.out = S(Bl.dMs);
-            if ((rc = act_bwd(Q))) return rc;
-            P.G = S(Bl.dMs); P.ldg = H; P.sym_rev = g->b2revb;
+            Q.rows = D.R; Q.rows_p = D.Rp; Q.cols = Hk; Q.ld = Hk; Q.out = S(Bl.dMs);
+            WD_TRY(act_bwd(Q));
+            P.G = S(Bl.dMs); P.ldg = Hk; P.sym_rev = g->b2revb;
         } else {
-            P.G = S(Bl.dX); P.ldg = H;
+            P.G = S(Bl.dX); P.ldg = Hk;
             P.ptr = g->msg_gather_t.ptr; P.idx = g->msg_gather_t.idx; P.coef = g->msg_gather_t.coef;
         }
         if (t - 1 == 0) P.add_in = S(Bl.dRes);
         else { P.res_out = S(Bl.dRes); P.res_init = 0; }
-        if ((rc = act_bwd(P))) return rc;
+        WD_TRY(act_bwd(P));
         cur = nxt;
     }
     if (D.T > 1) {
-        const int ldwh = D.atom ? H + D.Fb : H;
-        const int wcol[3] = {0, H, 0};
-        if ((rc = slab_reduce(tph, S(Bl.slab), H, Xh0, grads->W_h, ldwh, wcol, grads->b_h, st))) return rc;
+        if (D.atom)
+            WD_TRY(slab_reduce(tph, S(Bl.slab), H, {{0, 0, H}, {Hk, H, D.Fb}}, grads->W_h, H + D.Fb, grads->b_h,
+                               Xh0.s[1].kp0, st));
+        else
+            WD_TRY(slab_reduce(tph, S(Bl.slab), H, {{0, 0, H}}, grads->W_h, H, grads->b_h, Xh0.s[1].kp0, st));
     }
     // input layer: dW_i, db_i = dZ_0^T [f | 1]
     {
-        Src dZ = make_src(D.R, {seg_dense(dZbuf[cur], H, H, 0)});
-        Src X = x_src_in(g, D);
-        TnPlan tp = tn_plan(H, X.cols_p, D.R);
-        if ((rc = gemm_tn(dZ, X, H, D.R, tp, S(Bl.slab), 0, st))) return rc;
-        const int wcol[2] = {0, 0};
-        if ((rc = slab_reduce(tp, S(Bl.slab), H, X, grads->W_i, D.Kin, wcol, grads->b_i, st))) return rc;
+        Src dZ = make_src(D.R, {seg_dense(dZbuf[cur], Hk, Hk)});
+        Src X = x_in(g, D);
+        TnPlan tp = tn_plan(Hk, X.cols_p, D.R);
+        WD_TRY(gemm_tn(dZ, X, Hk, D.R, tp, S(Bl.slab), 0, st));
+        WD_TRY(slab_reduce(tp, S(Bl.slab), H, {{0, 0, D.Kin}}, grads->W_i, D.Kin, grads->b_i, X.s[1].kp0, st));
     }
     if (prelu && grads->prelu) {
         hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(256), 0, st, prelu_part, prelu_used, grads->prelu);

@@ -1,0 +1,29 @@
+#!/bin/bash
+# GPU-box driver for one gpurun call: each GPU step has its own time limit; any exit code other than
+# 0 (ok) or 1 (test failures) stops the call (fault / abort / timeout => start nothing more on the GPU).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+step() {
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=300 ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py ;;
+    benchq) step bench_quick 300 python bench.py --steps 100 --warmup 10 --cpu-seconds 5 ;;
+    prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu ;;
+    tune) step tune 600 python tools/tune_gemm.py ;;
+    counters) step counters 120 rocprofv3 -L ;;
+    pmc) step pmc 1500 bash tools/pmc.sh ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
