@@ -21,7 +21,7 @@
  *  - Row 0 of every atom / bond array is the reference's zero pad row (featurization.py:767-781);
  *    n_atoms / n_bonds INCLUDE it, exactly like BatchMolGraph.n_atoms / n_bonds.
  *  - fp32 storage and fp32 arithmetic (MFMA f32 in/out), int32 indices.
- *  - Padding: f_atoms / f_bonds / atom_desc rows are allocated up to a multiple of 64 and their row
+ *  - Padding: f_atoms / f_bonds / atom_desc rows are allocated up to a multiple of 128 and their row
  *    stride covers the feature width rounded up to 32; padding is zero.  (The host packer,
  *    BatchMolGraph.device_graph, lays them out this way.)  Weights are the unpadded nn.Linear
  *    tensors; wdmpnn_pack_params builds the padded GEMM operands from them.

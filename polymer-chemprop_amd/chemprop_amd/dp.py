@@ -1,0 +1,116 @@
+"""Data parallelism over the GPUs of one node.
+
+The reference has no distributed code; this module is the build's DP layer:
+one process per GPU, ``torch.distributed`` with backend ``nccl`` (= RCCL on ROCm, over xGMI) on
+GPUs and ``gloo`` on CPU (tests).  Molecules are independent, so:
+
+* forward throughput shards batches across ranks with no collective (rank r takes r, r+N, ...);
+* training is plain DP: identical initial parameters (broadcast from rank 0), local forward +
+  backward on the rank's own batch, then ONE all-reduce of a flat fp32 gradient bucket
+  (354,901 params = 1.42 MB at the default config), divided by the world size.
+
+The gradients of every parameter are views into the bucket, so autograd accumulates straight into
+it and the all-reduce needs no pack/unpack copies.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Iterable, List, Sequence, TypeVar
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+T = TypeVar('T')
+
+
+@dataclass
+class DistEnv:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device('cpu')
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+
+def init_distributed(backend: str = None) -> DistEnv:
+    """Read RANK / WORLD_SIZE / LOCAL_RANK (torch.distributed.run) and initialise the process group.
+    Single process (no env): no process group, rank 0 of 1."""
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if backend is None:
+        backend = 'nccl' if torch.cuda.is_available() else 'gloo'
+    if backend == 'nccl':
+        torch.cuda.set_device(local)
+        device = torch.device('cuda', local)
+    else:
+        device = torch.device('cpu')
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        kwargs = {'device_id': device} if backend == 'nccl' else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, **kwargs)
+    return DistEnv(rank, world, local, device)
+
+
+def shard(items: Sequence[T], rank: int, world_size: int) -> List[T]:
+    """Round-robin shard: rank r gets items r, r + N, r + 2N, ...  (disjoint, covering)."""
+    return list(items[rank::world_size])
+
+
+def broadcast_parameters(module: nn.Module, src: int = 0) -> None:
+    """Make every rank start from rank ``src``'s parameters and buffers."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            dist.broadcast(t.data, src)
+
+
+class GradBucket:
+    """One flat fp32 gradient buffer for all trainable parameters (grads are views into it)."""
+
+    def __init__(self, module: nn.Module):
+        self.params = [p for p in module.parameters() if p.requires_grad]
+        if not self.params:
+            raise ValueError('module has no trainable parameters')
+        dev = self.params[0].device
+        n = sum(p.numel() for p in self.params)
+        self.buffer = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        for p in self.params:
+            if p.dtype != torch.float32:
+                raise TypeError('GradBucket expects float32 parameters')
+            p.grad = self.buffer[off:off + p.numel()].view_as(p)
+            off += p.numel()
+
+    def zero(self) -> None:
+        """Zero in place (keeps the views; use instead of ``zero_grad(set_to_none=True)``)."""
+        self.buffer.zero_()
+        for p, v in zip(self.params, self._views()):
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                p.grad = v  # a grad replaced by an optimizer / user: re-attach the view
+
+    def _views(self) -> Iterable[torch.Tensor]:
+        off = 0
+        for p in self.params:
+            yield self.buffer[off:off + p.numel()].view_as(p)
+            off += p.numel()
+
+    def allreduce_mean(self) -> None:
+        """Sum the bucket over ranks (one collective) and divide by the world size."""
+        for p, v in zip(self.params, self._views()):
+            if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
+                v.copy_(p.grad)  # autograd created a fresh tensor: fold it into the bucket
+                p.grad = v
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(self.buffer, op=dist.ReduceOp.SUM)
+            self.buffer.div_(dist.get_world_size())
+
+    @property
+    def nbytes(self) -> int:
+        return self.buffer.numel() * 4

@@ -277,9 +277,9 @@ class BatchMolGraph:
             fb = fb[:, fb.shape[1] - nb_used:]
         Fa, Fb = fa.shape[1], fb.shape[1]
         lda, ldb = _round_up(Fa, 32), _round_up(Fb, 32)
-        fa_p = np.zeros((_round_up(fa.shape[0], 64), lda), np.float32)  # rows to the GEMM tile, K to 32
+        fa_p = np.zeros((_round_up(fa.shape[0], 128), lda), np.float32)  # rows to the GEMM tile, K to 32
         fa_p[:fa.shape[0], :Fa] = fa
-        fb_p = np.zeros((_round_up(fb.shape[0], 64), ldb), np.float32)
+        fb_p = np.zeros((_round_up(fb.shape[0], 128), ldb), np.float32)
         fb_p[:fb.shape[0], :Fb] = fb
         a_start = np.array([s for s, _ in self.a_scope], np.int32)
         a_size = np.array([n for _, n in self.a_scope], np.int32)

@@ -167,7 +167,7 @@ class MPNEncoder(nn.Module):
             if any(n == 0 for _, n in mol_graph.a_scope):
                 raise RuntimeError('stack expects each tensor to be equal size (empty molecule with atom '
                                    'descriptors, mpn.py:149 vs 171)')
-            padded = np.zeros((-(-rows.shape[0] // 64) * 64, -(-d // 32) * 32), np.float32)
+            padded = np.zeros((-(-rows.shape[0] // 128) * 128, -(-d // 32) * 32), np.float32)
             padded[:rows.shape[0], :d] = rows
             desc = torch.from_numpy(padded).to(device)
             gs.atom_desc, gs.desc_dim = desc.data_ptr(), d

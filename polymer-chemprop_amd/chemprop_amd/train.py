@@ -1,0 +1,133 @@
+"""Training-step counterpart of the reference loop.
+
+* ``train_step`` / ``train`` follow ``chemprop/train/train.py:17-113``: mask / targets from
+  ``None`` entries, target and data weights, ``loss_func(preds, targets) * w_t * w_d * mask``,
+  ``loss.sum() / mask.sum()``, backward, optional ``clip_grad_norm_``, ``optimizer.step()``,
+  per-batch scheduler step; plus the DP all-reduce of :mod:`chemprop_amd.dp` between backward and
+  the optimizer step.
+* ``NoamLR`` restates ``chemprop/nn_utils.py:115-194``; ``get_loss_func`` ``utils.py:338-364``
+  (regression / classification / multiclass); ``build_optimizer`` ``utils.py:295-310``.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence, Union
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch.optim import Adam, Optimizer
+from torch.optim.lr_scheduler import _LRScheduler
+
+from .dp import GradBucket
+
+
+class NoamLR(_LRScheduler):
+    """nn_utils.py:115-194: linear warm-up from init_lr to max_lr over warmup_epochs, then
+    exponential decay to final_lr at total_epochs."""
+
+    def __init__(self, optimizer: Optimizer, warmup_epochs: List[Union[float, int]], total_epochs: List[int],
+                 steps_per_epoch: int, init_lr: List[float], max_lr: List[float], final_lr: List[float]):
+        assert len(optimizer.param_groups) == len(warmup_epochs) == len(total_epochs) == len(init_lr) == \
+            len(max_lr) == len(final_lr)
+        self.num_lrs = len(optimizer.param_groups)
+        self.optimizer = optimizer
+        self.warmup_epochs = np.array(warmup_epochs)
+        self.total_epochs = np.array(total_epochs)
+        self.steps_per_epoch = steps_per_epoch
+        self.init_lr = np.array(init_lr)
+        self.max_lr = np.array(max_lr)
+        self.final_lr = np.array(final_lr)
+        self.current_step = 0
+        self.lr = init_lr
+        self.warmup_steps = (self.warmup_epochs * self.steps_per_epoch).astype(int)
+        self.total_steps = self.total_epochs * self.steps_per_epoch
+        self.linear_increment = (self.max_lr - self.init_lr) / self.warmup_steps
+        self.exponential_gamma = (self.final_lr / self.max_lr) ** (1 / (self.total_steps - self.warmup_steps))
+        super(NoamLR, self).__init__(optimizer)
+
+    def get_lr(self) -> List[float]:
+        return list(self.lr)
+
+    def step(self, current_step: int = None):
+        self.current_step = self.current_step + 1 if current_step is None else current_step
+        for i in range(self.num_lrs):
+            if self.current_step <= self.warmup_steps[i]:
+                self.lr[i] = self.init_lr[i] + self.current_step * self.linear_increment[i]
+            elif self.current_step <= self.total_steps[i]:
+                self.lr[i] = self.max_lr[i] * (self.exponential_gamma[i] ** (self.current_step - self.warmup_steps[i]))
+            else:
+                self.lr[i] = self.final_lr[i]
+            self.optimizer.param_groups[i]['lr'] = self.lr[i]
+
+
+def get_loss_func(dataset_type: str) -> nn.Module:
+    """utils.py:338-364 (no alternative losses, no spectra)."""
+    if dataset_type == 'classification':
+        return nn.BCEWithLogitsLoss(reduction='none')
+    if dataset_type == 'regression':
+        return nn.MSELoss(reduction='none')
+    if dataset_type == 'multiclass':
+        return nn.CrossEntropyLoss(reduction='none')
+    raise ValueError(f'Dataset type "{dataset_type}" not supported.')
+
+
+def build_optimizer(model: nn.Module, init_lr: float = 1e-4, weight_decay: float = 0.0) -> Optimizer:
+    """utils.py:295-310 (Adam)."""
+    return Adam([{'params': model.parameters(), 'lr': init_lr, 'weight_decay': weight_decay}])
+
+
+def batch_loss(preds: torch.Tensor, target_batch: Sequence[Sequence[Optional[float]]], loss_func: Callable,
+               dataset_type: str = 'regression', target_weights: Sequence[float] = None,
+               data_weights: Sequence[float] = None) -> torch.Tensor:
+    """train.py:46-74: masked, weighted loss averaged over the present targets."""
+    dev = preds.device
+    mask = torch.tensor([[x is not None for x in tb] for tb in target_batch], dtype=torch.bool, device=dev)
+    targets = torch.tensor([[0 if x is None else x for x in tb] for tb in target_batch], device=dev)
+    tw = torch.Tensor(target_weights).to(dev) if target_weights is not None else torch.ones_like(targets)
+    dw = torch.Tensor(data_weights if data_weights is not None else [1.0] * len(target_batch)).unsqueeze(1).to(dev)
+    if dataset_type == 'multiclass':
+        targets = targets.long()
+        loss = torch.cat([loss_func(preds[:, j, :], targets[:, j]).unsqueeze(1) for j in range(preds.size(1))],
+                         dim=1) * tw * dw * mask
+    else:
+        loss = loss_func(preds, targets) * tw * dw * mask
+    return loss.sum() / mask.sum()
+
+
+def train_step(model: nn.Module, mol_batch, target_batch, loss_func: Callable, optimizer: Optimizer,
+               scheduler: _LRScheduler = None, dataset_type: str = 'regression', features_batch=None,
+               target_weights=None, data_weights=None, grad_clip: float = None,
+               bucket: GradBucket = None) -> torch.Tensor:
+    """One optimisation step (train.py:55-86).  With ``bucket`` the gradients are averaged over the
+    data-parallel ranks (one all-reduce) before clipping and the optimizer step."""
+    model.train()
+    if bucket is not None:
+        bucket.zero()
+    else:
+        model.zero_grad()
+    preds = model(mol_batch, features_batch)
+    loss = batch_loss(preds, target_batch, loss_func, dataset_type, target_weights, data_weights)
+    loss.backward()
+    if bucket is not None:
+        bucket.allreduce_mean()
+    if grad_clip:
+        nn.utils.clip_grad_norm_(model.parameters(), grad_clip)
+    optimizer.step()
+    if scheduler is not None and isinstance(scheduler, (NoamLR, torch.optim.lr_scheduler.CosineAnnealingLR,
+                                                        torch.optim.lr_scheduler.CyclicLR)):
+        scheduler.step()
+    return loss.detach()
+
+
+def train(model: nn.Module, batches, loss_func: Callable, optimizer: Optimizer, scheduler: _LRScheduler = None,
+          dataset_type: str = 'regression', grad_clip: float = None, bucket: GradBucket = None) -> List[float]:
+    """One epoch over ``batches`` = iterable of (mol_batch, target_batch[, features_batch]) (train.py:17-113
+    without logging); returns the per-batch losses (one host sync per batch, like loss.item())."""
+    losses = []
+    for item in batches:
+        mol_batch, target_batch = item[0], item[1]
+        features_batch = item[2] if len(item) > 2 else None
+        loss = train_step(model, mol_batch, target_batch, loss_func, optimizer, scheduler, dataset_type,
+                          features_batch, grad_clip=grad_clip, bucket=bucket)
+        losses.append(float(loss))
+    return losses

@@ -219,6 +219,91 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_nt_kernel(NtParams P) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Panel kernel (forward NT layers with a narrow output): the workgroup's whole B panel
+// [BN][K] is loaded into LDS once; every wave then streams its own A rows straight from global
+// memory into the MFMA A-operand registers (lane l holds row l&31, 16 consecutive k of the chunk
+// = four float4 loads, prefetched two chunks ahead), reads B fragments from the resident panel
+// and runs 2 independent 32x32 accumulator chains.  The K loop has no barrier and no LDS write.
+// Workgroup = NW waves stacked along M (NW*32 rows) x BN = 64 columns.  LDS row stride K + 4
+// (K a multiple of 32 => stride = 4 mod 32... conflict-free ds_read_b128 needs stride = 4 mod 64,
+// which the launcher pads to).
+// ---------------------------------------------------------------------------------------------
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void gemm_panel_kernel(NtParams P, int ldp) {
+    constexpr int BN = 64, TN = 2, BM = 32 * NW;
+    extern __shared__ __attribute__((aligned(16))) float panel[];  // [BN][ldp]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
+    const int tile = xcd_tile(blockIdx.x, P.tiles_m * P.tiles_n);
+    const int mt = tile / P.tiles_n, nt = tile % P.tiles_n;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int K = P.ka0 + P.ka1;
+    const int kq = K / 4;
+
+    // B panel -> LDS (all threads, float4)
+    for (int q = tid; q < BN * kq; q += 64 * NW) {
+        const int r = q / kq, c = (q % kq) * 4;
+        st4(panel + r * ldp + c, ld4(P.b + (size_t)(n0 + r) * P.ldb + c));
+    }
+
+    // this lane's A row and the chunk -> (segment base, column) map
+    const int row = m0 + wave * 32 + l32;
+    const float *rowA0 = P.a0 + (size_t)row * P.lda0 + 16 * h;
+    const float *rowA1 = P.ka1 ? P.a1 + (size_t)row * P.lda1 + 16 * h - P.ka0 : nullptr;
+    struct Frag { float4 v[4]; };
+    auto load_a = [&](Frag &F, int k0) {
+        const float *p = (k0 < P.ka0 ? rowA0 : rowA1) + k0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) F.v[q] = ld4(p + 4 * q);
+    };
+
+    floatx16 acc[TN];
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+
+    const int nchunks = K / BK;
+    Frag F0, F1;
+    load_a(F0, 0);
+    load_a(F1, min(1, nchunks - 1) * BK);
+    __syncthreads();  // panel resident
+
+    auto step = [&](int kc, Frag &F, Frag &Fnext2) {
+        float bf[TN][16];
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+            const float *src = panel + (b * 32 + l32) * ldp + kc * BK + 16 * h;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 v = ld4(src + 4 * q);
+                bf[b][4 * q] = v.x; bf[b][4 * q + 1] = v.y; bf[b][4 * q + 2] = v.z; bf[b][4 * q + 3] = v.w;
+            }
+        }
+        const float af[16] = {F.v[0].x, F.v[0].y, F.v[0].z, F.v[0].w, F.v[1].x, F.v[1].y, F.v[1].z, F.v[1].w,
+                              F.v[2].x, F.v[2].y, F.v[2].z, F.v[2].w, F.v[3].x, F.v[3].y, F.v[3].z, F.v[3].w};
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+                acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[b][s], acc[b], 0, 0, 0);
+        // F's registers are free again: prefetch chunk kc+2 (clamped: branch-free, so the compiler
+        // keeps counted vmcnt waits instead of draining every load at the loop head)
+        load_a(Fnext2, min(kc + 2, nchunks - 1) * BK);
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch here (hipcc otherwise sinks it a step)
+    };
+    int kc = 0;
+    for (; kc + 1 < nchunks; kc += 2) {
+        step(kc, F0, F0);
+        step(kc + 1, F1, F1);
+    }
+    if (kc < nchunks) step(kc, F0, F0);
+    floatx16 acc2[1][TN];
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc2[0][b] = acc[b];
+    epilogue<1, TN>(P.epi, acc2, m0 + wave * 32, n0, h, l32, P.M, P.N, P.epi.Y);
+}
+
+// ---------------------------------------------------------------------------------------------
 // TN kernel (weight gradients): both operands k-major (rows = m), masked at the split's row range.
 // ---------------------------------------------------------------------------------------------
 enum SegKind : int { SEG_DENSE = 0, SEG_ONES = 2 };

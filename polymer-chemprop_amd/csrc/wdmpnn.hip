@@ -11,7 +11,7 @@
 //  (LT+1      hd = [h | desc] W_d^T + b_d                                   mpn.py:136-143)
 //   readout   out_i = Xn_i * sum_a w_a h_a / sum_a w_a (mean | sum | norm)   mpn.py:145-171
 //
-// Buffers are padded: rows to 64 (GEMM row tile), hidden columns to 64, K extents to 32, padding
+// Buffers are padded: rows to 128 (GEMM row tile), hidden columns to 64, K extents to 32, padding
 // zero; weights are packed once per parameter version (wdmpnn_pack_params) into the same padded
 // shapes (+ transposes for the backward data gradients).  Backward = the autograd graph of the
 // above with deterministic, atomics-free kernels.
@@ -87,8 +87,8 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     if (!(c->dropout >= 0.f && c->dropout < 1.f)) return fail(WD_ERR_ARG, "dropout must be in [0, 1)");
     D.H = p->hidden; D.Hk = rup(D.H, 64); D.T = c->depth;
     D.atom = g->atom_messages != 0; D.undirected = c->undirected != 0; D.save = c->save_for_backward != 0;
-    D.Va = g->n_atoms; D.Vap = rup(D.Va, 64); D.B = g->n_mols;
-    D.R = D.atom ? g->n_atoms : g->n_bonds; D.Rp = rup(D.R, 64);
+    D.Va = g->n_atoms; D.Vap = rup(D.Va, 128); D.B = g->n_mols;
+    D.R = D.atom ? g->n_atoms : g->n_bonds; D.Rp = rup(D.R, 128);
     D.Fa = g->atom_fdim; D.Fak = rup(D.Fa, 32); D.Fb = g->bond_fdim; D.Fbk = rup(D.Fb, 32);
     D.desc = g->atom_desc != nullptr && g->desc_dim > 0;
     D.d = D.desc ? g->desc_dim : 0; D.dk = rup(D.d, 32);
@@ -218,7 +218,26 @@ int gemm_nt(const float *a0, int lda0, int ka0, const float *a1, int lda1, int k
     // variants (tuning): 1 = 64x64 depth 1, 2 = 32x64 depth 1, 3 = 64x64 depth 2, 4 = 32x64 depth 2,
     // 5 = 64x64 depth 2 with 64-wide K chunks (needs K segments aligned to 64, else falls back to 3)
     const bool k64 = ka0 % 64 == 0 && ka1 % 64 == 0;
-    if (variant == 0) variant = k64 ? 5 : 3;
+    // 6 = B-panel-resident kernel (128x64 tiles, A streamed to registers), the default when the
+    // 64 x K panel fits in LDS
+    const int K = ka0 + ka1;
+    const int ldp = K + ((68 - K % 64) % 64);  // stride = 4 (mod 64): conflict-free ds_read_b128
+    const size_t panel_bytes = (size_t)64 * ldp * 4;
+    if (variant == 0) variant = panel_bytes <= 160 * 1024 ? 6 : 3;
+    if (variant == 6 && (panel_bytes > 160 * 1024 || Mp % 128)) variant = 3;
+    if (variant == 6) {
+        P.tiles_m = Mp / 128; P.tiles_n = Np / 64;
+        static bool lds_attr = false;  // idempotent: allow up to 160 KiB of dynamic LDS
+        if (!lds_attr) {
+            if (hipFuncSetAttribute((const void *)&gemm_panel_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024) != hipSuccess)
+                return fail(WD_ERR_ARG, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+            lds_attr = true;
+        }
+        hipLaunchKernelGGL((gemm_panel_kernel<4>), dim3(P.tiles_m * P.tiles_n), dim3(256), panel_bytes, st, P, ldp);
+        WD_CHECK_LAUNCH("gemm_panel");
+        return 0;
+    }
     if (variant == 5 && !k64) variant = 3;
     const dim3 blk64(64 * NWM * NWN);
     if (variant == 2 || variant == 4) {

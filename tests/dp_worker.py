@@ -1,0 +1,53 @@
+"""Worker functions for the world-size-2 gloo tests (spawned processes import this module)."""
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, 'polymer-chemprop_amd')]
+
+from chemprop_amd import dp  # noqa: E402
+from chemprop_amd.train import get_loss_func, train_step  # noqa: E402
+
+
+class TinyModel(nn.Module):
+    """Stand-in for MoleculeModel with the same forward signature (CPU, gloo tests only)."""
+
+    def __init__(self):
+        super().__init__()
+        self.net = nn.Sequential(nn.Linear(6, 16), nn.ReLU(), nn.Linear(16, 2))
+
+    def forward(self, batch, features_batch=None):
+        return self.net(batch)
+
+
+def data(seed, n=8):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, 6, generator=g)
+    y = [[float(v) if (i + j) % 5 else None for j, v in enumerate(row)] for i, row in enumerate(torch.randn(n, 2, generator=g))]
+    return x, y
+
+
+def run(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    env = dp.init_distributed('gloo')
+    torch.manual_seed(100 + rank)  # deliberately different init per rank
+    model = TinyModel()
+    dp.broadcast_parameters(model)
+    bucket = dp.GradBucket(model)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    batches = dp.shard([data(s) for s in range(6)], env.rank, env.world_size)
+    loss_func = get_loss_func('regression')
+    for x, y in batches[:2]:
+        train_step(model, x, y, loss_func, opt, bucket=bucket)
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    gathered = [torch.zeros_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    if rank == 0:
+        torch.save({'params': [g for g in gathered], 'nbytes': bucket.nbytes}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()

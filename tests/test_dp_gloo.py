@@ -1,0 +1,55 @@
+"""CPU, world size 2 over gloo: the data-parallel layer (chemprop_amd/dp.py) used by multi-GPU training
+(SURVEY.md §8(e)).  Ranks start from rank 0's parameters, train on disjoint shards, average
+gradients with one all-reduce of the flat bucket, and must end with identical parameters equal to
+a single-process run that averages the two shards' gradients."""
+import os
+import socket
+
+import torch
+import torch.multiprocessing as mp
+
+import dp_worker
+from chemprop_amd import dp
+from chemprop_amd.train import batch_loss, get_loss_func
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_is_disjoint_and_covering():
+    items = list(range(23))
+    parts = [dp.shard(items, r, 4) for r in range(4)]
+    assert sorted(x for p in parts for x in p) == items
+    assert all(len(set(a) & set(b)) == 0 for i, a in enumerate(parts) for b in parts[i + 1:])
+
+
+def test_two_rank_gradient_allreduce_matches_single_process(tmp_path):
+    out = str(tmp_path / 'dp.pt')
+    mp.spawn(dp_worker.run, args=(2, free_port(), out), nprocs=2, join=True)
+    res = torch.load(out, weights_only=True)
+    p0, p1 = res['params']
+    assert torch.equal(p0, p1), 'ranks diverged'
+    # single-process reference: rank 0's init, each step averages the two shards' gradients
+    torch.manual_seed(100)
+    model = dp_worker.TinyModel()
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    lf = get_loss_func('regression')
+    shards = [dp.shard([dp_worker.data(s) for s in range(6)], r, 2) for r in range(2)]
+    for step in range(2):
+        grads = []
+        for r in range(2):
+            model.zero_grad()
+            x, y = shards[r][step]
+            batch_loss(model(x), y, lf).backward()
+            grads.append([p.grad.clone() for p in model.parameters()])
+        for p, g0, g1 in zip(model.parameters(), *grads):
+            p.grad = (g0 + g1) / 2
+        opt.step()
+    ref = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    assert torch.allclose(p0, ref, atol=1e-6, rtol=1e-5)
+    assert res['nbytes'] == 4 * sum(p.numel() for p in model.parameters())

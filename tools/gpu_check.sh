@@ -24,6 +24,7 @@ for s in "$@"; do
     tune) step tune 600 python tools/tune_gemm.py ;;
     counters) step counters 120 rocprofv3 -L ;;
     pmc) step pmc 1500 bash tools/pmc.sh ;;
+    sweep) step sweep 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/sweep -o run -- python tools/size_sweep.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
