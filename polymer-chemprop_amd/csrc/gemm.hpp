@@ -219,6 +219,142 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_nt_kernel(NtParams P) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// 16x16x4 variant of gemm_nt_kernel: the wave's 32x32 block is 2x2 v_mfma_f32_16x16x4_f32 tiles (4
+// independent accumulator chains instead of one), same LDS staging / prefetch.  Lane l = (i = l&15,
+// g = l>>4) supplies k = 8g + s at step s (0..7 per 32-chunk): two ds_read_b128 per operand tile.
+// C/D map of 16x16: col = l&15, row = 4*(l>>4) + reg.
+// ---------------------------------------------------------------------------------------------
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_nt16_kernel(NtParams P) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+    constexpr int LD = BK + 4;
+    constexpr int A_V4 = BM * 8, B_V4 = BN * 8;
+    constexpr int PA = A_V4 / NT, PB = B_V4 / NT;
+    constexpr int STAGE = (BM + BN) * LD;
+    static_assert(A_V4 % NT == 0 && B_V4 % NT == 0, "tile must divide evenly over threads");
+    __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wi = wave / WN, wj = wave % WN, g = lane >> 4, i16 = lane & 15;
+    const int tile = xcd_tile(blockIdx.x, P.tiles_m * P.tiles_n);
+    const int mt = tile / P.tiles_n, nt = tile % P.tiles_n;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int K = P.ka0 + P.ka1;
+
+    floatx4 acc[TM][TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const float *pb[PB];
+#pragma unroll
+    for (int p = 0; p < PB; ++p) {
+        const int q = tid + p * NT, r = q >> 3, c = (q & 7) * 4;
+        pb[p] = P.b + (size_t)(n0 + r) * P.ldb + c;
+    }
+    struct Regs { float4 a[PA], b[PB]; };
+    auto load_chunk = [&](Regs &R, int k0) {
+        const bool seg1 = k0 >= P.ka0;
+        const float *base = seg1 ? P.a1 : P.a0;
+        const int ld = seg1 ? P.lda1 : P.lda0;
+        const int kk = seg1 ? k0 - P.ka0 : k0;
+#pragma unroll
+        for (int p = 0; p < PA; ++p) {
+            const int q = tid + p * NT, r = q >> 3, c = (q & 7) * 4;
+            R.a[p] = ld4(base + (size_t)(m0 + r) * ld + kk + c);
+        }
+#pragma unroll
+        for (int p = 0; p < PB; ++p) R.b[p] = ld4(pb[p] + k0);
+    };
+    auto store_chunk = [&](const Regs &R, float *st) {
+#pragma unroll
+        for (int p = 0; p < PA; ++p) {
+            const int q = tid + p * NT, r = q >> 3, c = (q & 7) * 4;
+            st4(st + r * LD + c, R.a[p]);
+        }
+#pragma unroll
+        for (int p = 0; p < PB; ++p) {
+            const int q = tid + p * NT, r = q >> 3, c = (q & 7) * 4;
+            st4(st + BM * LD + r * LD + c, R.b[p]);
+        }
+    };
+    auto compute = [&](const float *As) {
+        const float *Bs = As + BM * LD;
+        float af[TM][8], bf[TN][8];
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+            const float *src = As + (wi * (BM / WM) + a * 16 + i16) * LD + 8 * g;
+            const float4 v0 = ld4(src), v1 = ld4(src + 4);
+            af[a][0] = v0.x; af[a][1] = v0.y; af[a][2] = v0.z; af[a][3] = v0.w;
+            af[a][4] = v1.x; af[a][5] = v1.y; af[a][6] = v1.z; af[a][7] = v1.w;
+        }
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+            const float *src = Bs + (wj * (BN / WN) + b * 16 + i16) * LD + 8 * g;
+            const float4 v0 = ld4(src), v1 = ld4(src + 4);
+            bf[b][0] = v0.x; bf[b][1] = v0.y; bf[b][2] = v0.z; bf[b][3] = v0.w;
+            bf[b][4] = v1.x; bf[b][5] = v1.y; bf[b][6] = v1.z; bf[b][7] = v1.w;
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
+    };
+    const int nchunks = K / BK;
+    Regs R0, R1;
+    load_chunk(R0, 0);
+    load_chunk(R1, min(1, nchunks - 1) * BK);
+    store_chunk(R0, lds);
+    __syncthreads();
+    auto step = [&](int kc, Regs &Rnext, Regs &Rfree) {
+        load_chunk(Rfree, min(kc + 2, nchunks - 1) * BK);
+        compute(lds + (kc & 1) * STAGE);
+        if (kc + 1 < nchunks) store_chunk(Rnext, lds + ((kc + 1) & 1) * STAGE);
+        __syncthreads();
+    };
+    int kc = 0;
+    for (; kc + 1 < nchunks; kc += 2) {
+        step(kc, R1, R0);
+        step(kc + 1, R0, R1);
+    }
+    if (kc < nchunks) step(kc, R1, R0);
+
+    const Epi &E = P.epi;
+    const float slope = (E.kind == EPI_ACT && E.act == ACT_PRELU) ? E.slope[0] : 0.f;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+            const int j = n0 + wj * (BN / WN) + b * 16 + i16;
+            const float bias = (E.kind == EPI_ACT && E.bias) ? E.bias[j] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = m0 + wi * (BM / WM) + a * 16 + 4 * g + r;
+                if (i >= P.M || j >= P.N) continue;
+                const size_t o = (size_t)i * E.ld + j;
+                const float v = acc[a][b][r];
+                if (E.kind == EPI_ACT) {
+                    float z = v + bias;
+                    if (E.resid) z += E.resid[o];
+                    if (E.Z) E.Z[o] = z;
+                    float y = act_fwd(E.act, z, slope);
+                    if (E.p_drop > 0.f) y *= dropout_scale(E.seed, E.layer, i, j, E.p_drop);
+                    E.Y[o] = y;
+                } else {
+                    E.Y[o] = E.accumulate ? E.Y[o] + v : v;
+                }
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Panel kernel (forward NT layers with a narrow output): the workgroup's whole B panel
 // [BN][K] is loaded into LDS once; every wave then streams its own A rows straight from global
 // memory into the MFMA A-operand registers (lane l holds row l&31, 16 consecutive k of the chunk

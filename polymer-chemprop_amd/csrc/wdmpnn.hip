@@ -206,7 +206,7 @@ constexpr int NBM = 64, NBN = 64, NWM = 2, NWN = 2;
 
 // C[Mp][Np] = epi([A0 | A1] B^T); A segments [Mp][lda], K extents multiples of 32; B [Np][ldb].
 // Tile 64x64 (4 waves) or 32x64 (2 waves), global-load prefetch depth 1 or 2; WdConfig.gemm_variant
-// selects one for tuning (0 = default, 64x64 depth 2).
+// selects one for tuning (0 = default = 9, 64x64 tile of 16x16x4 MFMAs, measured fastest at every size).
 int gemm_nt(const float *a0, int lda0, int ka0, const float *a1, int lda1, int ka1, const float *b, int ldb, int Mp,
             int Np, const Epi &epi, hipStream_t st, int variant = 0) {
     if (Mp <= 0 || Np <= 0) return 0;
@@ -218,12 +218,11 @@ int gemm_nt(const float *a0, int lda0, int ka0, const float *a1, int lda1, int k
     // variants (tuning): 1 = 64x64 depth 1, 2 = 32x64 depth 1, 3 = 64x64 depth 2, 4 = 32x64 depth 2,
     // 5 = 64x64 depth 2 with 64-wide K chunks (needs K segments aligned to 64, else falls back to 3)
     const bool k64 = ka0 % 64 == 0 && ka1 % 64 == 0;
-    // 6 = B-panel-resident kernel (128x64 tiles, A streamed to registers), the default when the
-    // 64 x K panel fits in LDS
+    // 6 = B-panel-resident kernel (128x64 tiles, A streamed to registers; experimental, slower)
     const int K = ka0 + ka1;
     const int ldp = K + ((68 - K % 64) % 64);  // stride = 4 (mod 64): conflict-free ds_read_b128
     const size_t panel_bytes = (size_t)64 * ldp * 4;
-    if (variant == 0) variant = panel_bytes <= 160 * 1024 ? 6 : 3;
+    if (variant == 0) variant = 9;
     if (variant == 6 && (panel_bytes > 160 * 1024 || Mp % 128)) variant = 3;
     if (variant == 6) {
         P.tiles_m = Mp / 128; P.tiles_n = Np / 64;
@@ -240,6 +239,26 @@ int gemm_nt(const float *a0, int lda0, int ka0, const float *a1, int lda1, int k
     }
     if (variant == 5 && !k64) variant = 3;
     const dim3 blk64(64 * NWM * NWN);
+    // 9 = 64x64 with 16x16x4 MFMA (4 independent accumulators per wave)
+    if (variant == 9) {
+        P.tiles_m = Mp / 64; P.tiles_n = Np / 64;
+        hipLaunchKernelGGL((gemm_nt16_kernel<64, 64, 2, 2>), dim3(P.tiles_m * P.tiles_n), dim3(256), 0, st, P);
+        WD_CHECK_LAUNCH("gemm_nt16");
+        return 0;
+    }
+    // 7 = 128x64 (4 waves x 32x64, two accumulators per wave), 8 = 64x64 (2 waves x 32x64)
+    if (variant == 7 && Mp % 128 == 0) {
+        P.tiles_m = Mp / 128; P.tiles_n = Np / 64;
+        hipLaunchKernelGGL((gemm_nt_kernel<128, 64, 4, 1, 2, 32>), dim3(P.tiles_m * P.tiles_n), dim3(256), 0, st, P);
+        WD_CHECK_LAUNCH("gemm_nt 128x64");
+        return 0;
+    }
+    if (variant == 8 || variant == 7) {
+        P.tiles_m = Mp / 64; P.tiles_n = Np / 64;
+        hipLaunchKernelGGL((gemm_nt_kernel<64, 64, 2, 1, 2, 32>), dim3(P.tiles_m * P.tiles_n), dim3(128), 0, st, P);
+        WD_CHECK_LAUNCH("gemm_nt 64x64x2w");
+        return 0;
+    }
     if (variant == 2 || variant == 4) {
         P.tiles_m = Mp / 32; P.tiles_n = Np / 64;
         const dim3 grid(P.tiles_m * P.tiles_n);

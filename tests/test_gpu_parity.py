@@ -206,3 +206,19 @@ def test_index_select_nd():
     assert torch.equal(out, src[idx])
     with pytest.raises(IndexError):
         index_select_ND(src, torch.tensor([[50]], device=DEV))
+
+
+@pytest.mark.parametrize('variant', [1, 2, 3, 4, 5, 6, 7, 8, 9])
+def test_gemm_variants_agree(variant):
+    """Every GEMM tile variant (WdConfig.gemm_variant, tuning knob) computes the same forward."""
+    args = TrainArgs(hidden_size=300, depth=3, bias=True)
+    g = BatchMolGraph(synthetic.make_batch('polymer', 48, 9))
+    enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim())
+    synthetic.fill_parameters(enc, 8)
+    p = {n: t.detach().clone() for n, t in enc.named_parameters()}
+    ref = mpn_ref.encoder_forward(p, g, args)
+    enc = enc.to(DEV).eval()
+    enc._gemm_variant = variant
+    with torch.no_grad():
+        out = enc(g)
+    assert golden_io.normwise(out.cpu().numpy(), ref.numpy()) <= TOL

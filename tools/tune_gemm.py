@@ -21,7 +21,7 @@ for kind, b, H, T in (('polymer', 64, 300, 3), ('polymer', 128, 300, 3), ('zinc'
     enc = MPNEncoder(TrainArgs(hidden_size=H, depth=T), 133, 147)
     initialize_weights(enc)
     enc = enc.to(dev).eval()
-    res = {v: [] for v in (3, 6)}
+    res = {v: [] for v in (3, 9)}
     with torch.no_grad():
         for rnd in range(5):
             for v in res:
