@@ -170,7 +170,7 @@ def main():
                                    f'{a.n_batches} resident batches cycled per rank',
                        'global_batch': a.batch * world, 'depth': a.depth, 'hidden': H,
                        'parallelism': f'dp{world} (independent graphs, no collective in the forward)'},
-            'roofline': {'bound': 'mfma', 'kernel': 'gemm_kernel<64,64,2,2,NT> message passing (mpn.py:110-124)',
+            'roofline': {'bound': 'mfma', 'kernel': 'gemm_nt16_kernel<64,64,2,2>: W_h message update (mpn.py:122-124)',
                          'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                          'frac': achieved / FP32_MFMA_PEAK_TFLOPS if achieved else None, 'traffic': None,
                          'avg_launch_us': avg_launch_s * 1e6, 'flops_per_launch': flops_launch,

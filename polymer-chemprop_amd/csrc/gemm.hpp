@@ -226,6 +226,78 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_nt_kernel(NtParams P) {
 // ---------------------------------------------------------------------------------------------
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+// Row-major float4 epilogue of a BM x BN tile over NT threads: thread t owns float4 column c4 =
+// t % (BN/4) of rows t / (BN/4) + p * (NT*4/BN).  Requires ld % 4 == 0 and 16-byte aligned
+// resid / Z / Y (checked by the launcher).
+template <int BM, int BN, int NT>
+struct EpiPrefetch {
+    static constexpr int C4 = BN / 4, RS = NT / C4, NP = BM / RS;
+    float4 resid[NP];
+    float4 bias;
+    __device__ __forceinline__ void load(const Epi &E, int m0, int n0, int M, int N) {
+        const int t = threadIdx.x, c = n0 + (t % C4) * 4;
+        bias = f4zero();
+        if (E.kind == EPI_ACT && E.bias && c < N) bias = ld4(E.bias + c);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            const int i = m0 + t / C4 + p * RS;
+            resid[p] = (E.kind == EPI_ACT && E.resid && i < M && c < N) ? ld4(E.resid + (size_t)i * E.ld + c)
+                                                                       : f4zero();
+        }
+    }
+};
+
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void epilogue_v4(const Epi &E, const float *C, int ldc, int m0, int n0, int M, int N,
+                                            const EpiPrefetch<BM, BN, NT> &ep) {
+    using EP = EpiPrefetch<BM, BN, NT>;
+    const int t = threadIdx.x, cl = (t % EP::C4) * 4, j = n0 + cl;
+    if (j >= N) return;
+    const float slope = (E.kind == EPI_ACT && E.act == ACT_PRELU) ? E.slope[0] : 0.f;
+#pragma unroll
+    for (int p = 0; p < EP::NP; ++p) {
+        const int rl = t / EP::C4 + p * EP::RS, i = m0 + rl;
+        if (i >= M) continue;
+        const float4 v = ld4(C + rl * ldc + cl);
+        const size_t o = (size_t)i * E.ld + j;
+        float vv[4] = {v.x, v.y, v.z, v.w};
+        float out[4];
+        if (E.kind == EPI_ACT) {
+            const float bb[4] = {ep.bias.x, ep.bias.y, ep.bias.z, ep.bias.w};
+            const float rr[4] = {ep.resid[p].x, ep.resid[p].y, ep.resid[p].z, ep.resid[p].w};
+            float z[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                z[q] = vv[q] + bb[q] + rr[q];
+                float y = act_fwd(E.act, z[q], slope);
+                if (E.p_drop > 0.f) y *= dropout_scale(E.seed, E.layer, i, j + q, E.p_drop);
+                out[q] = y;
+            }
+            if (j + 4 <= N) {
+                if (E.Z) st4(E.Z + o, make_float4(z[0], z[1], z[2], z[3]));
+                st4(E.Y + o, make_float4(out[0], out[1], out[2], out[3]));
+            } else {
+                for (int q = 0; q < N - j; ++q) {
+                    if (E.Z) E.Z[o + q] = z[q];
+                    E.Y[o + q] = out[q];
+                }
+            }
+        } else {
+            if (j + 4 <= N) {
+                float4 r = v;
+                if (E.accumulate) {
+                    const float4 y0 = ld4(E.Y + o);
+                    r.x += y0.x; r.y += y0.y; r.z += y0.z; r.w += y0.w;
+                }
+                st4(E.Y + o, r);
+            } else {
+                for (int q = 0; q < N - j; ++q) E.Y[o + q] = E.accumulate ? E.Y[o + q] + vv[q] : vv[q];
+            }
+        }
+    }
+}
+
+
 template <int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_nt16_kernel(NtParams P) {
     constexpr int NT = 64 * WM * WN;
@@ -243,6 +315,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_nt16_kernel(NtParams P) {
     const int mt = tile / P.tiles_n, nt = tile % P.tiles_n;
     const int m0 = mt * BM, n0 = nt * BN;
     const int K = P.ka0 + P.ka1;
+    EpiPrefetch<BM, BN, NT> ep;
+    ep.load(P.epi, m0, n0, P.M, P.N);
 
     floatx4 acc[TM][TN];
 #pragma unroll
@@ -326,32 +400,20 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_nt16_kernel(NtParams P) {
     }
     if (kc < nchunks) step(kc, R1, R0);
 
-    const Epi &E = P.epi;
-    const float slope = (E.kind == EPI_ACT && E.act == ACT_PRELU) ? E.slope[0] : 0.f;
+    // epilogue: the C tile goes through LDS (row stride BN + 4: conflict-free for the 16x16 C/D
+    // layout) so that every lane loads resid and stores Z / Y as coalesced float4 (the scalar-store
+    // tail was store-issue bound); resid and bias were prefetched before the K loop.
+    constexpr int LDC = BN + 4;
+    static_assert(BM * LDC <= 2 * STAGE, "C tile must fit in the staging LDS");
 #pragma unroll
     for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < TN; ++b) {
-            const int j = n0 + wj * (BN / WN) + b * 16 + i16;
-            const float bias = (E.kind == EPI_ACT && E.bias) ? E.bias[j] : 0.f;
+        for (int b = 0; b < TN; ++b)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = m0 + wi * (BM / WM) + a * 16 + 4 * g + r;
-                if (i >= P.M || j >= P.N) continue;
-                const size_t o = (size_t)i * E.ld + j;
-                const float v = acc[a][b][r];
-                if (E.kind == EPI_ACT) {
-                    float z = v + bias;
-                    if (E.resid) z += E.resid[o];
-                    if (E.Z) E.Z[o] = z;
-                    float y = act_fwd(E.act, z, slope);
-                    if (E.p_drop > 0.f) y *= dropout_scale(E.seed, E.layer, i, j, E.p_drop);
-                    E.Y[o] = y;
-                } else {
-                    E.Y[o] = E.accumulate ? E.Y[o] + v : v;
-                }
-            }
-        }
+            for (int r = 0; r < 4; ++r)
+                lds[(wi * (BM / WM) + a * 16 + 4 * g + r) * LDC + wj * (BN / WN) + b * 16 + i16] = acc[a][b][r];
+    __syncthreads();
+    epilogue_v4<BM, BN, NT>(P.epi, lds, LDC, m0, n0, P.M, P.N, ep);
 }
 
 // ---------------------------------------------------------------------------------------------

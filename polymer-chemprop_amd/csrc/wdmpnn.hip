@@ -240,6 +240,10 @@ int gemm_nt(const float *a0, int lda0, int ka0, const float *a1, int lda1, int k
     if (variant == 5 && !k64) variant = 3;
     const dim3 blk64(64 * NWM * NWN);
     // 9 = 64x64 with 16x16x4 MFMA (4 independent accumulators per wave)
+    if (variant == 9) {  // float4 epilogue: ld and the resid / Z / Y bases must be 16-byte aligned
+        const uintptr_t al = (uintptr_t)epi.Y | (uintptr_t)epi.Z | (uintptr_t)epi.resid | (uintptr_t)epi.bias;
+        if (epi.ld % 4 || al % 16) variant = 3;
+    }
     if (variant == 9) {
         P.tiles_m = Mp / 64; P.tiles_n = Np / 64;
         hipLaunchKernelGGL((gemm_nt16_kernel<64, 64, 2, 2>), dim3(P.tiles_m * P.tiles_n), dim3(256), 0, st, P);

@@ -94,7 +94,10 @@ def _oracle_vs_hip(graphs, args, seed, desc=None):
     hip = {'output': out.detach().cpu().numpy()}
     hip.update({n: t.grad.cpu().numpy() for n, t in enc.named_parameters() if t.grad is not None})
     res = {}
-    kink = args.activation == 'ReLU' and len(graphs.a_scope) >= 64
+    # activations whose derivative jumps at 0 (ReLU 0|1, LeakyReLU/PReLU 0.1|1, SELU 1.758|1.051):
+    # pre-activations within rounding of 0 land on either side depending on summation order, so
+    # fp32 weight gradients at B >= 64 are ill-conditioned for the reference itself.
+    kink = args.activation in ('ReLU', 'LeakyReLU', 'PReLU', 'SELU') and len(graphs.a_scope) >= 64
     for k, r32 in refs[torch.float32].items():
         assert k in hip, f'missing {k}'
         if k == 'output':
