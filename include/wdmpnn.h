@@ -127,7 +127,7 @@ typedef struct WdConfig {
     int32_t prof_slot;      /* first event pair used when prof_pool != NULL                      */
     void   *prof_pool;      /* optional WdEventPool: an event pair is recorded around each message-
                                passing launch (the dominant kernel), pairs prof_slot + t - 1       */
-    int32_t gemm_variant;   /* 0 = default; 1..4 = tile 64x64|32x64 x prefetch depth 1|2 (tuning) */
+    int32_t gemm_variant;   /* 0 = default (9); 1..9 = GEMM tile variants, tuning only */
     int32_t reserved;
 } WdConfig;
 
