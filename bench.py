@@ -80,6 +80,8 @@ def main():
     ap.add_argument('--n-batches', type=int, default=8, help='distinct resident batches cycled per rank')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--fuse-gather', action='store_true', help='experimental fused gather->GEMM (WdConfig.fuse_gather)')
+    ap.add_argument('--variant', type=int, default=0, help='WdConfig.gemm_variant (tuning)')
     a = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -97,6 +99,8 @@ def main():
         g.device_graph(device)
     torch.cuda.synchronize(device)
     enc = make_encoder(args, device)
+    enc._fuse_gather = int(a.fuse_gather)
+    enc._gemm_variant = a.variant
     edges = [g.n_bonds - 1 for g in graphs]
 
     def step(i, prof=None):

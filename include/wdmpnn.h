@@ -56,7 +56,9 @@ enum WdError {
     WD_ERR_UNSUPPORTED = -1003
 };
 
-/* One row-gather list: row r of the gathered operand = sum_{e=ptr[r]}^{ptr[r+1]-1} coef[e] * src[idx[e]]. */
+/* One row-gather list: row r of the gathered operand = sum_{e=ptr[r]}^{ptr[r+1]-1} coef[e] * src[idx[e]].
+ * idx and coef must be readable (any value) for 4 entries past ptr[rows]: the fused kernels fetch the
+ * first four entries of a row unconditionally and discard the ones past its end. */
 typedef struct WdCsr {
     const int32_t *ptr;   /* [rows + 1] */
     const int32_t *idx;   /* [ptr[rows]] source row ids */
@@ -128,7 +130,9 @@ typedef struct WdConfig {
     void   *prof_pool;      /* optional WdEventPool: an event pair is recorded around each message-
                                passing launch (the dominant kernel), pairs prof_slot + t - 1       */
     int32_t gemm_variant;   /* 0 = default (9); 1..9 = GEMM tile variants, tuning only */
-    int32_t reserved;
+    int32_t fuse_gather;    /* 0 = separate gather + GEMM kernels (default, fastest measured);
+                               1 = gather fused into the GEMM's A-panel build (gemm_fused_kernel,
+                               experimental: DESIGN.md §4)                                          */
 } WdConfig;
 
 /* Gradients (device, caller-zeroed NOT required: every pointer is fully overwritten). NULL = skip. */

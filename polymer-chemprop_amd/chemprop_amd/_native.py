@@ -53,7 +53,7 @@ class WdConfig(Structure):
     _fields_ = [('depth', c_int32), ('undirected', c_int32), ('activation', c_int32), ('aggregation', c_int32),
                 ('aggregation_norm', c_float), ('dropout', c_float), ('seed', c_uint64),
                 ('save_for_backward', c_int32), ('prof_slot', c_int32), ('prof_pool', c_void_p),
-                ('gemm_variant', c_int32), ('reserved', c_int32)]
+                ('gemm_variant', c_int32), ('fuse_gather', c_int32)]
 
 
 class WdGrads(Structure):

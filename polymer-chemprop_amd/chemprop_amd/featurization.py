@@ -53,6 +53,9 @@ def _round_up(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
 
+CSR_PAD = 4  # WdCsr: idx / coef readable 4 entries past the end (branch-free first-4 fetch)
+
+
 class Csr:
     """Row-gather list: row r = sum_{e in [ptr[r], ptr[r+1])} coef[e] * source[idx[e]]."""
 
@@ -299,8 +302,9 @@ class BatchMolGraph:
         csrs = [('msg', msg), ('agg', agg), ('msg_t', msg_t), ('agg_t', agg_t)]
         if feat is not None:
             csrs.append(('feat', feat))
-        for name, c in csrs:
-            arrays += [(f'{name}_ptr', c.ptr), (f'{name}_idx', c.idx), (f'{name}_coef', c.coef)]
+        for name, c in csrs:  # idx / coef carry CSR_PAD readable dummy entries past ptr[rows] (header)
+            arrays += [(f'{name}_ptr', c.ptr), (f'{name}_idx', np.concatenate([c.idx, np.zeros(CSR_PAD, np.int32)])),
+                       (f'{name}_coef', np.concatenate([c.coef, np.zeros(CSR_PAD, np.float32)]))]
         offsets, total = {}, 0
         for name, a in arrays:
             offsets[name] = total

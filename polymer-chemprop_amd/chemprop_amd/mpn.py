@@ -121,6 +121,7 @@ class MPNEncoder(nn.Module):
         self._prof = None  # (event pool, first pair): bench.py measurement hook, see WdConfig.prof_pool
         self._pack_cache = None  # (parameter-version key, packed weight buffer)
         self._gemm_variant = 0  # WdConfig.gemm_variant (tuning knob; 0 = automatic)
+        self._fuse_gather = 0  # WdConfig.fuse_gather (1 = experimental fused gather->GEMM kernel)
 
     def _config(self, save: bool) -> _native.WdConfig:
         c = _native.WdConfig()
@@ -138,6 +139,7 @@ class MPNEncoder(nn.Module):
         if self._prof is not None:
             c.prof_pool, c.prof_slot = self._prof
         c.gemm_variant = self._gemm_variant
+        c.fuse_gather = self._fuse_gather
         return c
 
     def forward(self, mol_graph: BatchMolGraph, atom_descriptors_batch: List[np.ndarray] = None) -> torch.FloatTensor:

@@ -186,19 +186,30 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(ActBwd P) {
 //   plain:      segment s with dst cols [dc0_s, dc0_s + K_s): src[r][sc0_s + c - dc0_s]  (r < nrows)
 //   transpose:  src[c][sc0_0 + r]  for r < nrows (= K_0 source cols), c < K_0 (source rows)
 // ---------------------------------------------------------------------------------------------
+//   frag:       same values as plain, stored in the MFMA-fragment order of gemm_fused_kernel:
+//               [rows_p/64][cols_p/32][4 tiles][2 halves][64 lanes][4], lane (i, g) of tile b,
+//               half h holding row 64w + 16b + i, cols 32kc + 8g + 4h .. +3 (one 1 KB contiguous
+//               global_load_dwordx4 per wave per tile-half)
 struct PackJob {
     float *dst; int rows_p, cols_p;
     const float *src; int ld_src;
-    int transpose, nrows, nseg;
+    int transpose, frag, nrows, nseg;
     int dc0[2], sc0[2], K[2];
 };
-struct PackJobs { PackJob j[12]; int n; };
+struct PackJobs { PackJob j[16]; int n; };
 
 __global__ __launch_bounds__(256) void pack_kernel(PackJobs J) {
     const PackJob &P = J.j[blockIdx.y];
     const size_t total = (size_t)P.rows_p * P.cols_p;
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
-        const int r = (int)(t / P.cols_p), c = (int)(t % P.cols_p);
+        int r = (int)(t / P.cols_p), c = (int)(t % P.cols_p);
+        if (P.frag) {
+            const int lane = (int)(t >> 2) & 63, h = (int)(t >> 8) & 1, b = (int)(t >> 9) & 3;
+            const size_t rest = t >> 11;
+            const int nck = P.cols_p / 32, kc = (int)(rest % nck), w = (int)(rest / nck);
+            r = 64 * w + 16 * b + (lane & 15);
+            c = 32 * kc + 8 * (lane >> 4) + 4 * h + (int)(t & 3);
+        }
         float v = 0.f;
         if (P.src && r < P.nrows) {
             if (P.transpose) {

@@ -25,6 +25,7 @@
 #include <string>
 #include <vector>
 
+#include "fused.hpp"
 #include "gemm.hpp"
 #include "kernels.hpp"
 #include "wdmpnn.h"
@@ -115,6 +116,7 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
 // ------------------------------------------------------------------------------------------------
 struct PackLayout {
     size_t Wi = 0, bi = 0, Wh = 0, bh = 0, Wo = 0, bo = 0, Wd = 0, bd = 0, WhT = 0, WoT = 0, WdT = 0, total = 0;
+    size_t WiF = 0, WhF = 0, WoF = 0;  // fragment-order copies for gemm_fused_kernel
 };
 
 PackLayout pack_layout(const Dims &D) {
@@ -129,6 +131,9 @@ PackLayout pack_layout(const Dims &D) {
     L.bo = take(D.Hk);
     L.WhT = take((size_t)D.Hk * D.Hk);
     L.WoT = take((size_t)D.Hk * D.Hk);
+    L.WiF = take((size_t)D.Hk * D.Kink);
+    L.WhF = take((size_t)D.Hk * D.ldx);
+    L.WoF = take((size_t)D.Hk * D.Ko);
     if (D.desc) {
         L.Wd = take((size_t)D.Hdk * D.Kd);
         L.bd = take(D.Hdk);
@@ -175,6 +180,13 @@ int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
     // transposes for dX = dZ W_h[:, :H] and dA = dZo W_o[:, Fa:]
     add(job_transpose(F(L.WhT), D.Hk, D.Hk, p->W_h, D.atom ? H + D.Fb : H, 0, H, H));
     add(job_transpose(F(L.WoT), D.Hk, D.Hk, p->W_o, D.Fa + H, D.Fa, H, H));
+    // fragment-order copies of W_i / W_h / W_o (gemm_fused_kernel's B stream)
+    for (int f = 0; f < 3; ++f) {
+        PackJob j = J.j[f == 0 ? 0 : f == 1 ? 2 : 4];
+        j.dst = F(f == 0 ? L.WiF : f == 1 ? L.WhF : L.WoF);
+        j.frag = 1;
+        add(j);
+    }
     if (D.desc) {
         add(job_plain(F(L.Wd), D.Hdk, D.Kd, p->W_d, D.Hd, D.Hd, {{0, 0, H}, {D.Hk, H, D.d}}));
         add(job_plain(F(L.bd), 1, D.Hdk, p->b_d, D.Hd, 1, {{0, 0, D.Hd}}));
@@ -363,6 +375,56 @@ int gather(const float *src, int ld_src, int K, const WdCsr &csr, const int32_t 
     return 0;
 }
 
+FSeg fseg_dense(const float *src, int ld, int K, float *xout = nullptr, int ld_xout = 0) {
+    FSeg s{};
+    s.src = src; s.ld = ld; s.K = K; s.xout = xout; s.ld_xout = ld_xout;
+    return s;
+}
+
+FSeg fseg_gather(const float *src, int ld, int K, const WdCsr &csr, const int32_t *sym_rev, float *xout, int ld_xout) {
+    FSeg s{};
+    s.src = src; s.ld = ld; s.K = K; s.ptr = csr.ptr; s.idx = csr.idx; s.coef = csr.coef; s.sym_rev = sym_rev;
+    s.xout = xout; s.ld_xout = ld_xout;
+    return s;
+}
+
+constexpr size_t FUSED_LDS_MAX = 160 * 1024;
+
+size_t fused_lds_bytes(int K, int Np) { return (size_t)FP_ROWS * (std::max(K, Np) + 4) * 4; }
+
+// Can gemm_fused take this layer?  N = one wave per 64 columns (<= 512 threads), the panel fits
+// in LDS, float4-aligned epilogue.
+bool fused_eligible(int K, int Np, int ldb, const Epi &epi) {
+    const uintptr_t al = (uintptr_t)epi.Y | (uintptr_t)epi.Z | (uintptr_t)epi.resid | (uintptr_t)epi.bias;
+    return Np % 64 == 0 && Np <= 512 && K % BK == 0 && fused_lds_bytes(K, Np) <= FUSED_LDS_MAX && ldb % 4 == 0 &&
+           ldb == K && epi.ld % 4 == 0 && al % 16 == 0;
+}
+
+int gemm_fused(const FSeg &s0, const FSeg *s1, int rows, const float *b, int ldb, int Mp, int Np, const Epi &epi,
+               hipStream_t st) {
+    if (Mp <= 0) return 0;
+    FusedP P{};
+    P.seg[0] = s0; P.nseg = 1;
+    if (s1) { P.seg[1] = *s1; P.nseg = 2; }
+    const int K = s0.K + (s1 ? s1->K : 0);
+    if (Mp % FP_ROWS || !fused_eligible(K, Np, ldb, epi))
+        return fail(WD_ERR_SHAPE, "gemm_fused: ineligible shape (Mp %d Np %d K %d)", Mp, Np, K);
+    for (int i = 0; i < P.nseg; ++i)
+        if (P.seg[i].K % BK || P.seg[i].ld % 4 || (P.seg[i].xout && P.seg[i].ld_xout % 4))
+            return fail(WD_ERR_SHAPE, "gemm_fused: unaligned segment %d", i);
+    P.rows = rows; P.b = b; P.ldb = ldb; P.M = Mp; P.N = Np; P.epi = epi;
+    static bool lds_attr = false;
+    if (!lds_attr) {
+        if (hipFuncSetAttribute((const void *)gemm_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)FUSED_LDS_MAX) != hipSuccess)
+            return fail(WD_ERR_ARG, "hipFuncSetAttribute(gemm_fused_kernel) failed");
+        lds_attr = true;
+    }
+    hipLaunchKernelGGL(gemm_fused_kernel, dim3(Mp / FP_ROWS), dim3(Np), fused_lds_bytes(K, Np), st, P);
+    WD_CHECK_LAUNCH("gemm_fused");
+    return 0;
+}
+
 ReadoutP readout_params(const WdGraph *g, const WdParams *p, const WdConfig *c, const float *h, int ldh, int ncols,
                         float *out) {
     ReadoutP R{};
@@ -526,39 +588,63 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
     auto W = [&](size_t off) { return (const float *)(pk + off); };
     const int Hk = D.Hk;
 
+    const bool fuse = c->fuse_gather != 0;
+
     // L0: input layer (mpn.py:92-97)
     {
         const float *a = D.atom ? g->f_atoms : g->f_bonds;
         const int lda = D.atom ? g->ld_atoms : g->ld_bonds;
-        WD_TRY(gemm_nt(a, lda, D.Kink, nullptr, 0, 0, W(PL.Wi), D.Kink, D.Rp, Hk,
-                       epi_act(c->activation, p->prelu, W(PL.bi), nullptr, F(L.Z[0]), F(L.M[0]), Hk, c, 0), st,
-                       c->gemm_variant));
+        const Epi e = epi_act(c->activation, p->prelu, W(PL.bi), nullptr, F(L.Z[0]), F(L.M[0]), Hk, c, 0);
+        if (fuse && fused_eligible(D.Kink, Hk, D.Kink, e))
+            WD_TRY(gemm_fused(fseg_dense(a, lda, D.Kink), nullptr, D.R, W(PL.WiF), D.Kink, D.Rp, Hk, e, st));
+        else
+            WD_TRY(gemm_nt(a, lda, D.Kink, nullptr, 0, 0, W(PL.Wi), D.Kink, D.Rp, Hk, e, st, c->gemm_variant));
     }
-    // L1..T-1: message passing (mpn.py:100-124)
+    // L1..T-1: message passing (mpn.py:100-124): X_t = gather(M_{t-1}) [| bond features], then
+    // M_t = act(inp + X_t W_h^T (+ b_h)) -- one fused launch, or gather + GEMM
     int cur = 0;
     for (int t = 1; t < D.T; ++t) {
         const int prev = D.save ? t - 1 : cur;
         const int next = D.save ? t : 1 - cur;
         float *Xt = F(L.X[D.save ? t - 1 : 0]);
-        WD_TRY(gather(F(L.M[prev]), Hk, Hk, g->msg_gather, D.undirected ? g->b2revb : nullptr, Xt, D.ldx, D.R, D.Rp,
-                      st));
-        if (D.atom)
-            WD_TRY(gather(g->f_bonds, g->ld_bonds, D.Fbk, g->bond_feat_gather, nullptr, Xt + Hk, D.ldx, D.R, D.Rp, st));
         float *Zt = D.save ? F(L.Z[t]) : nullptr;
+        const Epi e = epi_act(c->activation, p->prelu, W(PL.bh), F(L.Z[0]), Zt, F(L.M[next]), Hk, c, t);
+        const int32_t *sym = D.undirected ? g->b2revb : nullptr;
         WD_TRY(record_prof(c, t - 1, 0, st));
-        WD_TRY(gemm_nt(Xt, D.ldx, D.ldx, nullptr, 0, 0, W(PL.Wh), D.ldx, D.Rp, Hk,
-                       epi_act(c->activation, p->prelu, W(PL.bh), F(L.Z[0]), Zt, F(L.M[next]), Hk, c, t), st,
-                       c->gemm_variant));
+        if (fuse && fused_eligible(D.ldx, Hk, D.ldx, e)) {
+            const FSeg s0 = fseg_gather(F(L.M[prev]), Hk, Hk, g->msg_gather, sym, D.save ? Xt : nullptr, D.ldx);
+            if (D.atom) {
+                const FSeg s1 = fseg_gather(g->f_bonds, g->ld_bonds, D.Fbk, g->bond_feat_gather, nullptr,
+                                           D.save ? Xt + Hk : nullptr, D.ldx);
+                WD_TRY(gemm_fused(s0, &s1, D.R, W(PL.WhF), D.ldx, D.Rp, Hk, e, st));
+            } else {
+                WD_TRY(gemm_fused(s0, nullptr, D.R, W(PL.WhF), D.ldx, D.Rp, Hk, e, st));
+            }
+        } else {
+            WD_TRY(gather(F(L.M[prev]), Hk, Hk, g->msg_gather, sym, Xt, D.ldx, D.R, D.Rp, st));
+            if (D.atom)
+                WD_TRY(gather(g->f_bonds, g->ld_bonds, D.Fbk, g->bond_feat_gather, nullptr, Xt + Hk, D.ldx, D.R, D.Rp,
+                              st));
+            WD_TRY(gemm_nt(Xt, D.ldx, D.ldx, nullptr, 0, 0, W(PL.Wh), D.ldx, D.Rp, Hk, e, st, c->gemm_variant));
+        }
         WD_TRY(record_prof(c, t - 1, 1, st));
         cur = next;
     }
     const float *M_last = F(L.M[D.save ? D.T - 1 : cur]);
-    // LT: atom hidden states (mpn.py:126-134)
-    WD_TRY(gather(M_last, Hk, Hk, g->atom_gather, nullptr, F(L.A), Hk, D.Va, D.Vap, st));
-    WD_TRY(gemm_nt(g->f_atoms, g->ld_atoms, D.Fak, F(L.A), Hk, Hk, W(PL.Wo), D.Ko, D.Vap, Hk,
-                   epi_act(c->activation, p->prelu, W(PL.bo), nullptr, D.save ? F(L.Zo) : nullptr, F(L.h), Hk, c,
-                           D.T),
-                   st, c->gemm_variant));
+    // LT: atom hidden states (mpn.py:126-134): h = act([f_atoms | gather(M)] W_o^T + b_o)
+    {
+        const Epi e = epi_act(c->activation, p->prelu, W(PL.bo), nullptr, D.save ? F(L.Zo) : nullptr, F(L.h), Hk, c,
+                              D.T);
+        if (fuse && fused_eligible(D.Ko, Hk, D.Ko, e)) {
+            const FSeg s0 = fseg_dense(g->f_atoms, g->ld_atoms, D.Fak);
+            const FSeg s1 = fseg_gather(M_last, Hk, Hk, g->atom_gather, nullptr, D.save ? F(L.A) : nullptr, Hk);
+            WD_TRY(gemm_fused(s0, &s1, D.Va, W(PL.WoF), D.Ko, D.Vap, Hk, e, st));
+        } else {
+            WD_TRY(gather(M_last, Hk, Hk, g->atom_gather, nullptr, F(L.A), Hk, D.Va, D.Vap, st));
+            WD_TRY(gemm_nt(g->f_atoms, g->ld_atoms, D.Fak, F(L.A), Hk, Hk, W(PL.Wo), D.Ko, D.Vap, Hk, e, st,
+                           c->gemm_variant));
+        }
+    }
     const float *hfin = F(L.h);
     int ldfin = Hk;
     // LT+1: atom descriptors layer (mpn.py:136-143): Linear + dropout, no activation

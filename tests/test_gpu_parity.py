@@ -211,9 +211,10 @@ def test_index_select_nd():
         index_select_ND(src, torch.tensor([[50]], device=DEV))
 
 
-@pytest.mark.parametrize('variant', [1, 2, 3, 4, 5, 6, 7, 8, 9])
-def test_gemm_variants_agree(variant):
-    """Every GEMM tile variant (WdConfig.gemm_variant, tuning knob) computes the same forward."""
+@pytest.mark.parametrize('variant,fuse', [(v, 0) for v in range(1, 10)] + [(0, 0), (0, 1)])
+def test_gemm_variants_agree(variant, fuse):
+    """Every GEMM tile variant (WdConfig.gemm_variant) and both the fused gather->GEMM and the separate
+    gather + GEMM paths (WdConfig.fuse_gather) compute the same forward."""
     args = TrainArgs(hidden_size=300, depth=3, bias=True)
     g = BatchMolGraph(synthetic.make_batch('polymer', 48, 9))
     enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim())
@@ -222,6 +223,29 @@ def test_gemm_variants_agree(variant):
     ref = mpn_ref.encoder_forward(p, g, args)
     enc = enc.to(DEV).eval()
     enc._gemm_variant = variant
+    enc._fuse_gather = fuse
     with torch.no_grad():
         out = enc(g)
     assert golden_io.normwise(out.cpu().numpy(), ref.numpy()) <= TOL
+
+
+@pytest.mark.parametrize('extra', [dict(bias=True), dict(undirected=True, activation='tanh'),
+                                   dict(atom_messages=True, bias=True, activation='ELU')])
+def test_fused_and_unfused_paths_agree_in_training(extra):
+    """Forward and all parameter gradients of the fused gather->GEMM path equal the separate-kernel path
+    (same accumulation order per element: differences only from the GEMM tile's summation order)."""
+    args = TrainArgs(hidden_size=128, depth=3, **extra)
+    g = BatchMolGraph(synthetic.make_batch('polymer', 24, 77))
+    res = []
+    for fuse in (1, 0):
+        enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim(atom_messages=args.atom_messages))
+        synthetic.fill_parameters(enc, 3)
+        enc = enc.to(DEV)
+        enc._fuse_gather = fuse
+        out = enc(g)
+        R = torch.randn(out.shape, generator=torch.Generator().manual_seed(1)).to(DEV)
+        (out * R).sum().backward()
+        res.append({'output': out.detach().cpu().numpy(),
+                    **{n: t.grad.cpu().numpy() for n, t in enc.named_parameters() if t.grad is not None}})
+    for k in res[0]:
+        assert golden_io.normwise(res[0][k], res[1][k]) <= TOL, k
