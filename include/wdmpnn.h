@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define WDMPNN_ABI_VERSION 1
+#define WDMPNN_ABI_VERSION 2
 
 enum WdActivation {     /* nn_utils.py:70-99 get_activation_function */
     WD_ACT_RELU = 0, WD_ACT_LEAKY_RELU = 1, WD_ACT_PRELU = 2, WD_ACT_TANH = 3,
@@ -57,8 +57,8 @@ enum WdError {
 };
 
 /* One row-gather list: row r of the gathered operand = sum_{e=ptr[r]}^{ptr[r+1]-1} coef[e] * src[idx[e]].
- * idx and coef must be readable (any value) for 4 entries past ptr[rows]: the fused kernels fetch the
- * first four entries of a row unconditionally and discard the ones past its end. */
+ * idx and coef must be readable (any value) for 8 entries past ptr[rows]: the gather kernels fetch the
+ * first eight entries of a row unconditionally and discard the ones past its end. */
 typedef struct WdCsr {
     const int32_t *ptr;   /* [rows + 1] */
     const int32_t *idx;   /* [ptr[rows]] source row ids */
@@ -97,6 +97,11 @@ typedef struct WdGraph {
     const float *atom_desc; /* [n_atoms, round32(desc_dim)] (row 0 zero pad) or NULL */
     int32_t desc_dim;
     int32_t atom_messages;  /* 1 = atom-message mode (mpn.py:47-53, 93-94, 104-108) */
+    /* Optional bf16x3 plane tiles of f_atoms / f_bonds (wdmpnn_split_planes over all padded rows and
+     * ld_atoms / ld_bonds columns), made once per packed graph: the exact split-plane form the bf16x6
+     * GEMMs read.  NULL: those GEMMs split the fp32 features in the kernel instead. */
+    const void *f_atoms_x6;
+    const void *f_bonds_x6;
 } WdGraph;
 
 /* nn.Module parameters of MPNEncoder (mpn.py:17-64); all device pointers, row-major like nn.Linear. */
@@ -129,7 +134,9 @@ typedef struct WdConfig {
     int32_t prof_slot;      /* first event pair used when prof_pool != NULL                      */
     void   *prof_pool;      /* optional WdEventPool: an event pair is recorded around each message-
                                passing launch (the dominant kernel), pairs prof_slot + t - 1       */
-    int32_t gemm_variant;   /* 0 = default (9); 1..9 = GEMM tile variants, tuning only */
+    int32_t gemm_variant;   /* 0 = default; 9 = f32-MFMA GEMMs; 10 = bf16x6 split GEMMs on plane tiles
+                               (gathers emit plane tiles); 11..14 = bf16x6 with in-kernel operand split;
+                               1..8 = older f32 tile variants (tuning only)           */
     int32_t fuse_gather;    /* 0 = separate gather + GEMM kernels (default, fastest measured);
                                1 = gather fused into the GEMM's A-panel build (gemm_fused_kernel,
                                experimental: DESIGN.md §4)                                          */
@@ -169,6 +176,13 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c,
 int wdmpnn_event_pool_create(int32_t n_pairs, void **pool);
 int wdmpnn_event_pool_destroy(void *pool);
 int wdmpnn_event_pool_elapsed_ms(void *pool, int32_t first, int32_t count, float *total_ms);
+
+/* bf16x3 plane tiles of the first kp columns of an fp32 [rows, ld] matrix (rows % 64 == 0,
+ * kp % 32 == 0, ld >= kp, ld % 4 == 0): the layout of WdGraph.f_atoms_x6 / f_bonds_x6.  The planes hold
+ * every fp32 value exactly (x = h + m + l).  plane_bytes = rows * kp * 6. */
+int wdmpnn_plane_bytes(int32_t rows, int32_t kp, size_t *bytes);
+int wdmpnn_split_planes(const float *src, int32_t ld, int32_t rows, int32_t kp, void *dst, size_t dst_bytes,
+                        void *stream);
 
 /* index_select_ND (nn_utils.py:50-67): out[i, :] = src[index[i], :], row_len floats per row.
  * Indices are int64 like the reference's LongTensor; out-of-range indices are an error checked by

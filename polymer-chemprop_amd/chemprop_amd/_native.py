@@ -21,12 +21,13 @@ LIB_PATH = os.environ.get('WDMPNN_LIB', os.path.join(HERE, 'libwdmpnn.so'))
 ACTIVATIONS = {'ReLU': 0, 'LeakyReLU': 1, 'PReLU': 2, 'tanh': 3, 'SELU': 4, 'ELU': 5}
 ACT_IDENTITY = 6
 AGGREGATIONS = {'mean': 0, 'sum': 1, 'norm': 2}
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace_bytes',
                     'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
                     'wdmpnn_index_select_rows', 'wdmpnn_event_pool_create', 'wdmpnn_event_pool_destroy',
-                    'wdmpnn_event_pool_elapsed_ms', 'wdmpnn_packed_params_bytes', 'wdmpnn_pack_params')
+                    'wdmpnn_event_pool_elapsed_ms', 'wdmpnn_packed_params_bytes', 'wdmpnn_pack_params',
+                    'wdmpnn_plane_bytes', 'wdmpnn_split_planes')
 
 
 class WdCsr(Structure):
@@ -40,7 +41,8 @@ class WdGraph(Structure):
                 ('mol_size', c_void_p), ('degree_of_polym', c_void_p),
                 ('msg_gather', WdCsr), ('bond_feat_gather', WdCsr), ('atom_gather', WdCsr), ('b2revb', c_void_p),
                 ('msg_gather_t', WdCsr), ('bond_feat_gather_t', WdCsr), ('atom_gather_t', WdCsr),
-                ('atom_desc', c_void_p), ('desc_dim', c_int32), ('atom_messages', c_int32)]
+                ('atom_desc', c_void_p), ('desc_dim', c_int32), ('atom_messages', c_int32),
+                ('f_atoms_x6', c_void_p), ('f_bonds_x6', c_void_p)]
 
 
 class WdParams(Structure):
@@ -90,12 +92,14 @@ def lib() -> ctypes.CDLL:
                                              POINTER(c_size_t)]
     L.wdmpnn_pack_params.argtypes = [POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig), c_void_p, c_size_t,
                                      c_void_p]
+    L.wdmpnn_plane_bytes.argtypes = [c_int32, c_int32, POINTER(c_size_t)]
+    L.wdmpnn_split_planes.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_size_t, c_void_p]
     L.wdmpnn_event_pool_create.argtypes = [c_int32, POINTER(c_void_p)]
     L.wdmpnn_event_pool_destroy.argtypes = [c_void_p]
     L.wdmpnn_event_pool_elapsed_ms.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_float)]
     for fn in ('wdmpnn_packed_params_bytes', 'wdmpnn_pack_params', 'wdmpnn_event_pool_create', 'wdmpnn_event_pool_destroy', 'wdmpnn_event_pool_elapsed_ms',
                'wdmpnn_workspace_bytes', 'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
-               'wdmpnn_index_select_rows'):
+               'wdmpnn_index_select_rows', 'wdmpnn_plane_bytes', 'wdmpnn_split_planes'):
         getattr(L, fn).restype = c_int
     v = L.wdmpnn_abi_version()
     if v != ABI_VERSION:

@@ -18,6 +18,7 @@ arrays with 16-byte aligned row strides, all in ONE device buffer filled by one 
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
@@ -53,7 +54,7 @@ def _round_up(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
 
-CSR_PAD = 4  # WdCsr: idx / coef readable 4 entries past the end (branch-free first-4 fetch)
+CSR_PAD = 8  # WdCsr: idx / coef readable 8 entries past the end (branch-free first-8 fetch)
 
 
 class Csr:
@@ -337,6 +338,16 @@ class BatchMolGraph:
         s.b2revb = P('b2revb')
         s.atom_desc, s.desc_dim = 0, 0
         s.atom_messages = int(bool(atom_messages))
+        if device.type == 'cuda':  # bf16x3 plane tiles of the features for the split GEMMs (exact copies)
+            L = _native.lib()
+            for name, rows, ld in (('f_atoms', fa_p.shape[0], lda), ('f_bonds', fb_p.shape[0], ldb)):
+                nbytes = ctypes.c_size_t()
+                _native.check(L.wdmpnn_plane_bytes(rows, ld, ctypes.byref(nbytes)), 'plane bytes')
+                planes = torch.empty(max(nbytes.value, 256), dtype=torch.uint8, device=device)
+                _native.check(L.wdmpnn_split_planes(P(name), ld, rows, ld, planes.data_ptr(), nbytes.value,
+                                                    _native.current_stream(device)), f'{name} planes')
+                views[name + '_x6'] = planes
+                setattr(s, name + '_x6', planes.data_ptr())
         dg = DeviceGraph(buf, views, s)
         dg.host_csr = dict(csrs)
         dg.n_edges = self.n_bonds - 1

@@ -14,7 +14,7 @@
 //   * the epilogue (bias + residual + activation + dropout) goes through LDS for float4 stores.
 // MFMA: v_mfma_f32_16x16x4_f32 (exact fp32), wave = 16 rows x 64 cols = 4 independent accumulators;
 // lane (i = l&15, g = l>>4) supplies k = 8g + s at step s of a 32-chunk (two b128 reads per operand).
-// Accumulation order per gathered element is the CSR order, identical to gather_rows_kernel.
+// Accumulation order per gathered element is the CSR order, identical to gather8_kernel.
 #pragma once
 #include "gemm.hpp"
 

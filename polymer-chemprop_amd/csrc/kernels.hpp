@@ -3,46 +3,98 @@
 // fused activation/gather backward, weight packing and the deterministic slab reduction.
 #pragma once
 #include "common.hpp"
+#include "planes.hpp"
 
 namespace wd {
 
 // ---------------------------------------------------------------------------------------------
-// Row gather:  out[r][c] = sum_{e in [ptr[r], ptr[r+1])} coef[e] * S(idx[e], c),  c < K,  r < rows
+// Row gather (the padded index_select_ND + weighted sum of mpn.py:112-131 as one CSR list per output
+// row), 8 columns per thread, first G8 CSR entries fetched together:
+//   out[r][c..c+7] = sum_{e in [ptr[r], ptr[r+1])} coef[e] * S(idx[e], c..c+7)
 //   S(j, c) = src[j][c]  or  (src[j][c] + src[rev[j]][c]) / 2 with sym_rev (mpn.py:101-102)
-// Rows [rows, rows_p) are zero filled (padding of the next GEMM's A operand).
-// One lane per (row, 4 columns): a 1,200-B message row is read by 75 consecutive lanes (coalesced
-// float4); the dependent chain is ptr -> idx -> row, hidden by having every row in flight at once.
+// The idx / coef of entries e0 .. e0+7 are loaded unconditionally (WdCsr lists are readable 8 entries
+// past their end; dead entries point at row 0 and are not added), then all their source rows are
+// loaded at once: a row costs three dependent hops (ptr -> idx -> rows) instead of one per entry.
+// Entries are added in CSR order (fixed order: deterministic, the order of the reference's slot sum).
+// Output: fp32 rows (out) and/or the plane tiles of the next split GEMM (planes, columns
+// pcol0 + c of a [rows_p][kp] plane-tile matrix).  Rows [rows, rows_p) are written as zeros.
 // ---------------------------------------------------------------------------------------------
-struct GatherP {
-    const float *src; int ld_src; int K;
+constexpr int G8 = 8;
+
+struct Gather8P {
+    const float *src; int ld_src; int K;   // K: columns gathered (multiple of 8)
     const int32_t *ptr; const int32_t *idx; const float *coef;
     const int32_t *sym_rev;
     float *out; int ld_out;
+    uint8_t *planes; int kp; int pcol0;
     int rows, rows_p;
 };
 
-__global__ __launch_bounds__(256) void gather_rows_kernel(GatherP P) {
-    const int nq = P.K >> 2;  // K multiple of 4
-    const size_t total = (size_t)P.rows_p * nq;
-    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
-        const int r = (int)(t / nq), c = (int)(t % nq) * 4;
-        float4 acc = f4zero();
-        if (r < P.rows) {
-            const int e0 = P.ptr[r], e1 = P.ptr[r + 1];
-            for (int e = e0; e < e1; ++e) {
-                const int j = P.idx[e];
-                const float w = P.coef ? P.coef[e] : 1.0f;
-                float4 v = ld4(P.src + (size_t)j * P.ld_src + c);
-                if (P.sym_rev) {
-                    const float4 u = ld4(P.src + (size_t)P.sym_rev[j] * P.ld_src + c);
-                    v.x = (v.x + u.x) / 2.0f; v.y = (v.y + u.y) / 2.0f;
-                    v.z = (v.z + u.z) / 2.0f; v.w = (v.w + u.w) / 2.0f;
-                }
-                fma4(acc, w, v);
+__global__ __launch_bounds__(256) void gather8_kernel(Gather8P P) {
+    const int nu = P.K >> 3;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= P.rows_p * nu) return;
+    const int r = t / nu, c = (t % nu) * 8;
+    float4 lo = f4zero(), hi = f4zero();
+    if (r < P.rows) {
+        const int e0 = P.ptr[r], e1 = P.ptr[r + 1];
+        int j[G8];
+        float w[G8];
+#pragma unroll
+        for (int k = 0; k < G8; ++k) {
+            const bool ok = e0 + k < e1;
+            const int jj = P.idx[e0 + k];
+            const float ww = P.coef ? P.coef[e0 + k] : 1.0f;
+            j[k] = ok ? jj : 0;
+            w[k] = ww;
+        }
+        float4 xa[G8], xb[G8];
+#pragma unroll
+        for (int k = 0; k < G8; ++k) {
+            const float *s = P.src + (size_t)j[k] * P.ld_src + c;
+            xa[k] = ld4(s);
+            xb[k] = ld4(s + 4);
+        }
+        if (P.sym_rev) {
+#pragma unroll
+            for (int k = 0; k < G8; ++k) {
+                const float *s = P.src + (size_t)P.sym_rev[j[k]] * P.ld_src + c;
+                const float4 ua = ld4(s), ub = ld4(s + 4);
+                xa[k].x = (xa[k].x + ua.x) / 2.0f; xa[k].y = (xa[k].y + ua.y) / 2.0f;
+                xa[k].z = (xa[k].z + ua.z) / 2.0f; xa[k].w = (xa[k].w + ua.w) / 2.0f;
+                xb[k].x = (xb[k].x + ub.x) / 2.0f; xb[k].y = (xb[k].y + ub.y) / 2.0f;
+                xb[k].z = (xb[k].z + ub.z) / 2.0f; xb[k].w = (xb[k].w + ub.w) / 2.0f;
             }
         }
-        st4(P.out + (size_t)r * P.ld_out + c, acc);
+#pragma unroll
+        for (int k = 0; k < G8; ++k)
+            if (e0 + k < e1) {
+                fma4(lo, w[k], xa[k]);
+                fma4(hi, w[k], xb[k]);
+            }
+        for (int e = e0 + G8; e < e1; ++e) {  // rows with more than G8 entries
+            const int jj = P.idx[e];
+            const float ww = P.coef ? P.coef[e] : 1.0f;
+            const float *s = P.src + (size_t)jj * P.ld_src + c;
+            float4 ya = ld4(s), yb = ld4(s + 4);
+            if (P.sym_rev) {
+                const float *u = P.src + (size_t)P.sym_rev[jj] * P.ld_src + c;
+                const float4 ua = ld4(u), ub = ld4(u + 4);
+                ya.x = (ya.x + ua.x) / 2.0f; ya.y = (ya.y + ua.y) / 2.0f;
+                ya.z = (ya.z + ua.z) / 2.0f; ya.w = (ya.w + ua.w) / 2.0f;
+                yb.x = (yb.x + ub.x) / 2.0f; yb.y = (yb.y + ub.y) / 2.0f;
+                yb.z = (yb.z + ub.z) / 2.0f; yb.w = (yb.w + ub.w) / 2.0f;
+            }
+            fma4(lo, ww, ya);
+            fma4(hi, ww, yb);
+        }
     }
+    if (P.out) {
+        float *o = P.out + (size_t)r * P.ld_out + c;
+        st4(o, lo);
+        st4(o + 4, hi);
+    }
+    if (P.planes) x6_store8(P.planes, P.kp, r, P.pcol0 + c, lo, hi);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -1,0 +1,80 @@
+// planes.hpp — exact three-way bf16 split of fp32 values ("bf16x3 planes") and the plane-tile
+// layout shared by the producers (gathers, weight packer, graph upload) and the split GEMMs.
+//
+// x = h + m + l with h = rne_bf16(x), m = rne_bf16(x - h), l = rne_bf16(x - h - m): both residual
+// subtractions are exact in fp32 and each piece carries 8 significant bits, so the planes hold x to
+// the last fp32 bit (barring bf16 underflow of l below 2^-126).
+//
+// Plane-tile layout of an fp32 matrix [Rp][Kp] (Rp % 64 == 0, Kp % 32 == 0): blocks of 64 rows x 32
+// columns; block (rb, kc) at byte (rb * (Kp / 32) + kc) * X6_BLOCK holds plane p (h, m, l), row r,
+// columns 8u .. 8u+7 (16 bytes) at p * X6_PLANE + 64 r + 16 u.  A GEMM K-chunk of 64 rows is then one
+// contiguous 12 KB block: LDS-DMA copies it 1 KB per wave-instruction (gemm_x6.hpp).
+#pragma once
+#include "common.hpp"
+
+namespace wd {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+// native vector (not HIP's uint4 class: arrays of that in register-staging structs went to scratch)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int X6_BN = 64;                  // GEMM column tile
+constexpr int X6_PLANE = 64 * 64;          // bytes of one plane of a 64-row x 32-column block
+constexpr int X6_BLOCK = 3 * X6_PLANE;     // one plane-tile block (12 KB)
+
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){a, b}, bf16x2v));  // v_cvt_pk_bf16_f32 (RNE)
+}
+__device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+// (a, b) -> three packed bf16 pairs with a = h + m + l (element 0 in the low half)
+__device__ __forceinline__ void split_pair(float a, float b, uint32_t &h, uint32_t &m, uint32_t &l) {
+    h = cvt_pk_bf16(a, b);
+    const float a1 = a - bf_lo(h), b1 = b - bf_hi(h);
+    m = cvt_pk_bf16(a1, b1);
+    const float a2 = a1 - bf_lo(m), b2 = b1 - bf_hi(m);
+    l = cvt_pk_bf16(a2, b2);
+}
+
+// byte offset of 16-byte unit u of row r in a plane image with BK-wide rows (2 BK bytes per row)
+template <int BK>
+__device__ __forceinline__ int x6_off(int r, int u) {
+    if constexpr (BK == 32) return r * 64 + 16 * (u ^ ((r >> 1) & 3));
+    else return r * 128 + 16 * (u ^ (r & 7));
+}
+__device__ __forceinline__ int x6_slot(int r, int u) { return x6_off<32>(r, u); }
+
+__device__ __forceinline__ size_t x6_tile_off(int r, int k, int kp) {  // byte offset of (r, k), plane 0
+    return ((size_t)(r >> 6) * (kp >> 5) + (k >> 5)) * X6_BLOCK + (r & 63) * 64 + 2 * (k & 31);
+}
+
+// write 8 consecutive values v[0..7] of row r, columns k..k+7 (k % 8 == 0) into a plane-tile matrix
+__device__ __forceinline__ void x6_store8(uint8_t *base, int kp, int r, int k, const float4 &lo, const float4 &hi) {
+    uint32_t h[4], m[4], l[4];
+    split_pair(lo.x, lo.y, h[0], m[0], l[0]);
+    split_pair(lo.z, lo.w, h[1], m[1], l[1]);
+    split_pair(hi.x, hi.y, h[2], m[2], l[2]);
+    split_pair(hi.z, hi.w, h[3], m[3], l[3]);
+    uint8_t *d = base + x6_tile_off(r, k, kp);
+    *reinterpret_cast<u32x4 *>(d) = u32x4{h[0], h[1], h[2], h[3]};
+    *reinterpret_cast<u32x4 *>(d + X6_PLANE) = u32x4{m[0], m[1], m[2], m[3]};
+    *reinterpret_cast<u32x4 *>(d + 2 * X6_PLANE) = u32x4{l[0], l[1], l[2], l[3]};
+}
+
+
+// fp32 [rows][ld] (first kp columns) -> plane tiles [rows][kp]; one thread per 8 values
+__global__ __launch_bounds__(256) void split_tiles_kernel(const float *__restrict__ src, int ld, int rows, int kp,
+                                                          uint8_t *__restrict__ dst) {
+    const int q8 = kp >> 3;
+    const size_t total = (size_t)rows * q8;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+        const int r = (int)(t / q8), k = (int)(t % q8) * 8;
+        const float *s = src + (size_t)r * ld + k;
+        x6_store8(dst, kp, r, k, ld4(s), ld4(s + 4));
+    }
+}
+
+}  // namespace wd

@@ -27,6 +27,7 @@
 
 #include "fused.hpp"
 #include "gemm.hpp"
+#include "gemm_x6.hpp"
 #include "kernels.hpp"
 #include "wdmpnn.h"
 
@@ -75,6 +76,7 @@ struct Dims {
     int H, Hk, T, R, Rp, Va, Vap, B, Fa, Fak, Fb, Fbk, d, dk, Hd, Hdk, Kin, Kink;
     int ldx, Ko, Kd;
     bool atom, undirected, save, desc;
+    bool x6;  // plane-tile pipeline: gathers emit bf16x3 plane tiles, GEMMs run gemm_x6g_kernel
 };
 
 int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
@@ -98,6 +100,7 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     D.ldx = D.atom ? D.Hk + D.Fbk : D.Hk;
     D.Ko = D.Fak + D.Hk;
     D.Kd = D.Hk + D.dk;
+    D.x6 = c->gemm_variant == 10 && !D.atom && !c->fuse_gather;
     if (D.atom && D.undirected)
         return fail(WD_ERR_UNSUPPORTED, "undirected with atom_messages (the reference indexes atom messages "
                                         "with b2revb, mpn.py:101-102)");
@@ -117,6 +120,7 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
 struct PackLayout {
     size_t Wi = 0, bi = 0, Wh = 0, bh = 0, Wo = 0, bo = 0, Wd = 0, bd = 0, WhT = 0, WoT = 0, WdT = 0, total = 0;
     size_t WiF = 0, WhF = 0, WoF = 0;  // fragment-order copies for gemm_fused_kernel
+    size_t WiX = 0, WhX = 0, WoX = 0;  // bf16x3 planes for gemm_x6_kernel
 };
 
 PackLayout pack_layout(const Dims &D) {
@@ -134,6 +138,9 @@ PackLayout pack_layout(const Dims &D) {
     L.WiF = take((size_t)D.Hk * D.Kink);
     L.WhF = take((size_t)D.Hk * D.ldx);
     L.WoF = take((size_t)D.Hk * D.Ko);
+    L.WiX = take((size_t)D.Hk * D.Kink * 3 / 2);  // 3 bf16 planes = 1.5 floats per value
+    L.WhX = take((size_t)D.Hk * D.ldx * 3 / 2);
+    L.WoX = take((size_t)D.Hk * D.Ko * 3 / 2);
     if (D.desc) {
         L.Wd = take((size_t)D.Hdk * D.Kd);
         L.bd = take(D.Hdk);
@@ -194,6 +201,15 @@ int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
     }
     hipLaunchKernelGGL(pack_kernel, dim3(64, J.n), dim3(256), 0, st, J);
     WD_CHECK_LAUNCH("pack_params");
+    // bf16x3 plane tiles of the padded W_i / W_h / W_o copies (B operands of gemm_x6g_kernel)
+    const std::array<std::array<size_t, 3>, 3> xs = {{{L.Wi, L.WiX, (size_t)D.Kink}, {L.Wh, L.WhX, (size_t)D.ldx},
+                                                      {L.Wo, L.WoX, (size_t)D.Ko}}};
+    for (const auto &x : xs) {
+        const int kp = (int)x[2];
+        hipLaunchKernelGGL(split_tiles_kernel, dim3(ew_blocks((size_t)D.Hk * kp / 8)), dim3(256), 0, st,
+                           (const float *)(base + x[0]), kp, D.Hk, kp, (uint8_t *)(base + x[1]));
+    }
+    WD_CHECK_LAUNCH("pack_params planes");
     return 0;
 }
 
@@ -224,6 +240,29 @@ int gemm_nt(const float *a0, int lda0, int ka0, const float *a1, int lda1, int k
     if (Mp <= 0 || Np <= 0) return 0;
     if (Mp % NBM || Np % NBN || ka0 % BK || ka1 % BK || ka0 <= 0 || lda0 % 4 || (ka1 && lda1 % 4) || ldb % 4)
         return fail(WD_ERR_SHAPE, "gemm_nt: unpadded operand (Mp %d Np %d ka %d/%d)", Mp, Np, ka0, ka1);
+    // 11-14 = bf16x6 split GEMM with fp32 operands split in the kernel (gemm_x6.hpp):
+    // 11 = 64x64 tile, 12 = 128x64, 13 = 64x64 with 64-wide K chunks, 14 = 128x64 with 64-wide chunks
+    if (variant >= 11 && variant <= 14) {
+        const uintptr_t al = (uintptr_t)epi.Y | (uintptr_t)epi.Z | (uintptr_t)epi.resid | (uintptr_t)epi.bias;
+        if (epi.ld % 4 || al % 16) variant = 9;
+        else if ((variant == 12 || variant == 14) && Mp % 128) variant -= 1;
+        if ((variant == 13 || variant == 14) && (ka0 % 64 || ka1 % 64)) variant -= 2;
+    }
+    if (variant >= 11 && variant <= 14) {
+        X6Params X{};
+        X.a0 = a0; X.lda0 = lda0; X.ka0 = ka0; X.a1 = a1; X.lda1 = lda1; X.ka1 = ka1;
+        X.bf = b; X.ldb = ldb;
+        X.M = Mp; X.N = Np; X.epi = epi; X.tiles_n = Np / X6_BN;
+        const int bm = (variant == 12 || variant == 14) ? 128 : 64;
+        X.tiles_m = Mp / bm;
+        const dim3 grid(X.tiles_m * X.tiles_n), blk(4 * bm);
+        if (variant == 11) hipLaunchKernelGGL((gemm_x6_kernel<64, 32>), grid, blk, 0, st, X);
+        else if (variant == 12) hipLaunchKernelGGL((gemm_x6_kernel<128, 32>), grid, blk, 0, st, X);
+        else if (variant == 13) hipLaunchKernelGGL((gemm_x6_kernel<64, 64>), grid, blk, 0, st, X);
+        else hipLaunchKernelGGL((gemm_x6_kernel<128, 64>), grid, blk, 0, st, X);
+        WD_CHECK_LAUNCH("gemm_x6");
+        return 0;
+    }
     NtParams P{};
     P.a0 = a0; P.lda0 = lda0; P.ka0 = ka0; P.a1 = a1; P.lda1 = lda1; P.ka1 = ka1; P.b = b; P.ldb = ldb;
     P.M = Mp; P.N = Np; P.epi = epi;
@@ -288,6 +327,46 @@ int gemm_nt(const float *a0, int lda0, int ka0, const float *a1, int lda1, int k
         else hipLaunchKernelGGL((gemm_nt_kernel<NBM, NBN, NWM, NWN, 2, 32>), grid, blk64, 0, st, P);
     }
     WD_CHECK_LAUNCH("gemm_nt");
+    return 0;
+}
+
+// C[Mp][Np] = epi([A0 | A1] B^T) with every operand in plane tiles (planes.hpp): A segment i is the
+// first ka_i columns of a [Mp][kp_i] plane-tile matrix, B a [Np][ka0 + ka1] one.
+bool x6g_eligible(const Epi &epi) {
+    const uintptr_t al = (uintptr_t)epi.Y | (uintptr_t)epi.Z | (uintptr_t)epi.resid | (uintptr_t)epi.bias;
+    return epi.ld % 4 == 0 && al % 16 == 0;
+}
+
+int gemm_x6g(const void *a0, int kp0, int ka0, const void *a1, int kp1, int ka1, const void *b, int Mp, int Np,
+             const Epi &epi, hipStream_t st) {
+    if (Mp <= 0 || Np <= 0) return 0;
+    if (Mp % 64 || Np % 64 || ka0 <= 0 || ka0 % 32 || ka1 % 32 || kp0 % 32 || (ka1 && kp1 % 32) || ka0 > kp0 ||
+        ka1 > kp1 || !x6g_eligible(epi))
+        return fail(WD_ERR_SHAPE, "gemm_x6g: operand not in plane tiles (Mp %d Np %d ka %d/%d)", Mp, Np, ka0, ka1);
+    X6PParams X{};
+    X.a0 = (const uint8_t *)a0; X.kp0 = kp0; X.ka0 = ka0;
+    X.a1 = (const uint8_t *)a1; X.kp1 = kp1; X.ka1 = ka1;
+    X.b = (const uint8_t *)b; X.kpb = ka0 + ka1;
+    X.M = Mp; X.N = Np; X.epi = epi; X.tiles_m = Mp / 64; X.tiles_n = Np / X6_BN;
+    hipLaunchKernelGGL(gemm_x6g_kernel<2>, dim3(X.tiles_m * X.tiles_n), dim3(256), 0, st, X);
+    WD_CHECK_LAUNCH("gemm_x6g");
+    return 0;
+}
+
+// gather8_kernel: fp32 rows into out (may be null) and/or plane tiles (planes, columns pcol0.. of a
+// [rows_p][kp] plane-tile matrix; may be null)
+int gather8(const float *src, int ld_src, int K, const WdCsr &csr, const int32_t *sym_rev, float *out, int ld_out,
+            void *planes, int kp, int pcol0, int rows, int rows_p, hipStream_t st) {
+    if (rows_p <= 0 || K <= 0) return 0;
+    if (K % 8 || ld_src % 4 || (out && ld_out % 4) || (planes && (rows_p % 64 || kp % 32 || pcol0 % 32)))
+        return fail(WD_ERR_SHAPE, "gather8: unaligned operand (K %d)", K);
+    Gather8P P{};
+    P.src = src; P.ld_src = ld_src; P.K = K; P.ptr = csr.ptr; P.idx = csr.idx; P.coef = csr.coef;
+    P.sym_rev = sym_rev; P.out = out; P.ld_out = ld_out; P.planes = (uint8_t *)planes; P.kp = kp; P.pcol0 = pcol0;
+    P.rows = rows; P.rows_p = rows_p;
+    const size_t total = (size_t)rows_p * (K / 8);
+    hipLaunchKernelGGL(gather8_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, P);
+    WD_CHECK_LAUNCH("gather8");
     return 0;
 }
 
@@ -363,18 +442,6 @@ int slab_reduce(const TnPlan &tp, const float *slab, int n_rows, std::initialize
     return 0;
 }
 
-int gather(const float *src, int ld_src, int K, const WdCsr &csr, const int32_t *sym_rev, float *out, int ld_out,
-           int rows, int rows_p, hipStream_t st) {
-    if (rows_p <= 0 || K <= 0) return 0;
-    GatherP P{};
-    P.src = src; P.ld_src = ld_src; P.K = K; P.ptr = csr.ptr; P.idx = csr.idx; P.coef = csr.coef;
-    P.sym_rev = sym_rev; P.out = out; P.ld_out = ld_out; P.rows = rows; P.rows_p = rows_p;
-    const size_t total = (size_t)rows_p * (K / 4);
-    hipLaunchKernelGGL(gather_rows_kernel, dim3(ew_blocks(total)), dim3(256), 0, st, P);
-    WD_CHECK_LAUNCH("gather_rows");
-    return 0;
-}
-
 FSeg fseg_dense(const float *src, int ld, int K, float *xout = nullptr, int ld_xout = 0) {
     FSeg s{};
     s.src = src; s.ld = ld; s.K = K; s.xout = xout; s.ld_xout = ld_xout;
@@ -440,6 +507,7 @@ ReadoutP readout_params(const WdGraph *g, const WdParams *p, const WdConfig *c, 
 struct FwdLayout {
     std::vector<size_t> Z, M, X;
     size_t packed = 0, A = 0, Zo = 0, h = 0, Zd = 0, hd = 0, total = 0;
+    size_t Xp = 0, Ap = 0;  // plane tiles of X_t and A (D.x6)
     bool own_pack = false;
 };
 
@@ -455,6 +523,10 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
     if (D.T > 1)
         for (int t = 0; t < (D.save ? D.T - 1 : 1); ++t) L.X.push_back(take((size_t)D.Rp * D.ldx * 4));
     L.A = take(atm);
+    if (D.x6) {
+        if (D.T > 1) L.Xp = take((size_t)D.Rp * D.Hk * 6);
+        L.Ap = take((size_t)D.Vap * D.Hk * 6);
+    }
     if (D.save) L.Zo = take(atm);
     L.h = take(atm);
     if (D.desc) {
@@ -589,6 +661,10 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
     const int Hk = D.Hk;
 
     const bool fuse = c->fuse_gather != 0;
+    const int var = c->gemm_variant;
+    // plane-tile pipeline (D.x6): a GEMM without a plane copy of its A operand splits in the kernel
+    const int var_split = var == 10 ? 12 : var;
+    const char *pkb = pk;
 
     // L0: input layer (mpn.py:92-97)
     {
@@ -597,11 +673,13 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
         const Epi e = epi_act(c->activation, p->prelu, W(PL.bi), nullptr, F(L.Z[0]), F(L.M[0]), Hk, c, 0);
         if (fuse && fused_eligible(D.Kink, Hk, D.Kink, e))
             WD_TRY(gemm_fused(fseg_dense(a, lda, D.Kink), nullptr, D.R, W(PL.WiF), D.Kink, D.Rp, Hk, e, st));
+        else if (D.x6 && g->f_bonds_x6 && x6g_eligible(e))
+            WD_TRY(gemm_x6g(g->f_bonds_x6, g->ld_bonds, D.Kink, nullptr, 0, 0, pkb + PL.WiX, D.Rp, Hk, e, st));
         else
-            WD_TRY(gemm_nt(a, lda, D.Kink, nullptr, 0, 0, W(PL.Wi), D.Kink, D.Rp, Hk, e, st, c->gemm_variant));
+            WD_TRY(gemm_nt(a, lda, D.Kink, nullptr, 0, 0, W(PL.Wi), D.Kink, D.Rp, Hk, e, st, var_split));
     }
     // L1..T-1: message passing (mpn.py:100-124): X_t = gather(M_{t-1}) [| bond features], then
-    // M_t = act(inp + X_t W_h^T (+ b_h)) -- one fused launch, or gather + GEMM
+    // M_t = act(inp + X_t W_h^T (+ b_h))
     int cur = 0;
     for (int t = 1; t < D.T; ++t) {
         const int prev = D.save ? t - 1 : cur;
@@ -620,12 +698,17 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
             } else {
                 WD_TRY(gemm_fused(s0, nullptr, D.R, W(PL.WhF), D.ldx, D.Rp, Hk, e, st));
             }
+        } else if (D.x6 && x6g_eligible(e)) {
+            // X_t as plane tiles (+ fp32 for the weight gradient when training)
+            WD_TRY(gather8(F(L.M[prev]), Hk, Hk, g->msg_gather, sym, D.save ? Xt : nullptr, D.ldx, ws + L.Xp, Hk, 0,
+                           D.R, D.Rp, st));
+            WD_TRY(gemm_x6g(ws + L.Xp, Hk, Hk, nullptr, 0, 0, pkb + PL.WhX, D.Rp, Hk, e, st));
         } else {
-            WD_TRY(gather(F(L.M[prev]), Hk, Hk, g->msg_gather, sym, Xt, D.ldx, D.R, D.Rp, st));
+            WD_TRY(gather8(F(L.M[prev]), Hk, Hk, g->msg_gather, sym, Xt, D.ldx, nullptr, 0, 0, D.R, D.Rp, st));
             if (D.atom)
-                WD_TRY(gather(g->f_bonds, g->ld_bonds, D.Fbk, g->bond_feat_gather, nullptr, Xt + Hk, D.ldx, D.R, D.Rp,
-                              st));
-            WD_TRY(gemm_nt(Xt, D.ldx, D.ldx, nullptr, 0, 0, W(PL.Wh), D.ldx, D.Rp, Hk, e, st, c->gemm_variant));
+                WD_TRY(gather8(g->f_bonds, g->ld_bonds, D.Fbk, g->bond_feat_gather, nullptr, Xt + Hk, D.ldx, nullptr, 0,
+                               0, D.R, D.Rp, st));
+            WD_TRY(gemm_nt(Xt, D.ldx, D.ldx, nullptr, 0, 0, W(PL.Wh), D.ldx, D.Rp, Hk, e, st, var_split));
         }
         WD_TRY(record_prof(c, t - 1, 1, st));
         cur = next;
@@ -639,10 +722,14 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
             const FSeg s0 = fseg_dense(g->f_atoms, g->ld_atoms, D.Fak);
             const FSeg s1 = fseg_gather(M_last, Hk, Hk, g->atom_gather, nullptr, D.save ? F(L.A) : nullptr, Hk);
             WD_TRY(gemm_fused(s0, &s1, D.Va, W(PL.WoF), D.Ko, D.Vap, Hk, e, st));
+        } else if (D.x6 && g->f_atoms_x6 && x6g_eligible(e)) {
+            WD_TRY(gather8(M_last, Hk, Hk, g->atom_gather, nullptr, D.save ? F(L.A) : nullptr, Hk, ws + L.Ap, Hk, 0,
+                           D.Va, D.Vap, st));
+            WD_TRY(gemm_x6g(g->f_atoms_x6, g->ld_atoms, D.Fak, ws + L.Ap, Hk, Hk, pkb + PL.WoX, D.Vap, Hk, e, st));
         } else {
-            WD_TRY(gather(M_last, Hk, Hk, g->atom_gather, nullptr, F(L.A), Hk, D.Va, D.Vap, st));
+            WD_TRY(gather8(M_last, Hk, Hk, g->atom_gather, nullptr, F(L.A), Hk, nullptr, 0, 0, D.Va, D.Vap, st));
             WD_TRY(gemm_nt(g->f_atoms, g->ld_atoms, D.Fak, F(L.A), Hk, Hk, W(PL.Wo), D.Ko, D.Vap, Hk, e, st,
-                           c->gemm_variant));
+                           var_split));
         }
     }
     const float *hfin = F(L.h);
@@ -837,6 +924,26 @@ int wdmpnn_event_pool_elapsed_ms(void *pool, int32_t first, int32_t count, float
         tot += ms;
     }
     *total_ms = (float)tot;
+    return 0;
+}
+
+int wdmpnn_plane_bytes(int32_t rows, int32_t kp, size_t *bytes) {
+    if (!bytes || rows < 0 || kp < 0) return fail(WD_ERR_ARG, "bad plane request");
+    *bytes = (size_t)rows * kp * 6;
+    return 0;
+}
+
+int wdmpnn_split_planes(const float *src, int32_t ld, int32_t rows, int32_t kp, void *dst, size_t dst_bytes,
+                        void *stream) {
+    if (rows == 0 || kp == 0) return 0;
+    if (!src || !dst) return fail(WD_ERR_ARG, "null pointer");
+    if (rows % 64 || kp % 32 || ld < kp || ld % 4 || !aligned16(src) || !aligned16(dst))
+        return fail(WD_ERR_SHAPE, "split_planes: rows %% 64, kp %% 32, ld >= kp, ld %% 4 and 16-byte alignment "
+                                  "required (rows %d kp %d ld %d)", rows, kp, ld);
+    if (dst_bytes < (size_t)rows * kp * 6) return fail(WD_ERR_WORKSPACE, "plane buffer too small");
+    hipLaunchKernelGGL(split_tiles_kernel, dim3(ew_blocks((size_t)rows * kp / 8)), dim3(256), 0, (hipStream_t)stream,
+                       src, ld, rows, kp, (uint8_t *)dst);
+    WD_CHECK_LAUNCH("split_planes");
     return 0;
 }
 

@@ -211,7 +211,7 @@ def test_index_select_nd():
         index_select_ND(src, torch.tensor([[50]], device=DEV))
 
 
-@pytest.mark.parametrize('variant,fuse', [(v, 0) for v in range(1, 10)] + [(0, 0), (0, 1)])
+@pytest.mark.parametrize('variant,fuse', [(v, 0) for v in range(1, 15)] + [(0, 0), (0, 1)])
 def test_gemm_variants_agree(variant, fuse):
     """Every GEMM tile variant (WdConfig.gemm_variant) and both the fused gather->GEMM and the separate
     gather + GEMM paths (WdConfig.fuse_gather) compute the same forward."""

@@ -1,0 +1,163 @@
+// gemm_lab.hip — standalone timing of the encoder's GEMM kernels at the benchmark shapes (tuning tool,
+// not part of the product).  Build: make -C tools gemm_lab (hipcc --offload-arch=gfx950).
+// Usage: ./gemm_lab [reps]   -> one line per (shape, kernel): avg µs per launch over `reps` launches,
+// cycling through 8 distinct A buffers (an A operand freshly produced by the previous kernel is not
+// L2-resident on the reading XCD), plus max normwise error against an fp64 host reference.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "gemm_x6.hpp"
+
+using namespace wd;
+
+#define CK(x)                                                                               \
+    do {                                                                                    \
+        hipError_t e = (x);                                                                 \
+        if (e != hipSuccess) {                                                              \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+            exit(1);                                                                        \
+        }                                                                                   \
+    } while (0)
+
+struct Shape { const char *name; int M, N, K; };
+
+__global__ void empty_kernel(int *p) {
+    if (p && threadIdx.x == 1023) p[blockIdx.x] = 0;
+}
+
+template <typename F>
+float time_it(int reps, F &&launch) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 10; ++i) launch(i);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i) launch(i);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    CK(hipEventDestroy(a));
+    CK(hipEventDestroy(b));
+    return ms * 1000.f / reps;
+}
+
+int main(int argc, char **argv) {
+    const int reps = argc > 1 ? atoi(argv[1]) : 200;
+    const Shape shapes[] = {{"K32  polymer B64", 6272, 320, 32}, {"K64  polymer B64", 6272, 320, 64},
+                            {"W_i  polymer B64", 6272, 320, 160}, {"W_h  polymer B64", 6272, 320, 320},
+                            {"W_o  polymer B64", 2304, 320, 480}, {"W_h  zinc B512 H512", 25728, 512, 512}};
+    {
+        float us = time_it(reps, [&](int) { hipLaunchKernelGGL(empty_kernel, dim3(490), dim3(256), 0, 0, nullptr); });
+        printf("%-22s %-26s %8.2f us\n", "launch", "empty 490 x 256", us);
+    }
+    std::mt19937 rng(1);
+    std::uniform_real_distribution<float> U(-1.f, 1.f);
+    for (const Shape &S : shapes) {
+        const int NA = 8;
+        std::vector<float> hA((size_t)S.M * S.K), hB((size_t)S.N * S.K), hR((size_t)S.M * S.N);
+        for (auto &v : hA) v = U(rng);
+        for (auto &v : hB) v = U(rng) * 0.05f;
+        for (auto &v : hR) v = U(rng);
+        float *dA[NA], *dB, *dY, *dR;
+        for (int i = 0; i < NA; ++i) {
+            CK(hipMalloc(&dA[i], hA.size() * 4));
+            CK(hipMemcpy(dA[i], hA.data(), hA.size() * 4, hipMemcpyHostToDevice));
+        }
+        CK(hipMalloc(&dB, hB.size() * 4));
+        CK(hipMalloc(&dY, hR.size() * 4));
+        CK(hipMalloc(&dR, hR.size() * 4));
+        CK(hipMemcpy(dB, hB.data(), hB.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(dR, hR.data(), hR.size() * 4, hipMemcpyHostToDevice));
+        // fp64 reference on 64 sampled rows: Y = relu(R + A B^T)
+        std::vector<int> rows;
+        for (int i = 0; i < 64; ++i) rows.push_back((int)((long long)i * 7919 % S.M));
+        std::vector<double> ref(rows.size() * S.N);
+        double refmax = 0;
+        for (size_t ri = 0; ri < rows.size(); ++ri)
+            for (int n = 0; n < S.N; ++n) {
+                double s = hR[(size_t)rows[ri] * S.N + n];
+                for (int k = 0; k < S.K; ++k) s += (double)hA[(size_t)rows[ri] * S.K + k] * hB[(size_t)n * S.K + k];
+                ref[ri * S.N + n] = s > 0 ? s : 0;
+                refmax = fmax(refmax, fabs(ref[ri * S.N + n]));
+            }
+        auto check = [&]() {
+            std::vector<float> y(hR.size());
+            CK(hipMemcpy(y.data(), dY, y.size() * 4, hipMemcpyDeviceToHost));
+            double e = 0;
+            for (size_t ri = 0; ri < rows.size(); ++ri)
+                for (int n = 0; n < S.N; ++n) e = fmax(e, fabs(y[(size_t)rows[ri] * S.N + n] - ref[ri * S.N + n]));
+            return e / refmax;
+        };
+        Epi epi{};
+        epi.kind = EPI_ACT; epi.act = ACT_RELU; epi.resid = dR; epi.Y = dY; epi.ld = S.N;
+        // f32 MFMA baseline (gemm_nt16_kernel<64,64,2,2>)
+        {
+            NtParams P{};
+            P.lda0 = S.K; P.ka0 = S.K; P.b = dB; P.ldb = S.K; P.M = S.M; P.N = S.N; P.epi = epi;
+            P.tiles_m = S.M / 64; P.tiles_n = S.N / 64;
+            float us = time_it(reps, [&](int i) {
+                P.a0 = dA[i % NA];
+                hipLaunchKernelGGL((gemm_nt16_kernel<64, 64, 2, 2>), dim3(P.tiles_m * P.tiles_n), dim3(256), 0, 0, P);
+            });
+            printf("%-22s %-26s %8.2f us  err %.2e\n", S.name, "f32 nt16 64x64", us, check());
+        }
+        auto run_x6 = [&](const char *name, auto kern, int bm) {
+            X6Params X{};
+            X.lda0 = S.K; X.ka0 = S.K; X.bf = dB; X.ldb = S.K; X.M = S.M; X.N = S.N; X.epi = epi;
+            X.tiles_m = S.M / bm; X.tiles_n = S.N / 64;
+            float us = time_it(reps, [&](int i) {
+                X.a0 = dA[i % NA];
+                hipLaunchKernelGGL(kern, dim3(X.tiles_m * X.tiles_n), dim3(4 * bm), 0, 0, X);
+            });
+            printf("%-22s %-26s %8.2f us  err %.2e\n", S.name, name, us, check());
+        };
+        run_x6("x6 64x64 k32 split", gemm_x6_kernel<64, 32>, 64);
+        if (S.M % 128 == 0) run_x6("x6 128x64 k32 split", gemm_x6_kernel<128, 32>, 128);
+        if (S.K % 64 == 0) run_x6("x6 64x64 k64 split", gemm_x6_kernel<64, 64>, 64);
+        // both operands pre-split into plane tiles (split once, outside the timing)
+        {
+            uint8_t *pA[NA], *pB;
+            const size_t abytes = (size_t)S.M * S.K * 6, bbytes = (size_t)S.N * S.K * 6;
+            for (int i = 0; i < NA; ++i) {
+                CK(hipMalloc(&pA[i], abytes));
+                hipLaunchKernelGGL(split_tiles_kernel, dim3(1024), dim3(256), 0, 0, dA[i], S.K, S.M, S.K, pA[i]);
+            }
+            CK(hipMalloc(&pB, bbytes));
+            hipLaunchKernelGGL(split_tiles_kernel, dim3(1024), dim3(256), 0, 0, dB, S.K, S.N, S.K, pB);
+            CK(hipDeviceSynchronize());
+            auto run_p = [&](const char *name, auto kern, int bm) {
+                X6PParams X{};
+                X.kp0 = S.K; X.ka0 = S.K; X.b = pB; X.kpb = S.K; X.M = S.M; X.N = S.N; X.epi = epi;
+                X.tiles_m = S.M / bm; X.tiles_n = S.N / 64;
+                float us = time_it(reps, [&](int i) {
+                    X.a0 = pA[i % NA];
+                    hipLaunchKernelGGL(kern, dim3(X.tiles_m * X.tiles_n), dim3(4 * bm), 0, 0, X);
+                });
+                printf("%-22s %-26s %8.2f us  err %.2e\n", S.name, name, us, check());
+            };
+            run_p("x6g 64x64 glds S=2", gemm_x6g_kernel<2>, 64);
+            run_p("x6g 64x64 glds S=3", gemm_x6g_kernel<3>, 64);
+            run_p("x6g 64x64 glds S=4", gemm_x6g_kernel<4>, 64);
+            // the split itself (what a producer pays to write A as planes instead of fp32)
+            float us = time_it(reps, [&](int i) {
+                hipLaunchKernelGGL(split_tiles_kernel, dim3(1024), dim3(256), 0, 0, dA[i % NA], S.K, S.M, S.K, pA[i % NA]);
+            });
+            printf("%-22s %-26s %8.2f us\n", S.name, "split A -> planes", us);
+            for (int i = 0; i < NA; ++i) CK(hipFree(pA[i]));
+            CK(hipFree(pB));
+        }
+        fflush(stdout);
+        for (int i = 0; i < NA; ++i) CK(hipFree(dA[i]));
+        CK(hipFree(dB));
+        CK(hipFree(dY));
+        CK(hipFree(dR));
+    }
+    return 0;
+}

@@ -22,7 +22,10 @@ for s in "$@"; do
     benchq) step bench_quick 300 python bench.py --steps 100 --warmup 10 --cpu-seconds 5 ;;
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu ;;
     tune) step tune 600 python tools/tune_gemm.py ;;
-    ab) step ab_fused 300 python bench.py --steps 200 --warmup 20 --no-cpu --fuse-gather && step ab_unfused 300 python bench.py --steps 200 --warmup 20 --no-cpu ;;
+    lab) step gemm_lab 300 ./tools/gemm_lab 200 ;;
+    ab) step ab_x6 300 python bench.py --steps 200 --warmup 20 --no-cpu --variant 10 && step ab_f32 300 python bench.py --steps 200 --warmup 20 --no-cpu --variant 9 ;;
+    x6prec) step x6prec 300 python tools/x6_precision.py ;;
+    profx6) step rocprof_x6 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof_x6 -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu --variant ${VARIANT:-10} ;;
     counters) step counters 120 rocprofv3 -L ;;
     pmc) step pmc 1500 bash tools/pmc.sh ;;
     sweep) step sweep 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/sweep -o run -- python tools/size_sweep.py ;;

@@ -14,6 +14,7 @@ from chemprop_amd.mpn import MPNEncoder  # noqa: E402
 from chemprop_amd.nn_utils import initialize_weights  # noqa: E402
 
 dev = torch.device('cuda:0')
+VARIANTS = [int(v) for v in os.environ.get('VARIANTS', '9 10 11 12').split()]
 for kind, b, H, T in (('polymer', 64, 300, 3), ('polymer', 128, 300, 3), ('zinc', 512, 512, 5)):
     g = BatchMolGraph(synthetic.make_batch(kind, b, 3))
     g.device_graph(dev)
@@ -21,7 +22,7 @@ for kind, b, H, T in (('polymer', 64, 300, 3), ('polymer', 128, 300, 3), ('zinc'
     enc = MPNEncoder(TrainArgs(hidden_size=H, depth=T), 133, 147)
     initialize_weights(enc)
     enc = enc.to(dev).eval()
-    res = {v: [] for v in (3, 9)}
+    res = {v: [] for v in VARIANTS}
     with torch.no_grad():
         for rnd in range(5):
             for v in res:
