@@ -102,6 +102,16 @@ typedef struct WdGraph {
      * GEMMs read.  NULL: those GEMMs split the fp32 features in the kernel instead. */
     const void *f_atoms_x6;
     const void *f_bonds_x6;
+    /* Optional molecule blocks for the fused inference forward: consecutive molecules
+     * grouped into blocks of <= 128 bond rows and <= 64 atom rows, so that every gather stays inside one
+     * block.  blocks[8 * k .. 8 * k + 5] = {bond_start, bond_count, atom_start, atom_count, mol_lo,
+     * mol_hi} (natural row ids, half-open molecule range).  bond_blk_row[r] (r < rows of f_bonds) =
+     * 128 * block + (r - bond_start) or -1; f_atoms_blk_x6 = plane tiles of f_atoms in the blocked atom
+     * layout (row 64 * block + (a - atom_start), zero rows elsewhere).  n_blocks = 0: unavailable. */
+    int32_t n_blocks;
+    const int32_t *blocks;
+    const int32_t *bond_blk_row;
+    const void *f_atoms_blk_x6;
 } WdGraph;
 
 /* nn.Module parameters of MPNEncoder (mpn.py:17-64); all device pointers, row-major like nn.Linear. */
@@ -183,6 +193,10 @@ int wdmpnn_event_pool_elapsed_ms(void *pool, int32_t first, int32_t count, float
 int wdmpnn_plane_bytes(int32_t rows, int32_t kp, size_t *bytes);
 int wdmpnn_split_planes(const float *src, int32_t ld, int32_t rows, int32_t kp, void *dst, size_t dst_bytes,
                         void *stream);
+/* The same with a row map: source row r goes to plane-tile row row_map[r] (skipped when < 0) of a
+ * [out_rows, kp] plane-tile matrix whose other rows are zero-filled. */
+int wdmpnn_split_planes_rows(const float *src, int32_t ld, int32_t rows, int32_t kp, const int32_t *row_map,
+                             int32_t out_rows, void *dst, size_t dst_bytes, void *stream);
 
 /* index_select_ND (nn_utils.py:50-67): out[i, :] = src[index[i], :], row_len floats per row.
  * Indices are int64 like the reference's LongTensor; out-of-range indices are an error checked by

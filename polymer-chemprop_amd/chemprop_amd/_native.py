@@ -27,7 +27,7 @@ EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace
                     'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
                     'wdmpnn_index_select_rows', 'wdmpnn_event_pool_create', 'wdmpnn_event_pool_destroy',
                     'wdmpnn_event_pool_elapsed_ms', 'wdmpnn_packed_params_bytes', 'wdmpnn_pack_params',
-                    'wdmpnn_plane_bytes', 'wdmpnn_split_planes')
+                    'wdmpnn_plane_bytes', 'wdmpnn_split_planes', 'wdmpnn_split_planes_rows')
 
 
 class WdCsr(Structure):
@@ -42,7 +42,8 @@ class WdGraph(Structure):
                 ('msg_gather', WdCsr), ('bond_feat_gather', WdCsr), ('atom_gather', WdCsr), ('b2revb', c_void_p),
                 ('msg_gather_t', WdCsr), ('bond_feat_gather_t', WdCsr), ('atom_gather_t', WdCsr),
                 ('atom_desc', c_void_p), ('desc_dim', c_int32), ('atom_messages', c_int32),
-                ('f_atoms_x6', c_void_p), ('f_bonds_x6', c_void_p)]
+                ('f_atoms_x6', c_void_p), ('f_bonds_x6', c_void_p),
+                ('n_blocks', c_int32), ('blocks', c_void_p), ('bond_blk_row', c_void_p), ('f_atoms_blk_x6', c_void_p)]
 
 
 class WdParams(Structure):
@@ -94,12 +95,14 @@ def lib() -> ctypes.CDLL:
                                      c_void_p]
     L.wdmpnn_plane_bytes.argtypes = [c_int32, c_int32, POINTER(c_size_t)]
     L.wdmpnn_split_planes.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_size_t, c_void_p]
+    L.wdmpnn_split_planes_rows.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_void_p, c_size_t,
+                                           c_void_p]
     L.wdmpnn_event_pool_create.argtypes = [c_int32, POINTER(c_void_p)]
     L.wdmpnn_event_pool_destroy.argtypes = [c_void_p]
     L.wdmpnn_event_pool_elapsed_ms.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_float)]
     for fn in ('wdmpnn_packed_params_bytes', 'wdmpnn_pack_params', 'wdmpnn_event_pool_create', 'wdmpnn_event_pool_destroy', 'wdmpnn_event_pool_elapsed_ms',
                'wdmpnn_workspace_bytes', 'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
-               'wdmpnn_index_select_rows', 'wdmpnn_plane_bytes', 'wdmpnn_split_planes'):
+               'wdmpnn_index_select_rows', 'wdmpnn_plane_bytes', 'wdmpnn_split_planes', 'wdmpnn_split_planes_rows'):
         getattr(L, fn).restype = c_int
     v = L.wdmpnn_abi_version()
     if v != ABI_VERSION:

@@ -55,6 +55,7 @@ def _round_up(x: int, m: int) -> int:
 
 
 CSR_PAD = 8  # WdCsr: idx / coef readable 8 entries past the end (branch-free first-8 fetch)
+BLK_BONDS, BLK_ATOMS = 128, 64  # molecule-block capacity of the fused forward (WdGraph.blocks)
 
 
 class Csr:
@@ -266,6 +267,26 @@ class BatchMolGraph:
         keep = coef != 0.0
         return Csr.from_rows(rows[keep], j[keep], coef[keep], V1)
 
+    def molecule_blocks(self):
+        """Consecutive molecules grouped greedily into blocks of <= BLK_BONDS bond rows and <= BLK_ATOMS
+        atom rows (WdGraph.blocks, int32 [n_blocks, 8]); None when a molecule alone exceeds a limit."""
+        rows = []
+        cur = None
+        for i, ((as_, an), (bs, bn)) in enumerate(zip(self.a_scope, self.b_scope)):
+            if bn > BLK_BONDS or an > BLK_ATOMS:
+                return None
+            if cur is not None and cur[1] + bn <= BLK_BONDS and cur[3] + an <= BLK_ATOMS:
+                cur[1] += bn
+                cur[3] += an
+                cur[5] = i + 1
+            else:
+                if cur is not None:
+                    rows.append(cur)
+                cur = [bs, bn, as_, an, i, i + 1, 0, 0]
+        if cur is not None:
+            rows.append(cur)
+        return np.array(rows, np.int32).reshape(-1, 8)
+
     # ------------------------------------------------------------------ device packing
     def device_graph(self, device, atom_messages: bool = False, bond_fdim: int = None) -> DeviceGraph:
         """Pack (once per device/mode) into one device buffer; returns the cached DeviceGraph."""
@@ -295,11 +316,30 @@ class BatchMolGraph:
             msg, feat = self.bond_message_gather(), None
             msg_rows = self.n_bonds
         agg = self.atom_aggregate_gather(atom_messages)
+        blocks = None if atom_messages else self.molecule_blocks()
+        if blocks is not None and len(blocks):
+            # every gather of a block's rows must stay inside the block (block-diagonal batches)
+            bond_blk = np.full(fb_p.shape[0], -1, np.int32)
+            atom_blk = np.full(fa_p.shape[0], -1, np.int32)
+            blk_of_bond = np.full(fb_p.shape[0], -1, np.int64)
+            blk_of_atom = np.full(fa_p.shape[0], -1, np.int64)
+            for k, (bs, bn, as_, an) in enumerate(blocks[:, :4]):
+                bond_blk[bs:bs + bn] = BLK_BONDS * k + np.arange(bn)
+                atom_blk[as_:as_ + an] = BLK_ATOMS * k + np.arange(an)
+                blk_of_bond[bs:bs + bn] = k
+                blk_of_atom[as_:as_ + an] = k
+            for c, rb in ((msg, blk_of_bond), (agg, blk_of_atom)):
+                row = np.repeat(np.arange(len(c.ptr) - 1), np.diff(c.ptr))
+                if len(row) and not np.array_equal(rb[row], blk_of_bond[c.idx]):
+                    blocks = None
+                    break
         msg_t = msg.transpose(msg_rows)
         agg_t = agg.transpose(msg_rows)
         arrays = [('f_atoms', fa_p), ('f_bonds', fb_p), ('w_atoms', self._np['w_atoms']),
                   ('mol_start', a_start), ('mol_size', a_size), ('xn', xn),
                   ('b2revb', self._np['b2revb'].astype(np.int32))]
+        if blocks is not None and len(blocks):
+            arrays += [('blocks', blocks), ('bond_blk_row', bond_blk), ('atom_blk_row', atom_blk)]
         csrs = [('msg', msg), ('agg', agg), ('msg_t', msg_t), ('agg_t', agg_t)]
         if feat is not None:
             csrs.append(('feat', feat))
@@ -348,6 +388,17 @@ class BatchMolGraph:
                                                     _native.current_stream(device)), f'{name} planes')
                 views[name + '_x6'] = planes
                 setattr(s, name + '_x6', planes.data_ptr())
+            if blocks is not None and len(blocks):  # f_atoms planes in the molecule-blocked atom layout
+                out_rows = BLK_ATOMS * len(blocks)
+                nbytes = ctypes.c_size_t()
+                _native.check(L.wdmpnn_plane_bytes(out_rows, lda, ctypes.byref(nbytes)), 'plane bytes')
+                planes = torch.empty(max(nbytes.value, 256), dtype=torch.uint8, device=device)
+                _native.check(L.wdmpnn_split_planes_rows(P('f_atoms'), lda, fa_p.shape[0], lda, P('atom_blk_row'),
+                                                         out_rows, planes.data_ptr(), nbytes.value,
+                                                         _native.current_stream(device)), 'blocked f_atoms planes')
+                views['f_atoms_blk_x6'] = planes
+                s.n_blocks, s.blocks, s.bond_blk_row = len(blocks), P('blocks'), P('bond_blk_row')
+                s.f_atoms_blk_x6 = planes.data_ptr()
         dg = DeviceGraph(buf, views, s)
         dg.host_csr = dict(csrs)
         dg.n_edges = self.n_bonds - 1

@@ -1,0 +1,259 @@
+// fused_mp.hpp — molecule-blocked fused message passing (inference forward, bond messages).
+//
+// Molecules are independent (block-diagonal batches, featurization.py:782-800), so a workgroup that
+// owns whole molecules needs no other workgroup's rows.  The host packer groups consecutive molecules
+// into blocks of <= 128 bond rows and <= 64 atom rows (WdGraph.blocks).  Intermediates live in
+// molecule-blocked plane tiles (planes.hpp, BR = 128 for bond rows, BR = 64 for atom rows), and
+// every stage after W_i is ONE launch per (block, 64-column tile):
+//
+//   mp_layer_kernel<LAST> P = M_{t-1} W_hᵀ (bf16x6 split-plane GEMM on the block's 128 rows), then the
+//                       CSR gather of P inside the block (GEMM first, gather second: X_t W_hᵀ =
+//                       (G M_{t-1}) W_hᵀ = G (M_{t-1} W_hᵀ), column-separable, mpn.py:110-124), bias,
+//                       residual inp and activation: M_t = act(inp + G P (+ b_h)) -> plane tiles of
+//                       the next layer.  The last layer also forms the atom aggregate
+//                       A = Σ_{b into a} w_b M_t[b] (mpn.py:126-131) for its columns -> atom plane tiles.
+//   wo_readout_kernel   h = act([f_atoms | A] W_oᵀ + b_o) (mpn.py:132-134) on the block's atoms, then the
+//                       molecule readout (mpn.py:145-171) of those columns straight to out[mol].
+//
+// So the forward is W_i + (T - 1) layer launches + 1, with no gather kernels, no fp32 message
+// round trips through HBM and no separate readout.  Arithmetic per output element: the P and h GEMMs
+// are fp32-accurate (gemm_x6.hpp), the gathers add in CSR order (the reference's slot order).
+#pragma once
+#include "gemm_x6.hpp"
+#include "kernels.hpp"
+
+namespace wd {
+
+constexpr int BLK_BONDS = 128, BLK_ATOMS = 64;  // block capacity (rows of the blocked layouts)
+
+// WdGraph.blocks row: {bond_start, bond_count, atom_start, atom_count, mol_lo, mol_hi, -, -}
+struct BlockRow { int bs, bn, as, an, ml, mh; };
+__device__ __forceinline__ BlockRow load_block(const int32_t *blocks, int i) {
+    const int4 a = *reinterpret_cast<const int4 *>(blocks + 8 * i);
+    const int2 b = *reinterpret_cast<const int2 *>(blocks + 8 * i + 4);
+    return BlockRow{a.x, a.y, a.z, a.w, b.x, b.y};
+}
+
+// s += w * T[j][c .. c+7] (LDS tile, row stride 68)
+__device__ __forceinline__ void lds_term(const float *T, int j, int c, float w, float4 &s0, float4 &s1) {
+    fma4(s0, w, ld4(T + j * 68 + c));
+    fma4(s1, w, ld4(T + j * 68 + c + 4));
+}
+
+// one message term of row j (natural id jn): P[j] or (P[j] + P[rev j]) / 2 (mpn.py:101-102)
+__device__ __forceinline__ void msg_term(const float *Pt, int jn, int bs, const int32_t *sym_rev, int c, float w,
+                                         float4 &s0, float4 &s1) {
+    const int j = jn - bs;
+    float4 p0 = ld4(Pt + j * 68 + c), p1 = ld4(Pt + j * 68 + c + 4);
+    if (sym_rev) {
+        const int jr = sym_rev[jn] - bs;
+        const float4 q0 = ld4(Pt + jr * 68 + c), q1 = ld4(Pt + jr * 68 + c + 4);
+        p0.x = (p0.x + q0.x) / 2.0f; p0.y = (p0.y + q0.y) / 2.0f;
+        p0.z = (p0.z + q0.z) / 2.0f; p0.w = (p0.w + q0.w) / 2.0f;
+        p1.x = (p1.x + q1.x) / 2.0f; p1.y = (p1.y + q1.y) / 2.0f;
+        p1.z = (p1.z + q1.z) / 2.0f; p1.w = (p1.w + q1.w) / 2.0f;
+    }
+    fma4(s0, w, p0);
+    fma4(s1, w, p1);
+}
+
+struct MpLayerP {
+    const uint8_t *mprev;       // M_{t-1}: blocked bond plane tiles [nblk * 128][kp]
+    uint8_t *mnext;             // M_t (not written by the last layer)
+    int kp;                     // Hk
+    const uint8_t *wh;          // W_h plane tiles [Hk][Hk] (64-row blocks)
+    const float *inp;           // fp32 [Rp][Hk] natural rows (mpn.py:95 input)
+    const float *bias;          // b_h (padded) or null
+    const int32_t *blocks;
+    const int32_t *ptr, *idx; const float *coef;   // msg gather, natural rows
+    const int32_t *sym_rev;     // undirected (mpn.py:101-102) or null
+    int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;
+    const int32_t *aptr, *aidx; const float *acoef;  // atom gather (natural atom rows -> natural bond rows)
+    uint8_t *aplanes;           // A: blocked atom plane tiles [nblk * 64][kp]
+    int n_tiles;                // Hk / 64
+};
+
+// grid = nblk * n_tiles (XCD-grouped: the column tiles of a block share an XCD), 512 threads = 8 waves
+// (4 x 2 of 32x32): a CU's L2 -> LDS rate grows with the waves issuing loads (tools/gemm_lab stream).
+// LDS: two 36 KB GEMM stages; the epilogue reuses them as P [128][68] and M [128][68] fp32.
+template <bool LAST>
+__global__ __launch_bounds__(512) void mp_layer_kernel(MpLayerP P) {
+    constexpr int BM = BLK_BONDS, LDC = 68;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * x6_stage_bytes<BM>()];
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * 64;
+    const BlockRow B = load_block(P.blocks, blk);
+    const int tid = threadIdx.x;
+    // epilogue units: (row lr = (tid >> 3) + 64 i, columns 8u .. 8u+7), i = 0..1, u = tid & 7
+    const int u = tid & 7, c = 8 * u;
+    float4 res[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int lr = (tid >> 3) + 64 * i;
+        res[i][0] = res[i][1] = f4zero();
+        if (lr < B.bn) {
+            const float *s = P.inp + (size_t)(B.bs + lr) * P.kp + n0 + c;
+            res[i][0] = ld4(s);
+            res[i][1] = ld4(s + 4);
+        }
+    }
+    X6Operands O{};
+    O.a0 = P.mprev; O.nkc0 = P.kp >> 5; O.kc0 = P.kp >> 5;
+    O.a1 = P.mprev; O.nkc1 = P.kp >> 5; O.kc1 = 0;  // no second segment (a non-null alias: no null arithmetic)
+    O.rb = blk;
+    O.b = P.wh + (size_t)nt * (P.kp >> 5) * X6_BLOCK;
+    floatx4 acc[2][2];
+    x6_mainloop<BM, 4, 2>(O, lds, acc);
+    __syncthreads();
+    float *Pt = reinterpret_cast<float *>(lds);
+    float *Mt = Pt + BM * LDC;
+    x6_acc_to_lds<BM, 4, 2>(acc, Pt);
+    __syncthreads();
+
+    float4 bia[2] = {f4zero(), f4zero()};
+    if (P.bias) { bia[0] = ld4(P.bias + n0 + c); bia[1] = ld4(P.bias + n0 + c + 4); }
+    const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int lr = (tid >> 3) + 64 * i;
+        float4 y0 = f4zero(), y1 = f4zero();
+        if (lr < B.bn) {
+            const int b = B.bs + lr;
+            const int e0 = P.ptr[b], e1 = P.ptr[b + 1];
+            float4 s0 = f4zero(), s1 = f4zero();
+            // first G8 entries fetched together (lists are readable G8 past their end), then the rest
+            int jj[G8];
+            float ww[G8];
+#pragma unroll
+            for (int k = 0; k < G8; ++k) {
+                jj[k] = P.idx[e0 + k];
+                ww[k] = P.coef ? P.coef[e0 + k] : 1.0f;
+            }
+            // CSR order: the reference's slot order
+#pragma unroll
+            for (int k = 0; k < G8; ++k)
+                if (e0 + k < e1) msg_term(Pt, jj[k], B.bs, P.sym_rev, c, ww[k], s0, s1);
+            for (int e = e0 + G8; e < e1; ++e)
+                msg_term(Pt, P.idx[e], B.bs, P.sym_rev, c, P.coef ? P.coef[e] : 1.0f, s0, s1);
+            float z[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+            const float r8[8] = {res[i][0].x, res[i][0].y, res[i][0].z, res[i][0].w,
+                                 res[i][1].x, res[i][1].y, res[i][1].z, res[i][1].w};
+            const float b8[8] = {bia[0].x, bia[0].y, bia[0].z, bia[0].w, bia[1].x, bia[1].y, bia[1].z, bia[1].w};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                float y = act_fwd(P.act, r8[q] + (z[q] + b8[q]), slope);  // mpn.py:123 input + message
+                if (P.p_drop > 0.f) y *= dropout_scale(P.seed, P.layer, b, n0 + c + q, P.p_drop);
+                z[q] = y;
+            }
+            y0 = make_float4(z[0], z[1], z[2], z[3]);
+            y1 = make_float4(z[4], z[5], z[6], z[7]);
+        }
+        if constexpr (LAST) {
+            st4(Mt + lr * LDC + c, y0);
+            st4(Mt + lr * LDC + c + 4, y1);
+        } else {
+            x6_store8<BM>(P.mnext, P.kp, blk * BM + lr, n0 + c, y0, y1);
+        }
+    }
+    if constexpr (LAST) {
+        __syncthreads();
+        // atom aggregate of this column tile: A[a] = Σ_{b into a} w_b M_t[b] (mpn.py:126-131)
+        {
+            const int la = tid >> 3;
+            float4 s0 = f4zero(), s1 = f4zero();
+            if (la < B.an) {
+                const int a = B.as + la, e0 = P.aptr[a], e1 = P.aptr[a + 1];
+                int jj[G8];
+                float ww[G8];
+    #pragma unroll
+                for (int k = 0; k < G8; ++k) {
+                    jj[k] = P.aidx[e0 + k];
+                    ww[k] = P.acoef ? P.acoef[e0 + k] : 1.0f;
+                }
+    #pragma unroll
+                for (int k = 0; k < G8; ++k)
+                    if (e0 + k < e1) lds_term(Mt, jj[k] - B.bs, c, ww[k], s0, s1);
+                for (int e = e0 + G8; e < e1; ++e) lds_term(Mt, P.aidx[e] - B.bs, c, P.acoef ? P.acoef[e] : 1.0f, s0, s1);
+            }
+            x6_store8<BLK_ATOMS>(P.aplanes, P.kp, blk * BLK_ATOMS + la, n0 + c, s0, s1);
+        }
+    }
+}
+
+struct WoReadoutP {
+    const uint8_t *fa; int kpa; int kca;     // f_atoms: blocked atom plane tiles [nblk * 64][kpa], kca chunks used
+    const uint8_t *ag; int kp;               // A: blocked atom plane tiles [nblk * 64][kp = Hk]
+    const uint8_t *wo;                       // W_o plane tiles [Hk][Fak + Hk]
+    const float *bias;                       // b_o (padded)
+    const int32_t *blocks;
+    const float *w_atoms; const int32_t *mol_start, *mol_size; const float *xn;
+    int agg; float norm; const float *zero_vec;
+    int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;
+    float *out; int ncols;                   // out [B][ncols] (ncols = H)
+    int n_tiles;
+};
+
+// grid = nblk * n_tiles, 512 threads: 64 atom rows x 64 columns, 8 waves (4 x 2 of 16x32).
+__global__ __launch_bounds__(512) void wo_readout_kernel(WoReadoutP P) {
+    constexpr int BM = BLK_ATOMS, LDC = 68;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * x6_stage_bytes<BM>()];
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * 64;
+    const BlockRow B = load_block(P.blocks, blk);
+    const int tid = threadIdx.x;
+    X6Operands O{};
+    O.a0 = P.fa; O.nkc0 = P.kpa >> 5; O.kc0 = P.kca;
+    O.a1 = P.ag; O.nkc1 = P.kp >> 5; O.kc1 = P.kp >> 5;
+    O.rb = blk;
+    O.b = P.wo + (size_t)nt * (P.kca + (P.kp >> 5)) * X6_BLOCK;
+    floatx4 acc[1][2];
+    x6_mainloop<BM, 4, 2>(O, lds, acc);
+    __syncthreads();
+    float *H = reinterpret_cast<float *>(lds);
+    x6_acc_to_lds<BM, 4, 2>(acc, H);
+    __syncthreads();
+    // h = act(. + b_o) (* dropout), in place: thread -> (row (tid >> 4) + 32 i, columns 4 (tid & 15) ..)
+    {
+        const int c = 4 * (tid & 15);
+        const float4 bb = ld4(P.bias + n0 + c);
+        const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int la = (tid >> 4) + 32 * i;
+            float4 v = ld4(H + la * LDC + c);
+            float z[4] = {v.x + bb.x, v.y + bb.y, v.z + bb.z, v.w + bb.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                z[q] = act_fwd(P.act, z[q], slope);
+                if (P.p_drop > 0.f && la < B.an)
+                    z[q] *= dropout_scale(P.seed, P.layer, B.as + la, n0 + c + q, P.p_drop);
+            }
+            st4(H + la * LDC + c, make_float4(z[0], z[1], z[2], z[3]));
+        }
+    }
+    __syncthreads();
+    // readout (mpn.py:145-171) of this block's molecules, columns n0 .. n0+63: thread -> (molecule, column)
+    const int nm = B.mh - B.ml;
+    for (int t = tid; t < nm * 64; t += 512) {
+        const int i = B.ml + (t >> 6), cc = t & 63, col = n0 + cc;
+        if (col >= P.ncols) continue;
+        const int n = P.mol_size[i];
+        float v;
+        if (n == 0) {
+            v = P.zero_vec[col];  // cached_zero_vector, no Xn factor (mpn.py:148-149)
+        } else {
+            const int a0 = P.mol_start[i] - B.as;
+            float s = 0.f, wsum = 0.f;
+            for (int a = 0; a < n; ++a) {
+                const float w = P.w_atoms[P.mol_start[i] + a];
+                s = fmaf(w, H[(a0 + a) * LDC + cc], s);
+                wsum += w;
+            }
+            const float m = P.agg == 0 ? s / wsum : (P.agg == 2 ? s / P.norm : s);
+            v = P.xn[i] * m;
+        }
+        P.out[(size_t)i * P.ncols + col] = v;
+    }
+}
+
+}  // namespace wd

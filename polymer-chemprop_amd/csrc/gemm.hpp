@@ -18,6 +18,7 @@
 // groups of MI355X_MICROARCH.md §LDS) feeds 16 MFMAs with four ds_read_b128 per operand.
 #pragma once
 #include "common.hpp"
+#include "planes.hpp"
 
 namespace wd {
 
@@ -30,8 +31,11 @@ struct Epi {
     const float *bias;     // [N] (EPI_ACT; packed, zero padded)
     const float *resid;    // [M][ld] or null (mpn.py:123 `input + message`)
     float *Z;              // pre-activation out or null
-    float *Y;              // output
+    float *Y;              // output (EPI_ACT: may be null when `planes` is set)
     int ld;                // row stride of resid / Z / Y
+    uint8_t *planes;       // EPI_ACT: also store Y as bf16x3 plane tiles with 128-row blocks (the
+    const int32_t *plane_row;  //   molecule-blocked bond layout) at row plane_row[i] (< 0: skipped)
+    int planes_kp;         //   column extent of that plane-tile matrix
     long long slab_stride; // EPI_STORE (tn): Y += blockIdx.y * slab_stride
     int accumulate;        // EPI_STORE: Y += C
     int act;
@@ -275,12 +279,16 @@ __device__ __forceinline__ void epilogue_v4(const Epi &E, const float *C, int ld
             }
             if (j + 4 <= N) {
                 if (E.Z) st4(E.Z + o, make_float4(z[0], z[1], z[2], z[3]));
-                st4(E.Y + o, make_float4(out[0], out[1], out[2], out[3]));
+                if (E.Y) st4(E.Y + o, make_float4(out[0], out[1], out[2], out[3]));
             } else {
                 for (int q = 0; q < N - j; ++q) {
                     if (E.Z) E.Z[o + q] = z[q];
-                    E.Y[o + q] = out[q];
+                    if (E.Y) E.Y[o + q] = out[q];
                 }
+            }
+            if (E.planes) {  // padded columns (>= N) of the plane tiles hold act(0) = 0 from the zero padding
+                const int pr = E.plane_row[i];
+                if (pr >= 0) x6_store4<128>(E.planes, E.planes_kp, pr, j, make_float4(out[0], out[1], out[2], out[3]));
             }
         } else {
             if (j + 4 <= N) {

@@ -159,22 +159,17 @@ __global__ __launch_bounds__(4 * BM) void gemm_x6_kernel(X6Params P) {
     epilogue_v4<BM, BN, NT>(P.epi, cl, LDC, m0, n0, P.M, P.N, ep);
 }
 
-struct X6PParams {
-    const uint8_t *a0; int kp0; int ka0;  // A segment 0: plane tiles of a [Mp][kp0] matrix, K extent ka0
-    const uint8_t *a1; int kp1; int ka1;  // A segment 1 (ka1 = 0: absent)
-    const uint8_t *b; int kpb;            // B plane tiles [Np][kpb], kpb == ka0 + ka1
-    int M, N;
-    int tiles_m, tiles_n;
-    Epi epi;
-};
-
 // ---------------------------------------------------------------------------------------------
-// gemm_x6g_kernel: both operands pre-split (plane tiles), staged by LDS-DMA (global_load_lds_dwordx4,
-// cdna_hip_programming.md §5 "Async global->LDS copy"): no staging registers, S LDS stages, S-1 chunks
-// in flight behind counted vmcnt waits and raw s_barrier (a __syncthreads would drain the DMA queue).
-// Each wave-instruction fills 1 KB of LDS lane-linearly; the bank swizzle is applied on the per-lane
-// global source address (rows stay 64 B, unit s of row r reads source unit s ^ ((r >> 1) & 3)).
-// Per 32-wide chunk: A 12 KB + B 12 KB = 24 pieces of 1 KB, 6 per wave (BM = 64).
+// Split-plane GEMM core on LDS-DMA staged plane tiles (cdna_hip_programming.md §5 "Async
+// global->LDS copy"): no staging registers, no arithmetic in the staging path, two LDS stages (one
+// chunk in flight behind the one being multiplied), raw s_barrier (a __syncthreads would drain the DMA
+// queue).  One wave-instruction fills 1 KB of LDS lane-linearly (16 rows x 64 B of one plane); the
+// bank swizzle goes on the per-lane global source address (unit s of row r reads unit
+// s ^ ((r >> 1) & 3)).
+//
+// A K-chunk is 32 columns.  A operand: up to two segments, each a plane-tile matrix with BM-row
+// blocks (BR = BM, planes.hpp), so chunk kc of row block rb is ONE contiguous 3 x BM x 64-byte block.
+// B operand: plane tiles with 64-row blocks (one 12 KB block per chunk of the column tile).
 // ---------------------------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void lds_void_t;
 
@@ -182,102 +177,146 @@ __device__ __forceinline__ void glds16(const void *g, uint8_t *lds_wave_base) {
     __builtin_amdgcn_global_load_lds(g, (lds_void_t *)lds_wave_base, 16, 0, 0);
 }
 
-template <int S>
-__global__ __launch_bounds__(256) void gemm_x6g_kernel(X6PParams P) {
-    constexpr int BM = 64, BN = X6_BN, NT = 256;
-    constexpr int APL = BM * 64, STAGE = 3 * APL + 3 * X6_PLANE;  // 24 KB
-    __shared__ __attribute__((aligned(16))) uint8_t lds[S * STAGE];
+struct X6Operands {
+    const uint8_t *a0; int nkc0, kc0;   // A segment 0: base of the matrix, its 32-column chunks per row block,
+                                        // chunks used (K extent / 32)
+    const uint8_t *a1; int nkc1, kc1;   // A segment 1 (kc1 = 0: absent)
+    int rb;                             // A row block (BM rows)
+    const uint8_t *b;                   // B: this column tile's first chunk block (12 KB blocks, one per chunk)
+};
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wi = wave >> 1, wj = wave & 1, g = lane >> 4, i16 = lane & 15;
-    const int tile = xcd_tile(blockIdx.x, P.tiles_m * P.tiles_n);
-    const int mt = tile / P.tiles_n, nt = tile % P.tiles_n;
-    const int m0 = mt * BM, n0 = nt * BN;
-    const int K = P.ka0 + P.ka1, nchunks = K >> 5;
-    EpiPrefetch<BM, BN, NT> ep;
-    ep.load(P.epi, m0, n0, P.M, P.N);
+template <int BM>
+constexpr int x6_stage_bytes() { return 3 * BM * 64 + 3 * 64 * 64; }
 
-    // this wave's 6 pieces of a stage: j = 0..2 -> A piece 3 wave + j, j = 3..5 -> B piece 3 wave + j - 3;
-    // piece c, lane l -> image unit q = 64 c + l = (plane q / 256, row (q / 4) % 64, slot q % 4)
-    int src[6];
+// acc[TM][TN] (+)= A(rb rows) · B(col tile)ᵀ; waves WM x WN, wave tile (BM / WM) x (64 / WN).
+// Uses lds[0 .. 2 * x6_stage_bytes<BM>()); on return every DMA has landed and all waves are past their
+// last LDS read (the caller may reuse the LDS after one __syncthreads()).
+template <int BM, int WM, int WN>
+__device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
+                                            floatx4 (&acc)[BM / WM / 16][64 / WN / 16]) {
+    constexpr int NW = WM * WN, TM = BM / WM / 16, TN = 64 / WN / 16;
+    constexpr int APL = BM * 64, STAGE = x6_stage_bytes<BM>();
+    constexpr int AP = 3 * BM / 16, BP = 12;                       // 1 KB pieces per chunk
+    constexpr int APW = (AP + NW - 1) / NW, BPW = (BP + NW - 1) / NW;  // per wave (the last ones predicated)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wi = wave / WN, wj = wave % WN, g = lane >> 4, i16 = lane & 15;
+
+    // piece c of wave w = c * NW + w (interleaved, so that uneven counts fall on the last pieces);
+    // lane l -> image unit q = 64 c + l = (plane, row, slot) -> source byte in the chunk block
+    int asrc[APW], bsrc[BPW];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        const int q = 64 * (3 * wave + (j % 3)) + lane, p = q >> 8, r = (q >> 2) & 63, sl = q & 3;
-        src[j] = p * X6_PLANE + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
+    for (int j = 0; j < APW; ++j) {
+        const int q = 64 * (j * NW + wave) + lane, p = q / (BM * 4), r = (q >> 2) % BM, sl = q & 3;
+        asrc[j] = p * APL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
     }
-    const uint8_t *bbase = P.b + (size_t)nt * (P.kpb >> 5) * X6_BLOCK;
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) {
+        const int q = 64 * (j * NW + wave) + lane, p = (q >> 8) % 3, r = (q >> 2) & 63, sl = q & 3;
+        bsrc[j] = p * X6_PLANE + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
+    }
+    const int nchunks = O.kc0 + O.kc1;
     auto issue = [&](int kc, int stage) {
-        const int k0 = kc << 5;
-        const bool s1 = k0 >= P.ka0;
-        const uint8_t *abase = s1 ? P.a1 : P.a0;
-        const int kp = s1 ? P.kp1 : P.kp0, kk = s1 ? k0 - P.ka0 : k0;
-        const uint8_t *ablk = abase + ((size_t)(m0 >> 6) * (kp >> 5) + (kk >> 5)) * X6_BLOCK;
-        const uint8_t *bblk = bbase + (size_t)kc * X6_BLOCK;
+        const bool s1 = kc >= O.kc0;
+        const uint8_t *abase = s1 ? O.a1 : O.a0;
+        const size_t aoff = ((size_t)O.rb * (s1 ? O.nkc1 : O.nkc0) + (s1 ? kc - O.kc0 : kc)) * (3 * APL);
+        const uint8_t *ablk = abase + aoff;
+        const uint8_t *bblk = O.b + (size_t)kc * X6_BLOCK;
         uint8_t *st = lds + stage * STAGE;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) glds16(ablk + src[j], st + 1024 * (3 * wave + j));
+        for (int j = 0; j < APW; ++j)
+            if (AP % NW == 0 || j * NW + wave < AP) glds16(ablk + asrc[j], st + 1024 * (j * NW + wave));
 #pragma unroll
-        for (int j = 0; j < 3; ++j) glds16(bblk + src[3 + j], st + 3 * APL + 1024 * (3 * wave + j));
+        for (int j = 0; j < BPW; ++j)
+            if (BP % NW == 0 || j * NW + wave < BP) glds16(bblk + bsrc[j], st + 3 * APL + 1024 * (j * NW + wave));
     };
-
-    floatx4 acc[2][2];
+    int ao[TM], bo[TN];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < TM; ++a) ao[a] = x6_slot(wi * (BM / WM) + a * 16 + i16, g);
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
-    int ao[2], bo[2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a) ao[a] = x6_slot(wi * 32 + a * 16 + i16, g);
-#pragma unroll
-    for (int b = 0; b < 2; ++b) bo[b] = 3 * APL + x6_slot(wj * 32 + b * 16 + i16, g);
+    for (int b = 0; b < TN; ++b) bo[b] = 3 * APL + x6_slot(wj * (64 / WN) + b * 16 + i16, g);
     auto compute = [&](const uint8_t *st) {
-        bf16x8 af[2][3], bfr[2][3];
+        bf16x8 af[TM][3], bfr[TN][3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
 #pragma unroll
-            for (int a = 0; a < 2; ++a) af[a][p] = *reinterpret_cast<const bf16x8 *>(st + p * APL + ao[a]);
+            for (int a = 0; a < TM; ++a) af[a][p] = *reinterpret_cast<const bf16x8 *>(st + p * APL + ao[a]);
 #pragma unroll
-            for (int b = 0; b < 2; ++b) bfr[b][p] = *reinterpret_cast<const bf16x8 *>(st + p * X6_PLANE + bo[b]);
+            for (int b = 0; b < TN; ++b) bfr[b][p] = *reinterpret_cast<const bf16x8 *>(st + p * X6_PLANE + bo[b]);
         }
+        // plane products hh, hm, mh, hl, lh, mm
         constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};
 #pragma unroll
         for (int t = 0; t < 6; ++t)
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+            for (int a = 0; a < TM; ++a)
 #pragma unroll
-                for (int b = 0; b < 2; ++b)
+                for (int b = 0; b < TN; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][PA[t]], bfr[b][PB[t]], acc[a][b], 0, 0, 0);
     };
-
-    // prologue: chunks 0 .. S-2 in flight (a missing chunk issues a repeat of the last one so that
-    // every wave always has the same number of DMA groups outstanding: the counted waits stay exact)
 #pragma unroll
-    for (int c = 0; c < S - 1; ++c) issue(min(c, nchunks - 1), c);
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    issue(0, 0);
     for (int kc = 0; kc < nchunks; ++kc) {
-        // chunk kc landed (this wave's 6 pieces; S-2 younger groups may stay in flight) ...
-        if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if constexpr (S == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        // ... for every wave, and every wave is done reading stage (kc - 1) % S
+        // chunk kc landed for this wave (vmcnt(0): per-wave piece counts may differ), then for every
+        // wave; every wave is done reading stage (kc + 1) % 2
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        issue(min(kc + S - 1, nchunks - 1), (kc + S - 1) % S);
-        compute(lds + (kc % S) * STAGE);
+        if (kc + 1 < nchunks) issue(kc + 1, (kc + 1) & 1);
+        compute(lds + (kc & 1) * STAGE);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing repeat DMAs before reusing LDS
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
 
-    float *cl = reinterpret_cast<float *>(lds);
-    constexpr int LDC = BN + 4;
-    static_assert(BM * LDC * 4 <= S * STAGE, "C tile must fit in the staging LDS");
+// acc tile -> LDS fp32 [BM][64 + 4] (C/D map of 16x16: col = lane & 15, row = 4 (lane >> 4) + reg)
+template <int BM, int WM, int WN>
+__device__ __forceinline__ void x6_acc_to_lds(const floatx4 (&acc)[BM / WM / 16][64 / WN / 16], float *cl) {
+    constexpr int TM = BM / WM / 16, TN = 64 / WN / 16, LDC = 68;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wi = wave / WN, wj = wave % WN, g = lane >> 4, i16 = lane & 15;
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < TN; ++b)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) cl[(wi * 32 + a * 16 + 4 * g + r) * LDC + wj * 32 + b * 16 + i16] = acc[a][b][r];
+            for (int r = 0; r < 4; ++r)
+                cl[(wi * (BM / WM) + a * 16 + 4 * g + r) * LDC + wj * (64 / WN) + b * 16 + i16] = acc[a][b][r];
+}
+
+struct X6PParams {
+    const uint8_t *a0; int kp0; int ka0;  // A segment 0: plane tiles (64-row blocks) of a [Mp][kp0] matrix, K extent ka0
+    const uint8_t *a1; int kp1; int ka1;  // A segment 1 (ka1 = 0: absent)
+    const uint8_t *b; int kpb;            // B plane tiles [Np][kpb], kpb == ka0 + ka1
+    int M, N;
+    int tiles_m, tiles_n;
+    Epi epi;
+};
+
+// C[Mp][Np] = epi([A0 | A1] · Bᵀ): 64x64 tile, 8 waves of 16x32 (more waves issuing loads: a CU's
+// L2 -> LDS rate grows with them, tools/gemm_lab stream), fused bias/residual/activation/dropout
+// epilogue (epilogue_v4: fp32 Z / Y and optionally the next layer's plane tiles).
+__global__ __launch_bounds__(512) void gemm_x6g_kernel(X6PParams P) {
+    constexpr int BM = 64, NT = 512;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * x6_stage_bytes<BM>()];
+    const int tile = xcd_tile(blockIdx.x, P.tiles_m * P.tiles_n);
+    const int mt = tile / P.tiles_n, nt = tile % P.tiles_n;
+    const int m0 = mt * BM, n0 = nt * X6_BN;
+    EpiPrefetch<BM, X6_BN, NT> ep;
+    ep.load(P.epi, m0, n0, P.M, P.N);
+    X6Operands O{};
+    O.a0 = P.a0; O.nkc0 = P.kp0 >> 5; O.kc0 = P.ka0 >> 5;
+    O.a1 = P.a1; O.nkc1 = P.kp1 >> 5; O.kc1 = P.ka1 >> 5;
+    O.rb = mt;
+    O.b = P.b + (size_t)nt * (P.kpb >> 5) * X6_BLOCK;
+    floatx4 acc[1][2];
+    x6_mainloop<BM, 4, 2>(O, lds, acc);
     __syncthreads();
-    epilogue_v4<BM, BN, NT>(P.epi, cl, LDC, m0, n0, P.M, P.N, ep);
+    float *cl = reinterpret_cast<float *>(lds);
+    x6_acc_to_lds<BM, 4, 2>(acc, cl);
+    __syncthreads();
+    epilogue_v4<BM, X6_BN, NT>(P.epi, cl, 68, m0, n0, P.M, P.N, ep);
 }
 
 }  // namespace wd

@@ -47,33 +47,54 @@ __device__ __forceinline__ int x6_off(int r, int u) {
 }
 __device__ __forceinline__ int x6_slot(int r, int u) { return x6_off<32>(r, u); }
 
-__device__ __forceinline__ size_t x6_tile_off(int r, int k, int kp) {  // byte offset of (r, k), plane 0
-    return ((size_t)(r >> 6) * (kp >> 5) + (k >> 5)) * X6_BLOCK + (r & 63) * 64 + 2 * (k & 31);
+// Byte offset of (row r, column k), plane 0, in a plane-tile matrix with BR-row blocks (BR = 64: the
+// natural-row layout; BR = 128: the molecule-blocked bond layout): block (r / BR, k / 32)
+// of 3 x BR x 64 bytes, plane stride BR * 64.
+template <int BR = 64>
+__device__ __forceinline__ size_t x6_tile_off(int r, int k, int kp) {
+    return ((size_t)(r / BR) * (kp >> 5) + (k >> 5)) * (3 * BR * 64) + (r % BR) * 64 + 2 * (k & 31);
 }
 
-// write 8 consecutive values v[0..7] of row r, columns k..k+7 (k % 8 == 0) into a plane-tile matrix
+// write values lo, hi = columns k..k+7 (k % 8 == 0) of row r into a plane-tile matrix
+template <int BR = 64>
 __device__ __forceinline__ void x6_store8(uint8_t *base, int kp, int r, int k, const float4 &lo, const float4 &hi) {
     uint32_t h[4], m[4], l[4];
     split_pair(lo.x, lo.y, h[0], m[0], l[0]);
     split_pair(lo.z, lo.w, h[1], m[1], l[1]);
     split_pair(hi.x, hi.y, h[2], m[2], l[2]);
     split_pair(hi.z, hi.w, h[3], m[3], l[3]);
-    uint8_t *d = base + x6_tile_off(r, k, kp);
+    uint8_t *d = base + x6_tile_off<BR>(r, k, kp);
     *reinterpret_cast<u32x4 *>(d) = u32x4{h[0], h[1], h[2], h[3]};
-    *reinterpret_cast<u32x4 *>(d + X6_PLANE) = u32x4{m[0], m[1], m[2], m[3]};
-    *reinterpret_cast<u32x4 *>(d + 2 * X6_PLANE) = u32x4{l[0], l[1], l[2], l[3]};
+    *reinterpret_cast<u32x4 *>(d + BR * 64) = u32x4{m[0], m[1], m[2], m[3]};
+    *reinterpret_cast<u32x4 *>(d + 2 * BR * 64) = u32x4{l[0], l[1], l[2], l[3]};
 }
 
+// columns k..k+3 (k % 4 == 0): three 8-byte pieces
+template <int BR = 64>
+__device__ __forceinline__ void x6_store4(uint8_t *base, int kp, int r, int k, const float4 &v) {
+    uint32_t h[2], m[2], l[2];
+    split_pair(v.x, v.y, h[0], m[0], l[0]);
+    split_pair(v.z, v.w, h[1], m[1], l[1]);
+    uint8_t *d = base + x6_tile_off<BR>(r, k, kp);
+    *reinterpret_cast<uint2 *>(d) = make_uint2(h[0], h[1]);
+    *reinterpret_cast<uint2 *>(d + BR * 64) = make_uint2(m[0], m[1]);
+    *reinterpret_cast<uint2 *>(d + 2 * BR * 64) = make_uint2(l[0], l[1]);
+}
 
-// fp32 [rows][ld] (first kp columns) -> plane tiles [rows][kp]; one thread per 8 values
+// fp32 [rows][ld] (first kp columns) -> plane tiles [out_rows][kp] (BR = 64); one thread per 8 values.
+// row_map == null: row r -> r (out_rows == rows); else row r -> row_map[r] (skipped when < 0) and every
+// output row that no source row maps to must be zero-filled by the caller.
 __global__ __launch_bounds__(256) void split_tiles_kernel(const float *__restrict__ src, int ld, int rows, int kp,
-                                                          uint8_t *__restrict__ dst) {
+                                                          uint8_t *__restrict__ dst,
+                                                          const int32_t *__restrict__ row_map = nullptr) {
     const int q8 = kp >> 3;
     const size_t total = (size_t)rows * q8;
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
         const int r = (int)(t / q8), k = (int)(t % q8) * 8;
+        const int ro = row_map ? row_map[r] : r;
+        if (ro < 0) continue;
         const float *s = src + (size_t)r * ld + k;
-        x6_store8(dst, kp, r, k, ld4(s), ld4(s + 4));
+        x6_store8(dst, kp, ro, k, ld4(s), ld4(s + 4));
     }
 }
 

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "fused.hpp"
+#include "fused_mp.hpp"
 #include "gemm.hpp"
 #include "gemm_x6.hpp"
 #include "kernels.hpp"
@@ -77,6 +78,8 @@ struct Dims {
     int ldx, Ko, Kd;
     bool atom, undirected, save, desc;
     bool x6;  // plane-tile pipeline: gathers emit bf16x3 plane tiles, GEMMs run gemm_x6g_kernel
+    bool blocked;  // molecule-blocked fused inference forward (fused_mp.hpp)
+    int nblk;
 };
 
 int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
@@ -101,6 +104,9 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     D.Ko = D.Fak + D.Hk;
     D.Kd = D.Hk + D.dk;
     D.x6 = c->gemm_variant == 10 && !D.atom && !c->fuse_gather;
+    D.blocked = D.x6 && !D.save && !D.desc && D.T >= 2 && g->n_blocks > 0 && g->blocks && g->bond_blk_row &&
+                g->f_atoms_blk_x6 && g->f_bonds_x6;
+    D.nblk = D.blocked ? g->n_blocks : 0;
     if (D.atom && D.undirected)
         return fail(WD_ERR_UNSUPPORTED, "undirected with atom_messages (the reference indexes atom messages "
                                         "with b2revb, mpn.py:101-102)");
@@ -345,10 +351,10 @@ int gemm_x6g(const void *a0, int kp0, int ka0, const void *a1, int kp1, int ka1,
         return fail(WD_ERR_SHAPE, "gemm_x6g: operand not in plane tiles (Mp %d Np %d ka %d/%d)", Mp, Np, ka0, ka1);
     X6PParams X{};
     X.a0 = (const uint8_t *)a0; X.kp0 = kp0; X.ka0 = ka0;
-    X.a1 = (const uint8_t *)a1; X.kp1 = kp1; X.ka1 = ka1;
+    X.a1 = (const uint8_t *)(a1 ? a1 : a0); X.kp1 = a1 ? kp1 : kp0; X.ka1 = ka1;
     X.b = (const uint8_t *)b; X.kpb = ka0 + ka1;
     X.M = Mp; X.N = Np; X.epi = epi; X.tiles_m = Mp / 64; X.tiles_n = Np / X6_BN;
-    hipLaunchKernelGGL(gemm_x6g_kernel<2>, dim3(X.tiles_m * X.tiles_n), dim3(256), 0, st, X);
+    hipLaunchKernelGGL(gemm_x6g_kernel, dim3(X.tiles_m * X.tiles_n), dim3(512), 0, st, X);
     WD_CHECK_LAUNCH("gemm_x6g");
     return 0;
 }
@@ -508,6 +514,7 @@ struct FwdLayout {
     std::vector<size_t> Z, M, X;
     size_t packed = 0, A = 0, Zo = 0, h = 0, Zd = 0, hd = 0, total = 0;
     size_t Xp = 0, Ap = 0;  // plane tiles of X_t and A (D.x6)
+    size_t Mb[2] = {0, 0}, Ab = 0;  // molecule-blocked plane tiles of M_t (ping-pong) and A (D.blocked)
     bool own_pack = false;
 };
 
@@ -523,7 +530,10 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
     if (D.T > 1)
         for (int t = 0; t < (D.save ? D.T - 1 : 1); ++t) L.X.push_back(take((size_t)D.Rp * D.ldx * 4));
     L.A = take(atm);
-    if (D.x6) {
+    if (D.blocked) {
+        for (int i = 0; i < 2; ++i) L.Mb[i] = take((size_t)D.nblk * BLK_BONDS * D.Hk * 6);
+        L.Ab = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 6);
+    } else if (D.x6) {
         if (D.T > 1) L.Xp = take((size_t)D.Rp * D.Hk * 6);
         L.Ap = take((size_t)D.Vap * D.Hk * 6);
     }
@@ -665,6 +675,45 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
     // plane-tile pipeline (D.x6): a GEMM without a plane copy of its A operand splits in the kernel
     const int var_split = var == 10 ? 12 : var;
     const char *pkb = pk;
+
+    if (D.blocked) {
+        // molecule-blocked fused forward (fused_mp.hpp): W_i -> (T-1) x mp_layer -> wo_readout
+        Epi e = epi_act(c->activation, p->prelu, W(PL.bi), nullptr, F(L.Z[0]), nullptr, Hk, c, 0);
+        e.planes = (uint8_t *)(ws + L.Mb[0]); e.plane_row = g->bond_blk_row; e.planes_kp = Hk;
+        if (!x6g_eligible(e)) return fail(WD_ERR_SHAPE, "fused forward: unaligned buffers");
+        WD_TRY(gemm_x6g(g->f_bonds_x6, g->ld_bonds, D.Kink, nullptr, 0, 0, pkb + PL.WiX, D.Rp, Hk, e, st));
+        for (int t = 1; t < D.T; ++t) {
+            MpLayerP M{};
+            M.mprev = (const uint8_t *)(ws + L.Mb[(t - 1) & 1]); M.mnext = (uint8_t *)(ws + L.Mb[t & 1]); M.kp = Hk;
+            M.wh = (const uint8_t *)(pkb + PL.WhX); M.inp = F(L.Z[0]); M.bias = p->b_h ? W(PL.bh) : nullptr;
+            M.blocks = g->blocks;
+            M.ptr = g->msg_gather.ptr; M.idx = g->msg_gather.idx; M.coef = g->msg_gather.coef;
+            M.sym_rev = D.undirected ? g->b2revb : nullptr;
+            M.act = c->activation; M.slope = p->prelu; M.p_drop = c->dropout; M.seed = c->seed; M.layer = t;
+            M.aptr = g->atom_gather.ptr; M.aidx = g->atom_gather.idx; M.acoef = g->atom_gather.coef;
+            M.aplanes = (uint8_t *)(ws + L.Ab);
+            M.n_tiles = Hk / 64;
+            WD_TRY(record_prof(c, t - 1, 0, st));
+            if (t == D.T - 1) hipLaunchKernelGGL(mp_layer_kernel<true>, dim3(D.nblk * M.n_tiles), dim3(512), 0, st, M);
+            else hipLaunchKernelGGL(mp_layer_kernel<false>, dim3(D.nblk * M.n_tiles), dim3(512), 0, st, M);
+            WD_CHECK_LAUNCH("mp_layer");
+            WD_TRY(record_prof(c, t - 1, 1, st));
+        }
+        if (D.B > 0) {
+            WoReadoutP R{};
+            R.fa = (const uint8_t *)g->f_atoms_blk_x6; R.kpa = g->ld_atoms; R.kca = D.Fak / 32;
+            R.ag = (const uint8_t *)(ws + L.Ab); R.kp = Hk;
+            R.wo = (const uint8_t *)(pkb + PL.WoX); R.bias = W(PL.bo);
+            R.blocks = g->blocks;
+            R.w_atoms = g->w_atoms; R.mol_start = g->mol_start; R.mol_size = g->mol_size; R.xn = g->degree_of_polym;
+            R.agg = c->aggregation; R.norm = c->aggregation_norm; R.zero_vec = p->zero_vec;
+            R.act = c->activation; R.slope = p->prelu; R.p_drop = c->dropout; R.seed = c->seed; R.layer = D.T;
+            R.out = out; R.ncols = D.H; R.n_tiles = Hk / 64;
+            hipLaunchKernelGGL(wo_readout_kernel, dim3(D.nblk * R.n_tiles), dim3(512), 0, st, R);
+            WD_CHECK_LAUNCH("wo_readout");
+        }
+        return 0;
+    }
 
     // L0: input layer (mpn.py:92-97)
     {
@@ -944,6 +993,24 @@ int wdmpnn_split_planes(const float *src, int32_t ld, int32_t rows, int32_t kp, 
     hipLaunchKernelGGL(split_tiles_kernel, dim3(ew_blocks((size_t)rows * kp / 8)), dim3(256), 0, (hipStream_t)stream,
                        src, ld, rows, kp, (uint8_t *)dst);
     WD_CHECK_LAUNCH("split_planes");
+    return 0;
+}
+
+int wdmpnn_split_planes_rows(const float *src, int32_t ld, int32_t rows, int32_t kp, const int32_t *row_map,
+                             int32_t out_rows, void *dst, size_t dst_bytes, void *stream) {
+    if (out_rows == 0 || kp == 0) return 0;
+    if (!src || !dst || !row_map) return fail(WD_ERR_ARG, "null pointer");
+    if (out_rows % 64 || kp % 32 || ld < kp || ld % 4 || !aligned16(src) || !aligned16(dst))
+        return fail(WD_ERR_SHAPE, "split_planes_rows: out_rows %% 64, kp %% 32, ld >= kp, ld %% 4 and 16-byte "
+                                  "alignment required (out_rows %d kp %d ld %d)", out_rows, kp, ld);
+    const size_t need = (size_t)out_rows * kp * 6;
+    if (dst_bytes < need) return fail(WD_ERR_WORKSPACE, "plane buffer too small");
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(dst, 0, need, st) != hipSuccess) return fail(WD_ERR_ARG, "memset failed");
+    if (rows > 0)
+        hipLaunchKernelGGL(split_tiles_kernel, dim3(ew_blocks((size_t)rows * kp / 8)), dim3(256), 0, st, src, ld, rows,
+                           kp, (uint8_t *)dst, row_map);
+    WD_CHECK_LAUNCH("split_planes_rows");
     return 0;
 }
 

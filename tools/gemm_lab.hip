@@ -30,6 +30,72 @@ __global__ void empty_kernel(int *p) {
     if (p && threadIdx.x == 1023) p[blockIdx.x] = 0;
 }
 
+// L2 -> LDS streaming ceiling: each workgroup LDS-DMA copies `chunks` x 24 KB (4 waves x 6 x 1 KB per
+// chunk) from a buffer of `span` bytes with S LDS stages (S - 1 chunks in flight)
+template <int S>
+__global__ __launch_bounds__(256) void stream_lds_kernel(const uint8_t *src, size_t span, int chunks, int *sink) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[S * 24576];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t base = ((size_t)blockIdx.x * 24576 * chunks) % span;
+    auto issue = [&](int c) {
+        uint8_t *st = lds + (c % S) * 24576;
+        const size_t off = base + (size_t)c * 24576;
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+            glds16(src + (off + (size_t)(6 * wave + j) * 1024 + 16 * lane) % span, st + 1024 * (6 * wave + j));
+    };
+    for (int c = 0; c < S - 1; ++c) issue(c);
+    for (int c = 0; c < chunks; ++c) {
+        if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if constexpr (S == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else if constexpr (S == 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        issue(c + S - 1);  // past the end: harmless re-reads inside span
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 && lds[blockIdx.x % 1024] == 123 && sink) sink[0] = 1;
+}
+
+// same traffic into VGPRs: each lane keeps D float4 loads in flight, waves x 1 KB per instruction
+template <int NW, int D>
+__global__ __launch_bounds__(64 * NW) void stream_reg_kernel(const uint8_t *src, size_t span, int chunks, int *sink) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t base = ((size_t)blockIdx.x * 24576 * chunks) % span;
+    u32x4 acc = {0, 0, 0, 0};
+    const int per = 24576 / 1024 / NW;  // wave-instructions per chunk per wave
+    for (int c = 0; c < chunks * per; c += D) {
+        u32x4 v[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+            v[d] = *reinterpret_cast<const u32x4 *>(src + (base + ((size_t)(c + d) * NW + wave) * 1024 + 16 * lane) % span);
+#pragma unroll
+        for (int d = 0; d < D; ++d) acc ^= v[d];
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u && sink) sink[0] = 1;
+}
+
+// glds with NW waves per workgroup (24 KB per chunk), S = 2
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void stream_glds_w_kernel(const uint8_t *src, size_t span, int chunks, int *sink) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 24576];
+    constexpr int P = 24 / NW;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t base = ((size_t)blockIdx.x * 24576 * chunks) % span;
+    for (int c = 0; c < chunks; ++c) {
+        uint8_t *st = lds + (c & 1) * 24576;
+        const size_t off = base + (size_t)c * 24576;
+#pragma unroll
+        for (int j = 0; j < P; ++j)
+            glds16(src + (off + (size_t)(P * wave + j) * 1024 + 16 * lane) % span, st + 1024 * (P * wave + j));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && lds[blockIdx.x % 1024] == 123 && sink) sink[0] = 1;
+}
+
 template <typename F>
 float time_it(int reps, F &&launch) {
     hipEvent_t a, b;
@@ -57,6 +123,36 @@ int main(int argc, char **argv) {
         float us = time_it(reps, [&](int) { hipLaunchKernelGGL(empty_kernel, dim3(490), dim3(256), 0, 0, nullptr); });
         printf("%-22s %-26s %8.2f us\n", "launch", "empty 490 x 256", us);
     }
+    {
+        uint8_t *buf;
+        const size_t big = (size_t)512 << 20;
+        CK(hipMalloc(&buf, big));
+        CK(hipMemset(buf, 1, big));
+        auto run_s = [&](const char *nm, auto kern, size_t span, int grid) {
+            const int chunks = 20;
+            float us = time_it(50, [&](int) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, buf, span, chunks, nullptr); });
+            const double bytes = (double)grid * chunks * 24576;
+            printf("stream %s span %4zu MB grid %4d: %7.2f us  %6.2f TB/s  %6.1f GB/s per CU\n", nm, span >> 20, grid, us,
+                   bytes / us * 1e-6, bytes / us * 1e-3 / 256);
+        };
+        auto run_w = [&](const char *nm, auto kern, int nt, size_t span, int grid) {
+            const int chunks = 20;
+            float us = time_it(50, [&](int) { hipLaunchKernelGGL(kern, dim3(grid), dim3(nt), 0, 0, buf, span, chunks, nullptr); });
+            const double bytes = (double)grid * chunks * 24576;
+            printf("stream %s span %4zu MB grid %4d: %7.2f us  %6.2f TB/s  %6.1f GB/s per CU\n", nm, span >> 20, grid, us,
+                   bytes / us * 1e-6, bytes / us * 1e-3 / 256);
+        };
+        for (size_t span : {(size_t)2 << 20, (size_t)64 << 20})
+            for (int grid : {256, 512, 1024}) {
+                run_s("glds4w S=2", stream_lds_kernel<2>, span, grid);
+                run_w("glds8w S=2", stream_glds_w_kernel<8>, 512, span, grid);
+                run_w("reg4w D=2", stream_reg_kernel<4, 2>, 256, span, grid);
+                run_w("reg4w D=6", stream_reg_kernel<4, 6>, 256, span, grid);
+                run_w("reg8w D=3", stream_reg_kernel<8, 3>, 512, span, grid);
+            }
+        CK(hipFree(buf));
+    }
+    if (argc > 2) return 0;  // streaming only
     std::mt19937 rng(1);
     std::uniform_real_distribution<float> U(-1.f, 1.f);
     for (const Shape &S : shapes) {
@@ -132,19 +228,17 @@ int main(int argc, char **argv) {
             CK(hipMalloc(&pB, bbytes));
             hipLaunchKernelGGL(split_tiles_kernel, dim3(1024), dim3(256), 0, 0, dB, S.K, S.N, S.K, pB);
             CK(hipDeviceSynchronize());
-            auto run_p = [&](const char *name, auto kern, int bm) {
+            auto run_p = [&](const char *name, auto kern, int bm, int nthreads) {
                 X6PParams X{};
                 X.kp0 = S.K; X.ka0 = S.K; X.b = pB; X.kpb = S.K; X.M = S.M; X.N = S.N; X.epi = epi;
                 X.tiles_m = S.M / bm; X.tiles_n = S.N / 64;
                 float us = time_it(reps, [&](int i) {
                     X.a0 = pA[i % NA];
-                    hipLaunchKernelGGL(kern, dim3(X.tiles_m * X.tiles_n), dim3(4 * bm), 0, 0, X);
+                    hipLaunchKernelGGL(kern, dim3(X.tiles_m * X.tiles_n), dim3(nthreads), 0, 0, X);
                 });
                 printf("%-22s %-26s %8.2f us  err %.2e\n", S.name, name, us, check());
             };
-            run_p("x6g 64x64 glds S=2", gemm_x6g_kernel<2>, 64);
-            run_p("x6g 64x64 glds S=3", gemm_x6g_kernel<3>, 64);
-            run_p("x6g 64x64 glds S=4", gemm_x6g_kernel<4>, 64);
+            run_p("x6g 64x64 glds 8w", gemm_x6g_kernel, 64, 512);
             // the split itself (what a producer pays to write A as planes instead of fp32)
             float us = time_it(reps, [&](int i) {
                 hipLaunchKernelGGL(split_tiles_kernel, dim3(1024), dim3(256), 0, 0, dA[i % NA], S.K, S.M, S.K, pA[i % NA]);

@@ -23,6 +23,8 @@ for s in "$@"; do
     prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu ;;
     tune) step tune 600 python tools/tune_gemm.py ;;
     lab) step gemm_lab 300 ./tools/gemm_lab 200 ;;
+    stream) step stream 120 ./tools/gemm_lab 50 stream ;;
+    host) step host 300 python tools/host_overhead.py ;;
     ab) step ab_x6 300 python bench.py --steps 200 --warmup 20 --no-cpu --variant 10 && step ab_f32 300 python bench.py --steps 200 --warmup 20 --no-cpu --variant 9 ;;
     x6prec) step x6prec 300 python tools/x6_precision.py ;;
     profx6) step rocprof_x6 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof_x6 -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu --variant ${VARIANT:-10} ;;
