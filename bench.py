@@ -35,6 +35,7 @@ from chemprop_amd.mpn import MPNEncoder  # noqa: E402
 from chemprop_amd.nn_utils import initialize_weights  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 (the split-plane GEMMs issue 6 bf16 products per fp32 product)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -81,7 +82,7 @@ def main():
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--fuse-gather', action='store_true', help='experimental fused gather->GEMM (WdConfig.fuse_gather)')
-    ap.add_argument('--variant', type=int, default=0, help='WdConfig.gemm_variant (tuning)')
+    ap.add_argument('--variant', type=int, default=0, help='WdConfig.gemm_variant (0 = default path; 9 = f32 MFMA)')
     a = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -96,7 +97,7 @@ def main():
     # inputs: packed + resident in HBM before timing (featurization.py:757-813 equivalent on host)
     graphs = [BatchMolGraph(synthetic.make_batch(a.kind, a.batch, 1000 + 7919 * rank + i)) for i in range(a.n_batches)]
     for g in graphs:
-        g.device_graph(device)
+        g.device_graph(device, False, get_bond_fdim())
     torch.cuda.synchronize(device)
     enc = make_encoder(args, device)
     enc._fuse_gather = int(a.fuse_gather)
@@ -123,7 +124,7 @@ def main():
         elapsed = time.perf_counter() - t0
         my_edges = sum(edges[i % len(edges)] for i in range(a.steps))
 
-        # second pass: HIP events around the dominant launches (message passing gather-GEMM) on the
+        # second pass: HIP events around the dominant launches (the message-passing layers) on the
         # stream they run on
         L = _native.lib()
         pairs = a.steps * max(a.depth - 1, 1)
@@ -153,9 +154,17 @@ def main():
     if rank == 0:
         H = a.hidden
         E_avg = sum(edges[i % len(edges)] for i in range(a.steps)) / a.steps
-        flops_launch = 2.0 * E_avg * H * H  # algorithmic W_h GEMM flops of one message-passing launch
+        # dominant kernel: one message-passing layer (mpn.py:110-124), E directed bonds, hidden H.
+        # Algorithmic FLOPs 2 E H^2 (W_h) + 2 E d H (weighted in-edge sums, d = CSR entries / row);
+        # algorithmic bytes (fp32, each tensor once): read M_{t-1}, inp, W_h, CSR; write M_t.
+        g0 = graphs[0]
+        nnz = float(g0.device_graph(device, False, get_bond_fdim()).host_csr["msg"].idx.shape[0])
+        d_avg = nnz / max(g0.n_bonds - 1, 1)
+        flops_launch = 2.0 * E_avg * H * H + 2.0 * E_avg * d_avg * H
+        bytes_launch = 4.0 * (3 * E_avg * H + H * H + H) + 8.0 * E_avg * d_avg + 4.0 * E_avg
         avg_launch_s = (kernel_ms.value / 1e3 / n_launch) if n_launch else float('nan')
         achieved = flops_launch / avg_launch_s / 1e12 if n_launch else None
+        hbm = bytes_launch / avg_launch_s / 1e9 if n_launch else None
         line = {
             'metric': 'edges/sec MPN forward, batch=64 polymer graphs, depth=3 hidden=300',
             'value': total_edges / elapsed,
@@ -168,16 +177,24 @@ def main():
             'scaling': 'weak',
             'vs_baseline': None,
             'dtype': 'fp32',
+            'arith': 'fp32-accurate GEMMs as exact bf16x3 operand splits on bf16 MFMA (6 products, fp32 '
+                     'accumulate); gathers, residual, activations and readout in fp32',
             'data': 'synthetic',
             'config': {'workload': f'MPNEncoder.forward on synthetic {a.kind} batches of {a.batch} graphs '
                                    f'(avg E={E_avg:.0f} directed edges), depth={a.depth}, hidden={H}, '
                                    f'{a.n_batches} resident batches cycled per rank',
                        'global_batch': a.batch * world, 'depth': a.depth, 'hidden': H,
                        'parallelism': f'dp{world} (independent graphs, no collective in the forward)'},
-            'roofline': {'bound': 'mfma', 'kernel': 'gemm_nt16_kernel<64,64,2,2>: W_h message update (mpn.py:122-124)',
+            'roofline': {'bound': 'mfma',
+                         'kernel': 'mp_layer_kernel: one message-passing layer, W_h split-plane GEMM + in-block CSR '
+                                   'gather + residual/activation (mpn.py:110-124)',
                          'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                          'frac': achieved / FP32_MFMA_PEAK_TFLOPS if achieved else None, 'traffic': None,
+                         'peak_note': 'fp32 dense MFMA peak; the kernel issues bf16 MFMAs, whose fp32-product '
+                                      f'equivalent peak is {BF16_MFMA_PEAK_TFLOPS / 6:.0f} TFLOP/s',
                          'avg_launch_us': avg_launch_s * 1e6, 'flops_per_launch': flops_launch,
+                         'bytes_per_launch': bytes_launch, 'hbm_gbs': hbm,
+                         'hbm_frac': hbm / HBM_PEAK_GBS if hbm else None,
                          'launches_timed': n_launch},
         }
         if not a.no_cpu:

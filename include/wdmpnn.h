@@ -144,9 +144,11 @@ typedef struct WdConfig {
     int32_t prof_slot;      /* first event pair used when prof_pool != NULL                      */
     void   *prof_pool;      /* optional WdEventPool: an event pair is recorded around each message-
                                passing launch (the dominant kernel), pairs prof_slot + t - 1       */
-    int32_t gemm_variant;   /* 0 = default; 9 = f32-MFMA GEMMs; 10 = bf16x6 split GEMMs on plane tiles
-                               (gathers emit plane tiles); 11..14 = bf16x6 with in-kernel operand split;
-                               1..8 = older f32 tile variants (tuning only)           */
+    int32_t gemm_variant;   /* 0 = default = 10: bf16x6 split-plane GEMMs (fp32-accurate) with the
+                               molecule-blocked fused inference forward when WdGraph.blocks allow it;
+                               9 = f32-MFMA GEMMs; 11..14 = bf16x6 with in-kernel operand split;
+                               1..8 = older f32 tile variants (tuning only).  The
+                               backward always runs the deterministic f32-MFMA kernels.             */
     int32_t fuse_gather;    /* 0 = separate gather + GEMM kernels (default, fastest measured);
                                1 = gather fused into the GEMM's A-panel build (gemm_fused_kernel,
                                experimental: DESIGN.md §4)                                          */

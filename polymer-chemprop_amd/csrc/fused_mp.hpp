@@ -4,9 +4,9 @@
 // owns whole molecules needs no other workgroup's rows.  The host packer groups consecutive molecules
 // into blocks of <= 128 bond rows and <= 64 atom rows (WdGraph.blocks).  Intermediates live in
 // molecule-blocked plane tiles (planes.hpp, BR = 128 for bond rows, BR = 64 for atom rows), and
-// every stage after W_i is ONE launch per (block, 64-column tile):
+// every stage after W_i is ONE launch per (block, 64- or 80-column tile):
 //
-//   mp_layer_kernel<LAST> P = M_{t-1} W_hᵀ (bf16x6 split-plane GEMM on the block's 128 rows), then the
+//   mp_layer_kernel   P = M_{t-1} W_hᵀ (bf16x6 split-plane GEMM on the block's 128 rows), then the
 //                       CSR gather of P inside the block (GEMM first, gather second: X_t W_hᵀ =
 //                       (G M_{t-1}) W_hᵀ = G (M_{t-1} W_hᵀ), column-separable, mpn.py:110-124), bias,
 //                       residual inp and activation: M_t = act(inp + G P (+ b_h)) -> plane tiles of
@@ -34,20 +34,22 @@ __device__ __forceinline__ BlockRow load_block(const int32_t *blocks, int i) {
     return BlockRow{a.x, a.y, a.z, a.w, b.x, b.y};
 }
 
-// s += w * T[j][c .. c+7] (LDS tile, row stride 68)
+// s += w * T[j][c .. c+7] (LDS tile, row stride LDC)
+template <int LDC>
 __device__ __forceinline__ void lds_term(const float *T, int j, int c, float w, float4 &s0, float4 &s1) {
-    fma4(s0, w, ld4(T + j * 68 + c));
-    fma4(s1, w, ld4(T + j * 68 + c + 4));
+    fma4(s0, w, ld4(T + j * LDC + c));
+    fma4(s1, w, ld4(T + j * LDC + c + 4));
 }
 
 // one message term of row j (natural id jn): P[j] or (P[j] + P[rev j]) / 2 (mpn.py:101-102)
+template <int LDC>
 __device__ __forceinline__ void msg_term(const float *Pt, int jn, int bs, const int32_t *sym_rev, int c, float w,
                                          float4 &s0, float4 &s1) {
     const int j = jn - bs;
-    float4 p0 = ld4(Pt + j * 68 + c), p1 = ld4(Pt + j * 68 + c + 4);
+    float4 p0 = ld4(Pt + j * LDC + c), p1 = ld4(Pt + j * LDC + c + 4);
     if (sym_rev) {
         const int jr = sym_rev[jn] - bs;
-        const float4 q0 = ld4(Pt + jr * 68 + c), q1 = ld4(Pt + jr * 68 + c + 4);
+        const float4 q0 = ld4(Pt + jr * LDC + c), q1 = ld4(Pt + jr * LDC + c + 4);
         p0.x = (p0.x + q0.x) / 2.0f; p0.y = (p0.y + q0.y) / 2.0f;
         p0.z = (p0.z + q0.z) / 2.0f; p0.w = (p0.w + q0.w) / 2.0f;
         p1.x = (p1.x + q1.x) / 2.0f; p1.y = (p1.y + q1.y) / 2.0f;
@@ -61,7 +63,7 @@ struct MpLayerP {
     const uint8_t *mprev;       // M_{t-1}: blocked bond plane tiles [nblk * 128][kp]
     uint8_t *mnext;             // M_t (not written by the last layer)
     int kp;                     // Hk
-    const uint8_t *wh;          // W_h plane tiles [Hk][Hk] (64-row blocks)
+    const uint8_t *wh;          // W_h plane tiles [Hk][Hk] with BN-row blocks
     const float *inp;           // fp32 [Rp][Hk] natural rows (mpn.py:95 input)
     const float *bias;          // b_h (padded) or null
     const int32_t *blocks;
@@ -70,28 +72,38 @@ struct MpLayerP {
     int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;
     const int32_t *aptr, *aidx; const float *acoef;  // atom gather (natural atom rows -> natural bond rows)
     uint8_t *aplanes;           // A: blocked atom plane tiles [nblk * 64][kp]
-    int n_tiles;                // Hk / 64
+    int n_tiles;                // Hk / BN
 };
 
-// grid = nblk * n_tiles (XCD-grouped: the column tiles of a block share an XCD), 512 threads = 8 waves
-// (4 x 2 of 32x32): a CU's L2 -> LDS rate grows with the waves issuing loads (tools/gemm_lab stream).
-// LDS: two 36 KB GEMM stages; the epilogue reuses them as P [128][68] and M [128][68] fp32.
-template <bool LAST>
-__global__ __launch_bounds__(512) void mp_layer_kernel(MpLayerP P) {
-    constexpr int BM = BLK_BONDS, LDC = 68;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * x6_stage_bytes<BM>()];
+// Wave layout of the fused kernels per column-tile width: BN = 64 -> 4 x 2 waves, BN = 80 -> 2 x 5.
+// 80-column tiles give 4 tiles for Hk = 320 and so exactly one workgroup per CU at the benchmark size
+// (64 blocks x 4 = 256): a grid of 1.25 workgroups per CU left a quarter of the CUs with twice the
+// bytes to stream.
+template <int BN> struct MpWaves;
+template <> struct MpWaves<64> { static constexpr int WM = 4, WN = 2; };
+template <> struct MpWaves<80> { static constexpr int WM = 2, WN = 5; };
+
+// grid = nblk * n_tiles (XCD-grouped: the column tiles of a block share an XCD), 64 WM WN threads.
+// LDS: two GEMM stages, reused by the epilogue as P [128][BN + 4] and M [128][BN + 4] fp32.
+template <int BN, bool LAST>
+__global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_layer_kernel(MpLayerP P) {
+    constexpr int BM = BLK_BONDS, LDC = BN + 4, WM = MpWaves<BN>::WM, WN = MpWaves<BN>::WN, NT = 64 * WM * WN;
+    constexpr int UPR = BN / 8, UNITS = BM * UPR, UPT = (UNITS + NT - 1) / NT;  // 8-column epilogue units
+    constexpr int S = 2;  // (3 stages measured slower: the chunk time is not load-latency bound)
+    constexpr int LDS_BYTES = 2 * BM * LDC * 4 > S * x6_stage_bytes<BM, BN>() ? 2 * BM * LDC * 4
+                                                                             : S * x6_stage_bytes<BM, BN>();
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
     const int tile = xcd_tile(blockIdx.x, gridDim.x);
-    const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * 64;
+    const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
     const int tid = threadIdx.x;
-    // epilogue units: (row lr = (tid >> 3) + 64 i, columns 8u .. 8u+7), i = 0..1, u = tid & 7
-    const int u = tid & 7, c = 8 * u;
-    float4 res[2][2];
+    // residual rows prefetched ahead of the GEMM (unit v = tid + NT i: row v / UPR, columns 8 (v % UPR) ..)
+    float4 res[UPT][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int lr = (tid >> 3) + 64 * i;
+    for (int i = 0; i < UPT; ++i) {
+        const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
         res[i][0] = res[i][1] = f4zero();
-        if (lr < B.bn) {
+        if (v < UNITS && lr < B.bn) {
             const float *s = P.inp + (size_t)(B.bs + lr) * P.kp + n0 + c;
             res[i][0] = ld4(s);
             res[i][1] = ld4(s + 4);
@@ -101,21 +113,21 @@ __global__ __launch_bounds__(512) void mp_layer_kernel(MpLayerP P) {
     O.a0 = P.mprev; O.nkc0 = P.kp >> 5; O.kc0 = P.kp >> 5;
     O.a1 = P.mprev; O.nkc1 = P.kp >> 5; O.kc1 = 0;  // no second segment (a non-null alias: no null arithmetic)
     O.rb = blk;
-    O.b = P.wh + (size_t)nt * (P.kp >> 5) * X6_BLOCK;
-    floatx4 acc[2][2];
-    x6_mainloop<BM, 4, 2>(O, lds, acc);
+    O.a_rows = B.bn;
+    O.b = P.wh + (size_t)nt * (P.kp >> 5) * (3 * BN * 64);
+    floatx4 acc[BM / WM / 16][BN / WN / 16];
+    x6_mainloop<BM, BN, WM, WN, S>(O, lds, acc);
     __syncthreads();
     float *Pt = reinterpret_cast<float *>(lds);
     float *Mt = Pt + BM * LDC;
-    x6_acc_to_lds<BM, 4, 2>(acc, Pt);
+    x6_acc_to_lds<BM, BN, WM, WN>(acc, Pt);
     __syncthreads();
 
-    float4 bia[2] = {f4zero(), f4zero()};
-    if (P.bias) { bia[0] = ld4(P.bias + n0 + c); bia[1] = ld4(P.bias + n0 + c + 4); }
     const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int lr = (tid >> 3) + 64 * i;
+    for (int i = 0; i < UPT; ++i) {
+        const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
+        if (v >= UNITS) break;
         float4 y0 = f4zero(), y1 = f4zero();
         if (lr < B.bn) {
             const int b = B.bs + lr;
@@ -132,13 +144,15 @@ __global__ __launch_bounds__(512) void mp_layer_kernel(MpLayerP P) {
             // CSR order: the reference's slot order
 #pragma unroll
             for (int k = 0; k < G8; ++k)
-                if (e0 + k < e1) msg_term(Pt, jj[k], B.bs, P.sym_rev, c, ww[k], s0, s1);
+                if (e0 + k < e1) msg_term<LDC>(Pt, jj[k], B.bs, P.sym_rev, c, ww[k], s0, s1);
             for (int e = e0 + G8; e < e1; ++e)
-                msg_term(Pt, P.idx[e], B.bs, P.sym_rev, c, P.coef ? P.coef[e] : 1.0f, s0, s1);
+                msg_term<LDC>(Pt, P.idx[e], B.bs, P.sym_rev, c, P.coef ? P.coef[e] : 1.0f, s0, s1);
+            float4 b0 = f4zero(), b1 = f4zero();
+            if (P.bias) { b0 = ld4(P.bias + n0 + c); b1 = ld4(P.bias + n0 + c + 4); }
             float z[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
             const float r8[8] = {res[i][0].x, res[i][0].y, res[i][0].z, res[i][0].w,
                                  res[i][1].x, res[i][1].y, res[i][1].z, res[i][1].w};
-            const float b8[8] = {bia[0].x, bia[0].y, bia[0].z, bia[0].w, bia[1].x, bia[1].y, bia[1].z, bia[1].w};
+            const float b8[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 float y = act_fwd(P.act, r8[q] + (z[q] + b8[q]), slope);  // mpn.py:123 input + message
@@ -151,29 +165,30 @@ __global__ __launch_bounds__(512) void mp_layer_kernel(MpLayerP P) {
         if constexpr (LAST) {
             st4(Mt + lr * LDC + c, y0);
             st4(Mt + lr * LDC + c + 4, y1);
-        } else {
+        } else if (lr < B.bn) {  // rows past the block's bonds are never loaded by the next layer
             x6_store8<BM>(P.mnext, P.kp, blk * BM + lr, n0 + c, y0, y1);
         }
     }
     if constexpr (LAST) {
         __syncthreads();
         // atom aggregate of this column tile: A[a] = Σ_{b into a} w_b M_t[b] (mpn.py:126-131)
-        {
-            const int la = tid >> 3;
+        for (int v = tid; v < B.an * UPR; v += NT) {  // rows past the block's atoms are never loaded
+            const int la = v / UPR, c = 8 * (v % UPR);
             float4 s0 = f4zero(), s1 = f4zero();
             if (la < B.an) {
                 const int a = B.as + la, e0 = P.aptr[a], e1 = P.aptr[a + 1];
                 int jj[G8];
                 float ww[G8];
-    #pragma unroll
+#pragma unroll
                 for (int k = 0; k < G8; ++k) {
                     jj[k] = P.aidx[e0 + k];
                     ww[k] = P.acoef ? P.acoef[e0 + k] : 1.0f;
                 }
-    #pragma unroll
+#pragma unroll
                 for (int k = 0; k < G8; ++k)
-                    if (e0 + k < e1) lds_term(Mt, jj[k] - B.bs, c, ww[k], s0, s1);
-                for (int e = e0 + G8; e < e1; ++e) lds_term(Mt, P.aidx[e] - B.bs, c, P.acoef ? P.acoef[e] : 1.0f, s0, s1);
+                    if (e0 + k < e1) lds_term<LDC>(Mt, jj[k] - B.bs, c, ww[k], s0, s1);
+                for (int e = e0 + G8; e < e1; ++e)
+                    lds_term<LDC>(Mt, P.aidx[e] - B.bs, c, P.acoef ? P.acoef[e] : 1.0f, s0, s1);
             }
             x6_store8<BLK_ATOMS>(P.aplanes, P.kp, blk * BLK_ATOMS + la, n0 + c, s0, s1);
         }
@@ -183,7 +198,7 @@ __global__ __launch_bounds__(512) void mp_layer_kernel(MpLayerP P) {
 struct WoReadoutP {
     const uint8_t *fa; int kpa; int kca;     // f_atoms: blocked atom plane tiles [nblk * 64][kpa], kca chunks used
     const uint8_t *ag; int kp;               // A: blocked atom plane tiles [nblk * 64][kp = Hk]
-    const uint8_t *wo;                       // W_o plane tiles [Hk][Fak + Hk]
+    const uint8_t *wo;                       // W_o plane tiles [Hk][Fak + Hk] with BN-row blocks
     const float *bias;                       // b_o (padded)
     const int32_t *blocks;
     const float *w_atoms; const int32_t *mol_start, *mol_size; const float *xn;
@@ -193,35 +208,39 @@ struct WoReadoutP {
     int n_tiles;
 };
 
-// grid = nblk * n_tiles, 512 threads: 64 atom rows x 64 columns, 8 waves (4 x 2 of 16x32).
-__global__ __launch_bounds__(512) void wo_readout_kernel(WoReadoutP P) {
-    constexpr int BM = BLK_ATOMS, LDC = 68;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * x6_stage_bytes<BM>()];
+template <int BN> struct WoWaves;
+template <> struct WoWaves<64> { static constexpr int WM = 4, WN = 2; };
+template <> struct WoWaves<80> { static constexpr int WM = 2, WN = 5; };
+
+// grid = nblk * n_tiles: 64 atom rows x BN columns per workgroup.
+template <int BN>
+__global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_readout_kernel(WoReadoutP P) {
+    constexpr int BM = BLK_ATOMS, LDC = BN + 4, WM = WoWaves<BN>::WM, WN = WoWaves<BN>::WN, NT = 64 * WM * WN;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * x6_stage_bytes<BM, BN>()];
     const int tile = xcd_tile(blockIdx.x, gridDim.x);
-    const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * 64;
+    const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
     const int tid = threadIdx.x;
     X6Operands O{};
     O.a0 = P.fa; O.nkc0 = P.kpa >> 5; O.kc0 = P.kca;
     O.a1 = P.ag; O.nkc1 = P.kp >> 5; O.kc1 = P.kp >> 5;
     O.rb = blk;
-    O.b = P.wo + (size_t)nt * (P.kca + (P.kp >> 5)) * X6_BLOCK;
-    floatx4 acc[1][2];
-    x6_mainloop<BM, 4, 2>(O, lds, acc);
+    O.a_rows = B.an;
+    O.b = P.wo + (size_t)nt * (P.kca + (P.kp >> 5)) * (3 * BN * 64);
+    floatx4 acc[BM / WM / 16][BN / WN / 16];
+    x6_mainloop<BM, BN, WM, WN>(O, lds, acc);
     __syncthreads();
     float *H = reinterpret_cast<float *>(lds);
-    x6_acc_to_lds<BM, 4, 2>(acc, H);
+    x6_acc_to_lds<BM, BN, WM, WN>(acc, H);
     __syncthreads();
-    // h = act(. + b_o) (* dropout), in place: thread -> (row (tid >> 4) + 32 i, columns 4 (tid & 15) ..)
+    // h = act(. + b_o) (* dropout), in place (mpn.py:133-134)
     {
-        const int c = 4 * (tid & 15);
-        const float4 bb = ld4(P.bias + n0 + c);
         const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int la = (tid >> 4) + 32 * i;
-            float4 v = ld4(H + la * LDC + c);
-            float z[4] = {v.x + bb.x, v.y + bb.y, v.z + bb.z, v.w + bb.w};
+        for (int v = tid; v < BM * (BN / 4); v += NT) {
+            const int la = v / (BN / 4), c = 4 * (v % (BN / 4));
+            const float4 bb = ld4(P.bias + n0 + c);
+            const float4 hv = ld4(H + la * LDC + c);
+            float z[4] = {hv.x + bb.x, hv.y + bb.y, hv.z + bb.z, hv.w + bb.w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 z[q] = act_fwd(P.act, z[q], slope);
@@ -232,10 +251,10 @@ __global__ __launch_bounds__(512) void wo_readout_kernel(WoReadoutP P) {
         }
     }
     __syncthreads();
-    // readout (mpn.py:145-171) of this block's molecules, columns n0 .. n0+63: thread -> (molecule, column)
+    // readout (mpn.py:145-171) of this block's molecules, columns n0 .. n0 + BN - 1: thread -> (molecule, column)
     const int nm = B.mh - B.ml;
-    for (int t = tid; t < nm * 64; t += 512) {
-        const int i = B.ml + (t >> 6), cc = t & 63, col = n0 + cc;
+    for (int t = tid; t < nm * BN; t += NT) {
+        const int i = B.ml + t / BN, cc = t % BN, col = n0 + cc;
         if (col >= P.ncols) continue;
         const int n = P.mol_size[i];
         float v;

@@ -180,24 +180,48 @@ __device__ __forceinline__ void glds16(const void *g, uint8_t *lds_wave_base) {
 struct X6Operands {
     const uint8_t *a0; int nkc0, kc0;   // A segment 0: base of the matrix, its 32-column chunks per row block,
                                         // chunks used (K extent / 32)
-    const uint8_t *a1; int nkc1, kc1;   // A segment 1 (kc1 = 0: absent)
+    const uint8_t *a1; int nkc1, kc1;   // A segment 1 (kc1 = 0: absent; a1 must still be a valid pointer)
     int rb;                             // A row block (BM rows)
-    const uint8_t *b;                   // B: this column tile's first chunk block (12 KB blocks, one per chunk)
+    int a_rows;                         // rows of the block that hold data (<= BM): 16-row groups past it
+                                        // are not loaded (their accumulator rows are garbage, never read)
+    const uint8_t *b;                   // B: this column tile's first chunk block (3 x BN x 64 B per chunk)
 };
 
-template <int BM>
-constexpr int x6_stage_bytes() { return 3 * BM * 64 + 3 * 64 * 64; }
+template <int BM, int BN>
+constexpr int x6_stage_bytes() { return 3 * BM * 64 + 3 * BN * 64; }
 
-// acc[TM][TN] (+)= A(rb rows) · B(col tile)ᵀ; waves WM x WN, wave tile (BM / WM) x (64 / WN).
-// Uses lds[0 .. 2 * x6_stage_bytes<BM>()); on return every DMA has landed and all waves are past their
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the counter field is an immediate)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+    switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+
+// acc[TM][TN] (+)= A(rb rows) · B(col tile)ᵀ for a BM x BN tile (BN = 64 or 80), waves WM x WN, wave
+// tile (BM / WM) x (BN / WN), S LDS stages (S - 1 chunks in flight behind the one multiplied).  Uses
+// lds[0 .. S * x6_stage_bytes<BM, BN>()); on return every DMA has landed and all waves are past their
 // last LDS read (the caller may reuse the LDS after one __syncthreads()).
-template <int BM, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int S = 2>
 __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
-                                            floatx4 (&acc)[BM / WM / 16][64 / WN / 16]) {
-    constexpr int NW = WM * WN, TM = BM / WM / 16, TN = 64 / WN / 16;
-    constexpr int APL = BM * 64, STAGE = x6_stage_bytes<BM>();
-    constexpr int AP = 3 * BM / 16, BP = 12;                       // 1 KB pieces per chunk
+                                            floatx4 (&acc)[BM / WM / 16][BN / WN / 16]) {
+    constexpr int NW = WM * WN, TM = BM / WM / 16, TN = BN / WN / 16;
+    constexpr int APL = BM * 64, BPL = BN * 64, STAGE = x6_stage_bytes<BM, BN>();
+    constexpr int AP = 3 * BM / 16, BP = 3 * BN / 16;                 // 1 KB pieces per chunk
     constexpr int APW = (AP + NW - 1) / NW, BPW = (BP + NW - 1) / NW;  // per wave (the last ones predicated)
+    static_assert(BM % (16 * WM) == 0 && BN % (16 * WN) == 0, "wave tiles of 16x16 MFMAs");
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wi = wave / WN, wj = wave % WN, g = lane >> 4, i16 = lane & 15;
 
@@ -206,13 +230,13 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
     int asrc[APW], bsrc[BPW];
 #pragma unroll
     for (int j = 0; j < APW; ++j) {
-        const int q = 64 * (j * NW + wave) + lane, p = q / (BM * 4), r = (q >> 2) % BM, sl = q & 3;
+        const int q = 64 * (j * NW + wave) + lane, p = (q / (BM * 4)) % 3, r = (q >> 2) % BM, sl = q & 3;
         asrc[j] = p * APL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
     }
 #pragma unroll
     for (int j = 0; j < BPW; ++j) {
-        const int q = 64 * (j * NW + wave) + lane, p = (q >> 8) % 3, r = (q >> 2) & 63, sl = q & 3;
-        bsrc[j] = p * X6_PLANE + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
+        const int q = 64 * (j * NW + wave) + lane, p = (q / (BN * 4)) % 3, r = (q >> 2) % BN, sl = q & 3;
+        bsrc[j] = p * BPL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
     }
     const int nchunks = O.kc0 + O.kc1;
     auto issue = [&](int kc, int stage) {
@@ -220,11 +244,13 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
         const uint8_t *abase = s1 ? O.a1 : O.a0;
         const size_t aoff = ((size_t)O.rb * (s1 ? O.nkc1 : O.nkc0) + (s1 ? kc - O.kc0 : kc)) * (3 * APL);
         const uint8_t *ablk = abase + aoff;
-        const uint8_t *bblk = O.b + (size_t)kc * X6_BLOCK;
+        const uint8_t *bblk = O.b + (size_t)kc * (3 * BPL);
         uint8_t *st = lds + stage * STAGE;
 #pragma unroll
-        for (int j = 0; j < APW; ++j)
-            if (AP % NW == 0 || j * NW + wave < AP) glds16(ablk + asrc[j], st + 1024 * (j * NW + wave));
+        for (int j = 0; j < APW; ++j) {
+            const int c = j * NW + wave;  // piece = (plane c / (BM / 16), 16-row group c % (BM / 16))
+            if ((AP % NW == 0 || c < AP) && 16 * (c % (BM / 16)) < O.a_rows) glds16(ablk + asrc[j], st + 1024 * c);
+        }
 #pragma unroll
         for (int j = 0; j < BPW; ++j)
             if (BP % NW == 0 || j * NW + wave < BP) glds16(bblk + bsrc[j], st + 3 * APL + 1024 * (j * NW + wave));
@@ -233,7 +259,7 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
 #pragma unroll
     for (int a = 0; a < TM; ++a) ao[a] = x6_slot(wi * (BM / WM) + a * 16 + i16, g);
 #pragma unroll
-    for (int b = 0; b < TN; ++b) bo[b] = 3 * APL + x6_slot(wj * (64 / WN) + b * 16 + i16, g);
+    for (int b = 0; b < TN; ++b) bo[b] = 3 * APL + x6_slot(wj * (BN / WN) + b * 16 + i16, g);
     auto compute = [&](const uint8_t *st) {
         bf16x8 af[TM][3], bfr[TN][3];
 #pragma unroll
@@ -241,7 +267,7 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
 #pragma unroll
             for (int a = 0; a < TM; ++a) af[a][p] = *reinterpret_cast<const bf16x8 *>(st + p * APL + ao[a]);
 #pragma unroll
-            for (int b = 0; b < TN; ++b) bfr[b][p] = *reinterpret_cast<const bf16x8 *>(st + p * X6_PLANE + bo[b]);
+            for (int b = 0; b < TN; ++b) bfr[b][p] = *reinterpret_cast<const bf16x8 *>(st + p * BPL + bo[b]);
         }
         // plane products hh, hm, mh, hl, lh, mm
         constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};
@@ -257,23 +283,35 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
     for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
-    issue(0, 0);
+    // this wave's DMA instructions per chunk (the same for every chunk)
+    int mine = 0;
+#pragma unroll
+    for (int j = 0; j < APW; ++j) {
+        const int c = j * NW + wave;
+        mine += (AP % NW == 0 || c < AP) && 16 * (c % (BM / 16)) < O.a_rows;
+    }
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) mine += BP % NW == 0 || j * NW + wave < BP;
+#pragma unroll
+    for (int c = 0; c < S - 1; ++c)
+        if (c < nchunks) issue(c, c);
     for (int kc = 0; kc < nchunks; ++kc) {
-        // chunk kc landed for this wave (vmcnt(0): per-wave piece counts may differ), then for every
-        // wave; every wave is done reading stage (kc + 1) % 2
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // chunk kc landed for this wave (younger chunks kc+1 .. kc+S-2 may stay in flight), then for
+        // every wave; every wave is done reading stage (kc + S - 1) % S (= the one read at kc - 1)
+        if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else wait_vmcnt(min(S - 2, nchunks - 1 - kc) * mine);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (kc + 1 < nchunks) issue(kc + 1, (kc + 1) & 1);
-        compute(lds + (kc & 1) * STAGE);
+        if (kc + S - 1 < nchunks) issue(kc + S - 1, (kc + S - 1) % S);
+        compute(lds + (kc % S) * STAGE);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
-// acc tile -> LDS fp32 [BM][64 + 4] (C/D map of 16x16: col = lane & 15, row = 4 (lane >> 4) + reg)
-template <int BM, int WM, int WN>
-__device__ __forceinline__ void x6_acc_to_lds(const floatx4 (&acc)[BM / WM / 16][64 / WN / 16], float *cl) {
-    constexpr int TM = BM / WM / 16, TN = 64 / WN / 16, LDC = 68;
+// acc tile -> LDS fp32 [BM][BN + 4] (C/D map of 16x16: col = lane & 15, row = 4 (lane >> 4) + reg)
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void x6_acc_to_lds(const floatx4 (&acc)[BM / WM / 16][BN / WN / 16], float *cl) {
+    constexpr int TM = BM / WM / 16, TN = BN / WN / 16, LDC = BN + 4;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wi = wave / WN, wj = wave % WN, g = lane >> 4, i16 = lane & 15;
 #pragma unroll
@@ -282,7 +320,7 @@ __device__ __forceinline__ void x6_acc_to_lds(const floatx4 (&acc)[BM / WM / 16]
         for (int b = 0; b < TN; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                cl[(wi * (BM / WM) + a * 16 + 4 * g + r) * LDC + wj * (64 / WN) + b * 16 + i16] = acc[a][b][r];
+                cl[(wi * (BM / WM) + a * 16 + 4 * g + r) * LDC + wj * (BN / WN) + b * 16 + i16] = acc[a][b][r];
 }
 
 struct X6PParams {
@@ -299,7 +337,7 @@ struct X6PParams {
 // epilogue (epilogue_v4: fp32 Z / Y and optionally the next layer's plane tiles).
 __global__ __launch_bounds__(512) void gemm_x6g_kernel(X6PParams P) {
     constexpr int BM = 64, NT = 512;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * x6_stage_bytes<BM>()];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * x6_stage_bytes<BM, 64>()];
     const int tile = xcd_tile(blockIdx.x, P.tiles_m * P.tiles_n);
     const int mt = tile / P.tiles_n, nt = tile % P.tiles_n;
     const int m0 = mt * BM, n0 = nt * X6_BN;
@@ -309,12 +347,13 @@ __global__ __launch_bounds__(512) void gemm_x6g_kernel(X6PParams P) {
     O.a0 = P.a0; O.nkc0 = P.kp0 >> 5; O.kc0 = P.ka0 >> 5;
     O.a1 = P.a1; O.nkc1 = P.kp1 >> 5; O.kc1 = P.ka1 >> 5;
     O.rb = mt;
+    O.a_rows = BM;
     O.b = P.b + (size_t)nt * (P.kpb >> 5) * X6_BLOCK;
     floatx4 acc[1][2];
-    x6_mainloop<BM, 4, 2>(O, lds, acc);
+    x6_mainloop<BM, 64, 4, 2>(O, lds, acc);
     __syncthreads();
     float *cl = reinterpret_cast<float *>(lds);
-    x6_acc_to_lds<BM, 4, 2>(acc, cl);
+    x6_acc_to_lds<BM, 64, 4, 2>(acc, cl);
     __syncthreads();
     epilogue_v4<BM, X6_BN, NT>(P.epi, cl, 68, m0, n0, P.M, P.N, ep);
 }

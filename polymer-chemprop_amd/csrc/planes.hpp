@@ -81,9 +81,11 @@ __device__ __forceinline__ void x6_store4(uint8_t *base, int kp, int r, int k, c
     *reinterpret_cast<uint2 *>(d + 2 * BR * 64) = make_uint2(l[0], l[1]);
 }
 
-// fp32 [rows][ld] (first kp columns) -> plane tiles [out_rows][kp] (BR = 64); one thread per 8 values.
+// fp32 [rows][ld] (first kp columns) -> plane tiles [out_rows][kp] with BR-row blocks; one thread per 8
+// values.
 // row_map == null: row r -> r (out_rows == rows); else row r -> row_map[r] (skipped when < 0) and every
 // output row that no source row maps to must be zero-filled by the caller.
+template <int BR = 64>
 __global__ __launch_bounds__(256) void split_tiles_kernel(const float *__restrict__ src, int ld, int rows, int kp,
                                                           uint8_t *__restrict__ dst,
                                                           const int32_t *__restrict__ row_map = nullptr) {
@@ -94,7 +96,7 @@ __global__ __launch_bounds__(256) void split_tiles_kernel(const float *__restric
         const int ro = row_map ? row_map[r] : r;
         if (ro < 0) continue;
         const float *s = src + (size_t)r * ld + k;
-        x6_store8(dst, kp, ro, k, ld4(s), ld4(s + 4));
+        x6_store8<BR>(dst, kp, ro, k, ld4(s), ld4(s + 4));
     }
 }
 

@@ -21,6 +21,7 @@
 #include <array>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -103,7 +104,8 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     D.ldx = D.atom ? D.Hk + D.Fbk : D.Hk;
     D.Ko = D.Fak + D.Hk;
     D.Kd = D.Hk + D.dk;
-    D.x6 = c->gemm_variant == 10 && !D.atom && !c->fuse_gather;
+    // default (0) = 10: bf16x6 split-plane GEMMs (fp32-accurate)
+    D.x6 = (c->gemm_variant == 10 || c->gemm_variant == 0) && !D.atom && !c->fuse_gather;
     D.blocked = D.x6 && !D.save && !D.desc && D.T >= 2 && g->n_blocks > 0 && g->blocks && g->bond_blk_row &&
                 g->f_atoms_blk_x6 && g->f_bonds_x6;
     D.nblk = D.blocked ? g->n_blocks : 0;
@@ -126,7 +128,8 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
 struct PackLayout {
     size_t Wi = 0, bi = 0, Wh = 0, bh = 0, Wo = 0, bo = 0, Wd = 0, bd = 0, WhT = 0, WoT = 0, WdT = 0, total = 0;
     size_t WiF = 0, WhF = 0, WoF = 0;  // fragment-order copies for gemm_fused_kernel
-    size_t WiX = 0, WhX = 0, WoX = 0;  // bf16x3 planes for gemm_x6_kernel
+    size_t WiX = 0, WhX = 0, WoX = 0;  // bf16x3 plane tiles (64-row blocks) of W_i / W_h / W_o
+    size_t WhX80 = 0, WoX80 = 0;       // the same with 80-row blocks (fused forward, Hk % 80 == 0)
 };
 
 PackLayout pack_layout(const Dims &D) {
@@ -147,6 +150,10 @@ PackLayout pack_layout(const Dims &D) {
     L.WiX = take((size_t)D.Hk * D.Kink * 3 / 2);  // 3 bf16 planes = 1.5 floats per value
     L.WhX = take((size_t)D.Hk * D.ldx * 3 / 2);
     L.WoX = take((size_t)D.Hk * D.Ko * 3 / 2);
+    if (D.Hk % 80 == 0) {
+        L.WhX80 = take((size_t)D.Hk * D.ldx * 3 / 2);
+        L.WoX80 = take((size_t)D.Hk * D.Ko * 3 / 2);
+    }
     if (D.desc) {
         L.Wd = take((size_t)D.Hdk * D.Kd);
         L.bd = take(D.Hdk);
@@ -212,8 +219,14 @@ int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
                                                       {L.Wo, L.WoX, (size_t)D.Ko}}};
     for (const auto &x : xs) {
         const int kp = (int)x[2];
-        hipLaunchKernelGGL(split_tiles_kernel, dim3(ew_blocks((size_t)D.Hk * kp / 8)), dim3(256), 0, st,
+        hipLaunchKernelGGL(split_tiles_kernel<64>, dim3(ew_blocks((size_t)D.Hk * kp / 8)), dim3(256), 0, st,
                            (const float *)(base + x[0]), kp, D.Hk, kp, (uint8_t *)(base + x[1]));
+    }
+    if (D.Hk % 80 == 0) {
+        hipLaunchKernelGGL(split_tiles_kernel<80>, dim3(ew_blocks((size_t)D.Hk * D.ldx / 8)), dim3(256), 0, st,
+                           (const float *)(base + L.Wh), D.ldx, D.Hk, D.ldx, (uint8_t *)(base + L.WhX80));
+        hipLaunchKernelGGL(split_tiles_kernel<80>, dim3(ew_blocks((size_t)D.Hk * D.Ko / 8)), dim3(256), 0, st,
+                           (const float *)(base + L.Wo), D.Ko, D.Hk, D.Ko, (uint8_t *)(base + L.WoX80));
     }
     WD_CHECK_LAUNCH("pack_params planes");
     return 0;
@@ -671,7 +684,7 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
     const int Hk = D.Hk;
 
     const bool fuse = c->fuse_gather != 0;
-    const int var = c->gemm_variant;
+    const int var = c->gemm_variant ? c->gemm_variant : 10;
     // plane-tile pipeline (D.x6): a GEMM without a plane copy of its A operand splits in the kernel
     const int var_split = var == 10 ? 12 : var;
     const char *pkb = pk;
@@ -682,20 +695,34 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
         e.planes = (uint8_t *)(ws + L.Mb[0]); e.plane_row = g->bond_blk_row; e.planes_kp = Hk;
         if (!x6g_eligible(e)) return fail(WD_ERR_SHAPE, "fused forward: unaligned buffers");
         WD_TRY(gemm_x6g(g->f_bonds_x6, g->ld_bonds, D.Kink, nullptr, 0, 0, pkb + PL.WiX, D.Rp, Hk, e, st));
+        // 80-column tiles when they divide Hk (Hk = 320: 4 tiles, one workgroup per CU at the benchmark
+        // size), else 64
+        const bool bn80 = Hk % 80 == 0;
+        const int BNf = bn80 ? 80 : 64;
         for (int t = 1; t < D.T; ++t) {
             MpLayerP M{};
             M.mprev = (const uint8_t *)(ws + L.Mb[(t - 1) & 1]); M.mnext = (uint8_t *)(ws + L.Mb[t & 1]); M.kp = Hk;
-            M.wh = (const uint8_t *)(pkb + PL.WhX); M.inp = F(L.Z[0]); M.bias = p->b_h ? W(PL.bh) : nullptr;
+            M.wh = (const uint8_t *)(pkb + (bn80 ? PL.WhX80 : PL.WhX)); M.inp = F(L.Z[0]);
+            M.bias = p->b_h ? W(PL.bh) : nullptr;
             M.blocks = g->blocks;
             M.ptr = g->msg_gather.ptr; M.idx = g->msg_gather.idx; M.coef = g->msg_gather.coef;
             M.sym_rev = D.undirected ? g->b2revb : nullptr;
             M.act = c->activation; M.slope = p->prelu; M.p_drop = c->dropout; M.seed = c->seed; M.layer = t;
             M.aptr = g->atom_gather.ptr; M.aidx = g->atom_gather.idx; M.acoef = g->atom_gather.coef;
             M.aplanes = (uint8_t *)(ws + L.Ab);
-            M.n_tiles = Hk / 64;
+            M.n_tiles = Hk / BNf;
+            const dim3 grid(D.nblk * M.n_tiles);
+            const bool last = t == D.T - 1;
             WD_TRY(record_prof(c, t - 1, 0, st));
-            if (t == D.T - 1) hipLaunchKernelGGL(mp_layer_kernel<true>, dim3(D.nblk * M.n_tiles), dim3(512), 0, st, M);
-            else hipLaunchKernelGGL(mp_layer_kernel<false>, dim3(D.nblk * M.n_tiles), dim3(512), 0, st, M);
+            if (bn80) {
+                const dim3 blk(64 * MpWaves<80>::WM * MpWaves<80>::WN);
+                if (last) hipLaunchKernelGGL((mp_layer_kernel<80, true>), grid, blk, 0, st, M);
+                else hipLaunchKernelGGL((mp_layer_kernel<80, false>), grid, blk, 0, st, M);
+            } else {
+                const dim3 blk(64 * MpWaves<64>::WM * MpWaves<64>::WN);
+                if (last) hipLaunchKernelGGL((mp_layer_kernel<64, true>), grid, blk, 0, st, M);
+                else hipLaunchKernelGGL((mp_layer_kernel<64, false>), grid, blk, 0, st, M);
+            }
             WD_CHECK_LAUNCH("mp_layer");
             WD_TRY(record_prof(c, t - 1, 1, st));
         }
@@ -703,13 +730,17 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
             WoReadoutP R{};
             R.fa = (const uint8_t *)g->f_atoms_blk_x6; R.kpa = g->ld_atoms; R.kca = D.Fak / 32;
             R.ag = (const uint8_t *)(ws + L.Ab); R.kp = Hk;
-            R.wo = (const uint8_t *)(pkb + PL.WoX); R.bias = W(PL.bo);
+            R.wo = (const uint8_t *)(pkb + (bn80 ? PL.WoX80 : PL.WoX)); R.bias = W(PL.bo);
             R.blocks = g->blocks;
             R.w_atoms = g->w_atoms; R.mol_start = g->mol_start; R.mol_size = g->mol_size; R.xn = g->degree_of_polym;
             R.agg = c->aggregation; R.norm = c->aggregation_norm; R.zero_vec = p->zero_vec;
             R.act = c->activation; R.slope = p->prelu; R.p_drop = c->dropout; R.seed = c->seed; R.layer = D.T;
-            R.out = out; R.ncols = D.H; R.n_tiles = Hk / 64;
-            hipLaunchKernelGGL(wo_readout_kernel, dim3(D.nblk * R.n_tiles), dim3(512), 0, st, R);
+            R.out = out; R.ncols = D.H; R.n_tiles = Hk / BNf;
+            const dim3 grid(D.nblk * R.n_tiles);
+            if (bn80)
+                hipLaunchKernelGGL(wo_readout_kernel<80>, grid, dim3(64 * WoWaves<80>::WM * WoWaves<80>::WN), 0, st, R);
+            else
+                hipLaunchKernelGGL(wo_readout_kernel<64>, grid, dim3(64 * WoWaves<64>::WM * WoWaves<64>::WN), 0, st, R);
             WD_CHECK_LAUNCH("wo_readout");
         }
         return 0;
@@ -990,7 +1021,7 @@ int wdmpnn_split_planes(const float *src, int32_t ld, int32_t rows, int32_t kp, 
         return fail(WD_ERR_SHAPE, "split_planes: rows %% 64, kp %% 32, ld >= kp, ld %% 4 and 16-byte alignment "
                                   "required (rows %d kp %d ld %d)", rows, kp, ld);
     if (dst_bytes < (size_t)rows * kp * 6) return fail(WD_ERR_WORKSPACE, "plane buffer too small");
-    hipLaunchKernelGGL(split_tiles_kernel, dim3(ew_blocks((size_t)rows * kp / 8)), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(split_tiles_kernel<64>, dim3(ew_blocks((size_t)rows * kp / 8)), dim3(256), 0, (hipStream_t)stream,
                        src, ld, rows, kp, (uint8_t *)dst);
     WD_CHECK_LAUNCH("split_planes");
     return 0;
@@ -1008,7 +1039,7 @@ int wdmpnn_split_planes_rows(const float *src, int32_t ld, int32_t rows, int32_t
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(dst, 0, need, st) != hipSuccess) return fail(WD_ERR_ARG, "memset failed");
     if (rows > 0)
-        hipLaunchKernelGGL(split_tiles_kernel, dim3(ew_blocks((size_t)rows * kp / 8)), dim3(256), 0, st, src, ld, rows,
+        hipLaunchKernelGGL(split_tiles_kernel<64>, dim3(ew_blocks((size_t)rows * kp / 8)), dim3(256), 0, st, src, ld, rows,
                            kp, (uint8_t *)dst, row_map);
     WD_CHECK_LAUNCH("split_planes_rows");
     return 0;

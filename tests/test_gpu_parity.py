@@ -249,3 +249,45 @@ def test_fused_and_unfused_paths_agree_in_training(extra):
                     **{n: t.grad.cpu().numpy() for n, t in enc.named_parameters() if t.grad is not None}})
     for k in res[0]:
         assert golden_io.normwise(res[0][k], res[1][k]) <= TOL, k
+
+
+@pytest.mark.parametrize('kind,b,hidden,depth,extra', [
+    ('polymer', 64, 300, 3, {}),                                        # bench config: 80-column tiles
+    ('polymer', 64, 300, 3, dict(activation='tanh', bias=True, aggregation='sum')),
+    ('polymer', 32, 300, 4, dict(undirected=True, activation='ELU', aggregation='norm')),
+    ('zinc', 64, 512, 5, dict(activation='LeakyReLU')),                 # 64-column tiles
+    ('qm9', 96, 128, 3, dict(activation='SELU', bias=True)),           # many molecules per block
+    ('polymer', 16, 70, 2, dict(activation='PReLU', bias=True)),       # Hk = 128, T = 2 (single layer)
+])
+def test_blocked_fused_forward(kind, b, hidden, depth, extra):
+    """The molecule-blocked fused inference forward (WdConfig.gemm_variant 10, no grad) matches the
+    fp32 oracle at 1e-5 normwise."""
+    args = TrainArgs(hidden_size=hidden, depth=depth, **extra)
+    g = BatchMolGraph(synthetic.make_batch(kind, b, 400 + b))
+    assert g.molecule_blocks() is not None
+    enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim())
+    synthetic.fill_parameters(enc, 12)
+    p = {n: t.detach().clone() for n, t in enc.named_parameters()}
+    ref = mpn_ref.encoder_forward(p, g, args)
+    enc = enc.to(DEV).eval()
+    enc._gemm_variant = 10
+    with torch.no_grad():
+        out = enc(g)
+    assert golden_io.normwise(out.cpu().numpy(), ref.numpy()) <= TOL
+
+
+def test_blocked_forward_edge_cases_and_fallback():
+    """Empty / single-atom molecules in blocks, and a 130-leaf hub molecule that exceeds a block (the
+    forward falls back to the unblocked plane-tile path)."""
+    args = TrainArgs(hidden_size=64, depth=3, bias=True)
+    for mols in (synthetic.edge_case_batch(9, star_leaves=20), synthetic.edge_case_batch(9, star_leaves=130)):
+        g = BatchMolGraph(mols)
+        enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim())
+        synthetic.fill_parameters(enc, 5)
+        p = {n: t.detach().clone() for n, t in enc.named_parameters()}
+        ref = mpn_ref.encoder_forward(p, g, args)
+        enc = enc.to(DEV).eval()
+        enc._gemm_variant = 10
+        with torch.no_grad():
+            out = enc(g)
+        assert golden_io.normwise(out.cpu().numpy(), ref.numpy()) <= TOL

@@ -76,22 +76,32 @@ __global__ __launch_bounds__(64 * NW) void stream_reg_kernel(const uint8_t *src,
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u && sink) sink[0] = 1;
 }
 
-// glds with NW waves per workgroup (24 KB per chunk), S = 2
-template <int NW>
+// glds with NW waves per workgroup (CB KB per chunk), S stages (S - 1 chunks in flight)
+template <int NW, int S, int CB = 24>
 __global__ __launch_bounds__(64 * NW) void stream_glds_w_kernel(const uint8_t *src, size_t span, int chunks, int *sink) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 24576];
-    constexpr int P = 24 / NW;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[S * CB * 1024];
+    constexpr int P = CB / NW;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const size_t base = ((size_t)blockIdx.x * 24576 * chunks) % span;
-    for (int c = 0; c < chunks; ++c) {
-        uint8_t *st = lds + (c & 1) * 24576;
-        const size_t off = base + (size_t)c * 24576;
+    auto issue = [&](int c) {
+        uint8_t *st = lds + (c % S) * CB * 1024;
+        const size_t off = base + (size_t)c * CB * 1024;
 #pragma unroll
         for (int j = 0; j < P; ++j)
             glds16(src + (off + (size_t)(P * wave + j) * 1024 + 16 * lane) % span, st + 1024 * (P * wave + j));
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    for (int c = 0; c < S - 1; ++c) issue(c);
+    for (int c = 0; c < chunks * 24 / CB; ++c) {
+        if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if constexpr (S * P == 9) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else if constexpr (S * P == 12) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else if constexpr (S * P == 6) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else if constexpr (S * P == 8) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        issue(c + S - 1);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0 && lds[blockIdx.x % 1024] == 123 && sink) sink[0] = 1;
 }
@@ -145,7 +155,12 @@ int main(int argc, char **argv) {
         for (size_t span : {(size_t)2 << 20, (size_t)64 << 20})
             for (int grid : {256, 512, 1024}) {
                 run_s("glds4w S=2", stream_lds_kernel<2>, span, grid);
-                run_w("glds8w S=2", stream_glds_w_kernel<8>, 512, span, grid);
+                run_w("glds8w S=2", stream_glds_w_kernel<8, 2>, 512, span, grid);
+                run_w("glds8w S=3", stream_glds_w_kernel<8, 3>, 512, span, grid);
+                run_w("glds8w S=4", stream_glds_w_kernel<8, 4>, 512, span, grid);
+                run_w("glds8w S=3 36K", stream_glds_w_kernel<8, 3, 32>, 512, span, grid);
+                run_w("glds16w S=2", stream_glds_w_kernel<16, 2, 32>, 1024, span, grid);
+                run_w("glds16w S=3", stream_glds_w_kernel<16, 3, 32>, 1024, span, grid);
                 run_w("reg4w D=2", stream_reg_kernel<4, 2>, 256, span, grid);
                 run_w("reg4w D=6", stream_reg_kernel<4, 6>, 256, span, grid);
                 run_w("reg8w D=3", stream_reg_kernel<8, 3>, 512, span, grid);
