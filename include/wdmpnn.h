@@ -112,6 +112,15 @@ typedef struct WdGraph {
     const int32_t *blocks;
     const int32_t *bond_blk_row;
     const void *f_atoms_blk_x6;
+    /* Required with blocks: the first 8 entries of every msg_gather / atom_gather row in block-local
+     * form ("ELL-8"), so that the fused kernels fetch a row's list with two independent loads instead
+     * of a ptr -> idx chain.  *_ell_idx[8 r + k] = idx - bond_start of the row's block (uint8, < 128),
+     * *_ell_coef[8 r + k] = coef; unused slots coef 0 and a valid index; bit 7 of slot 7 set when the
+     * row has more than 8 entries (the rest are read from the CSR lists). */
+    const uint8_t *msg_ell_idx;
+    const float *msg_ell_coef;
+    const uint8_t *atom_ell_idx;
+    const float *atom_ell_coef;
 } WdGraph;
 
 /* nn.Module parameters of MPNEncoder (mpn.py:17-64); all device pointers, row-major like nn.Linear. */

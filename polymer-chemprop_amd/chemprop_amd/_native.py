@@ -43,7 +43,9 @@ class WdGraph(Structure):
                 ('msg_gather_t', WdCsr), ('bond_feat_gather_t', WdCsr), ('atom_gather_t', WdCsr),
                 ('atom_desc', c_void_p), ('desc_dim', c_int32), ('atom_messages', c_int32),
                 ('f_atoms_x6', c_void_p), ('f_bonds_x6', c_void_p),
-                ('n_blocks', c_int32), ('blocks', c_void_p), ('bond_blk_row', c_void_p), ('f_atoms_blk_x6', c_void_p)]
+                ('n_blocks', c_int32), ('blocks', c_void_p), ('bond_blk_row', c_void_p), ('f_atoms_blk_x6', c_void_p),
+                ('msg_ell_idx', c_void_p), ('msg_ell_coef', c_void_p), ('atom_ell_idx', c_void_p),
+                ('atom_ell_coef', c_void_p)]
 
 
 class WdParams(Structure):

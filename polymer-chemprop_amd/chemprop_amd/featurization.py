@@ -92,6 +92,26 @@ class Csr:
         return out
 
 
+def ell8(c: 'Csr', rows_p: int, base: np.ndarray):
+    """First 8 entries of every CSR row in block-local form (WdGraph.*_ell_idx / *_ell_coef): index
+    idx - base[row] as uint8 (< 128), coefficient; unused slots (index 0, coef 0); bit 7 of slot 7 set
+    on rows with more than 8 entries."""
+    n = len(c.ptr) - 1
+    idx = np.zeros((rows_p, 8), np.uint8)
+    coef = np.zeros((rows_p, 8), np.float32)
+    cnt = np.diff(c.ptr)
+    row = np.repeat(np.arange(n), cnt)
+    slot = np.arange(len(row)) - np.repeat(c.ptr[:-1], cnt)
+    keep = slot < 8
+    local = c.idx[:len(row)].astype(np.int64) - base[row]
+    if len(local) and (local[keep].min() < 0 or local[keep].max() >= 128):
+        raise ValueError('ell8: an entry leaves its molecule block')
+    idx[row[keep], slot[keep]] = local[keep].astype(np.uint8)
+    coef[row[keep], slot[keep]] = c.coef[:len(row)][keep]
+    idx[:n, 7] |= np.where(cnt > 8, 0x80, 0).astype(np.uint8)
+    return idx.reshape(-1), coef.reshape(-1)
+
+
 class DeviceGraph:
     """Device-resident packed graph + the ctypes ``WdGraph`` pointing into it."""
 
@@ -340,6 +360,12 @@ class BatchMolGraph:
                   ('b2revb', self._np['b2revb'].astype(np.int32))]
         if blocks is not None and len(blocks):
             arrays += [('blocks', blocks), ('bond_blk_row', bond_blk), ('atom_blk_row', atom_blk)]
+            bstart = np.zeros(len(blocks) + 1, np.int64)
+            bstart[:-1] = blocks[:, 0]
+            for name, c, rows_p, rb in (('msg_ell', msg, fb_p.shape[0], blk_of_bond), ('agg_ell', agg, fa_p.shape[0],
+                                                                                     blk_of_atom)):
+                ell_idx, ell_coef = ell8(c, rows_p, bstart[rb[:len(c.ptr) - 1]])
+                arrays += [(name + '_idx', ell_idx), (name + '_coef', ell_coef)]
         csrs = [('msg', msg), ('agg', agg), ('msg_t', msg_t), ('agg_t', agg_t)]
         if feat is not None:
             csrs.append(('feat', feat))
@@ -398,6 +424,8 @@ class BatchMolGraph:
                                                          _native.current_stream(device)), 'blocked f_atoms planes')
                 views['f_atoms_blk_x6'] = planes
                 s.n_blocks, s.blocks, s.bond_blk_row = len(blocks), P('blocks'), P('bond_blk_row')
+                s.msg_ell_idx, s.msg_ell_coef = P('msg_ell_idx'), P('msg_ell_coef')
+                s.atom_ell_idx, s.atom_ell_coef = P('agg_ell_idx'), P('agg_ell_coef')
                 s.f_atoms_blk_x6 = planes.data_ptr()
         dg = DeviceGraph(buf, views, s)
         dg.host_csr = dict(csrs)

@@ -68,9 +68,11 @@ struct MpLayerP {
     const float *bias;          // b_h (padded) or null
     const int32_t *blocks;
     const int32_t *ptr, *idx; const float *coef;   // msg gather, natural rows
+    const uint8_t *ell_idx; const float *ell_coef;  // its first 8 entries per row, block-local (WdGraph)
     const int32_t *sym_rev;     // undirected (mpn.py:101-102) or null
     int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;
     const int32_t *aptr, *aidx; const float *acoef;  // atom gather (natural atom rows -> natural bond rows)
+    const uint8_t *aell_idx; const float *aell_coef;
     uint8_t *aplanes;           // A: blocked atom plane tiles [nblk * 64][kp]
     int n_tiles;                // Hk / BN
 };
@@ -89,24 +91,34 @@ template <int BN, bool LAST>
 __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_layer_kernel(MpLayerP P) {
     constexpr int BM = BLK_BONDS, LDC = BN + 4, WM = MpWaves<BN>::WM, WN = MpWaves<BN>::WN, NT = 64 * WM * WN;
     constexpr int UPR = BN / 8, UNITS = BM * UPR, UPT = (UNITS + NT - 1) / NT;  // 8-column epilogue units
-    constexpr int S = 2;  // (3 stages measured slower: the chunk time is not load-latency bound)
-    constexpr int LDS_BYTES = 2 * BM * LDC * 4 > S * x6_stage_bytes<BM, BN>() ? 2 * BM * LDC * 4
-                                                                             : S * x6_stage_bytes<BM, BN>();
+    // two stages of one chunk (measured: 3 stages slower; two-chunk stages, one barrier per two
+    // chunks, no faster: the chunk time is not bound by load latency or barriers)
+    constexpr int S = 2, CPS = 1;
+    constexpr int LDS_BYTES = 2 * BM * LDC * 4 > S * CPS * x6_stage_bytes<BM, BN>()
+                                  ? 2 * BM * LDC * 4
+                                  : S * CPS * x6_stage_bytes<BM, BN>();
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
     const int tile = xcd_tile(blockIdx.x, gridDim.x);
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
     const int tid = threadIdx.x;
-    // residual rows prefetched ahead of the GEMM (unit v = tid + NT i: row v / UPR, columns 8 (v % UPR) ..)
-    float4 res[UPT][2];
+    // residual rows and the rows' gather lists (ELL-8) prefetched ahead of the GEMM
+    // (unit v = tid + NT i: row v / UPR, columns 8 (v % UPR) ..)
+    float4 res[UPT][2], ecf[UPT][2];
+    uint2 eix[UPT];
 #pragma unroll
     for (int i = 0; i < UPT; ++i) {
         const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
-        res[i][0] = res[i][1] = f4zero();
+        res[i][0] = res[i][1] = ecf[i][0] = ecf[i][1] = f4zero();
+        eix[i] = make_uint2(0, 0);
         if (v < UNITS && lr < B.bn) {
-            const float *s = P.inp + (size_t)(B.bs + lr) * P.kp + n0 + c;
+            const size_t b = B.bs + lr;
+            const float *s = P.inp + b * P.kp + n0 + c;
             res[i][0] = ld4(s);
             res[i][1] = ld4(s + 4);
+            eix[i] = *reinterpret_cast<const uint2 *>(P.ell_idx + 8 * b);
+            ecf[i][0] = ld4(P.ell_coef + 8 * b);
+            ecf[i][1] = ld4(P.ell_coef + 8 * b + 4);
         }
     }
     X6Operands O{};
@@ -116,7 +128,7 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
     O.a_rows = B.bn;
     O.b = P.wh + (size_t)nt * (P.kp >> 5) * (3 * BN * 64);
     floatx4 acc[BM / WM / 16][BN / WN / 16];
-    x6_mainloop<BM, BN, WM, WN, S>(O, lds, acc);
+    x6_mainloop<BM, BN, WM, WN, S, CPS>(O, lds, acc);
     __syncthreads();
     float *Pt = reinterpret_cast<float *>(lds);
     float *Mt = Pt + BM * LDC;
@@ -131,22 +143,22 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
         float4 y0 = f4zero(), y1 = f4zero();
         if (lr < B.bn) {
             const int b = B.bs + lr;
-            const int e0 = P.ptr[b], e1 = P.ptr[b + 1];
             float4 s0 = f4zero(), s1 = f4zero();
-            // first G8 entries fetched together (lists are readable G8 past their end), then the rest
-            int jj[G8];
-            float ww[G8];
+            // the first 8 entries from the prefetched ELL row, in CSR order (the reference's slot order);
+            // unused slots have weight 0 and are skipped (the CSR lists hold no zero weights)
+            const uint32_t ix[2] = {eix[i].x, eix[i].y};
+            const float w8[8] = {ecf[i][0].x, ecf[i][0].y, ecf[i][0].z, ecf[i][0].w,
+                                 ecf[i][1].x, ecf[i][1].y, ecf[i][1].z, ecf[i][1].w};
 #pragma unroll
-            for (int k = 0; k < G8; ++k) {
-                jj[k] = P.idx[e0 + k];
-                ww[k] = P.coef ? P.coef[e0 + k] : 1.0f;
+            for (int k = 0; k < 8; ++k) {
+                const int j = (ix[k >> 2] >> (8 * (k & 3))) & 0x7f;
+                if (w8[k] == 0.f) continue;
+                if (P.sym_rev) msg_term<LDC>(Pt, B.bs + j, B.bs, P.sym_rev, c, w8[k], s0, s1);
+                else lds_term<LDC>(Pt, j, c, w8[k], s0, s1);
             }
-            // CSR order: the reference's slot order
-#pragma unroll
-            for (int k = 0; k < G8; ++k)
-                if (e0 + k < e1) msg_term<LDC>(Pt, jj[k], B.bs, P.sym_rev, c, ww[k], s0, s1);
-            for (int e = e0 + G8; e < e1; ++e)
-                msg_term<LDC>(Pt, P.idx[e], B.bs, P.sym_rev, c, P.coef ? P.coef[e] : 1.0f, s0, s1);
+            if (ix[1] & 0x80000000u)  // more than 8 entries: the rest from the CSR list
+                for (int e = P.ptr[b] + 8; e < P.ptr[b + 1]; ++e)
+                    msg_term<LDC>(Pt, P.idx[e], B.bs, P.sym_rev, c, P.coef ? P.coef[e] : 1.0f, s0, s1);
             float4 b0 = f4zero(), b1 = f4zero();
             if (P.bias) { b0 = ld4(P.bias + n0 + c); b1 = ld4(P.bias + n0 + c + 4); }
             float z[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
@@ -176,19 +188,17 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
             const int la = v / UPR, c = 8 * (v % UPR);
             float4 s0 = f4zero(), s1 = f4zero();
             if (la < B.an) {
-                const int a = B.as + la, e0 = P.aptr[a], e1 = P.aptr[a + 1];
-                int jj[G8];
-                float ww[G8];
+                const int a = B.as + la;
+                const uint2 e = *reinterpret_cast<const uint2 *>(P.aell_idx + 8 * (size_t)a);
+                const float4 w0 = ld4(P.aell_coef + 8 * (size_t)a), w1 = ld4(P.aell_coef + 8 * (size_t)a + 4);
+                const uint32_t ix[2] = {e.x, e.y};
+                const float w8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
-                for (int k = 0; k < G8; ++k) {
-                    jj[k] = P.aidx[e0 + k];
-                    ww[k] = P.acoef ? P.acoef[e0 + k] : 1.0f;
-                }
-#pragma unroll
-                for (int k = 0; k < G8; ++k)
-                    if (e0 + k < e1) lds_term<LDC>(Mt, jj[k] - B.bs, c, ww[k], s0, s1);
-                for (int e = e0 + G8; e < e1; ++e)
-                    lds_term<LDC>(Mt, P.aidx[e] - B.bs, c, P.acoef ? P.acoef[e] : 1.0f, s0, s1);
+                for (int k = 0; k < 8; ++k)
+                    if (w8[k] != 0.f) lds_term<LDC>(Mt, (ix[k >> 2] >> (8 * (k & 3))) & 0x7f, c, w8[k], s0, s1);
+                if (ix[1] & 0x80000000u)
+                    for (int q = P.aptr[a] + 8; q < P.aptr[a + 1]; ++q)
+                        lds_term<LDC>(Mt, P.aidx[q] - B.bs, c, P.acoef ? P.acoef[q] : 1.0f, s0, s1);
             }
             x6_store8<BLK_ATOMS>(P.aplanes, P.kp, blk * BLK_ATOMS + la, n0 + c, s0, s1);
         }
@@ -216,7 +226,8 @@ template <> struct WoWaves<80> { static constexpr int WM = 2, WN = 5; };
 template <int BN>
 __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_readout_kernel(WoReadoutP P) {
     constexpr int BM = BLK_ATOMS, LDC = BN + 4, WM = WoWaves<BN>::WM, WN = WoWaves<BN>::WN, NT = 64 * WM * WN;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * x6_stage_bytes<BM, BN>()];
+    constexpr int CPS = 1;  // chunks per barrier (see mp_layer_kernel)
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * CPS * x6_stage_bytes<BM, BN>()];
     const int tile = xcd_tile(blockIdx.x, gridDim.x);
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
@@ -228,7 +239,7 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     O.a_rows = B.an;
     O.b = P.wo + (size_t)nt * (P.kca + (P.kp >> 5)) * (3 * BN * 64);
     floatx4 acc[BM / WM / 16][BN / WN / 16];
-    x6_mainloop<BM, BN, WM, WN>(O, lds, acc);
+    x6_mainloop<BM, BN, WM, WN, 2, CPS>(O, lds, acc);
     __syncthreads();
     float *H = reinterpret_cast<float *>(lds);
     x6_acc_to_lds<BM, BN, WM, WN>(acc, H);

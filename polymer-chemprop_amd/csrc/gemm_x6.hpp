@@ -211,10 +211,10 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 }
 
 // acc[TM][TN] (+)= A(rb rows) · B(col tile)ᵀ for a BM x BN tile (BN = 64 or 80), waves WM x WN, wave
-// tile (BM / WM) x (BN / WN), S LDS stages (S - 1 chunks in flight behind the one multiplied).  Uses
-// lds[0 .. S * x6_stage_bytes<BM, BN>()); on return every DMA has landed and all waves are past their
-// last LDS read (the caller may reuse the LDS after one __syncthreads()).
-template <int BM, int BN, int WM, int WN, int S = 2>
+// tile (BM / WM) x (BN / WN), S LDS stages (S - 1 chunks in flight behind the one multiplied) of CPS
+// chunks each.  Uses lds[0 .. S * CPS * x6_stage_bytes<BM, BN>()); on return every DMA has landed and
+// all waves are past their last LDS read (the caller may reuse the LDS after one __syncthreads()).
+template <int BM, int BN, int WM, int WN, int S = 2, int CPS = 1>
 __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
                                             floatx4 (&acc)[BM / WM / 16][BN / WN / 16]) {
     constexpr int NW = WM * WN, TM = BM / WM / 16, TN = BN / WN / 16;
@@ -292,18 +292,40 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
     }
 #pragma unroll
     for (int j = 0; j < BPW; ++j) mine += BP % NW == 0 || j * NW + wave < BP;
+    if constexpr (CPS > 1) {
+        // CPS chunks per stage (two stages): one barrier per CPS chunks; stage s holds the chunk images
+        // of super-chunk s back to back
+        static_assert(S == 2, "multi-chunk stages use two stages");
+        const int nsc = (nchunks + CPS - 1) / CPS;
+        auto issue_sc = [&](int sc, int stage) {
 #pragma unroll
-    for (int c = 0; c < S - 1; ++c)
-        if (c < nchunks) issue(c, c);
-    for (int kc = 0; kc < nchunks; ++kc) {
-        // chunk kc landed for this wave (younger chunks kc+1 .. kc+S-2 may stay in flight), then for
-        // every wave; every wave is done reading stage (kc + S - 1) % S (= the one read at kc - 1)
-        if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else wait_vmcnt(min(S - 2, nchunks - 1 - kc) * mine);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (kc + S - 1 < nchunks) issue(kc + S - 1, (kc + S - 1) % S);
-        compute(lds + (kc % S) * STAGE);
+            for (int q = 0; q < CPS; ++q)
+                if (sc * CPS + q < nchunks) issue(sc * CPS + q, stage * CPS + q);
+        };
+        issue_sc(0, 0);
+        for (int sc = 0; sc < nsc; ++sc) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (sc + 1 < nsc) issue_sc(sc + 1, (sc + 1) & 1);
+#pragma unroll
+            for (int q = 0; q < CPS; ++q)
+                if (sc * CPS + q < nchunks) compute(lds + ((sc & 1) * CPS + q) * STAGE);
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < S - 1; ++c)
+            if (c < nchunks) issue(c, c);
+        for (int kc = 0; kc < nchunks; ++kc) {
+            // chunk kc landed for this wave (younger chunks kc+1 .. kc+S-2 may stay in flight), then for
+            // every wave; every wave is done reading stage (kc + S - 1) % S (= the one read at kc - 1)
+            if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else wait_vmcnt(min(S - 2, nchunks - 1 - kc) * mine);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (kc + S - 1 < nchunks) issue(kc + S - 1, (kc + S - 1) % S);
+            compute(lds + (kc % S) * STAGE);
+        }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }

@@ -107,7 +107,8 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     // default (0) = 10: bf16x6 split-plane GEMMs (fp32-accurate)
     D.x6 = (c->gemm_variant == 10 || c->gemm_variant == 0) && !D.atom && !c->fuse_gather;
     D.blocked = D.x6 && !D.save && !D.desc && D.T >= 2 && g->n_blocks > 0 && g->blocks && g->bond_blk_row &&
-                g->f_atoms_blk_x6 && g->f_bonds_x6;
+                g->f_atoms_blk_x6 && g->f_bonds_x6 && g->msg_ell_idx && g->msg_ell_coef && g->atom_ell_idx &&
+                g->atom_ell_coef;
     D.nblk = D.blocked ? g->n_blocks : 0;
     if (D.atom && D.undirected)
         return fail(WD_ERR_UNSUPPORTED, "undirected with atom_messages (the reference indexes atom messages "
@@ -706,9 +707,11 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
             M.bias = p->b_h ? W(PL.bh) : nullptr;
             M.blocks = g->blocks;
             M.ptr = g->msg_gather.ptr; M.idx = g->msg_gather.idx; M.coef = g->msg_gather.coef;
+            M.ell_idx = g->msg_ell_idx; M.ell_coef = g->msg_ell_coef;
             M.sym_rev = D.undirected ? g->b2revb : nullptr;
             M.act = c->activation; M.slope = p->prelu; M.p_drop = c->dropout; M.seed = c->seed; M.layer = t;
             M.aptr = g->atom_gather.ptr; M.aidx = g->atom_gather.idx; M.acoef = g->atom_gather.coef;
+            M.aell_idx = g->atom_ell_idx; M.aell_coef = g->atom_ell_coef;
             M.aplanes = (uint8_t *)(ws + L.Ab);
             M.n_tiles = Hk / BNf;
             const dim3 grid(D.nblk * M.n_tiles);

@@ -86,6 +86,60 @@ def test_get_b2b_matches_reference_definition():
     assert torch.equal(b2b, ref)
 
 
+@pytest.mark.parametrize('kind', sorted(GRAPHS))
+def test_molecule_blocks_cover_molecules_and_contain_their_gathers(kind):
+    """WdGraph.blocks (fused forward): consecutive whole molecules, capacity limits respected, every
+    bond / atom row in exactly one block, and every gather entry of a row inside the row's block."""
+    from chemprop_amd.featurization import BLK_ATOMS, BLK_BONDS
+    g = BatchMolGraph(GRAPHS[kind]() if kind != 'edge' else synthetic.edge_case_batch(3, star_leaves=40))
+    blocks = g.molecule_blocks()
+    assert blocks is not None
+    assert blocks[0, 4] == 0 and blocks[-1, 5] == len(g.a_scope)
+    assert np.all(blocks[1:, 4] == blocks[:-1, 5])
+    assert np.all(blocks[:, 1] <= BLK_BONDS) and np.all(blocks[:, 3] <= BLK_ATOMS)
+    for k, (bs, bn, as_, an, ml, mh, _, _) in enumerate(blocks):
+        assert bn == sum(n for _, n in g.b_scope[ml:mh]) and an == sum(n for _, n in g.a_scope[ml:mh])
+    blk_b = np.full(g.n_bonds, -1)
+    for k, (bs, bn) in enumerate(blocks[:, :2]):
+        blk_b[bs:bs + bn] = k
+    assert np.all(blk_b[1:] >= 0)  # every real bond row in a block
+    csr = g.bond_message_gather()
+    row = np.repeat(np.arange(csr.rows), np.diff(csr.ptr))
+    assert np.array_equal(blk_b[row], blk_b[csr.idx])
+
+
+def test_molecule_blocks_refuse_an_oversized_molecule():
+    g = BatchMolGraph(synthetic.edge_case_batch(5, star_leaves=130))  # 131 atoms > BLK_ATOMS
+    assert g.molecule_blocks() is None
+
+
+@pytest.mark.parametrize('kind', sorted(GRAPHS))
+def test_ell8_restates_the_gather_lists(kind):
+    """The block-local ELL-8 rows (WdGraph.*_ell_*) hold the first 8 CSR entries of every row (unused
+    slots weight 0, bit 7 of slot 7 marks longer rows): applying them plus the CSR tail equals the CSR."""
+    from chemprop_amd.featurization import ell8
+    g = BatchMolGraph(GRAPHS[kind]() if kind != 'edge' else synthetic.edge_case_batch(3, star_leaves=40))
+    blocks = g.molecule_blocks()
+    bstart = np.zeros(len(blocks) + 1, np.int64)
+    bstart[:-1] = blocks[:, 0]
+    blk_b = np.full(g.n_bonds, -1)
+    for k, (bs, bn) in enumerate(blocks[:, :2]):
+        blk_b[bs:bs + bn] = k
+    csr = g.bond_message_gather()
+    idx, coef = ell8(csr, csr.rows, bstart[blk_b])
+    idx, coef = idx.reshape(-1, 8), coef.reshape(-1, 8)
+    S = rand((g.n_bonds, 4), 9)
+    out = np.zeros((csr.rows, 4))
+    for r in range(1, csr.rows):
+        base = bstart[blk_b[r]]
+        for k in range(8):
+            out[r] += coef[r, k] * S[base + (idx[r, k] & 0x7f)]
+        assert bool(idx[r, 7] & 0x80) == (csr.ptr[r + 1] - csr.ptr[r] > 8)
+        for e in range(csr.ptr[r] + 8, csr.ptr[r + 1]):
+            out[r] += csr.coef[e] * S[csr.idx[e]]
+    np.testing.assert_allclose(out[1:], csr.apply(S)[1:], rtol=1e-6, atol=1e-6)
+
+
 @pytest.mark.parametrize('name', golden_io.golden_names())
 def test_golden_graphs_gather_lists_consistent(name):
     case = golden_io.load(name)
