@@ -37,6 +37,7 @@ from chemprop_amd.nn_utils import initialize_weights  # noqa: E402
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 (the split-plane GEMMs issue 6 bf16 products per fp32 product)
 HBM_PEAK_GBS = 8000.0
+PMC_TRAFFIC = "round1_pmc_traffic.json"  # per-kernel HBM bytes per launch (tools/pmc_summary.py)
 
 
 def log(*a):
@@ -67,6 +68,21 @@ def cpu_baseline(args, graph, seconds):
     return {'value': (graph.n_bonds - 1) / med, 'unit': 'edges/s', 'cores': torch.get_num_threads(), 'kind': 'port',
             'sample': f'{len(times)} forwards of one polymer B={len(graph.a_scope)} batch (E={graph.n_bonds - 1} '
                       f'directed edges), median {med * 1e3:.2f} ms, torch {torch.__version__} CPU, eval/no_grad'}
+
+
+def pmc_traffic(prefix):
+    """HBM bytes per launch of the kernels named prefix* (mean over their variants), from the PMC
+    summary tools/pmc.sh + tools/pmc_summary.py committed for this build (counters need their own
+    rocprofv3 pass, so the bench cannot collect them while it times)."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', PMC_TRAFFIC)
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    v = [x['traffic_bytes'] for k, x in d.items() if k.startswith(prefix)]
+    if not v:
+        return None, None
+    return sum(v) / len(v), f'profiles/{PMC_TRAFFIC}: {d.get("_note", "")}'
 
 
 def main():
@@ -163,6 +179,7 @@ def main():
         flops_launch = 2.0 * E_avg * H * H + 2.0 * E_avg * d_avg * H
         bytes_launch = 4.0 * (3 * E_avg * H + H * H + H) + 8.0 * E_avg * d_avg + 4.0 * E_avg
         avg_launch_s = (kernel_ms.value / 1e3 / n_launch) if n_launch else float('nan')
+        traffic, traffic_src = pmc_traffic('mp_layer_kernel')
         achieved = flops_launch / avg_launch_s / 1e12 if n_launch else None
         hbm = bytes_launch / avg_launch_s / 1e9 if n_launch else None
         line = {
@@ -189,7 +206,8 @@ def main():
                          'kernel': 'mp_layer_kernel: one message-passing layer, W_h split-plane GEMM + in-block CSR '
                                    'gather + residual/activation (mpn.py:110-124)',
                          'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                         'frac': achieved / FP32_MFMA_PEAK_TFLOPS if achieved else None, 'traffic': None,
+                         'frac': achieved / FP32_MFMA_PEAK_TFLOPS if achieved else None, 'traffic': traffic,
+                         'traffic_source': traffic_src,
                          'peak_note': 'fp32 dense MFMA peak; the kernel issues bf16 MFMAs, whose fp32-product '
                                       f'equivalent peak is {BF16_MFMA_PEAK_TFLOPS / 6:.0f} TFLOP/s',
                          'avg_launch_us': avg_launch_s * 1e6, 'flops_per_launch': flops_launch,

@@ -112,6 +112,16 @@ def ell8(c: 'Csr', rows_p: int, base: np.ndarray):
     return idx.reshape(-1), coef.reshape(-1)
 
 
+def _packer():
+    """The native packer extension (built in-tree by __graft_entry__.build()); no Python fallback."""
+    try:
+        from . import _wdpack
+    except ImportError as e:  # pragma: no cover - exercised only on an unbuilt tree
+        raise ImportError('chemprop_amd._wdpack is not built: run `python -c "import __graft_entry__ as g; '
+                          'g.build()"` (g++ csrc/packer.cpp)') from e
+    return _wdpack
+
+
 class DeviceGraph:
     """Device-resident packed graph + the ctypes ``WdGraph`` pointing into it."""
 
@@ -123,7 +133,7 @@ class DeviceGraph:
 
 
 class BatchMolGraph:
-    """featurization.py:742-875, packed with numpy."""
+    """featurization.py:742-875; the tables are concatenated by the native packer (csrc/packer.cpp)."""
 
     def __init__(self, mol_graphs: Sequence):
         self.overwrite_default_atom_features = mol_graphs[0].overwrite_default_atom_features
@@ -131,45 +141,33 @@ class BatchMolGraph:
         self.atom_fdim = get_atom_fdim(overwrite_default_atom=self.overwrite_default_atom_features)
         self.bond_fdim = get_bond_fdim(overwrite_default_bond=self.overwrite_default_bond_features,
                                        overwrite_default_atom=self.overwrite_default_atom_features)
-        na = np.array([g.n_atoms for g in mol_graphs], np.int64)
-        nb = np.array([g.n_bonds for g in mol_graphs], np.int64)
+        fa_w = next((len(g.f_atoms[0]) for g in mol_graphs if g.n_atoms), self.atom_fdim)
+        fb_w = next((len(g.f_bonds[0]) for g in mol_graphs if g.n_bonds), self.bond_fdim)
+        # native packer (csrc/packer.cpp): concatenation at the reference's offsets, pad row 0
+        # (featurization.py:767-793), a2b as CSR (deg + in_idx in slot order)
+        (f_atoms, f_bonds, w_atoms, w_bonds, b2a, b2revb, deg, in_idx, na, nb) = \
+            _packer().pack(mol_graphs, int(fa_w), int(fb_w))
+        na = np.frombuffer(na, np.int64)
+        nb = np.frombuffer(nb, np.int64)
+        V, E = int(na.sum()), int(nb.sum())
+        f_atoms = np.frombuffer(f_atoms, np.float32).reshape(V + 1, fa_w)
+        f_bonds = np.frombuffer(f_bonds, np.float32).reshape(E + 1, fb_w)
+        w_atoms = np.frombuffer(w_atoms, np.float32)
+        w_bonds = np.frombuffer(w_bonds, np.float32)
+        b2a = np.frombuffer(b2a, np.int64)
+        b2revb = np.frombuffer(b2revb, np.int64)
+        deg = np.frombuffer(deg, np.int64)
         a_off = 1 + np.concatenate([[0], np.cumsum(na)[:-1]]).astype(np.int64)
         b_off = 1 + np.concatenate([[0], np.cumsum(nb)[:-1]]).astype(np.int64)
-        V, E = int(na.sum()), int(nb.sum())
         self.n_atoms = V + 1
         self.n_bonds = E + 1
         self.a_scope: List[Tuple[int, int]] = [(int(s), int(n)) for s, n in zip(a_off, na)]
         self.b_scope: List[Tuple[int, int]] = [(int(s), int(n)) for s, n in zip(b_off, nb)]
         self.degree_of_polym = [g.degree_of_polym for g in mol_graphs]
-
-        def stack_rows(name, width):
-            parts = [np.asarray(getattr(g, name), np.float32).reshape(-1, width) for g in mol_graphs
-                     if len(getattr(g, name))]
-            body = np.concatenate(parts) if parts else np.zeros((0, width), np.float32)
-            return np.concatenate([np.zeros((1, width), np.float32), body])
-
-        fa_w = next((len(g.f_atoms[0]) for g in mol_graphs if g.n_atoms), self.atom_fdim)
-        fb_w = next((len(g.f_bonds[0]) for g in mol_graphs if g.n_bonds), self.bond_fdim)
-        f_atoms = stack_rows('f_atoms', fa_w)
-        f_bonds = stack_rows('f_bonds', fb_w)
-        w_atoms = np.concatenate([[0.0]] + [np.asarray(g.w_atoms, np.float32) for g in mol_graphs]).astype(np.float32)
-        w_bonds = np.concatenate([[0.0]] + [np.asarray(g.w_bonds, np.float32) for g in mol_graphs]).astype(np.float32)
-        b2a = np.concatenate([[0]] + [np.asarray(g.b2a, np.int64) + o for g, o in zip(mol_graphs, a_off)])
-        b2revb = np.concatenate([[0]] + [np.asarray(g.b2revb, np.int64) + o for g, o in zip(mol_graphs, b_off)])
-        # a2b as CSR over atoms 0..V (atom 0 = pad, empty list)
-        deg = np.zeros(V + 1, np.int64)
-        idx_parts = []
-        for g, ao, bo in zip(mol_graphs, a_off, b_off):
-            lens = [len(l) for l in g.a2b]
-            if lens:
-                deg[ao:ao + len(lens)] = lens
-            flat = [b for l in g.a2b for b in l]
-            if flat:
-                idx_parts.append(np.asarray(flat, np.int64) + bo)
         in_ptr = np.zeros(V + 2, np.int64)
         np.cumsum(deg, out=in_ptr[1:])
         self._in_ptr = in_ptr
-        self._in_idx = np.concatenate(idx_parts) if idx_parts else np.zeros(0, np.int64)
+        self._in_idx = np.frombuffer(in_idx, np.int64)
         self._deg = deg
         self.max_num_bonds = max(1, int(deg.max()) if len(deg) else 0)  # featurization.py:802-803
 

@@ -1,0 +1,294 @@
+// packer.cpp — native batch packer for BatchMolGraph.
+//
+// Replaces the Python loops of the reference's BatchMolGraph.__init__ (featurization.py:757-813):
+// the per-molecule MolGraph lists (f_atoms / f_bonds rows, w_atoms, w_bonds, a2b, b2a, b2revb,
+// featurization.py:489-637 builds them as Python lists) are concatenated with the reference's
+// offsets — row 0 of every atom / bond table is the zero pad (featurization.py:767-781), atom ids
+// shift by 1 + atoms before the molecule, bond ids by 1 + bonds before it (:788-793) — straight into
+// contiguous float32 / int64 buffers, reading the Python objects once.  The reference then builds
+// torch tensors from nested lists (:805-811); that conversion is what costs the 77 ms per 64-polymer
+// batch.  The CSR form of a2b (in_ptr from deg, in_idx in a2b slot order) replaces
+// the padded a2b tensor, which the host rebuilds on demand (BatchMolGraph.a2b).
+//
+// CPython extension, no numpy headers: the outputs are bytearrays the caller views with
+// np.frombuffer (no copy).  Rows may be lists / tuples of numbers or objects with the buffer
+// protocol (a 2-D numpy table per molecule, or 1-D rows), float32/float64/int.  Single-threaded (it
+// reads Python objects, so it holds the GIL); data parallelism comes from one packer per DataLoader
+// worker / rank.
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+namespace {
+
+struct PyErrAlready {};  // a Python exception is set; unwind to the entry point
+
+[[noreturn]] void fail(PyObject *type, const std::string &msg) {
+    PyErr_SetString(type, msg.c_str());
+    throw PyErrAlready{};
+}
+
+struct Ref {  // owned reference
+    PyObject *p;
+    explicit Ref(PyObject *o) : p(o) { if (!p) throw PyErrAlready{}; }
+    ~Ref() { Py_XDECREF(p); }
+    Ref(const Ref &) = delete;
+    Ref &operator=(const Ref &) = delete;
+};
+
+inline double to_double(PyObject *o) {
+    if (PyFloat_CheckExact(o)) return PyFloat_AS_DOUBLE(o);
+    if (PyLong_CheckExact(o)) {
+        const double v = PyLong_AsDouble(o);
+        if (v == -1.0 && PyErr_Occurred()) throw PyErrAlready{};
+        return v;
+    }
+    const double v = PyFloat_AsDouble(o);  // bool, numpy scalars, __float__
+    if (v == -1.0 && PyErr_Occurred()) throw PyErrAlready{};
+    return v;
+}
+
+inline int64_t to_int64(PyObject *o) {
+    if (PyLong_CheckExact(o)) {
+        const long long v = PyLong_AsLongLong(o);
+        if (v == -1 && PyErr_Occurred()) throw PyErrAlready{};
+        return v;
+    }
+    Ref i(PyNumber_Index(o));  // numpy integers
+    const long long v = PyLong_AsLongLong(i.p);
+    if (v == -1 && PyErr_Occurred()) throw PyErrAlready{};
+    return v;
+}
+
+// copy n elements of a C-contiguous buffer (format f/d/e-less ints) converting to T
+template <typename T>
+void buffer_copy(const Py_buffer &b, Py_ssize_t n, T *dst, const char *what) {
+    const char *f = b.format ? b.format : "B";
+    if (*f == '<' || *f == '=' || *f == '@') ++f;
+    const char *src = static_cast<const char *>(b.buf);
+    switch (*f) {
+    case 'f': for (Py_ssize_t i = 0; i < n; ++i) { float v; std::memcpy(&v, src + 4 * i, 4); dst[i] = (T)v; } break;
+    case 'd': for (Py_ssize_t i = 0; i < n; ++i) { double v; std::memcpy(&v, src + 8 * i, 8); dst[i] = (T)v; } break;
+    case 'q': case 'l':
+        if (b.itemsize != 8) goto bad;
+        for (Py_ssize_t i = 0; i < n; ++i) { int64_t v; std::memcpy(&v, src + 8 * i, 8); dst[i] = (T)v; } break;
+    case 'i': for (Py_ssize_t i = 0; i < n; ++i) { int32_t v; std::memcpy(&v, src + 4 * i, 4); dst[i] = (T)v; } break;
+    case 'B': case '?': for (Py_ssize_t i = 0; i < n; ++i) dst[i] = (T)(uint8_t)src[i]; break;
+    case 'b': for (Py_ssize_t i = 0; i < n; ++i) dst[i] = (T)(int8_t)src[i]; break;
+    default:
+    bad:
+        fail(PyExc_TypeError, std::string(what) + ": unsupported buffer element format '" + f + "'");
+    }
+}
+
+struct Buf {  // a C-contiguous Py_buffer, released on scope exit
+    Py_buffer b{};
+    bool ok = false;
+    Buf(PyObject *o) {
+        if (PyObject_GetBuffer(o, &b, PyBUF_C_CONTIGUOUS | PyBUF_FORMAT) == 0) ok = true;
+        else PyErr_Clear();
+    }
+    ~Buf() { if (ok) PyBuffer_Release(&b); }
+};
+
+// `rows`: n_rows rows of `width` numbers -> dst[r * width ..]
+void fill_table(PyObject *rows, Py_ssize_t n_rows, Py_ssize_t width, float *dst, const char *what) {
+    if (n_rows == 0) return;
+    if (!PyList_Check(rows) && !PyTuple_Check(rows) && PyObject_CheckBuffer(rows)) {
+        Buf t(rows);
+        if (t.ok) {
+            if (t.b.ndim != 2 || t.b.shape[0] != n_rows || t.b.shape[1] != width)
+                fail(PyExc_ValueError, std::string(what) + ": table shape does not match (rows, width)");
+            buffer_copy(t.b, n_rows * width, dst, what);
+            return;
+        }
+    }
+    Ref seq(PySequence_Fast(rows, what));
+    if (PySequence_Fast_GET_SIZE(seq.p) != n_rows)
+        fail(PyExc_ValueError, std::string(what) + ": row count differs from the graph's count");
+    PyObject **items = PySequence_Fast_ITEMS(seq.p);
+    for (Py_ssize_t r = 0; r < n_rows; ++r) {
+        PyObject *row = items[r];
+        float *d = dst + r * width;
+        if (PyList_Check(row) || PyTuple_Check(row)) {
+            const Py_ssize_t n = PyList_Check(row) ? PyList_GET_SIZE(row) : PyTuple_GET_SIZE(row);
+            if (n != width) fail(PyExc_ValueError, std::string(what) + ": ragged feature rows");
+            PyObject **it = PyList_Check(row) ? &PyList_GET_ITEM(row, 0) : &PyTuple_GET_ITEM(row, 0);
+            for (Py_ssize_t k = 0; k < n; ++k) d[k] = (float)to_double(it[k]);
+            continue;
+        }
+        Buf rb(row);
+        if (rb.ok) {
+            if (rb.b.ndim != 1 || rb.b.shape[0] != width)
+                fail(PyExc_ValueError, std::string(what) + ": ragged feature rows");
+            buffer_copy(rb.b, width, d, what);
+            continue;
+        }
+        Ref rs(PySequence_Fast(row, what));
+        if (PySequence_Fast_GET_SIZE(rs.p) != width) fail(PyExc_ValueError, std::string(what) + ": ragged feature rows");
+        PyObject **it = PySequence_Fast_ITEMS(rs.p);
+        for (Py_ssize_t k = 0; k < width; ++k) d[k] = (float)to_double(it[k]);
+    }
+}
+
+// a 1-D sequence of n numbers -> dst[i] = conv(x_i) + add
+template <typename T>
+void fill_vector(PyObject *v, Py_ssize_t n, T *dst, T add, const char *what) {
+    if (n == 0) return;
+    if (!PyList_Check(v) && !PyTuple_Check(v) && PyObject_CheckBuffer(v)) {
+        Buf t(v);
+        if (t.ok) {
+            if (t.b.ndim != 1 || t.b.shape[0] != n)
+                fail(PyExc_ValueError, std::string(what) + ": length differs from the graph's count");
+            buffer_copy(t.b, n, dst, what);
+            for (Py_ssize_t i = 0; i < n; ++i) dst[i] += add;
+            return;
+        }
+    }
+    Ref seq(PySequence_Fast(v, what));
+    if (PySequence_Fast_GET_SIZE(seq.p) != n)
+        fail(PyExc_ValueError, std::string(what) + ": length differs from the graph's count");
+    PyObject **it = PySequence_Fast_ITEMS(seq.p);
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        if constexpr (std::is_integral<T>::value) dst[i] = (T)to_int64(it[i]) + add;
+        else dst[i] = (T)to_double(it[i]) + add;
+    }
+}
+
+Py_ssize_t attr_int(PyObject *g, const char *name) {
+    Ref a(PyObject_GetAttrString(g, name));
+    return (Py_ssize_t)to_int64(a.p);
+}
+
+PyObject *new_bytes(Py_ssize_t n) {
+    PyObject *b = PyByteArray_FromStringAndSize(nullptr, n);
+    if (!b) throw PyErrAlready{};
+    if (n) std::memset(PyByteArray_AS_STRING(b), 0, (size_t)n);
+    return b;
+}
+
+// pack(mol_graphs, fa_w, fb_w) -> (f_atoms, f_bonds, w_atoms, w_bonds, b2a, b2revb, deg, in_idx,
+// n_atoms_per_mol, n_bonds_per_mol) as bytearrays (float32 [V+1][fa_w], float32 [E+1][fb_w],
+// float32 [V+1], float32 [E+1], int64 [E+1] x 2, int64 [V+1], int64 [nnz], int64 [B] x 2)
+PyObject *pack(PyObject *, PyObject *args) {
+    PyObject *graphs_obj;
+    Py_ssize_t fa_w, fb_w;
+    if (!PyArg_ParseTuple(args, "Onn", &graphs_obj, &fa_w, &fb_w)) return nullptr;
+    PyObject *out[10] = {};
+    try {
+        Ref graphs(PySequence_Fast(graphs_obj, "mol_graphs must be a sequence"));
+        const Py_ssize_t B = PySequence_Fast_GET_SIZE(graphs.p);
+        PyObject **gs = PySequence_Fast_ITEMS(graphs.p);
+        // pass 1: counts (featurization.py:784-786 read n_atoms / n_bonds), a2b sizes
+        std::vector<int64_t> na(B), nb(B), nnz_of(B);
+        int64_t V = 0, E = 0, nnz = 0;
+        for (Py_ssize_t i = 0; i < B; ++i) {
+            na[i] = attr_int(gs[i], "n_atoms");
+            nb[i] = attr_int(gs[i], "n_bonds");
+            if (na[i] < 0 || nb[i] < 0) fail(PyExc_ValueError, "negative n_atoms / n_bonds");
+            Ref a2b(PyObject_GetAttrString(gs[i], "a2b"));
+            Ref seq(PySequence_Fast(a2b.p, "a2b must be a sequence of sequences"));
+            if (PySequence_Fast_GET_SIZE(seq.p) != na[i]) fail(PyExc_ValueError, "len(a2b) != n_atoms");
+            int64_t c = 0;
+            for (Py_ssize_t a = 0; a < na[i]; ++a) {
+                const Py_ssize_t l = PyObject_Length(PySequence_Fast_GET_ITEM(seq.p, a));
+                if (l < 0) throw PyErrAlready{};
+                c += l;
+            }
+            nnz_of[i] = c;
+            V += na[i]; E += nb[i]; nnz += c;
+        }
+        out[0] = new_bytes((V + 1) * fa_w * 4);
+        out[1] = new_bytes((E + 1) * fb_w * 4);
+        out[2] = new_bytes((V + 1) * 4);
+        out[3] = new_bytes((E + 1) * 4);
+        out[4] = new_bytes((E + 1) * 8);
+        out[5] = new_bytes((E + 1) * 8);
+        out[6] = new_bytes((V + 1) * 8);
+        out[7] = new_bytes(nnz * 8);
+        out[8] = new_bytes(B * 8);
+        out[9] = new_bytes(B * 8);
+        float *f_atoms = reinterpret_cast<float *>(PyByteArray_AS_STRING(out[0]));
+        float *f_bonds = reinterpret_cast<float *>(PyByteArray_AS_STRING(out[1]));
+        float *w_atoms = reinterpret_cast<float *>(PyByteArray_AS_STRING(out[2]));
+        float *w_bonds = reinterpret_cast<float *>(PyByteArray_AS_STRING(out[3]));
+        int64_t *b2a = reinterpret_cast<int64_t *>(PyByteArray_AS_STRING(out[4]));
+        int64_t *b2revb = reinterpret_cast<int64_t *>(PyByteArray_AS_STRING(out[5]));
+        int64_t *deg = reinterpret_cast<int64_t *>(PyByteArray_AS_STRING(out[6]));
+        int64_t *in_idx = reinterpret_cast<int64_t *>(PyByteArray_AS_STRING(out[7]));
+        std::memcpy(PyByteArray_AS_STRING(out[8]), na.data(), B * 8);
+        std::memcpy(PyByteArray_AS_STRING(out[9]), nb.data(), B * 8);
+        // pass 2: rows at the reference's offsets (row 0 stays the zero pad)
+        int64_t ao = 1, bo = 1, eo = 0;
+        for (Py_ssize_t i = 0; i < B; ++i) {
+            PyObject *g = gs[i];
+            {
+                Ref t(PyObject_GetAttrString(g, "f_atoms"));
+                fill_table(t.p, na[i], fa_w, f_atoms + ao * fa_w, "f_atoms");
+            }
+            {
+                Ref t(PyObject_GetAttrString(g, "f_bonds"));
+                fill_table(t.p, nb[i], fb_w, f_bonds + bo * fb_w, "f_bonds");
+            }
+            {
+                Ref t(PyObject_GetAttrString(g, "w_atoms"));
+                fill_vector<float>(t.p, na[i], w_atoms + ao, 0.f, "w_atoms");
+            }
+            {
+                Ref t(PyObject_GetAttrString(g, "w_bonds"));
+                fill_vector<float>(t.p, nb[i], w_bonds + bo, 0.f, "w_bonds");
+            }
+            {
+                Ref t(PyObject_GetAttrString(g, "b2a"));
+                fill_vector<int64_t>(t.p, nb[i], b2a + bo, ao, "b2a");
+            }
+            {
+                Ref t(PyObject_GetAttrString(g, "b2revb"));
+                fill_vector<int64_t>(t.p, nb[i], b2revb + bo, bo, "b2revb");
+            }
+            {
+                Ref a2b(PyObject_GetAttrString(g, "a2b"));
+                Ref seq(PySequence_Fast(a2b.p, "a2b must be a sequence of sequences"));
+                int64_t c = 0;
+                for (Py_ssize_t a = 0; a < na[i]; ++a) {
+                    PyObject *l = PySequence_Fast_GET_ITEM(seq.p, a);
+                    const Py_ssize_t n = PyObject_Length(l);
+                    if (n < 0) throw PyErrAlready{};
+                    if (c + n > nnz_of[i]) fail(PyExc_ValueError, "a2b changed while packing");
+                    deg[ao + a] = n;
+                    fill_vector<int64_t>(l, n, in_idx + eo + c, bo, "a2b");
+                    c += n;
+                }
+            }
+            ao += na[i]; bo += nb[i]; eo += nnz_of[i];
+        }
+        PyObject *res = PyTuple_New(10);
+        if (!res) throw PyErrAlready{};
+        for (int k = 0; k < 10; ++k) PyTuple_SET_ITEM(res, k, out[k]);  // steals
+        return res;
+    } catch (const PyErrAlready &) {
+    } catch (const std::exception &e) {
+        PyErr_SetString(PyExc_RuntimeError, e.what());
+    }
+    for (PyObject *o : out) Py_XDECREF(o);
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_RuntimeError, "pack failed");
+    return nullptr;
+}
+
+PyMethodDef methods[] = {
+    {"pack", pack, METH_VARARGS,
+     "pack(mol_graphs, fa_w, fb_w) -> 10 bytearrays: the concatenated BatchMolGraph tables "
+     "(featurization.py:757-813)"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyModuleDef module = {PyModuleDef_HEAD_INIT, "_wdpack", "native BatchMolGraph packer", -1, methods,
+                      nullptr, nullptr, nullptr, nullptr};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__wdpack(void) { return PyModule_Create(&module); }

@@ -12,13 +12,15 @@ names = [re.sub(r'\(.*', '', r['Kernel_Name']).replace('void ', '').replace('(an
          for r in rows]
 dur = [(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1000 for r in rows]
 start = [int(r['Start_Timestamp']) / 1000 for r in rows]
+# a forward ends with its readout: readout_kernel (unblocked path) or wo_readout_kernel (fused path)
+END = 'wo_readout_kernel' if any(n.startswith('wo_readout_kernel') for n in names) else 'readout_kernel'
 if period is None:  # period = distance between readout launches
-    ro = [i for i, n in enumerate(names) if n.startswith('readout_kernel')]
+    ro = [i for i, n in enumerate(names) if n.startswith(END)]
     period = ro[-1] - ro[-2]
-last = max(i for i, n in enumerate(names) if n.startswith('readout_kernel'))
+last = max(i for i, n in enumerate(names) if n.startswith(END))
 seqs = []
 i = last
-while i - period + 1 >= 0 and names[i].startswith('readout_kernel'):
+while i - period + 1 >= 0 and names[i].startswith(END):
     seqs.append(list(range(i - period + 1, i + 1)))
     i -= period
 print(f'{len(seqs)} forwards x {period} kernels')
