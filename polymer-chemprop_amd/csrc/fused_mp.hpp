@@ -26,6 +26,13 @@ namespace wd {
 
 constexpr int BLK_BONDS = 128, BLK_ATOMS = 64;  // block capacity (rows of the blocked layouts)
 
+// WD_EXP (timing experiments only, never set in the product build): 1 = skip the layer GEMM,
+// 2 = skip the layer's plane stores, 3 = skip the in-block gather, 4 = skip the residual prefetch,
+// 5 = store fp32 instead of planes, 6 = skip residual and ELL prefetch
+#ifndef WD_EXP
+#define WD_EXP 0
+#endif
+
 // WdGraph.blocks row: {bond_start, bond_count, atom_start, atom_count, mol_lo, mol_hi, -, -}
 struct BlockRow { int bs, bn, as, an, ml, mh; };
 __device__ __forceinline__ BlockRow load_block(const int32_t *blocks, int i) {
@@ -83,7 +90,13 @@ struct MpLayerP {
 // bytes to stream.
 template <int BN> struct MpWaves;
 template <> struct MpWaves<64> { static constexpr int WM = 4, WN = 2; };
+#if WD_EXP == 7
+template <> struct MpWaves<80> { static constexpr int WM = 8, WN = 1; };
+#elif WD_EXP == 8
+template <> struct MpWaves<80> { static constexpr int WM = 4, WN = 1; };
+#else
 template <> struct MpWaves<80> { static constexpr int WM = 2, WN = 5; };
+#endif
 
 // grid = nblk * n_tiles (XCD-grouped: the column tiles of a block share an XCD), 64 WM WN threads.
 // LDS: two GEMM stages, reused by the epilogue as P [128][BN + 4] and M [128][BN + 4] fp32.
@@ -102,25 +115,34 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
     const int tid = threadIdx.x;
-    // residual rows and the rows' gather lists (ELL-8) prefetched ahead of the GEMM
-    // (unit v = tid + NT i: row v / UPR, columns 8 (v % UPR) ..)
+    // residual rows and the rows' gather lists (ELL-8) prefetched during the GEMM (unit v = tid + NT i:
+    // row v / UPR, columns 8 (v % UPR) ..)
     float4 res[UPT][2], ecf[UPT][2];
     uint2 eix[UPT];
+    auto prefetch = [&]() {
 #pragma unroll
-    for (int i = 0; i < UPT; ++i) {
-        const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
-        res[i][0] = res[i][1] = ecf[i][0] = ecf[i][1] = f4zero();
-        eix[i] = make_uint2(0, 0);
-        if (v < UNITS && lr < B.bn) {
-            const size_t b = B.bs + lr;
-            const float *s = P.inp + b * P.kp + n0 + c;
-            res[i][0] = ld4(s);
-            res[i][1] = ld4(s + 4);
-            eix[i] = *reinterpret_cast<const uint2 *>(P.ell_idx + 8 * b);
-            ecf[i][0] = ld4(P.ell_coef + 8 * b);
-            ecf[i][1] = ld4(P.ell_coef + 8 * b + 4);
+        for (int i = 0; i < UPT; ++i) {
+            const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
+            res[i][0] = res[i][1] = ecf[i][0] = ecf[i][1] = f4zero();
+            eix[i] = make_uint2(0, 0);
+            if (v < UNITS && lr < B.bn) {
+                const size_t b = B.bs + lr;
+                const float *s = P.inp + b * P.kp + n0 + c;
+                if (WD_EXP != 4 && WD_EXP != 6) {
+                    res[i][0] = ld4(s);
+                    res[i][1] = ld4(s + 4);
+                }
+                if (WD_EXP != 6) {
+                    eix[i] = *reinterpret_cast<const uint2 *>(P.ell_idx + 8 * b);
+                    ecf[i][0] = ld4(P.ell_coef + 8 * b);
+                    ecf[i][1] = ld4(P.ell_coef + 8 * b + 4);
+                }
+            }
         }
-    }
+    };
+#if WD_EXP == 13
+    prefetch();
+#endif
     X6Operands O{};
     O.a0 = P.mprev; O.nkc0 = P.kp >> 5; O.kc0 = P.kp >> 5;
     O.a1 = P.mprev; O.nkc1 = P.kp >> 5; O.kc1 = 0;  // no second segment (a non-null alias: no null arithmetic)
@@ -128,7 +150,17 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
     O.a_rows = B.bn;
     O.b = P.wh + (size_t)nt * (P.kp >> 5) * (3 * BN * 64);
     floatx4 acc[BM / WM / 16][BN / WN / 16];
-    x6_mainloop<BM, BN, WM, WN, S, CPS>(O, lds, acc);
+    if (WD_EXP == 1) {
+        for (auto &r : acc)
+            for (auto &x : r) x = floatx4{0.f, 0.f, 0.f, 0.f};
+        prefetch();
+    } else {
+#if WD_EXP == 13
+        x6_mainloop<BM, BN, WM, WN, S, CPS>(O, lds, acc);
+#else
+        x6_mainloop<BM, BN, WM, WN, S, CPS>(O, lds, acc, prefetch);
+#endif
+    }
     __syncthreads();
     float *Pt = reinterpret_cast<float *>(lds);
     float *Mt = Pt + BM * LDC;
@@ -136,6 +168,7 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
     __syncthreads();
 
     const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
+    const __amdgpu_buffer_rsrc_t mrs = x6_block_rsrc<BM>(LAST ? P.aplanes : P.mnext, P.kp, blk);
 #pragma unroll
     for (int i = 0; i < UPT; ++i) {
         const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
@@ -152,7 +185,7 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int j = (ix[k >> 2] >> (8 * (k & 3))) & 0x7f;
-                if (w8[k] == 0.f) continue;
+                if (w8[k] == 0.f || WD_EXP == 3) continue;
                 if (P.sym_rev) msg_term<LDC>(Pt, B.bs + j, B.bs, P.sym_rev, c, w8[k], s0, s1);
                 else lds_term<LDC>(Pt, j, c, w8[k], s0, s1);
             }
@@ -177,13 +210,18 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
         if constexpr (LAST) {
             st4(Mt + lr * LDC + c, y0);
             st4(Mt + lr * LDC + c + 4, y1);
-        } else if (lr < B.bn) {  // rows past the block's bonds are never loaded by the next layer
-            x6_store8<BM>(P.mnext, P.kp, blk * BM + lr, n0 + c, y0, y1);
+        } else if (lr < B.bn && WD_EXP == 5) {
+            float *d = reinterpret_cast<float *>(P.mnext) + (size_t)(blk * BM + lr) * P.kp + n0 + c;
+            st4(d, y0);
+            st4(d + 4, y1);
+        } else if (lr < B.bn && WD_EXP != 2) {  // rows past the block's bonds are never loaded by the next layer
+            x6_store8_blk<BM>(mrs, lr, n0 + c, y0, y1);
         }
     }
     if constexpr (LAST) {
         __syncthreads();
         // atom aggregate of this column tile: A[a] = Σ_{b into a} w_b M_t[b] (mpn.py:126-131)
+        const __amdgpu_buffer_rsrc_t ars = x6_block_rsrc<BLK_ATOMS>(P.aplanes, P.kp, blk);
         for (int v = tid; v < B.an * UPR; v += NT) {  // rows past the block's atoms are never loaded
             const int la = v / UPR, c = 8 * (v % UPR);
             float4 s0 = f4zero(), s1 = f4zero();
@@ -200,7 +238,7 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
                     for (int q = P.aptr[a] + 8; q < P.aptr[a + 1]; ++q)
                         lds_term<LDC>(Mt, P.aidx[q] - B.bs, c, P.acoef ? P.acoef[q] : 1.0f, s0, s1);
             }
-            x6_store8<BLK_ATOMS>(P.aplanes, P.kp, blk * BLK_ATOMS + la, n0 + c, s0, s1);
+            x6_store8_blk<BLK_ATOMS>(ars, la, n0 + c, s0, s1);
         }
     }
 }
@@ -220,7 +258,11 @@ struct WoReadoutP {
 
 template <int BN> struct WoWaves;
 template <> struct WoWaves<64> { static constexpr int WM = 4, WN = 2; };
+#if WD_EXP == 8
+template <> struct WoWaves<80> { static constexpr int WM = 4, WN = 1; };
+#else
 template <> struct WoWaves<80> { static constexpr int WM = 2, WN = 5; };
+#endif
 
 // grid = nblk * n_tiles: 64 atom rows x BN columns per workgroup.
 template <int BN>

@@ -279,7 +279,8 @@ __device__ __forceinline__ void epilogue_v4(const Epi &E, const float *C, int ld
             }
             if (j + 4 <= N) {
                 if (E.Z) st4(E.Z + o, make_float4(z[0], z[1], z[2], z[3]));
-                if (E.Y) st4(E.Y + o, make_float4(out[0], out[1], out[2], out[3]));
+                if (E.Y) gst16(E.Y + o, u32x4{__float_as_uint(out[0]), __float_as_uint(out[1]), __float_as_uint(out[2]),
+                                               __float_as_uint(out[3])});
             } else {
                 for (int q = 0; q < N - j; ++q) {
                     if (E.Z) E.Z[o + q] = z[q];

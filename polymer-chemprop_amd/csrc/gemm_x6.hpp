@@ -214,9 +214,13 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // tile (BM / WM) x (BN / WN), S LDS stages (S - 1 chunks in flight behind the one multiplied) of CPS
 // chunks each.  Uses lds[0 .. S * CPS * x6_stage_bytes<BM, BN>()); on return every DMA has landed and
 // all waves are past their last LDS read (the caller may reuse the LDS after one __syncthreads()).
-template <int BM, int BN, int WM, int WN, int S = 2, int CPS = 1>
+struct NoHook { __device__ void operator()() const {} };
+
+// hook(): called once, right after the DMA of the second chunk is issued (register prefetches placed
+// there land behind the first chunk's MFMAs instead of delaying the first chunk's wait)
+template <int BM, int BN, int WM, int WN, int S = 2, int CPS = 1, typename Hook = NoHook>
 __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
-                                            floatx4 (&acc)[BM / WM / 16][BN / WN / 16]) {
+                                            floatx4 (&acc)[BM / WM / 16][BN / WN / 16], const Hook &hook = Hook()) {
     constexpr int NW = WM * WN, TM = BM / WM / 16, TN = BN / WN / 16;
     constexpr int APL = BM * 64, BPL = BN * 64, STAGE = x6_stage_bytes<BM, BN>();
     constexpr int AP = 3 * BM / 16, BP = 3 * BN / 16;                 // 1 KB pieces per chunk
@@ -308,6 +312,7 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             if (sc + 1 < nsc) issue_sc(sc + 1, (sc + 1) & 1);
+            if (sc == 0) hook();
 #pragma unroll
             for (int q = 0; q < CPS; ++q)
                 if (sc * CPS + q < nchunks) compute(lds + ((sc & 1) * CPS + q) * STAGE);
@@ -324,6 +329,7 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             if (kc + S - 1 < nchunks) issue(kc + S - 1, (kc + S - 1) % S);
+            if (kc == 0) hook();
             compute(lds + (kc % S) * STAGE);
         }
     }

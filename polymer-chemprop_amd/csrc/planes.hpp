@@ -55,6 +55,36 @@ __device__ __forceinline__ size_t x6_tile_off(int r, int k, int kp) {
     return ((size_t)(r / BR) * (kp >> 5) + (k >> 5)) * (3 * BR * 64) + (r % BR) * 64 + 2 * (k & 31);
 }
 
+// 16- and 8-byte global stores of produced activations, write-through (sc1: measured 1 us faster per
+// fused layer than default-policy stores, which leave the lines dirty for the kernel-end write-back).
+// Emitted as relaxed agent-scope 8-byte atomic stores (global_store_dwordx2 ... sc1), which the
+// compiler tracks in its vmcnt accounting (inline-asm stores are invisible to it and broke later
+// waits).  WD_WT (experiments): 0 = default policy, 1 = sc1, 3 = nt.
+#ifndef WD_WT
+#define WD_WT 1
+#endif
+__device__ __forceinline__ void gst8(void *p, const uint2 &v) {
+    if constexpr (WD_WT == 1) {
+        const unsigned long long w = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
+        __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if constexpr (WD_WT == 3) {
+        __builtin_nontemporal_store(v.x, reinterpret_cast<uint32_t *>(p));
+        __builtin_nontemporal_store(v.y, reinterpret_cast<uint32_t *>(p) + 1);
+    } else {
+        *reinterpret_cast<uint2 *>(p) = v;
+    }
+}
+__device__ __forceinline__ void gst16(void *p, const u32x4 &v) {
+    if constexpr (WD_WT == 1) {
+        gst8(p, make_uint2(v.x, v.y));
+        gst8(reinterpret_cast<uint8_t *>(p) + 8, make_uint2(v.z, v.w));
+    } else if constexpr (WD_WT == 3) {
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+    } else {
+        *reinterpret_cast<u32x4 *>(p) = v;
+    }
+}
+
 // write values lo, hi = columns k..k+7 (k % 8 == 0) of row r into a plane-tile matrix
 template <int BR = 64>
 __device__ __forceinline__ void x6_store8(uint8_t *base, int kp, int r, int k, const float4 &lo, const float4 &hi) {
@@ -64,9 +94,31 @@ __device__ __forceinline__ void x6_store8(uint8_t *base, int kp, int r, int k, c
     split_pair(hi.x, hi.y, h[2], m[2], l[2]);
     split_pair(hi.z, hi.w, h[3], m[3], l[3]);
     uint8_t *d = base + x6_tile_off<BR>(r, k, kp);
-    *reinterpret_cast<u32x4 *>(d) = u32x4{h[0], h[1], h[2], h[3]};
-    *reinterpret_cast<u32x4 *>(d + BR * 64) = u32x4{m[0], m[1], m[2], m[3]};
-    *reinterpret_cast<u32x4 *>(d + 2 * BR * 64) = u32x4{l[0], l[1], l[2], l[3]};
+    gst16(d, u32x4{h[0], h[1], h[2], h[3]});
+    gst16(d + BR * 64, u32x4{m[0], m[1], m[2], m[3]});
+    gst16(d + 2 * BR * 64, u32x4{l[0], l[1], l[2], l[3]});
+}
+
+// The same for a row of ONE row block whose base is wave-uniform (a workgroup's own block): three
+// 16-byte buffer stores with the sc1 (write-through) policy, offsets relative to the block base
+template <int BR>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t x6_block_rsrc(uint8_t *base, int kp, int blk) {
+    uint8_t *b = base + (size_t)blk * (kp >> 5) * (3 * BR * 64);
+    return __builtin_amdgcn_make_buffer_rsrc(b, 0, (kp >> 5) * (3 * BR * 64), 0x00020000);
+}
+template <int BR>
+__device__ __forceinline__ void x6_store8_blk(__amdgpu_buffer_rsrc_t rs, int r, int k, const float4 &lo,
+                                              const float4 &hi) {
+    uint32_t h[4], m[4], l[4];
+    split_pair(lo.x, lo.y, h[0], m[0], l[0]);
+    split_pair(lo.z, lo.w, h[1], m[1], l[1]);
+    split_pair(hi.x, hi.y, h[2], m[2], l[2]);
+    split_pair(hi.z, hi.w, h[3], m[3], l[3]);
+    const int o = (k >> 5) * (3 * BR * 64) + r * 64 + 2 * (k & 31);
+    constexpr int POL = WD_WT == 1 ? 16 : WD_WT == 3 ? 2 : 0;  // aux: sc1 = 16, nt = 2
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{h[0], h[1], h[2], h[3]}, rs, o, 0, POL);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{m[0], m[1], m[2], m[3]}, rs, o + BR * 64, 0, POL);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{l[0], l[1], l[2], l[3]}, rs, o + 2 * BR * 64, 0, POL);
 }
 
 // columns k..k+3 (k % 4 == 0): three 8-byte pieces
@@ -76,9 +128,9 @@ __device__ __forceinline__ void x6_store4(uint8_t *base, int kp, int r, int k, c
     split_pair(v.x, v.y, h[0], m[0], l[0]);
     split_pair(v.z, v.w, h[1], m[1], l[1]);
     uint8_t *d = base + x6_tile_off<BR>(r, k, kp);
-    *reinterpret_cast<uint2 *>(d) = make_uint2(h[0], h[1]);
-    *reinterpret_cast<uint2 *>(d + BR * 64) = make_uint2(m[0], m[1]);
-    *reinterpret_cast<uint2 *>(d + 2 * BR * 64) = make_uint2(l[0], l[1]);
+    gst8(d, make_uint2(h[0], h[1]));
+    gst8(d + BR * 64, make_uint2(m[0], m[1]));
+    gst8(d + 2 * BR * 64, make_uint2(l[0], l[1]));
 }
 
 // fp32 [rows][ld] (first kp columns) -> plane tiles [out_rows][kp] with BR-row blocks; one thread per 8

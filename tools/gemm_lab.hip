@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "gemm_x6.hpp"
@@ -124,8 +125,172 @@ float time_it(int reps, F &&launch) {
     return ms * 1000.f / reps;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Mainloop lab: the fused layer's GEMM phase alone (64 blocks x 128 rows, K = 320 as plane tiles,
+// 4 column tiles of 80), wave layouts WM x WN per K-group, KG K-groups (group g multiplies the
+// chunks c with c % KG == g; one barrier per KG chunks), DMA / MFMA switchable to find the bound.
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN, int KG, bool DMA, bool MFMA, int S = 2>
+__global__ __launch_bounds__(64 * WM * WN * KG) void ml_kernel(const uint8_t *A, const uint8_t *Bw, int nkc, int n_tiles,
+                                                             float *sink) {
+    constexpr int NW = WM * WN * KG, TM = BM / WM / 16, TN = BN / WN / 16;
+    constexpr int APL = BM * 64, BPL = BN * 64, STAGE = 3 * APL + 3 * BPL;
+    constexpr int AP = 3 * BM / 16, BP = 3 * BN / 16;
+    constexpr int APW = (AP + NW - 1) / NW, BPW = (BP + NW - 1) / NW;
+    static_assert(KG == 1 || S == 2, "K-groups use two stages");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[(S > 2 ? S : 2 * KG) * STAGE];
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int blk = tile / n_tiles, nt = tile % n_tiles;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int grp = wave / (WM * WN), wl = wave % (WM * WN);
+    const int wi = wl / WN, wj = wl % WN, g = lane >> 4, i16 = lane & 15;
+    int asrc[APW], bsrc[BPW];
+#pragma unroll
+    for (int j = 0; j < APW; ++j) {
+        const int q = 64 * (j * NW + wave) + lane, p = (q / (BM * 4)) % 3, r = (q >> 2) % BM, sl = q & 3;
+        asrc[j] = p * APL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
+    }
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) {
+        const int q = 64 * (j * NW + wave) + lane, p = (q / (BN * 4)) % 3, r = (q >> 2) % BN, sl = q & 3;
+        bsrc[j] = p * BPL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
+    }
+    const uint8_t *ab = A + (size_t)blk * nkc * 3 * APL;
+    const uint8_t *bb = Bw + (size_t)nt * nkc * 3 * BPL;
+    auto issue = [&](int kc, int buf) {
+        if constexpr (DMA) {
+            uint8_t *st = lds + buf * STAGE;
+#pragma unroll
+            for (int j = 0; j < APW; ++j)
+                if (AP % NW == 0 || j * NW + wave < AP) glds16(ab + (size_t)kc * 3 * APL + asrc[j], st + 1024 * (j * NW + wave));
+#pragma unroll
+            for (int j = 0; j < BPW; ++j)
+                if (BP % NW == 0 || j * NW + wave < BP)
+                    glds16(bb + (size_t)kc * 3 * BPL + bsrc[j], st + 3 * APL + 1024 * (j * NW + wave));
+        }
+    };
+    int ao[TM], bo[TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) ao[a] = x6_slot(wi * (BM / WM) + a * 16 + i16, g);
+#pragma unroll
+    for (int b = 0; b < TN; ++b) bo[b] = 3 * APL + x6_slot(wj * (BN / WN) + b * 16 + i16, g);
+    floatx4 acc[TM][TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](const uint8_t *st) {
+        bf16x8 af[TM][3], bfr[TN][3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+#pragma unroll
+            for (int a = 0; a < TM; ++a) af[a][p] = *reinterpret_cast<const bf16x8 *>(st + p * APL + ao[a]);
+#pragma unroll
+            for (int b = 0; b < TN; ++b) bfr[b][p] = *reinterpret_cast<const bf16x8 *>(st + p * BPL + bo[b]);
+        }
+        if constexpr (MFMA) {
+            constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};
+#pragma unroll
+            for (int t = 0; t < 6; ++t)
+#pragma unroll
+                for (int a = 0; a < TM; ++a)
+#pragma unroll
+                    for (int b = 0; b < TN; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][PA[t]], bfr[b][PB[t]], acc[a][b], 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b) acc[a][b][0] += (float)(af[a][0][0] + bfr[b][2][1]);
+        }
+    };
+    if constexpr (S > 2) {
+        int mine = 0;
+#pragma unroll
+        for (int j = 0; j < APW; ++j) mine += AP % NW == 0 || j * NW + wave < AP;
+#pragma unroll
+        for (int j = 0; j < BPW; ++j) mine += BP % NW == 0 || j * NW + wave < BP;
+        for (int c = 0; c < S - 1; ++c) issue(c, c);
+        for (int kc = 0; kc < nkc; ++kc) {
+            wait_vmcnt(min(S - 2, nkc - 1 - kc) * mine);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (kc + S - 1 < nkc) issue(kc + S - 1, (kc + S - 1) % S);
+            compute(lds + (kc % S) * STAGE);
+        }
+    }
+    const int nsc = S > 2 ? 0 : (nkc + KG - 1) / KG;
+    if (S == 2)
+        for (int q = 0; q < KG; ++q) issue(q, q);
+    for (int sc = 0; sc < nsc; ++sc) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (sc + 1 < nsc)
+            for (int q = 0; q < KG; ++q)
+                if ((sc + 1) * KG + q < nkc) issue((sc + 1) * KG + q, ((sc + 1) & 1) * KG + q);
+        if (sc * KG + grp < nkc) compute(lds + ((sc & 1) * KG + grp) * STAGE);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) s += acc[a][b][0] + acc[a][b][3];
+    if (s == 1234.5f) sink[threadIdx.x] = s;
+}
+
+static void mainloop_lab(int reps) {
+    const int nblk = 64, nkc = 10, BM = 128, NTILES = 4;
+    const size_t abytes = (size_t)nblk * nkc * 3 * BM * 64, bbytes = (size_t)NTILES * nkc * 3 * 80 * 64;
+    const int NA = 8;
+    uint8_t *A[NA], *B;
+    float *sink;
+    for (int i = 0; i < NA; ++i) {
+        CK(hipMalloc(&A[i], abytes));
+        CK(hipMemset(A[i], 0x3c, abytes));
+    }
+    CK(hipMalloc(&B, bbytes));
+    CK(hipMemset(B, 0x3c, bbytes));
+    CK(hipMalloc(&sink, 4096 * 4));
+    auto run = [&](const char *name, auto kern, int nthreads) {
+        float us = time_it(reps, [&](int i) {
+            hipLaunchKernelGGL(kern, dim3(nblk * NTILES), dim3(nthreads), 0, 0, A[i % NA], B, nkc, NTILES, sink);
+        });
+        printf("mainloop %-40s %8.2f us\n", name, us);
+    };
+    run("2x5 KG1 (current)", ml_kernel<128, 80, 2, 5, 1, true, true>, 640);
+    run("2x5 KG1 no-DMA", ml_kernel<128, 80, 2, 5, 1, false, true>, 640);
+    run("2x5 KG1 no-MFMA", ml_kernel<128, 80, 2, 5, 1, true, false>, 640);
+    run("2x5 KG1 LDS-only", ml_kernel<128, 80, 2, 5, 1, false, false>, 640);
+    run("4x1 KG1", ml_kernel<128, 80, 4, 1, 1, true, true>, 256);
+    run("4x1 KG1 no-DMA", ml_kernel<128, 80, 4, 1, 1, false, true>, 256);
+    run("4x1 KG1 no-MFMA", ml_kernel<128, 80, 4, 1, 1, true, false>, 256);
+    run("4x1 KG2", ml_kernel<128, 80, 4, 1, 2, true, true>, 512);
+    run("4x1 KG2 no-DMA", ml_kernel<128, 80, 4, 1, 2, false, true>, 512);
+    run("8x1 KG1", ml_kernel<128, 80, 8, 1, 1, true, true>, 512);
+    run("8x1 KG1 no-DMA", ml_kernel<128, 80, 8, 1, 1, false, true>, 512);
+    run("2x1 KG2", ml_kernel<128, 80, 2, 1, 2, true, true>, 256);
+    run("4x1 KG1 DMA-only", ml_kernel<128, 80, 4, 1, 1, true, false>, 256);
+    run("8x1 KG1 DMA-only", ml_kernel<128, 80, 8, 1, 1, true, false>, 512);
+    run("8x1 S3", ml_kernel<128, 80, 8, 1, 1, true, true, 3>, 512);
+    run("8x1 S3 DMA-only", ml_kernel<128, 80, 8, 1, 1, true, false, 3>, 512);
+    run("8x1 S4 DMA-only", ml_kernel<128, 80, 8, 1, 1, true, false, 4>, 512);
+    run("4x1 S3", ml_kernel<128, 80, 4, 1, 1, true, true, 3>, 256);
+    run("4x1 S3 DMA-only", ml_kernel<128, 80, 4, 1, 1, true, false, 3>, 256);
+    run("2x5 S3", ml_kernel<128, 80, 2, 5, 1, true, true, 3>, 640);
+    run("2x5 S3 DMA-only", ml_kernel<128, 80, 2, 5, 1, true, false, 3>, 640);
+    for (int i = 0; i < NA; ++i) CK(hipFree(A[i]));
+    CK(hipFree(B));
+    CK(hipFree(sink));
+}
+
 int main(int argc, char **argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 200;
+    if (argc > 2 && std::string(argv[2]) == "mainloop") {
+        mainloop_lab(reps);
+        return 0;
+    }
     const Shape shapes[] = {{"K32  polymer B64", 6272, 320, 32}, {"K64  polymer B64", 6272, 320, 64},
                             {"W_i  polymer B64", 6272, 320, 160}, {"W_h  polymer B64", 6272, 320, 320},
                             {"W_o  polymer B64", 2304, 320, 480}, {"W_h  zinc B512 H512", 25728, 512, 512}};

@@ -24,6 +24,7 @@ for s in "$@"; do
     tune) step tune 600 python tools/tune_gemm.py ;;
     lab) step gemm_lab 300 ./tools/gemm_lab 200 ;;
     stream) step stream 120 ./tools/gemm_lab 50 stream ;;
+    mainloop) step mainloop 120 ./tools/gemm_lab 200 mainloop ;;
     host) step host 300 python tools/host_overhead.py ;;
     ab) step ab_x6 300 python bench.py --steps 200 --warmup 20 --no-cpu --variant 10 && step ab_f32 300 python bench.py --steps 200 --warmup 20 --no-cpu --variant 9 ;;
     x6prec) step x6prec 300 python tools/x6_precision.py ;;
