@@ -22,6 +22,8 @@
 #include "gemm.hpp"
 #include "planes.hpp"
 
+#include <type_traits>
+
 namespace wd {
 
 struct X6Params {
@@ -216,6 +218,17 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // all waves are past their last LDS read (the caller may reuse the LDS after one __syncthreads()).
 struct NoHook { __device__ void operator()() const {} };
 
+// f(std::integral_constant<int, n>) for a wave-uniform runtime n in [0, N]
+template <int N, typename F>
+__device__ __forceinline__ void dispatch_upto(int n, F &&f) {
+    if constexpr (N == 0) {
+        f(std::integral_constant<int, 0>{});
+    } else {
+        if (n >= N) f(std::integral_constant<int, N>{});
+        else dispatch_upto<N - 1>(n, f);
+    }
+}
+
 // hook(): called once, right after the DMA of the second chunk is issued (register prefetches placed
 // there land behind the first chunk's MFMAs instead of delaying the first chunk's wait)
 template <int BM, int BN, int WM, int WN, int S = 2, int CPS = 1, typename Hook = NoHook>
@@ -264,12 +277,16 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
     for (int a = 0; a < TM; ++a) ao[a] = x6_slot(wi * (BM / WM) + a * 16 + i16, g);
 #pragma unroll
     for (int b = 0; b < TN; ++b) bo[b] = 3 * APL + x6_slot(wj * (BN / WN) + b * 16 + i16, g);
-    auto compute = [&](const uint8_t *st) {
+    // only this wave's 16-row A tiles that hold block rows (< a_rows) are read and multiplied: a
+    // molecule block is ~3/4 full, and the skipped accumulators stay zero
+    const int na = min(TM, max(0, (O.a_rows - wi * (BM / WM) + 15) >> 4));
+    auto compute_n = [&](const uint8_t *st, auto na_c) {
+        constexpr int NA = decltype(na_c)::value;
         bf16x8 af[TM][3], bfr[TN][3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
 #pragma unroll
-            for (int a = 0; a < TM; ++a) af[a][p] = *reinterpret_cast<const bf16x8 *>(st + p * APL + ao[a]);
+            for (int a = 0; a < NA; ++a) af[a][p] = *reinterpret_cast<const bf16x8 *>(st + p * APL + ao[a]);
 #pragma unroll
             for (int b = 0; b < TN; ++b) bfr[b][p] = *reinterpret_cast<const bf16x8 *>(st + p * BPL + bo[b]);
         }
@@ -278,11 +295,12 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
 #pragma unroll
         for (int t = 0; t < 6; ++t)
 #pragma unroll
-            for (int a = 0; a < TM; ++a)
+            for (int a = 0; a < NA; ++a)
 #pragma unroll
                 for (int b = 0; b < TN; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][PA[t]], bfr[b][PB[t]], acc[a][b], 0, 0, 0);
     };
+    auto compute = [&](const uint8_t *st) { dispatch_upto<TM>(na, [&](auto c) { compute_n(st, c); }); };
 #pragma unroll
     for (int a = 0; a < TM; ++a)
 #pragma unroll

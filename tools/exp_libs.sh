@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/exp
-for v in prod ${EXPS:-1 2 3}; do
+for v in prod ${EXPS-1 2 3}; do
   lib=polymer-chemprop_amd/chemprop_amd/libwdmpnn.so
   [ "$v" != prod ] && lib=$PWD/gpurun_exp_$v.so
   WDMPNN_LIB=$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/exp/$v -o run -- \
