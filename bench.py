@@ -85,6 +85,37 @@ def pmc_traffic(prefix):
     return sum(v) / len(v), f'profiles/{PMC_TRAFFIC}: {d.get("_note", "")}'
 
 
+def packing_report(a, device, t_fwd):
+    """Host side of one batch, outside the timed region (pack + H2D reported separately,
+    and end to end): native packer time, device_graph() time (gather lists, blocks, one pinned H2D,
+    device-side bond featurisation and plane split, synchronised), H2D bytes per edge, both with the
+    bond rows built on the host and on the device."""
+    mols = synthetic.make_batch(a.kind, a.batch, 4242)
+    rep = {}
+    for mode, kw in (('host_bond_features', {}), ('device_bond_features', {'device_bond_features': True})):
+        BatchMolGraph(mols, **kw)
+        n, t0 = 0, time.perf_counter()
+        while n < 5 or time.perf_counter() - t0 < 0.5:
+            g = BatchMolGraph(mols, **kw)
+            n += 1
+        pack = (time.perf_counter() - t0) / n
+        ups = []
+        for _ in range(3):
+            g = BatchMolGraph(mols, **kw)
+            torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            dg = g.device_graph(device, False, get_bond_fdim())
+            torch.cuda.synchronize(device)
+            ups.append(time.perf_counter() - t0)
+        up = statistics.median(ups)
+        E = g.n_bonds - 1
+        rep[mode] = {'pack_ms': pack * 1e3, 'device_graph_ms': up * 1e3, 'h2d_bytes_per_edge': dg.h2d_bytes / E,
+                     'end_to_end_edges_per_s': E / (pack + up + t_fwd)}
+    rep['note'] = ('one batch of the bench workload; end_to_end = edges / (pack + device_graph + one forward), '
+                   'serial on one host thread (the reference packs in 77 ms per batch, SURVEY §8(a) a2)')
+    return rep
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -111,7 +142,9 @@ def main():
     args = TrainArgs(hidden_size=a.hidden, depth=a.depth, device=device)
 
     # inputs: packed + resident in HBM before timing (featurization.py:757-813 equivalent on host)
-    graphs = [BatchMolGraph(synthetic.make_batch(a.kind, a.batch, 1000 + 7919 * rank + i)) for i in range(a.n_batches)]
+    # (bond features rebuilt on the device from f_atoms + bond tail + b2a: SURVEY §8(f) row 2)
+    graphs = [BatchMolGraph(synthetic.make_batch(a.kind, a.batch, 1000 + 7919 * rank + i), device_bond_features=True)
+              for i in range(a.n_batches)]
     for g in graphs:
         g.device_graph(device, False, get_bond_fdim())
     torch.cuda.synchronize(device)
@@ -215,6 +248,7 @@ def main():
                          'hbm_frac': hbm / HBM_PEAK_GBS if hbm else None,
                          'launches_timed': n_launch},
         }
+        line['packing'] = packing_report(a, device, elapsed / a.steps)
         if not a.no_cpu:
             cpu = cpu_baseline(TrainArgs(hidden_size=H, depth=a.depth, device=torch.device('cpu')), graphs[0],
                                a.cpu_seconds)

@@ -209,6 +209,15 @@ int wdmpnn_split_planes(const float *src, int32_t ld, int32_t rows, int32_t kp, 
 int wdmpnn_split_planes_rows(const float *src, int32_t ld, int32_t rows, int32_t kp, const int32_t *row_map,
                              int32_t out_rows, void *dst, size_t dst_bytes, void *stream);
 
+/* Device-side bond featurisation, replacing the host-side construction of every
+ * f_bonds row as f_atoms[a1] + f_bond (featurization.py:467-468, 545-546, 616-617) and its H2D copy:
+ * f_bonds[r][0 .. atom_fdim) = f_atoms[b2a[r]], f_bonds[r][atom_fdim .. + tail_dim) = bond_tail[r],
+ * the rest of the ld_bonds columns 0, for r < rows.  b2a entries must index f_atoms rows
+ * (< atom_rows); an out-of-range entry fills its row's atom part with NaN. */
+int wdmpnn_build_bond_features(const float *f_atoms, int32_t ld_atoms, int32_t atom_fdim, int32_t atom_rows,
+                               const int32_t *b2a, const float *bond_tail, int32_t ld_tail, int32_t tail_dim,
+                               int32_t rows, float *f_bonds, int32_t ld_bonds, void *stream);
+
 /* index_select_ND (nn_utils.py:50-67): out[i, :] = src[index[i], :], row_len floats per row.
  * Indices are int64 like the reference's LongTensor; out-of-range indices are an error checked by
  * the caller (the kernel clamps nothing and reads src[index]). */

@@ -27,7 +27,8 @@ EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace
                     'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
                     'wdmpnn_index_select_rows', 'wdmpnn_event_pool_create', 'wdmpnn_event_pool_destroy',
                     'wdmpnn_event_pool_elapsed_ms', 'wdmpnn_packed_params_bytes', 'wdmpnn_pack_params',
-                    'wdmpnn_plane_bytes', 'wdmpnn_split_planes', 'wdmpnn_split_planes_rows')
+                    'wdmpnn_plane_bytes', 'wdmpnn_split_planes', 'wdmpnn_split_planes_rows',
+                    'wdmpnn_build_bond_features')
 
 
 class WdCsr(Structure):
@@ -99,12 +100,15 @@ def lib() -> ctypes.CDLL:
     L.wdmpnn_split_planes.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_size_t, c_void_p]
     L.wdmpnn_split_planes_rows.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_void_p, c_size_t,
                                            c_void_p]
+    L.wdmpnn_build_bond_features.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_int32, c_int32,
+                                             c_int32, c_void_p, c_int32, c_void_p]
     L.wdmpnn_event_pool_create.argtypes = [c_int32, POINTER(c_void_p)]
     L.wdmpnn_event_pool_destroy.argtypes = [c_void_p]
     L.wdmpnn_event_pool_elapsed_ms.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_float)]
     for fn in ('wdmpnn_packed_params_bytes', 'wdmpnn_pack_params', 'wdmpnn_event_pool_create', 'wdmpnn_event_pool_destroy', 'wdmpnn_event_pool_elapsed_ms',
                'wdmpnn_workspace_bytes', 'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
-               'wdmpnn_index_select_rows', 'wdmpnn_plane_bytes', 'wdmpnn_split_planes', 'wdmpnn_split_planes_rows'):
+               'wdmpnn_index_select_rows', 'wdmpnn_plane_bytes', 'wdmpnn_split_planes', 'wdmpnn_split_planes_rows',
+               'wdmpnn_build_bond_features'):
         getattr(L, fn).restype = c_int
     v = L.wdmpnn_abi_version()
     if v != ABI_VERSION:

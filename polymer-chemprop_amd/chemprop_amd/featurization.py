@@ -135,7 +135,12 @@ class DeviceGraph:
 class BatchMolGraph:
     """featurization.py:742-875; the tables are concatenated by the native packer (csrc/packer.cpp)."""
 
-    def __init__(self, mol_graphs: Sequence):
+    def __init__(self, mol_graphs: Sequence, device_bond_features: bool = False, check_bond_features: bool = False):
+        """``device_bond_features``: keep only the bond-feature tail of every f_bonds
+        row on the host; ``device_graph`` uploads f_atoms + tail + b2a and rebuilds
+        ``f_bonds = f_atoms[b2a] ‖ tail`` on the device (featurization.py:467-468, 545-546, 616-617 build
+        the rows that way), cutting the H2D per edge from 4·bond_fdim bytes to 4·(tail + 1).
+        ``check_bond_features`` verifies that layout while packing (ValueError otherwise)."""
         self.overwrite_default_atom_features = mol_graphs[0].overwrite_default_atom_features
         self.overwrite_default_bond_features = mol_graphs[0].overwrite_default_bond_features
         self.atom_fdim = get_atom_fdim(overwrite_default_atom=self.overwrite_default_atom_features)
@@ -145,13 +150,14 @@ class BatchMolGraph:
         fb_w = next((len(g.f_bonds[0]) for g in mol_graphs if g.n_bonds), self.bond_fdim)
         # native packer (csrc/packer.cpp): concatenation at the reference's offsets, pad row 0
         # (featurization.py:767-793), a2b as CSR (deg + in_idx in slot order)
+        tail_from = int(fa_w) if device_bond_features else 0
         (f_atoms, f_bonds, w_atoms, w_bonds, b2a, b2revb, deg, in_idx, na, nb) = \
-            _packer().pack(mol_graphs, int(fa_w), int(fb_w))
+            _packer().pack(mol_graphs, int(fa_w), int(fb_w), tail_from, bool(check_bond_features))
         na = np.frombuffer(na, np.int64)
         nb = np.frombuffer(nb, np.int64)
         V, E = int(na.sum()), int(nb.sum())
         f_atoms = np.frombuffer(f_atoms, np.float32).reshape(V + 1, fa_w)
-        f_bonds = np.frombuffer(f_bonds, np.float32).reshape(E + 1, fb_w)
+        f_bonds = np.frombuffer(f_bonds, np.float32).reshape(E + 1, fb_w - tail_from)
         w_atoms = np.frombuffer(w_atoms, np.float32)
         w_bonds = np.frombuffer(w_bonds, np.float32)
         b2a = np.frombuffer(b2a, np.int64)
@@ -171,9 +177,14 @@ class BatchMolGraph:
         self._deg = deg
         self.max_num_bonds = max(1, int(deg.max()) if len(deg) else 0)  # featurization.py:802-803
 
-        self._np = dict(f_atoms=f_atoms, f_bonds=f_bonds, w_atoms=w_atoms, w_bonds=w_bonds, b2a=b2a, b2revb=b2revb)
+        self._np = dict(f_atoms=f_atoms, w_atoms=w_atoms, w_bonds=w_bonds, b2a=b2a, b2revb=b2revb)
+        if device_bond_features:
+            self._np['bond_tail'] = f_bonds  # [E+1][fb_w - fa_w]; the full rows are rebuilt on demand
+            self._f_bonds = None
+        else:
+            self._np['f_bonds'] = f_bonds
+            self._f_bonds = torch.from_numpy(f_bonds)
         self.f_atoms = torch.from_numpy(f_atoms)
-        self.f_bonds = torch.from_numpy(f_bonds)
         self.w_atoms = torch.from_numpy(w_atoms)
         self.w_bonds = torch.from_numpy(w_bonds)
         self.b2a = torch.from_numpy(b2a)
@@ -184,6 +195,19 @@ class BatchMolGraph:
         self._device_cache: Dict[tuple, DeviceGraph] = {}
 
     # ------------------------------------------------------------------ reference API
+    @property
+    def f_bonds(self) -> torch.Tensor:
+        """[n_bonds, bond_fdim] float32 (featurization.py:806); with device_bond_features, assembled on
+        first access from f_atoms[b2a] ‖ bond tail (the layout the reference builds)."""
+        if self._f_bonds is None:
+            self._np['f_bonds'] = self._host_f_bonds()
+            self._f_bonds = torch.from_numpy(self._np['f_bonds'])
+        return self._f_bonds
+
+    def _host_f_bonds(self) -> np.ndarray:
+        fa, tail = self._np['f_atoms'], self._np['bond_tail']
+        return np.ascontiguousarray(np.concatenate([fa[self._np['b2a']], tail], axis=1))
+
     @property
     def a2b(self) -> torch.Tensor:
         """[n_atoms, max_num_bonds] LongTensor padded with 0 (featurization.py:809)."""
@@ -314,16 +338,31 @@ class BatchMolGraph:
         if dg is not None:
             return dg
         fa = self._np['f_atoms']
-        fb = self._np['f_bonds']
+        tail = self._np.get('bond_tail')
+        dev_bonds = tail is not None and device.type == 'cuda'  # rebuild f_bonds on the device
         if atom_messages:
             nb_used = bond_fdim if bond_fdim is not None else get_bond_fdim(atom_messages=True)
-            fb = fb[:, fb.shape[1] - nb_used:]
-        Fa, Fb = fa.shape[1], fb.shape[1]
+            src = tail if tail is not None and nb_used <= tail.shape[1] else self.f_bonds.numpy()
+            fb = src[:, src.shape[1] - nb_used:]
+            dev_bonds = False
+        elif tail is not None and not dev_bonds:
+            fb = self.f_bonds.numpy()
+        else:
+            fb = tail if dev_bonds else self._np['f_bonds']
+        Fa = fa.shape[1]
+        Fb = Fa + tail.shape[1] if dev_bonds else fb.shape[1]
         lda, ldb = _round_up(Fa, 32), _round_up(Fb, 32)
         fa_p = np.zeros((_round_up(fa.shape[0], 128), lda), np.float32)  # rows to the GEMM tile, K to 32
         fa_p[:fa.shape[0], :Fa] = fa
-        fb_p = np.zeros((_round_up(fb.shape[0], 128), ldb), np.float32)
-        fb_p[:fb.shape[0], :Fb] = fb
+        rows_b = _round_up(fb.shape[0], 128)
+        if dev_bonds:  # upload the tail + b2a only (pad rows: source atom 0 = the zero pad row, tail 0)
+            fb_p = np.zeros((rows_b, tail.shape[1]), np.float32)
+            fb_p[:tail.shape[0]] = tail
+            b2a_p = np.zeros(rows_b, np.int32)
+            b2a_p[:tail.shape[0]] = self._np['b2a']
+        else:
+            fb_p = np.zeros((rows_b, ldb), np.float32)
+            fb_p[:fb.shape[0], :Fb] = fb
         a_start = np.array([s for s, _ in self.a_scope], np.int32)
         a_size = np.array([n for _, n in self.a_scope], np.int32)
         xn = np.array(self.degree_of_polym, np.float32)
@@ -353,9 +392,11 @@ class BatchMolGraph:
                     break
         msg_t = msg.transpose(msg_rows)
         agg_t = agg.transpose(msg_rows)
-        arrays = [('f_atoms', fa_p), ('f_bonds', fb_p), ('w_atoms', self._np['w_atoms']),
+        arrays = [('f_atoms', fa_p), ('bond_tail' if dev_bonds else 'f_bonds', fb_p), ('w_atoms', self._np['w_atoms']),
                   ('mol_start', a_start), ('mol_size', a_size), ('xn', xn),
                   ('b2revb', self._np['b2revb'].astype(np.int32))]
+        if dev_bonds:
+            arrays.append(('b2a', b2a_p))
         if blocks is not None and len(blocks):
             arrays += [('blocks', blocks), ('bond_blk_row', bond_blk), ('atom_blk_row', atom_blk)]
             bstart = np.zeros(len(blocks) + 1, np.int64)
@@ -390,6 +431,13 @@ class BatchMolGraph:
         def csr(name):
             return _native.WdCsr(P(f'{name}_ptr'), P(f'{name}_idx'), P(f'{name}_coef'))
 
+        if dev_bonds:  # f_bonds = f_atoms[b2a] ‖ tail, built on the device from the uploaded pieces
+            fbd = torch.empty(rows_b * ldb, dtype=torch.float32, device=device)
+            _native.check(_native.lib().wdmpnn_build_bond_features(
+                P('f_atoms'), lda, Fa, fa_p.shape[0], P('b2a'), P('bond_tail'), fb_p.shape[1], fb_p.shape[1], rows_b,
+                fbd.data_ptr(), ldb, _native.current_stream(device)), 'device bond features')
+            views['f_bonds'] = fbd
+            offsets['f_bonds'] = fbd.data_ptr() - base
         s = _native.WdGraph()
         s.n_atoms, s.n_bonds, s.n_mols = self.n_atoms, self.n_bonds, len(self.a_scope)
         s.atom_fdim, s.bond_fdim, s.ld_atoms, s.ld_bonds, s.bond_col0 = Fa, Fb, lda, ldb, 0
@@ -404,7 +452,7 @@ class BatchMolGraph:
         s.atom_messages = int(bool(atom_messages))
         if device.type == 'cuda':  # bf16x3 plane tiles of the features for the split GEMMs (exact copies)
             L = _native.lib()
-            for name, rows, ld in (('f_atoms', fa_p.shape[0], lda), ('f_bonds', fb_p.shape[0], ldb)):
+            for name, rows, ld in (('f_atoms', fa_p.shape[0], lda), ('f_bonds', rows_b, ldb)):
                 nbytes = ctypes.c_size_t()
                 _native.check(L.wdmpnn_plane_bytes(rows, ld, ctypes.byref(nbytes)), 'plane bytes')
                 planes = torch.empty(max(nbytes.value, 256), dtype=torch.uint8, device=device)
@@ -428,6 +476,7 @@ class BatchMolGraph:
         dg = DeviceGraph(buf, views, s)
         dg.host_csr = dict(csrs)
         dg.n_edges = self.n_bonds - 1
+        dg.h2d_bytes = total
         self._device_cache[key] = dg
         return dg
 

@@ -185,7 +185,7 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int j = (ix[k >> 2] >> (8 * (k & 3))) & 0x7f;
-                if (w8[k] == 0.f || WD_EXP == 3) continue;
+                if (WD_EXP == 3 || (WD_EXP != 14 && w8[k] == 0.f)) continue;
                 if (P.sym_rev) msg_term<LDC>(Pt, B.bs + j, B.bs, P.sym_rev, c, w8[k], s0, s1);
                 else lds_term<LDC>(Pt, j, c, w8[k], s0, s1);
             }

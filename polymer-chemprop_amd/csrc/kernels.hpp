@@ -328,4 +328,25 @@ __global__ __launch_bounds__(256) void index_select_rows_kernel(const float *__r
     }
 }
 
+// f_bonds[r] = f_atoms[b2a[r]] ‖ bond_tail[r] ‖ 0 (featurization.py:467-468, 545-546, 616-617 build each
+// directed bond row as its source atom's features followed by the bond's own), one thread per output
+// value.  An out-of-range source atom writes NaN to the row (never read past f_atoms).
+__global__ __launch_bounds__(256) void build_bond_features_kernel(const float *__restrict__ fa, int lda, int Fa,
+                                                                  int atom_rows, const int32_t *__restrict__ b2a,
+                                                                  const float *__restrict__ tail, int ldt, int Ft,
+                                                                  int rows, float *__restrict__ fb, int ldb) {
+    const size_t total = (size_t)rows * ldb;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+        const int r = (int)(t / ldb), c = (int)(t % ldb);
+        float v = 0.f;
+        if (c < Fa) {
+            const int a = b2a[r];
+            v = (a >= 0 && a < atom_rows) ? fa[(size_t)a * lda + c] : __builtin_nanf("");
+        } else if (c < Fa + Ft) {
+            v = tail[(size_t)r * ldt + (c - Fa)];
+        }
+        fb[t] = v;
+    }
+}
+
 }  // namespace wd

@@ -96,15 +96,24 @@ struct Buf {  // a C-contiguous Py_buffer, released on scope exit
     ~Buf() { if (ok) PyBuffer_Release(&b); }
 };
 
-// `rows`: n_rows rows of `width` numbers -> dst[r * width ..]
-void fill_table(PyObject *rows, Py_ssize_t n_rows, Py_ssize_t width, float *dst, const char *what) {
+// `rows`: n_rows rows of `src_w` numbers; columns [col0, col0 + width) of each -> dst[r * width ..]
+void fill_table(PyObject *rows, Py_ssize_t n_rows, Py_ssize_t src_w, Py_ssize_t col0, Py_ssize_t width, float *dst,
+                const char *what) {
     if (n_rows == 0) return;
     if (!PyList_Check(rows) && !PyTuple_Check(rows) && PyObject_CheckBuffer(rows)) {
         Buf t(rows);
         if (t.ok) {
-            if (t.b.ndim != 2 || t.b.shape[0] != n_rows || t.b.shape[1] != width)
+            if (t.b.ndim != 2 || t.b.shape[0] != n_rows || t.b.shape[1] != src_w)
                 fail(PyExc_ValueError, std::string(what) + ": table shape does not match (rows, width)");
-            buffer_copy(t.b, n_rows * width, dst, what);
+            if (col0 == 0 && width == src_w) {
+                buffer_copy(t.b, n_rows * width, dst, what);
+            } else {
+                Py_buffer row = t.b;
+                for (Py_ssize_t r = 0; r < n_rows; ++r) {
+                    row.buf = static_cast<char *>(t.b.buf) + (r * src_w + col0) * t.b.itemsize;
+                    buffer_copy(row, width, dst + r * width, what);
+                }
+            }
             return;
         }
     }
@@ -117,22 +126,43 @@ void fill_table(PyObject *rows, Py_ssize_t n_rows, Py_ssize_t width, float *dst,
         float *d = dst + r * width;
         if (PyList_Check(row) || PyTuple_Check(row)) {
             const Py_ssize_t n = PyList_Check(row) ? PyList_GET_SIZE(row) : PyTuple_GET_SIZE(row);
-            if (n != width) fail(PyExc_ValueError, std::string(what) + ": ragged feature rows");
+            if (n != src_w) fail(PyExc_ValueError, std::string(what) + ": ragged feature rows");
             PyObject **it = PyList_Check(row) ? &PyList_GET_ITEM(row, 0) : &PyTuple_GET_ITEM(row, 0);
-            for (Py_ssize_t k = 0; k < n; ++k) d[k] = (float)to_double(it[k]);
+            for (Py_ssize_t k = 0; k < width; ++k) d[k] = (float)to_double(it[col0 + k]);
             continue;
         }
         Buf rb(row);
         if (rb.ok) {
-            if (rb.b.ndim != 1 || rb.b.shape[0] != width)
+            if (rb.b.ndim != 1 || rb.b.shape[0] != src_w)
                 fail(PyExc_ValueError, std::string(what) + ": ragged feature rows");
-            buffer_copy(rb.b, width, d, what);
+            Py_buffer part = rb.b;
+            part.buf = static_cast<char *>(rb.b.buf) + col0 * rb.b.itemsize;
+            buffer_copy(part, width, d, what);
             continue;
         }
         Ref rs(PySequence_Fast(row, what));
-        if (PySequence_Fast_GET_SIZE(rs.p) != width) fail(PyExc_ValueError, std::string(what) + ": ragged feature rows");
+        if (PySequence_Fast_GET_SIZE(rs.p) != src_w) fail(PyExc_ValueError, std::string(what) + ": ragged feature rows");
         PyObject **it = PySequence_Fast_ITEMS(rs.p);
-        for (Py_ssize_t k = 0; k < width; ++k) d[k] = (float)to_double(it[k]);
+        for (Py_ssize_t k = 0; k < width; ++k) d[k] = (float)to_double(it[col0 + k]);
+    }
+}
+
+// The reference builds every bond row as f_atoms[source atom] + bond features (featurization.py:467-468,
+// 545-546, 616-617).  Checks columns [0, fa_w) of the molecule's f_bonds rows against its packed
+// f_atoms rows (float32 values), at the molecule-local source atom of each bond.
+void check_bond_rows(PyObject *rows, Py_ssize_t n_rows, Py_ssize_t fa_w, const float *f_atoms_mol,
+                     const int64_t *b2a_local) {
+    std::vector<float> tmp((size_t)fa_w);
+    for (Py_ssize_t r = 0; r < n_rows; ++r) {
+        Ref seq(PySequence_GetItem(rows, r));
+        // reuse fill_table on a one-row view: wrap the row in a 1-tuple
+        Ref one(PyTuple_Pack(1, seq.p));
+        const Py_ssize_t src_w = PyObject_Length(seq.p);
+        if (src_w < fa_w) fail(PyExc_ValueError, "f_bonds rows are shorter than f_atoms rows");
+        fill_table(one.p, 1, src_w, 0, fa_w, tmp.data(), "f_bonds");
+        if (std::memcmp(tmp.data(), f_atoms_mol + b2a_local[r] * fa_w, (size_t)fa_w * 4) != 0)
+            fail(PyExc_ValueError, "f_bonds[b][:atom_fdim] != f_atoms[b2a[b]]: the bond rows do not start with "
+                                   "their source atom's features, so they cannot be rebuilt on the device");
     }
 }
 
@@ -172,13 +202,22 @@ PyObject *new_bytes(Py_ssize_t n) {
     return b;
 }
 
-// pack(mol_graphs, fa_w, fb_w) -> (f_atoms, f_bonds, w_atoms, w_bonds, b2a, b2revb, deg, in_idx,
-// n_atoms_per_mol, n_bonds_per_mol) as bytearrays (float32 [V+1][fa_w], float32 [E+1][fb_w],
+// pack(mol_graphs, fa_w, fb_w[, tail_from[, check]]) -> (f_atoms, f_bonds, w_atoms, w_bonds, b2a, b2revb,
+// deg, in_idx, n_atoms_per_mol, n_bonds_per_mol) as bytearrays (float32 [V+1][fa_w],
+// float32 [E+1][fb_w - tail_from] (tail_from = 0: whole rows; = fa_w: only the bond-feature tail, the
+// device rebuilds the rest from f_atoms, wdmpnn_build_bond_features; check = 1 verifies that the skipped
+// columns equal the source atom's row),
 // float32 [V+1], float32 [E+1], int64 [E+1] x 2, int64 [V+1], int64 [nnz], int64 [B] x 2)
 PyObject *pack(PyObject *, PyObject *args) {
     PyObject *graphs_obj;
-    Py_ssize_t fa_w, fb_w;
-    if (!PyArg_ParseTuple(args, "Onn", &graphs_obj, &fa_w, &fb_w)) return nullptr;
+    Py_ssize_t fa_w, fb_w, tail_from = 0;
+    int check = 0;
+    if (!PyArg_ParseTuple(args, "Onn|np", &graphs_obj, &fa_w, &fb_w, &tail_from, &check)) return nullptr;
+    if (tail_from < 0 || tail_from > fb_w || (tail_from != 0 && tail_from != fa_w)) {
+        PyErr_SetString(PyExc_ValueError, "tail_from must be 0 or the f_atoms row width");
+        return nullptr;
+    }
+    const Py_ssize_t fbo_w = fb_w - tail_from;  // f_bonds columns written
     PyObject *out[10] = {};
     try {
         Ref graphs(PySequence_Fast(graphs_obj, "mol_graphs must be a sequence"));
@@ -204,7 +243,7 @@ PyObject *pack(PyObject *, PyObject *args) {
             V += na[i]; E += nb[i]; nnz += c;
         }
         out[0] = new_bytes((V + 1) * fa_w * 4);
-        out[1] = new_bytes((E + 1) * fb_w * 4);
+        out[1] = new_bytes((E + 1) * fbo_w * 4);
         out[2] = new_bytes((V + 1) * 4);
         out[3] = new_bytes((E + 1) * 4);
         out[4] = new_bytes((E + 1) * 8);
@@ -229,11 +268,11 @@ PyObject *pack(PyObject *, PyObject *args) {
             PyObject *g = gs[i];
             {
                 Ref t(PyObject_GetAttrString(g, "f_atoms"));
-                fill_table(t.p, na[i], fa_w, f_atoms + ao * fa_w, "f_atoms");
+                fill_table(t.p, na[i], fa_w, 0, fa_w, f_atoms + ao * fa_w, "f_atoms");
             }
             {
                 Ref t(PyObject_GetAttrString(g, "f_bonds"));
-                fill_table(t.p, nb[i], fb_w, f_bonds + bo * fb_w, "f_bonds");
+                fill_table(t.p, nb[i], fb_w, tail_from, fbo_w, f_bonds + bo * fbo_w, "f_bonds");
             }
             {
                 Ref t(PyObject_GetAttrString(g, "w_atoms"));
@@ -246,6 +285,15 @@ PyObject *pack(PyObject *, PyObject *args) {
             {
                 Ref t(PyObject_GetAttrString(g, "b2a"));
                 fill_vector<int64_t>(t.p, nb[i], b2a + bo, ao, "b2a");
+            }
+            if (tail_from && check) {
+                std::vector<int64_t> local((size_t)nb[i]);
+                for (int64_t r = 0; r < nb[i]; ++r) {
+                    local[r] = b2a[bo + r] - ao;
+                    if (local[r] < 0 || local[r] >= na[i]) fail(PyExc_ValueError, "b2a out of range");
+                }
+                Ref t(PyObject_GetAttrString(g, "f_bonds"));
+                check_bond_rows(t.p, nb[i], fa_w, f_atoms + ao * fa_w, local.data());
             }
             {
                 Ref t(PyObject_GetAttrString(g, "b2revb"));
@@ -282,7 +330,7 @@ PyObject *pack(PyObject *, PyObject *args) {
 
 PyMethodDef methods[] = {
     {"pack", pack, METH_VARARGS,
-     "pack(mol_graphs, fa_w, fb_w) -> 10 bytearrays: the concatenated BatchMolGraph tables "
+     "pack(mol_graphs, fa_w, fb_w, tail_from=0, check=False) -> 10 bytearrays: the concatenated BatchMolGraph tables "
      "(featurization.py:757-813)"},
     {nullptr, nullptr, 0, nullptr}};
 

@@ -1048,6 +1048,23 @@ int wdmpnn_split_planes_rows(const float *src, int32_t ld, int32_t rows, int32_t
     return 0;
 }
 
+int wdmpnn_build_bond_features(const float *f_atoms, int32_t ld_atoms, int32_t atom_fdim, int32_t atom_rows,
+                               const int32_t *b2a, const float *bond_tail, int32_t ld_tail, int32_t tail_dim,
+                               int32_t rows, float *f_bonds, int32_t ld_bonds, void *stream) {
+    if (rows == 0) return 0;
+    if (!f_atoms || !b2a || !f_bonds || (tail_dim && !bond_tail)) return fail(WD_ERR_ARG, "null pointer");
+    if (rows < 0 || atom_rows <= 0 || atom_fdim < 0 || tail_dim < 0 || atom_fdim > ld_atoms || tail_dim > ld_tail ||
+        atom_fdim + tail_dim > ld_bonds)
+        return fail(WD_ERR_SHAPE, "build_bond_features: need atom_fdim <= ld_atoms, tail_dim <= ld_tail, "
+                                  "atom_fdim + tail_dim <= ld_bonds (got %d/%d, %d/%d, ld_bonds %d)",
+                    atom_fdim, ld_atoms, tail_dim, ld_tail, ld_bonds);
+    hipLaunchKernelGGL(build_bond_features_kernel, dim3(ew_blocks((size_t)rows * ld_bonds)), dim3(256), 0,
+                       (hipStream_t)stream, f_atoms, ld_atoms, atom_fdim, atom_rows, b2a, bond_tail, ld_tail, tail_dim,
+                       rows, f_bonds, ld_bonds);
+    WD_CHECK_LAUNCH("build_bond_features");
+    return 0;
+}
+
 int wdmpnn_index_select_rows(const float *src, int64_t n_src_rows, int64_t row_len, const int64_t *index,
                              int64_t n_index, float *out, void *stream) {
     if (n_index < 0 || row_len < 0 || n_src_rows < 0) return fail(WD_ERR_ARG, "negative size");

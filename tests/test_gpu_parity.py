@@ -291,3 +291,38 @@ def test_blocked_forward_edge_cases_and_fallback():
         with torch.no_grad():
             out = enc(g)
         assert golden_io.normwise(out.cpu().numpy(), ref.numpy()) <= TOL
+
+
+@pytest.mark.parametrize('kind,b,extra', [('polymer', 64, {}), ('qm9', 32, dict(bias=True)),
+                                          ('edge', 9, dict(activation='ELU')),
+                                          ('polymer', 8, dict(atom_messages=True, hidden_size=64))])
+def test_device_bond_features(kind, b, extra):
+    """f_bonds rebuilt on the device from f_atoms + bond tail + b2a
+    (wdmpnn_build_bond_features) equals the host-packed f_bonds bit for bit, and the encoder's output
+    (forward and gradients) is bitwise identical to the host-featurised graph's."""
+    mols = synthetic.make_batch(kind, b, 77) if kind != 'edge' else synthetic.edge_case_batch(b, star_leaves=30)
+    g_host = BatchMolGraph(mols)
+    g_dev = BatchMolGraph(mols, device_bond_features=True, check_bond_features=True)
+    am = bool(extra.get('atom_messages'))
+    fdim = get_bond_fdim(atom_messages=am)
+    d_host = g_host.device_graph(DEV, am, fdim)
+    d_dev = g_dev.device_graph(DEV, am, fdim)
+    assert d_dev.h2d_bytes <= d_host.h2d_bytes if am else d_dev.h2d_bytes < 0.5 * d_host.h2d_bytes
+    if not am:
+        assert torch.equal(d_dev.views['f_bonds'].view(torch.uint8).reshape(-1)[:d_host.views['f_bonds'].numel()],
+                           d_host.views['f_bonds'])
+    args = TrainArgs(**{'hidden_size': 128, 'depth': 3, **extra})
+    outs = []
+    for g in (g_host, g_dev):
+        torch.manual_seed(0)
+        enc = MPNEncoder(args, get_atom_fdim(), fdim)
+        synthetic.fill_parameters(enc, 3)
+        enc = enc.to(DEV)
+        out = enc(g)
+        out.square().sum().backward()
+        outs.append((out.detach().cpu(), [p.grad.detach().cpu() for p in enc.parameters() if p.grad is not None]))
+        with torch.no_grad():
+            outs[-1] += (enc.eval()(g).cpu(),)
+    (o1, g1, e1), (o2, g2, e2) = outs
+    assert torch.equal(o1, o2) and torch.equal(e1, e2)
+    assert all(torch.equal(a, b) for a, b in zip(g1, g2))

@@ -6,6 +6,7 @@ import copy
 
 import numpy as np
 import pytest
+import torch
 
 from chemprop_amd import synthetic
 from chemprop_amd.featurization import BatchMolGraph
@@ -78,3 +79,35 @@ def test_native_packer_rejects_malformed_graphs():
     bad.b2a = list(mgs[1].b2a) + [0]
     with pytest.raises(ValueError, match='b2a'):
         BatchMolGraph([bad])
+
+
+@pytest.mark.parametrize('kind', sorted(BATCHES))
+def test_bond_tail_mode_rebuilds_the_same_f_bonds(kind):
+    """device_bond_features keeps only the bond-feature tail of f_bonds on the host (the device rebuilds
+    f_atoms[b2a] ‖ tail); the host view assembled from it equals the full packing bit for bit."""
+    mgs = BATCHES[kind]()
+    full = BatchMolGraph(mgs)
+    tail = BatchMolGraph(mgs, device_bond_features=True, check_bond_features=True)
+    fa_w = full.f_atoms.shape[1]
+    np.testing.assert_array_equal(tail._np['bond_tail'], full.f_bonds.numpy()[:, fa_w:])
+    np.testing.assert_array_equal(tail.f_bonds.numpy(), full.f_bonds.numpy())
+    for a, b in zip(tail.get_components(), full.get_components()):
+        if isinstance(a, torch.Tensor):
+            assert torch.equal(a, b)
+        else:
+            assert a == b
+
+
+def test_bond_tail_check_rejects_rows_that_are_not_atom_plus_bond():
+    mgs = synthetic.make_batch('qm9', 3, 8)
+    bad = copy.copy(mgs[1])
+    bad.f_bonds = [list(r) for r in mgs[1].f_bonds]
+    bad.f_bonds[0][3] += 1.0  # atom part of bond 0 no longer equals f_atoms[b2a[0]]
+    with pytest.raises(ValueError, match='source atom'):
+        BatchMolGraph([mgs[0], bad], device_bond_features=True, check_bond_features=True)
+    BatchMolGraph([mgs[0], bad], device_bond_features=True)  # unchecked: the caller vouches for the layout
+    # numpy tables work in tail mode too
+    h = copy.copy(mgs[2])
+    h.f_bonds = np.asarray(mgs[2].f_bonds, np.float64)
+    t = BatchMolGraph([h], device_bond_features=True, check_bond_features=True)
+    np.testing.assert_array_equal(t.f_bonds.numpy(), BatchMolGraph([mgs[2]]).f_bonds.numpy())
