@@ -380,11 +380,13 @@ class BatchMolGraph:
             atom_blk = np.full(fa_p.shape[0], -1, np.int32)
             blk_of_bond = np.full(fb_p.shape[0], -1, np.int64)
             blk_of_atom = np.full(fa_p.shape[0], -1, np.int64)
-            for k, (bs, bn, as_, an) in enumerate(blocks[:, :4]):
-                bond_blk[bs:bs + bn] = BLK_BONDS * k + np.arange(bn)
-                atom_blk[as_:as_ + an] = BLK_ATOMS * k + np.arange(an)
-                blk_of_bond[bs:bs + bn] = k
-                blk_of_atom[as_:as_ + an] = k
+            for (start, count, cap, blk_row, blk_of) in ((blocks[:, 0], blocks[:, 1], BLK_BONDS, bond_blk, blk_of_bond),
+                                                         (blocks[:, 2], blocks[:, 3], BLK_ATOMS, atom_blk, blk_of_atom)):
+                k = np.repeat(np.arange(len(blocks)), count)  # rows of a block are contiguous from its start
+                within = np.arange(len(k)) - np.repeat(np.cumsum(count) - count, count)
+                rows = np.repeat(start, count) + within
+                blk_row[rows] = cap * k + within
+                blk_of[rows] = k
             for c, rb in ((msg, blk_of_bond), (agg, blk_of_atom)):
                 row = np.repeat(np.arange(len(c.ptr) - 1), np.diff(c.ptr))
                 if len(row) and not np.array_equal(rb[row], blk_of_bond[c.idx]):
@@ -419,7 +421,7 @@ class BatchMolGraph:
         host = torch.empty(total, dtype=torch.uint8, pin_memory=device.type == 'cuda' and torch.cuda.is_available())
         hv = host.numpy()
         for name, a in arrays:
-            hv[offsets[name]:offsets[name] + a.nbytes] = np.frombuffer(np.ascontiguousarray(a).tobytes(), np.uint8)
+            hv[offsets[name]:offsets[name] + a.nbytes] = np.ascontiguousarray(a).reshape(-1).view(np.uint8)
         buf = host.to(device, non_blocking=True)
         base = buf.data_ptr() if device.type == 'cuda' else 0
         views = {name: buf[offsets[name]:offsets[name] + a.nbytes] for name, a in arrays}

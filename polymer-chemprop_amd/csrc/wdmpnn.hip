@@ -240,7 +240,9 @@ Epi epi_act(int act, const float *slope, const float *bias, const float *resid, 
             const WdConfig *c, uint32_t layer) {
     Epi e{};
     e.kind = EPI_ACT; e.act = act; e.slope = slope; e.bias = bias; e.resid = resid; e.Z = Z; e.Y = Y; e.ld = ld;
-    e.p_drop = c->dropout; e.seed = c->seed; e.layer = layer;
+    // dropout follows every W_h update, W_o and the descriptor layer (mpn.py:124, 134, 143), never the
+    // input layer's message = act(input) (mpn.py:97): layer 0 is not dropped
+    e.p_drop = layer == 0 ? 0.f : c->dropout; e.seed = c->seed; e.layer = layer;
     return e;
 }
 
@@ -872,7 +874,8 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
     };
     auto base_bwd = [&](const float *Z, uint32_t layer, int act, int rows, int rows_p, int cols, float *out) {
         ActBwd P{};
-        P.Z = Z; P.act = act; P.slope = p->prelu; P.p_drop = c->dropout; P.seed = c->seed; P.layer = layer;
+        P.Z = Z; P.act = act; P.slope = p->prelu; P.p_drop = layer == 0 ? 0.f : c->dropout;  // (see epi_act)
+        P.seed = c->seed; P.layer = layer;
         P.rows = rows; P.rows_p = rows_p; P.cols = cols; P.ld = cols; P.out = out;
         return P;
     };

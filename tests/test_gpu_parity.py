@@ -326,3 +326,21 @@ def test_device_bond_features(kind, b, extra):
     (o1, g1, e1), (o2, g2, e2) = outs
     assert torch.equal(o1, o2) and torch.equal(e1, e2)
     assert all(torch.equal(a, b) for a, b in zip(g1, g2))
+
+
+@pytest.mark.parametrize('extra', [dict(), dict(activation='PReLU', bias=True)])
+def test_dropout_masks_agree_across_paths(extra):
+    """Training-mode dropout (counter-hash masks on each W_h update and on W_o, none on the input
+    layer's message = act(input), mpn.py:97/124/134): the grad-enabled forward (unblocked kernels)
+    and the no-grad forward (molecule-blocked fused kernels) drop the same elements."""
+    args = TrainArgs(hidden_size=96, depth=3, dropout=0.25, **extra)
+    g = BatchMolGraph(synthetic.make_batch('polymer', 32, 21))
+    enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim())
+    synthetic.fill_parameters(enc, 8)
+    enc = enc.to(DEV).train()
+    enc._seed_counter = 0
+    with torch.no_grad():
+        a = enc(g)
+    enc._seed_counter = 0
+    b = enc(g)
+    assert golden_io.normwise(a.cpu().numpy(), b.detach().cpu().numpy()) <= TOL
