@@ -41,6 +41,7 @@ extern "C" {
 #endif
 
 #define WDMPNN_ABI_VERSION 2
+#define WDMPNN_ELL_WIDTH 8
 
 enum WdActivation {     /* nn_utils.py:70-99 get_activation_function */
     WD_ACT_RELU = 0, WD_ACT_LEAKY_RELU = 1, WD_ACT_PRELU = 2, WD_ACT_TANH = 3,
@@ -112,11 +113,12 @@ typedef struct WdGraph {
     const int32_t *blocks;
     const int32_t *bond_blk_row;
     const void *f_atoms_blk_x6;
-    /* Required with blocks: the first 8 entries of every msg_gather / atom_gather row in block-local
-     * form ("ELL-8"), so that the fused kernels fetch a row's list with two independent loads instead
-     * of a ptr -> idx chain.  *_ell_idx[8 r + k] = idx - bond_start of the row's block (uint8, < 128),
-     * *_ell_coef[8 r + k] = coef; unused slots coef 0 and a valid index; bit 7 of slot 7 set when the
-     * row has more than 8 entries (the rest are read from the CSR lists). */
+    /* Required with blocks: the first WDMPNN_ELL_WIDTH (W = 8) entries of every msg_gather / atom_gather
+     * row in block-local ELL form, so that the fused kernels prefetch a row's list with independent
+     * loads during the GEMM instead of a ptr -> idx chain after it.  *_ell_idx[W r + k] = idx -
+     * bond_start of the row's block (uint8, < 128), *_ell_coef[W r + k] = coef; unused slots coef 0 and
+     * a valid index; bit 7 of slot W - 1 set when the row has more than W entries (the rest are read
+     * from the CSR lists). */
     const uint8_t *msg_ell_idx;
     const float *msg_ell_coef;
     const uint8_t *atom_ell_idx;

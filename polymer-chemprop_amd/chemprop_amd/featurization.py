@@ -92,23 +92,26 @@ class Csr:
         return out
 
 
-def ell8(c: 'Csr', rows_p: int, base: np.ndarray):
-    """First 8 entries of every CSR row in block-local form (WdGraph.*_ell_idx / *_ell_coef): index
-    idx - base[row] as uint8 (< 128), coefficient; unused slots (index 0, coef 0); bit 7 of slot 7 set
-    on rows with more than 8 entries."""
+ELLW = 8  # gather entries per row held in the block-local ELL form (WdGraph.*_ell_*)
+
+
+def ell_rows(c: 'Csr', rows_p: int, base: np.ndarray, width: int = ELLW):
+    """First ``width`` entries of every CSR row in block-local form (WdGraph.*_ell_idx / *_ell_coef):
+    index idx - base[row] as uint8 (< 128), coefficient; unused slots (index 0, coef 0); bit 7 of the
+    last slot set on rows with more entries (the kernels take the rest from the CSR list)."""
     n = len(c.ptr) - 1
-    idx = np.zeros((rows_p, 8), np.uint8)
-    coef = np.zeros((rows_p, 8), np.float32)
+    idx = np.zeros((rows_p, width), np.uint8)
+    coef = np.zeros((rows_p, width), np.float32)
     cnt = np.diff(c.ptr)
     row = np.repeat(np.arange(n), cnt)
     slot = np.arange(len(row)) - np.repeat(c.ptr[:-1], cnt)
-    keep = slot < 8
+    keep = slot < width
     local = c.idx[:len(row)].astype(np.int64) - base[row]
     if len(local) and (local[keep].min() < 0 or local[keep].max() >= 128):
-        raise ValueError('ell8: an entry leaves its molecule block')
+        raise ValueError('ell_rows: an entry leaves its molecule block')
     idx[row[keep], slot[keep]] = local[keep].astype(np.uint8)
     coef[row[keep], slot[keep]] = c.coef[:len(row)][keep]
-    idx[:n, 7] |= np.where(cnt > 8, 0x80, 0).astype(np.uint8)
+    idx[:n, width - 1] |= np.where(cnt > width, 0x80, 0).astype(np.uint8)
     return idx.reshape(-1), coef.reshape(-1)
 
 
@@ -405,7 +408,7 @@ class BatchMolGraph:
             bstart[:-1] = blocks[:, 0]
             for name, c, rows_p, rb in (('msg_ell', msg, fb_p.shape[0], blk_of_bond), ('agg_ell', agg, fa_p.shape[0],
                                                                                      blk_of_atom)):
-                ell_idx, ell_coef = ell8(c, rows_p, bstart[rb[:len(c.ptr) - 1]])
+                ell_idx, ell_coef = ell_rows(c, rows_p, bstart[rb[:len(c.ptr) - 1]])
                 arrays += [(name + '_idx', ell_idx), (name + '_coef', ell_coef)]
         csrs = [('msg', msg), ('agg', agg), ('msg_t', msg_t), ('agg_t', agg_t)]
         if feat is not None:

@@ -25,10 +25,41 @@
 namespace wd {
 
 constexpr int BLK_BONDS = 128, BLK_ATOMS = 64;  // block capacity (rows of the blocked layouts)
+// gather entries per row in the block-local ELL form (WdGraph.*_ell_*, WDMPNN_ELL_WIDTH; 12 measured
+// no faster than 8 on the polymer benchmark, whose longest rows have 9 entries)
+constexpr int ELLW = 8;
+static_assert(ELLW % 4 == 0, "ELL rows of whole 4-byte index words and float4 weight groups");
+
+// one prefetched ELL row: ELLW uint8 indices (bit 7 of the last = "more entries in the CSR list") and
+// ELLW weights (0 = empty slot)
+struct EllRow {
+    uint32_t ix[ELLW / 4];
+    float w[ELLW];
+};
+__device__ __forceinline__ EllRow ell_zero() {
+    EllRow e;
+    for (int k = 0; k < ELLW / 4; ++k) e.ix[k] = 0;
+    for (int k = 0; k < ELLW; ++k) e.w[k] = 0.f;
+    return e;
+}
+__device__ __forceinline__ EllRow ell_load(const uint8_t *idx, const float *coef, size_t row) {
+    EllRow e;
+    const uint32_t *ip = reinterpret_cast<const uint32_t *>(idx + ELLW * row);
+    const float *cp = coef + ELLW * row;
+#pragma unroll
+    for (int q = 0; q < ELLW / 4; ++q) {
+        e.ix[q] = ip[q];
+        const float4 w = ld4(cp + 4 * q);
+        e.w[4 * q] = w.x; e.w[4 * q + 1] = w.y; e.w[4 * q + 2] = w.z; e.w[4 * q + 3] = w.w;
+    }
+    return e;
+}
+__device__ __forceinline__ int ell_idx(const EllRow &e, int k) { return (e.ix[k >> 2] >> (8 * (k & 3))) & 0x7f; }
+__device__ __forceinline__ bool ell_more(const EllRow &e) { return e.ix[ELLW / 4 - 1] & 0x80000000u; }
 
 // WD_EXP (timing experiments only, never set in the product build): 1 = skip the layer GEMM,
 // 2 = skip the layer's plane stores, 3 = skip the in-block gather, 4 = skip the residual prefetch,
-// 5 = store fp32 instead of planes, 6 = skip residual and ELL prefetch
+// 6 = skip residual and ELL prefetch
 #ifndef WD_EXP
 #define WD_EXP 0
 #endif
@@ -75,7 +106,7 @@ struct MpLayerP {
     const float *bias;          // b_h (padded) or null
     const int32_t *blocks;
     const int32_t *ptr, *idx; const float *coef;   // msg gather, natural rows
-    const uint8_t *ell_idx; const float *ell_coef;  // its first 8 entries per row, block-local (WdGraph)
+    const uint8_t *ell_idx; const float *ell_coef;  // its first ELLW entries per row, block-local (WdGraph)
     const int32_t *sym_rev;     // undirected (mpn.py:101-102) or null
     int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;
     const int32_t *aptr, *aidx; const float *acoef;  // atom gather (natural atom rows -> natural bond rows)
@@ -115,16 +146,20 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
     const int tid = threadIdx.x;
-    // residual rows and the rows' gather lists (ELL-8) prefetched during the GEMM (unit v = tid + NT i:
-    // row v / UPR, columns 8 (v % UPR) ..)
-    float4 res[UPT][2], ecf[UPT][2];
-    uint2 eix[UPT];
+    // residual rows and the rows' gather lists (ELL) prefetched during the GEMM (unit v = tid + NT i:
+    // row v / UPR, columns 8 (v % UPR) ..); the last layer also prefetches the atom gather rows of its
+    // atom-aggregate units (unit v = tid: atom v / UPR)
+    constexpr int AUNITS = BLK_ATOMS * UPR;
+    static_assert(!LAST || AUNITS <= NT, "one atom-aggregate unit per thread");
+    float4 res[UPT][2];
+    EllRow ell[UPT];
+    EllRow aell = ell_zero();
     auto prefetch = [&]() {
 #pragma unroll
         for (int i = 0; i < UPT; ++i) {
             const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
-            res[i][0] = res[i][1] = ecf[i][0] = ecf[i][1] = f4zero();
-            eix[i] = make_uint2(0, 0);
+            res[i][0] = res[i][1] = f4zero();
+            ell[i] = ell_zero();
             if (v < UNITS && lr < B.bn) {
                 const size_t b = B.bs + lr;
                 const float *s = P.inp + b * P.kp + n0 + c;
@@ -132,13 +167,11 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
                     res[i][0] = ld4(s);
                     res[i][1] = ld4(s + 4);
                 }
-                if (WD_EXP != 6) {
-                    eix[i] = *reinterpret_cast<const uint2 *>(P.ell_idx + 8 * b);
-                    ecf[i][0] = ld4(P.ell_coef + 8 * b);
-                    ecf[i][1] = ld4(P.ell_coef + 8 * b + 4);
-                }
+                if (WD_EXP != 6) ell[i] = ell_load(P.ell_idx, P.ell_coef, b);
             }
         }
+        if constexpr (LAST)
+            if (tid / UPR < B.an) aell = ell_load(P.aell_idx, P.aell_coef, (size_t)B.as + tid / UPR);
     };
 #if WD_EXP == 13
     prefetch();
@@ -177,20 +210,18 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
         if (lr < B.bn) {
             const int b = B.bs + lr;
             float4 s0 = f4zero(), s1 = f4zero();
-            // the first 8 entries from the prefetched ELL row, in CSR order (the reference's slot order);
-            // unused slots have weight 0 and are skipped (the CSR lists hold no zero weights)
-            const uint32_t ix[2] = {eix[i].x, eix[i].y};
-            const float w8[8] = {ecf[i][0].x, ecf[i][0].y, ecf[i][0].z, ecf[i][0].w,
-                                 ecf[i][1].x, ecf[i][1].y, ecf[i][1].z, ecf[i][1].w};
+            // the first ELLW entries from the prefetched ELL row, in CSR order (the reference's slot
+            // order); unused slots have weight 0 and are skipped (the CSR lists hold no zero weights)
+            const EllRow &E = ell[i];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int j = (ix[k >> 2] >> (8 * (k & 3))) & 0x7f;
-                if (WD_EXP == 3 || (WD_EXP != 14 && w8[k] == 0.f)) continue;
-                if (P.sym_rev) msg_term<LDC>(Pt, B.bs + j, B.bs, P.sym_rev, c, w8[k], s0, s1);
-                else lds_term<LDC>(Pt, j, c, w8[k], s0, s1);
+            for (int k = 0; k < ELLW; ++k) {
+                const int j = ell_idx(E, k);
+                if (WD_EXP == 3 || (WD_EXP != 14 && E.w[k] == 0.f)) continue;
+                if (P.sym_rev) msg_term<LDC>(Pt, B.bs + j, B.bs, P.sym_rev, c, E.w[k], s0, s1);
+                else lds_term<LDC>(Pt, j, c, E.w[k], s0, s1);
             }
-            if (ix[1] & 0x80000000u)  // more than 8 entries: the rest from the CSR list
-                for (int e = P.ptr[b] + 8; e < P.ptr[b + 1]; ++e)
+            if (ell_more(E))  // more than ELLW entries: the rest from the CSR list
+                for (int e = P.ptr[b] + ELLW; e < P.ptr[b + 1]; ++e)
                     msg_term<LDC>(Pt, P.idx[e], B.bs, P.sym_rev, c, P.coef ? P.coef[e] : 1.0f, s0, s1);
             float4 b0 = f4zero(), b1 = f4zero();
             if (P.bias) { b0 = ld4(P.bias + n0 + c); b1 = ld4(P.bias + n0 + c + 4); }
@@ -210,10 +241,6 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
         if constexpr (LAST) {
             st4(Mt + lr * LDC + c, y0);
             st4(Mt + lr * LDC + c + 4, y1);
-        } else if (lr < B.bn && WD_EXP == 5) {
-            float *d = reinterpret_cast<float *>(P.mnext) + (size_t)(blk * BM + lr) * P.kp + n0 + c;
-            st4(d, y0);
-            st4(d + 4, y1);
         } else if (lr < B.bn && WD_EXP != 2) {  // rows past the block's bonds are never loaded by the next layer
             x6_store8_blk<BM>(mrs, lr, n0 + c, y0, y1);
         }
@@ -222,22 +249,15 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
         __syncthreads();
         // atom aggregate of this column tile: A[a] = Σ_{b into a} w_b M_t[b] (mpn.py:126-131)
         const __amdgpu_buffer_rsrc_t ars = x6_block_rsrc<BLK_ATOMS>(P.aplanes, P.kp, blk);
-        for (int v = tid; v < B.an * UPR; v += NT) {  // rows past the block's atoms are never loaded
-            const int la = v / UPR, c = 8 * (v % UPR);
+        if (tid < B.an * UPR) {  // rows past the block's atoms are never loaded
+            const int la = tid / UPR, c = 8 * (tid % UPR), a = B.as + la;
             float4 s0 = f4zero(), s1 = f4zero();
-            if (la < B.an) {
-                const int a = B.as + la;
-                const uint2 e = *reinterpret_cast<const uint2 *>(P.aell_idx + 8 * (size_t)a);
-                const float4 w0 = ld4(P.aell_coef + 8 * (size_t)a), w1 = ld4(P.aell_coef + 8 * (size_t)a + 4);
-                const uint32_t ix[2] = {e.x, e.y};
-                const float w8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    if (w8[k] != 0.f) lds_term<LDC>(Mt, (ix[k >> 2] >> (8 * (k & 3))) & 0x7f, c, w8[k], s0, s1);
-                if (ix[1] & 0x80000000u)
-                    for (int q = P.aptr[a] + 8; q < P.aptr[a + 1]; ++q)
-                        lds_term<LDC>(Mt, P.aidx[q] - B.bs, c, P.acoef ? P.acoef[q] : 1.0f, s0, s1);
-            }
+            for (int k = 0; k < ELLW; ++k)
+                if (aell.w[k] != 0.f) lds_term<LDC>(Mt, ell_idx(aell, k), c, aell.w[k], s0, s1);
+            if (ell_more(aell))
+                for (int q = P.aptr[a] + ELLW; q < P.aptr[a + 1]; ++q)
+                    lds_term<LDC>(Mt, P.aidx[q] - B.bs, c, P.acoef ? P.acoef[q] : 1.0f, s0, s1);
             x6_store8_blk<BLK_ATOMS>(ars, la, n0 + c, s0, s1);
         }
     }

@@ -307,7 +307,7 @@ def test_device_bond_features(kind, b, extra):
     fdim = get_bond_fdim(atom_messages=am)
     d_host = g_host.device_graph(DEV, am, fdim)
     d_dev = g_dev.device_graph(DEV, am, fdim)
-    assert d_dev.h2d_bytes <= d_host.h2d_bytes if am else d_dev.h2d_bytes < 0.5 * d_host.h2d_bytes
+    assert d_dev.h2d_bytes <= d_host.h2d_bytes if am else d_dev.h2d_bytes < d_host.h2d_bytes
     if not am:
         assert torch.equal(d_dev.views['f_bonds'].view(torch.uint8).reshape(-1)[:d_host.views['f_bonds'].numel()],
                            d_host.views['f_bonds'])

@@ -114,10 +114,11 @@ def test_molecule_blocks_refuse_an_oversized_molecule():
 
 
 @pytest.mark.parametrize('kind', sorted(GRAPHS))
-def test_ell8_restates_the_gather_lists(kind):
-    """The block-local ELL-8 rows (WdGraph.*_ell_*) hold the first 8 CSR entries of every row (unused
-    slots weight 0, bit 7 of slot 7 marks longer rows): applying them plus the CSR tail equals the CSR."""
-    from chemprop_amd.featurization import ell8
+def test_ell_rows_restate_the_gather_lists(kind):
+    """The block-local ELL rows (WdGraph.*_ell_*) hold the first ELLW CSR entries of every row (unused
+    slots weight 0, bit 7 of the last slot marks longer rows): applying them plus the CSR tail equals
+    the CSR."""
+    from chemprop_amd.featurization import ELLW, ell_rows
     g = BatchMolGraph(GRAPHS[kind]() if kind != 'edge' else synthetic.edge_case_batch(3, star_leaves=40))
     blocks = g.molecule_blocks()
     bstart = np.zeros(len(blocks) + 1, np.int64)
@@ -126,16 +127,20 @@ def test_ell8_restates_the_gather_lists(kind):
     for k, (bs, bn) in enumerate(blocks[:, :2]):
         blk_b[bs:bs + bn] = k
     csr = g.bond_message_gather()
-    idx, coef = ell8(csr, csr.rows, bstart[blk_b])
-    idx, coef = idx.reshape(-1, 8), coef.reshape(-1, 8)
-    S = rand((g.n_bonds, 4), 9)
+    for W in (ELLW, 8, 2):  # the shipped width, and narrow ones so that the tail path is exercised
+        check_ell(csr, blk_b, bstart, *ell_rows(csr, csr.rows, bstart[blk_b], W), W)
+
+
+def check_ell(csr, blk_b, bstart, idx, coef, W):
+    idx, coef = idx.reshape(-1, W), coef.reshape(-1, W)
+    S = rand((csr.rows, 4), 9)
     out = np.zeros((csr.rows, 4))
     for r in range(1, csr.rows):
         base = bstart[blk_b[r]]
-        for k in range(8):
+        for k in range(W):
             out[r] += coef[r, k] * S[base + (idx[r, k] & 0x7f)]
-        assert bool(idx[r, 7] & 0x80) == (csr.ptr[r + 1] - csr.ptr[r] > 8)
-        for e in range(csr.ptr[r] + 8, csr.ptr[r + 1]):
+        assert bool(idx[r, W - 1] & 0x80) == (csr.ptr[r + 1] - csr.ptr[r] > W)
+        for e in range(csr.ptr[r] + W, csr.ptr[r + 1]):
             out[r] += csr.coef[e] * S[csr.idx[e]]
     np.testing.assert_allclose(out[1:], csr.apply(S)[1:], rtol=1e-6, atol=1e-6)
 
