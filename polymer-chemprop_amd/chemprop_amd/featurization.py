@@ -428,7 +428,10 @@ class BatchMolGraph:
         buf = host.to(device, non_blocking=True)
         base = buf.data_ptr() if device.type == 'cuda' else 0
         views = {name: buf[offsets[name]:offsets[name] + a.nbytes] for name, a in arrays}
-        views['_host'] = host  # keep the pinned source alive until the copy has run
+        # the pinned staging block goes back to torch's caching host allocator, which records the copy's
+        # stream event and recycles the block only after the copy has run: later batches reuse pinned
+        # memory instead of pinning fresh pages
+        del host, hv
 
         def P(name):
             return base + offsets[name]
