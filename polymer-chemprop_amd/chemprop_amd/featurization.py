@@ -98,21 +98,11 @@ ELLW = 8  # gather entries per row held in the block-local ELL form (WdGraph.*_e
 def ell_rows(c: 'Csr', rows_p: int, base: np.ndarray, width: int = ELLW):
     """First ``width`` entries of every CSR row in block-local form (WdGraph.*_ell_idx / *_ell_coef):
     index idx - base[row] as uint8 (< 128), coefficient; unused slots (index 0, coef 0); bit 7 of the
-    last slot set on rows with more entries (the kernels take the rest from the CSR list)."""
-    n = len(c.ptr) - 1
-    idx = np.zeros((rows_p, width), np.uint8)
-    coef = np.zeros((rows_p, width), np.float32)
-    cnt = np.diff(c.ptr)
-    row = np.repeat(np.arange(n), cnt)
-    slot = np.arange(len(row)) - np.repeat(c.ptr[:-1], cnt)
-    keep = slot < width
-    local = c.idx[:len(row)].astype(np.int64) - base[row]
-    if len(local) and (local[keep].min() < 0 or local[keep].max() >= 128):
-        raise ValueError('ell_rows: an entry leaves its molecule block')
-    idx[row[keep], slot[keep]] = local[keep].astype(np.uint8)
-    coef[row[keep], slot[keep]] = c.coef[:len(row)][keep]
-    idx[:n, width - 1] |= np.where(cnt > width, 0x80, 0).astype(np.uint8)
-    return idx.reshape(-1), coef.reshape(-1)
+    last slot set on rows with more entries (the kernels take the rest from the CSR list).  Built by
+    the native packer (csrc/packer.cpp ``ell``)."""
+    idx, coef = _packer().ell(c.ptr, c.idx, c.coef, int(rows_p), np.ascontiguousarray(base[:c.rows], np.int64),
+                              int(width))
+    return np.frombuffer(idx, np.uint8), np.frombuffer(coef, np.float32)
 
 
 def _packer():
@@ -193,6 +183,7 @@ class BatchMolGraph:
         self.b2a = torch.from_numpy(b2a)
         self.b2revb = torch.from_numpy(b2revb)
         self._a2b = None
+        self._gathers = None
         self.b2b = None
         self.a2a = None
         self._device_cache: Dict[tuple, DeviceGraph] = {}
@@ -257,27 +248,21 @@ class BatchMolGraph:
         slot = np.arange(len(rows), dtype=np.int64) - np.repeat(np.cumsum(counts) - counts, counts)
         return rows, self._in_idx[starts + slot]
 
+    def _native_gathers(self):
+        """(msg, agg, msg_t, agg_t) built by the native packer (csrc/packer.cpp ``gathers``), cached."""
+        if self._gathers is None:
+            out = _packer().gathers(self._np['b2a'], self._np['b2revb'], self._np['w_bonds'], self._deg,
+                                    self._in_idx)
+            self._gathers = tuple(Csr(np.frombuffer(p, np.int32), np.frombuffer(i, np.int32),
+                                      np.frombuffer(c, np.float32)) for p, i, c in out)
+        return self._gathers
+
     def bond_message_gather(self) -> Csr:
-        """mpn.py:112-120 as a row gather over bonds:
+        """mpn.py:112-120 as a row gather over bonds, built natively (csrc/packer.cpp ``gathers``; the
+        numpy restatement it is tested against is oracle/pack_ref.bond_message_gather):
         X_b = sum_{j in in(b2a[b])} w_j M_j - M_{b2revb[b]}.  The reverse bond normally is in
         in(b2a[b]); its coefficient becomes w_rev - 1 and is dropped when 0 (w = 1 bonds)."""
-        E1 = self.n_bonds
-        w = self._np['w_bonds']
-        b2a, rev = self._np['b2a'], self._np['b2revb']
-        bonds = np.arange(1, E1, dtype=np.int64)
-        rows, j = self._entries_of_in(b2a[bonds])
-        rows = bonds[rows]
-        coef = w[j].astype(np.float64)
-        is_rev = j == rev[rows]
-        coef[is_rev] -= 1.0
-        has_rev = np.zeros(E1, bool)
-        has_rev[rows[is_rev]] = True
-        missing = bonds[~has_rev[bonds]]  # reverse bond not among the in-bonds: explicit -1 entry
-        rows = np.concatenate([rows, missing])
-        j = np.concatenate([j, rev[missing]])
-        coef = np.concatenate([coef, -np.ones(len(missing))])
-        keep = coef != 0.0
-        return Csr.from_rows(rows[keep], j[keep], coef[keep].astype(np.float32), E1)
+        return self._native_gathers()[0]
 
     def atom_message_gather(self) -> Tuple[Csr, Csr]:
         """mpn.py:104-108 (atom messages): nei_a = sum over a2b slots of M[a2a] (pad slots gather atom 0,
@@ -297,20 +282,18 @@ class BatchMolGraph:
     def atom_aggregate_gather(self, atom_messages: bool = False) -> Csr:
         """mpn.py:126-131: A_a = sum_{slots} M[a2x] * w_bonds[a2x] (a2x = a2b, or a2a in atom-message
         mode where the weights are w_bonds indexed by ATOM ids, a reference quirk kept as is)."""
+        if not atom_messages:  # native (oracle/pack_ref.atom_aggregate_gather restates it)
+            return self._native_gathers()[1]
         V1 = self.n_atoms
         rows, j = self._entries_of_in(np.arange(V1, dtype=np.int64))
         w = self._np['w_bonds']
-        if atom_messages:
-            src = self._np['b2a'][j]
-            if len(src) and src.max() >= len(w):
-                raise IndexError('atom_messages readout indexes w_bonds with atom ids (mpn.py:128) and an atom id '
-                                 'exceeds the number of bonds')
-            coef = w[src]
-            keep = coef != 0.0
-            return Csr.from_rows(rows[keep], src[keep], coef[keep], V1)
-        coef = w[j]
+        src = self._np['b2a'][j]
+        if len(src) and src.max() >= len(w):
+            raise IndexError('atom_messages readout indexes w_bonds with atom ids (mpn.py:128) and an atom id '
+                             'exceeds the number of bonds')
+        coef = w[src]
         keep = coef != 0.0
-        return Csr.from_rows(rows[keep], j[keep], coef[keep], V1)
+        return Csr.from_rows(rows[keep], src[keep], coef[keep], V1)
 
     def molecule_blocks(self):
         """Consecutive molecules grouped greedily into blocks of <= BLK_BONDS bond rows and <= BLK_ATOMS
@@ -395,8 +378,11 @@ class BatchMolGraph:
                 if len(row) and not np.array_equal(rb[row], blk_of_bond[c.idx]):
                     blocks = None
                     break
-        msg_t = msg.transpose(msg_rows)
-        agg_t = agg.transpose(msg_rows)
+        if atom_messages:
+            msg_t = msg.transpose(msg_rows)
+            agg_t = agg.transpose(msg_rows)
+        else:
+            msg_t, agg_t = self._native_gathers()[2:]
         arrays = [('f_atoms', fa_p), ('bond_tail' if dev_bonds else 'f_bonds', fb_p), ('w_atoms', self._np['w_atoms']),
                   ('mol_start', a_start), ('mol_size', a_size), ('xn', xn),
                   ('b2revb', self._np['b2revb'].astype(np.int32))]

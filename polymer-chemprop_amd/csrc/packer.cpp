@@ -328,10 +328,189 @@ PyObject *pack(PyObject *, PyObject *args) {
     return nullptr;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Gather lists (the CSR forms of mpn.py:112-131 that the kernels consume), built natively.
+// ---------------------------------------------------------------------------------------------
+// A read-only typed view of a 1-D C-contiguous buffer argument.
+template <typename T>
+struct In {
+    Py_buffer b{};
+    const T *p = nullptr;
+    Py_ssize_t n = 0;
+    In(PyObject *o, const char *fmt, const char *what) {
+        if (PyObject_GetBuffer(o, &b, PyBUF_C_CONTIGUOUS | PyBUF_FORMAT) != 0) throw PyErrAlready{};
+        const char *f = b.format ? b.format : "B";
+        if (*f == '<' || *f == '=' || *f == '@') ++f;
+        bool ok = b.itemsize == (Py_ssize_t)sizeof(T);
+        if (ok && fmt[0] == 'i') ok = *f == 'q' || *f == 'l' || *f == 'i';
+        if (ok && fmt[0] == 'f') ok = *f == 'f';
+        if (!ok) {
+            PyBuffer_Release(&b);
+            fail(PyExc_TypeError, std::string(what) + ": unexpected dtype");
+        }
+        p = static_cast<const T *>(b.buf);
+        n = b.len / (Py_ssize_t)sizeof(T);
+    }
+    ~In() { PyBuffer_Release(&b); }
+};
+
+struct CsrOut {
+    std::vector<int32_t> ptr, idx;
+    std::vector<float> coef;
+};
+
+PyObject *csr_tuple(const CsrOut &c) {
+    PyObject *t = PyTuple_New(3);
+    if (!t) throw PyErrAlready{};
+    auto put = [&](int k, const void *d, size_t bytes) {
+        PyObject *b = PyByteArray_FromStringAndSize(static_cast<const char *>(d), (Py_ssize_t)bytes);
+        if (!b) { Py_DECREF(t); throw PyErrAlready{}; }
+        PyTuple_SET_ITEM(t, k, b);
+    };
+    put(0, c.ptr.data(), c.ptr.size() * 4);
+    put(1, c.idx.data(), c.idx.size() * 4);
+    put(2, c.coef.data(), c.coef.size() * 4);
+    return t;
+}
+
+// stable counting-sort transpose: source row j lists (row r, coef) in entry order
+CsrOut transpose(const CsrOut &c, int64_t n_src) {
+    CsrOut t;
+    t.ptr.assign((size_t)n_src + 1, 0);
+    for (int32_t j : c.idx) {
+        if (j < 0 || j >= n_src) fail(PyExc_ValueError, "gather index out of range");
+        ++t.ptr[(size_t)j + 1];
+    }
+    for (int64_t j = 0; j < n_src; ++j) t.ptr[j + 1] += t.ptr[j];
+    t.idx.resize(c.idx.size());
+    t.coef.resize(c.idx.size());
+    std::vector<int32_t> fill(t.ptr.begin(), t.ptr.end() - 1);
+    const int64_t rows = (int64_t)c.ptr.size() - 1;
+    for (int64_t r = 0; r < rows; ++r)
+        for (int32_t e = c.ptr[r]; e < c.ptr[r + 1]; ++e) {
+            const int32_t q = fill[c.idx[e]]++;
+            t.idx[q] = (int32_t)r;
+            t.coef[q] = c.coef[e];
+        }
+    return t;
+}
+
+// gathers(b2a, b2revb, w_bonds, deg, in_idx) -> (msg, agg, msg_t, agg_t), each (ptr, idx, coef)
+// bytearrays (int32, int32, float32):
+//   msg row b >= 1 (bond_message_gather, mpn.py:112-120): X_b = sum_{j in in(b2a[b])} w_j M_j - M_rev(b),
+//     entries in a2b slot order, the reverse bond's coefficient w_rev - 1 (evaluated in double, then
+//     rounded to float once) and dropped when 0; a reverse bond that is not among the in-bonds gets
+//     its own -1 entry at the end of the row; row 0 (pad) is empty;
+//   agg row a (atom_aggregate_gather, mpn.py:126-131): A_a = sum_{j in in(a)} w_j M_j (zero weights
+//     dropped);
+//   *_t: the transposes over the E + 1 source rows (the data-gradient gathers).
+PyObject *gathers(PyObject *, PyObject *args) {
+    PyObject *o_b2a, *o_rev, *o_w, *o_deg, *o_in;
+    if (!PyArg_ParseTuple(args, "OOOOO", &o_b2a, &o_rev, &o_w, &o_deg, &o_in)) return nullptr;
+    try {
+        In<int64_t> b2a(o_b2a, "i", "b2a"), rev(o_rev, "i", "b2revb"), deg(o_deg, "i", "deg"), in(o_in, "i", "in_idx");
+        In<float> w(o_w, "f", "w_bonds");
+        const int64_t E1 = b2a.n, V1 = deg.n;
+        if (rev.n != E1 || w.n != E1) fail(PyExc_ValueError, "b2a / b2revb / w_bonds lengths differ");
+        std::vector<int64_t> iptr((size_t)V1 + 1, 0);
+        for (int64_t a = 0; a < V1; ++a) iptr[a + 1] = iptr[a] + deg.p[a];
+        if (iptr[V1] != in.n) fail(PyExc_ValueError, "sum(deg) != len(in_idx)");
+        for (int64_t e = 0; e < in.n; ++e)
+            if (in.p[e] < 0 || in.p[e] >= E1) fail(PyExc_ValueError, "in_idx out of range");
+        CsrOut msg, agg;
+        msg.ptr.reserve((size_t)E1 + 1);
+        msg.ptr.push_back(0);
+        if (E1 > 0) msg.ptr.push_back(0);  // row 0: pad bond, no entries
+        for (int64_t b = 1; b < E1; ++b) {
+            const int64_t a = b2a.p[b], r = rev.p[b];
+            if (a < 0 || a >= V1 || r < 0 || r >= E1) fail(PyExc_ValueError, "b2a / b2revb out of range");
+            bool has_rev = false;
+            for (int64_t e = iptr[a]; e < iptr[a + 1]; ++e) {
+                const int64_t j = in.p[e];
+                double c = (double)w.p[j];
+                if (j == r) { c -= 1.0; has_rev = true; }
+                if (c != 0.0) { msg.idx.push_back((int32_t)j); msg.coef.push_back((float)c); }
+            }
+            if (!has_rev) { msg.idx.push_back((int32_t)r); msg.coef.push_back(-1.0f); }
+            msg.ptr.push_back((int32_t)msg.idx.size());
+        }
+        agg.ptr.reserve((size_t)V1 + 1);
+        agg.ptr.push_back(0);
+        for (int64_t a = 0; a < V1; ++a) {
+            for (int64_t e = iptr[a]; e < iptr[a + 1]; ++e) {
+                const int64_t j = in.p[e];
+                if (w.p[j] != 0.0f) { agg.idx.push_back((int32_t)j); agg.coef.push_back(w.p[j]); }
+            }
+            agg.ptr.push_back((int32_t)agg.idx.size());
+        }
+        const CsrOut msg_t = transpose(msg, E1), agg_t = transpose(agg, E1);
+        PyObject *res = PyTuple_New(4);
+        if (!res) throw PyErrAlready{};
+        const CsrOut *all[4] = {&msg, &agg, &msg_t, &agg_t};
+        for (int k = 0; k < 4; ++k) {
+            PyObject *t;
+            try { t = csr_tuple(*all[k]); } catch (...) { Py_DECREF(res); throw; }
+            PyTuple_SET_ITEM(res, k, t);
+        }
+        return res;
+    } catch (const PyErrAlready &) {
+    } catch (const std::exception &e) {
+        PyErr_SetString(PyExc_RuntimeError, e.what());
+    }
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_RuntimeError, "gathers failed");
+    return nullptr;
+}
+
+// ell(ptr, idx, coef, rows_p, row_base, width) -> (idx u8 [rows_p * width], coef f32 [rows_p * width]):
+// the first `width` entries of every row in block-local form (idx - row_base[row], < 128), unused
+// slots (0, 0), bit 7 of the last slot on rows with more entries (WdGraph.*_ell_*)
+PyObject *ell(PyObject *, PyObject *args) {
+    PyObject *o_ptr, *o_idx, *o_coef, *o_base;
+    Py_ssize_t rows_p, width;
+    if (!PyArg_ParseTuple(args, "OOOnOn", &o_ptr, &o_idx, &o_coef, &rows_p, &o_base, &width)) return nullptr;
+    try {
+        In<int32_t> ptr(o_ptr, "i", "ptr"), idx(o_idx, "i", "idx");
+        In<float> coef(o_coef, "f", "coef");
+        In<int64_t> base(o_base, "i", "row_base");
+        const Py_ssize_t rows = ptr.n - 1;
+        if (rows < 0 || rows > rows_p || base.n < rows || width < 1 || width > 64)
+            fail(PyExc_ValueError, "ell: bad sizes");
+        PyObject *oi = new_bytes(rows_p * width), *oc = nullptr;
+        try { oc = new_bytes(rows_p * width * 4); } catch (...) { Py_DECREF(oi); throw; }
+        uint8_t *di = reinterpret_cast<uint8_t *>(PyByteArray_AS_STRING(oi));
+        float *dc = reinterpret_cast<float *>(PyByteArray_AS_STRING(oc));
+        for (Py_ssize_t r = 0; r < rows; ++r) {
+            const int32_t e0 = ptr.p[r], e1 = ptr.p[r + 1];
+            for (int32_t e = e0; e < e1 && e - e0 < width; ++e) {
+                const int64_t l = (int64_t)idx.p[e] - base.p[r];
+                if (l < 0 || l >= 128) {
+                    Py_DECREF(oi); Py_DECREF(oc);
+                    fail(PyExc_ValueError, "ell_rows: an entry leaves its molecule block");
+                }
+                di[r * width + (e - e0)] = (uint8_t)l;
+                dc[r * width + (e - e0)] = coef.p[e];
+            }
+            if (e1 - e0 > width) di[r * width + width - 1] |= 0x80;
+        }
+        PyObject *res = PyTuple_Pack(2, oi, oc);
+        Py_DECREF(oi); Py_DECREF(oc);
+        return res;
+    } catch (const PyErrAlready &) {
+    } catch (const std::exception &e) {
+        PyErr_SetString(PyExc_RuntimeError, e.what());
+    }
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_RuntimeError, "ell failed");
+    return nullptr;
+}
+
 PyMethodDef methods[] = {
     {"pack", pack, METH_VARARGS,
      "pack(mol_graphs, fa_w, fb_w, tail_from=0, check=False) -> 10 bytearrays: the concatenated BatchMolGraph tables "
      "(featurization.py:757-813)"},
+    {"gathers", gathers, METH_VARARGS,
+     "gathers(b2a, b2revb, w_bonds, deg, in_idx) -> (msg, agg, msg_t, agg_t) CSR gather lists (mpn.py:112-131)"},
+    {"ell", ell, METH_VARARGS, "ell(ptr, idx, coef, rows_p, row_base, width) -> block-local ELL rows"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef module = {PyModuleDef_HEAD_INIT, "_wdpack", "native BatchMolGraph packer", -1, methods,

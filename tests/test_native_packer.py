@@ -111,3 +111,31 @@ def test_bond_tail_check_rejects_rows_that_are_not_atom_plus_bond():
     h.f_bonds = np.asarray(mgs[2].f_bonds, np.float64)
     t = BatchMolGraph([h], device_bond_features=True, check_bond_features=True)
     np.testing.assert_array_equal(t.f_bonds.numpy(), BatchMolGraph([mgs[2]]).f_bonds.numpy())
+
+
+@pytest.mark.parametrize('kind', sorted(BATCHES))
+def test_native_gather_lists_match_restatement(kind):
+    """csrc/packer.cpp ``gathers`` / ``ell`` against the numpy restatements (oracle/pack_ref.py): the
+    same entries in the same order, bit for bit, including the transposes and the ELL rows."""
+    from chemprop_amd.featurization import ELLW, ell_rows
+    g = BatchMolGraph(BATCHES[kind]())
+    b2a, rev, w = g._np['b2a'], g._np['b2revb'], g._np['w_bonds']
+    ref_msg = pack_ref.bond_message_gather(b2a, rev, w, g._deg, g._in_idx)
+    ref_agg = pack_ref.atom_aggregate_gather(w, g._deg, g._in_idx)
+    msg, agg, msg_t, agg_t = g._native_gathers()
+    for got, ref in ((msg, ref_msg), (agg, ref_agg),
+                     (msg_t, pack_ref.transpose(*ref_msg, g.n_bonds)), (agg_t, pack_ref.transpose(*ref_agg, g.n_bonds))):
+        for a, b in zip((got.ptr, got.idx, got.coef), ref):
+            np.testing.assert_array_equal(a, b)
+    g2 = BatchMolGraph(BATCHES[kind]() if kind != 'edge' else synthetic.edge_case_batch(3, star_leaves=40))
+    blocks = g2.molecule_blocks()
+    blk_b = np.full(g2.n_bonds, -1)
+    for k, (bs, bn) in enumerate(blocks[:, :2]):
+        blk_b[bs:bs + bn] = k
+    bstart = np.append(blocks[:, 0], 0).astype(np.int64)
+    m2 = g2.bond_message_gather()
+    for W in (ELLW, 3):
+        a = ell_rows(m2, m2.rows + 5, bstart[blk_b], W)
+        b = pack_ref.ell_rows(m2.ptr, m2.idx, m2.coef, m2.rows + 5, bstart[blk_b], W)
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
