@@ -104,8 +104,8 @@ typedef struct WdGraph {
     const void *f_atoms_x6;
     const void *f_bonds_x6;
     /* Optional molecule blocks for the fused inference forward: consecutive molecules
-     * grouped into blocks of <= 128 bond rows and <= 64 atom rows, so that every gather stays inside one
-     * block.  blocks[8 * k .. 8 * k + 5] = {bond_start, bond_count, atom_start, atom_count, mol_lo,
+     * grouped into blocks of <= 128 bond rows, <= 64 atom rows and <= 64 molecules, so that every gather
+     * stays inside one block.  blocks[8 * k .. 8 * k + 5] = {bond_start, bond_count, atom_start, atom_count, mol_lo,
      * mol_hi} (natural row ids, half-open molecule range).  bond_blk_row[r] (r < rows of f_bonds) =
      * 128 * block + (r - bond_start) or -1; f_atoms_blk_x6 = plane tiles of f_atoms in the blocked atom
      * layout (row 64 * block + (a - atom_start), zero rows elsewhere).  n_blocks = 0: unavailable. */

@@ -55,7 +55,7 @@ def _round_up(x: int, m: int) -> int:
 
 
 CSR_PAD = 8  # WdCsr: idx / coef readable 8 entries past the end (branch-free first-8 fetch)
-BLK_BONDS, BLK_ATOMS = 128, 64  # molecule-block capacity of the fused forward (WdGraph.blocks)
+BLK_BONDS, BLK_ATOMS, BLK_MOLS = 128, 64, 64  # molecule-block capacity of the fused forward (WdGraph.blocks)
 
 
 class Csr:
@@ -296,14 +296,15 @@ class BatchMolGraph:
         return Csr.from_rows(rows[keep], src[keep], coef[keep], V1)
 
     def molecule_blocks(self):
-        """Consecutive molecules grouped greedily into blocks of <= BLK_BONDS bond rows and <= BLK_ATOMS
-        atom rows (WdGraph.blocks, int32 [n_blocks, 8]); None when a molecule alone exceeds a limit."""
+        """Consecutive molecules grouped greedily into blocks of <= BLK_BONDS bond rows, <= BLK_ATOMS atom
+        rows and <= BLK_MOLS molecules (WdGraph.blocks, int32 [n_blocks, 8]); None when a molecule alone
+        exceeds a limit."""
         rows = []
         cur = None
         for i, ((as_, an), (bs, bn)) in enumerate(zip(self.a_scope, self.b_scope)):
             if bn > BLK_BONDS or an > BLK_ATOMS:
                 return None
-            if cur is not None and cur[1] + bn <= BLK_BONDS and cur[3] + an <= BLK_ATOMS:
+            if cur is not None and cur[1] + bn <= BLK_BONDS and cur[3] + an <= BLK_ATOMS and i - cur[4] < BLK_MOLS:
                 cur[1] += bn
                 cur[3] += an
                 cur[5] = i + 1

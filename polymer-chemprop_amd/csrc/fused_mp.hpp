@@ -25,6 +25,7 @@
 namespace wd {
 
 constexpr int BLK_BONDS = 128, BLK_ATOMS = 64;  // block capacity (rows of the blocked layouts)
+constexpr int BLK_MOLS = 64;                     // molecules per block (empty molecules have no rows)
 // gather entries per row in the block-local ELL form (WdGraph.*_ell_*, WDMPNN_ELL_WIDTH; 12 measured
 // no faster than 8 on the polymer benchmark, whose longest rows have 9 entries)
 constexpr int ELLW = 8;
@@ -300,18 +301,44 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     O.rb = blk;
     O.a_rows = B.an;
     O.b = P.wo + (size_t)nt * (P.kca + (P.kp >> 5)) * (3 * BN * 64);
+    // prefetched during the GEMM (mainloop hook): this thread's bias columns, the block's atom weights
+    // (thread a < an: w_atoms[as + a]) and its molecules' scope / Xn (thread i < nm)
+    constexpr int C4 = BN / 4;
+    static_assert(NT % C4 == 0 && BM <= NT, "one bias group per thread, one atom weight per thread");
+    const int nm = min(B.mh - B.ml, BLK_MOLS);  // (the packer never exceeds BLK_MOLS)
+    float4 bb = f4zero();
+    float watom = 0.f, mxn = 0.f;
+    int mstart = 0, msize = 0;
+    auto prefetch = [&]() {
+        bb = ld4(P.bias + n0 + 4 * (tid % C4));
+        if (tid < B.an) watom = P.w_atoms[B.as + tid];
+        if (tid < nm) {
+            mstart = P.mol_start[B.ml + tid];
+            msize = P.mol_size[B.ml + tid];
+            mxn = P.xn[B.ml + tid];
+        }
+    };
     floatx4 acc[BM / WM / 16][BN / WN / 16];
-    x6_mainloop<BM, BN, WM, WN, 2, CPS>(O, lds, acc);
+    x6_mainloop<BM, BN, WM, WN, 2, CPS>(O, lds, acc, prefetch);
     __syncthreads();
     float *H = reinterpret_cast<float *>(lds);
+    float *Wl = H + BM * LDC;           // [BM] atom weights of the block
+    float *Ml = Wl + BM;                // [3][BLK_MOLS] per molecule: start (as float bits), size, Xn
+    static_assert((BM * LDC + BM + 3 * BLK_MOLS) * 4 <= 2 * CPS * x6_stage_bytes<BM, BN>(), "readout staging fits");
+    static_assert(BLK_MOLS <= NT, "one molecule per thread in the prefetch");
     x6_acc_to_lds<BM, BN, WM, WN>(acc, H);
+    if (tid < BM) Wl[tid] = watom;
+    if (tid < nm) {
+        Ml[tid] = __int_as_float(mstart);
+        Ml[BLK_MOLS + tid] = __int_as_float(msize);
+        Ml[2 * BLK_MOLS + tid] = mxn;
+    }
     __syncthreads();
     // h = act(. + b_o) (* dropout), in place (mpn.py:133-134)
     {
         const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
-        for (int v = tid; v < BM * (BN / 4); v += NT) {
-            const int la = v / (BN / 4), c = 4 * (v % (BN / 4));
-            const float4 bb = ld4(P.bias + n0 + c);
+        for (int v = tid; v < BM * C4; v += NT) {
+            const int la = v / C4, c = 4 * (v % C4);
             const float4 hv = ld4(H + la * LDC + c);
             float z[4] = {hv.x + bb.x, hv.y + bb.y, hv.z + bb.z, hv.w + bb.w};
 #pragma unroll
@@ -324,25 +351,25 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
         }
     }
     __syncthreads();
-    // readout (mpn.py:145-171) of this block's molecules, columns n0 .. n0 + BN - 1: thread -> (molecule, column)
-    const int nm = B.mh - B.ml;
+    // readout (mpn.py:145-171) of this block's molecules, columns n0 .. n0 + BN - 1: thread -> (molecule,
+    // column); the atom weights and molecule scopes come from LDS, summed in atom order
     for (int t = tid; t < nm * BN; t += NT) {
-        const int i = B.ml + t / BN, cc = t % BN, col = n0 + cc;
+        const int im = t / BN, i = B.ml + im, cc = t % BN, col = n0 + cc;
         if (col >= P.ncols) continue;
-        const int n = P.mol_size[i];
+        const int n = __float_as_int(Ml[BLK_MOLS + im]);
         float v;
         if (n == 0) {
             v = P.zero_vec[col];  // cached_zero_vector, no Xn factor (mpn.py:148-149)
         } else {
-            const int a0 = P.mol_start[i] - B.as;
+            const int a0 = __float_as_int(Ml[im]) - B.as;
             float s = 0.f, wsum = 0.f;
             for (int a = 0; a < n; ++a) {
-                const float w = P.w_atoms[P.mol_start[i] + a];
+                const float w = Wl[a0 + a];
                 s = fmaf(w, H[(a0 + a) * LDC + cc], s);
                 wsum += w;
             }
             const float m = P.agg == 0 ? s / wsum : (P.agg == 2 ? s / P.norm : s);
-            v = P.xn[i] * m;
+            v = Ml[2 * BLK_MOLS + im] * m;
         }
         P.out[(size_t)i * P.ncols + col] = v;
     }

@@ -280,7 +280,11 @@ def test_blocked_forward_edge_cases_and_fallback():
     """Empty / single-atom molecules in blocks, and a 130-leaf hub molecule that exceeds a block (the
     forward falls back to the unblocked plane-tile path)."""
     args = TrainArgs(hidden_size=64, depth=3, bias=True)
-    for mols in (synthetic.edge_case_batch(9, star_leaves=20), synthetic.edge_case_batch(9, star_leaves=130)):
+    rng = np.random.default_rng(4)
+    many_empty = [synthetic.empty_graph() for _ in range(150)] + [synthetic.polymer_graph(rng, 3, 5)] + \
+        [synthetic.empty_graph() for _ in range(70)]  # blocks capped at BLK_MOLS molecules
+    for mols in (synthetic.edge_case_batch(9, star_leaves=20), synthetic.edge_case_batch(9, star_leaves=130),
+                 many_empty):
         g = BatchMolGraph(mols)
         enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim())
         synthetic.fill_parameters(enc, 5)

@@ -152,3 +152,14 @@ def test_golden_graphs_gather_lists_consistent(name):
         csr = g.bond_message_gather()
         assert csr.rows == g.n_bonds
         assert np.all(csr.idx >= 0) and np.all(csr.idx < g.n_bonds)
+
+
+def test_molecule_blocks_cap_the_molecule_count():
+    """Empty molecules take no rows; a block still holds at most BLK_MOLS molecules (the readout
+    stages one scope per molecule)."""
+    from chemprop_amd.featurization import BLK_MOLS
+    rng = np.random.default_rng(3)
+    mols = [synthetic.empty_graph() for _ in range(150)] + [synthetic.polymer_graph(rng, 3, 5)]
+    g = BatchMolGraph(mols)
+    blocks = g.molecule_blocks()
+    assert blocks is not None and np.all(blocks[:, 5] - blocks[:, 4] <= BLK_MOLS) and len(blocks) >= 3
