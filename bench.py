@@ -85,6 +85,49 @@ def pmc_traffic(prefix):
     return sum(v) / len(v), f'profiles/{PMC_TRAFFIC}: {d.get("_note", "")}'
 
 
+def forward_roofline(graphs, a, t_fwd):
+    """Whole-forward fractions per SURVEY §8(d): algorithmic bytes (fp32, each logical tensor read or
+    written once, gathers at unique size, int32 indices) and FLOPs of mpn.py:92-171 for the average
+    timed batch, over the measured time per forward, against 8 TB/s HBM and 157.3 TF/s fp32 MFMA."""
+    s, H, T = 4.0, a.hidden, a.depth
+    Fa, Fb = get_atom_fdim(), get_bond_fdim()
+    n = len(graphs)
+    E = sum(g.n_bonds - 1 for g in graphs) / n
+    V = sum(g.n_atoms - 1 for g in graphs) / n
+    B = sum(len(g.a_scope) for g in graphs) / n
+    byt = (s * (E * Fb + Fb * H + E * H)
+           + (T - 1) * (s * (3 * E * H + 2 * V * H + H * H + E) + 4 * (4 * E + V + 1))
+           + s * (E * H + E + V * H) + 4 * (E + V + 1)
+           + s * (V * Fa + 2 * V * H + (Fa + H) * H + H)
+           + s * (V * H + V + B * H + B) + 4 * (B + 1))
+    flops = 2 * E * Fb * H + (T - 1) * 2 * E * H * H + 2 * V * (Fa + H) * H
+    t_hbm, t_mfma = byt / (HBM_PEAK_GBS * 1e9), flops / (FP32_MFMA_PEAK_TFLOPS * 1e12)
+    return {'algorithmic_bytes': byt, 'algorithmic_flops': flops, 'us_per_forward': t_fwd * 1e6,
+            'hbm_frac': t_hbm / t_fwd, 'mfma_fp32_frac': t_mfma / t_fwd,
+            'combined_frac': max(t_hbm, t_mfma) / t_fwd,
+            'note': 'SURVEY 8(d) formulas; combined = max(bytes/8 TB/s, flops/157.3 TF/s) / measured time'}
+
+
+def secondary_workload(a, device, enc, steps=200, warmup=20):
+    """BASELINE.json configs[1] shape (QM9-like molecules, batch 64, depth 3, hidden 300): the same
+    resident-graph forward throughput, reported beside the headline polymer number."""
+    graphs = [BatchMolGraph(synthetic.make_batch('qm9', 64, 5000 + i), device_bond_features=True) for i in range(8)]
+    for g in graphs:
+        g.device_graph(device, False, get_bond_fdim())
+    with torch.no_grad():
+        for i in range(warmup):
+            enc(graphs[i % len(graphs)])
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            enc(graphs[i % len(graphs)])
+        torch.cuda.synchronize(device)
+        dt = time.perf_counter() - t0
+    E = sum(graphs[i % len(graphs)].n_bonds - 1 for i in range(steps))
+    return {'workload': 'QM9-like synthetic batches of 64 molecules (5-9 heavy atoms), depth 3, hidden 300',
+            'value': E / dt, 'unit': 'edges/s', 'ms_per_step': dt / steps * 1e3, 'steps': steps}
+
+
 def packing_report(a, device, t_fwd):
     """Host side of one batch, outside the timed region (pack + H2D reported separately,
     and end to end): native packer time, device_graph() time (gather lists, blocks, one pinned H2D,
@@ -248,7 +291,10 @@ def main():
                          'hbm_frac': hbm / HBM_PEAK_GBS if hbm else None,
                          'launches_timed': n_launch},
         }
+        line['forward'] = forward_roofline(graphs, a, elapsed / a.steps)
         line['packing'] = packing_report(a, device, elapsed / a.steps)
+        if world == 1 and a.kind == 'polymer':
+            line['secondary'] = secondary_workload(a, device, enc)
         if not a.no_cpu:
             cpu = cpu_baseline(TrainArgs(hidden_size=H, depth=a.depth, device=torch.device('cpu')), graphs[0],
                                a.cpu_seconds)
