@@ -123,6 +123,7 @@ class DeviceGraph:
         self.views = views
         self.struct = struct
         self.device = buffer.device
+        self.encoder_structs = {}  # (atom_fdim, bond_fdim) -> the WdGraph copy an encoder passes (mpn.py)
 
 
 class BatchMolGraph:

@@ -29,6 +29,20 @@ def _f32(t):
     return t
 
 
+def _forward_call(gstruct, cfg, pstruct, hidden_out, device):
+    """One wdmpnn_forward on the current stream into caller-owned (caching-allocator) buffers."""
+    L = _native.lib()
+    nbytes = ctypes.c_size_t()
+    _native.check(L.wdmpnn_workspace_bytes(ctypes.byref(gstruct), ctypes.byref(pstruct), ctypes.byref(cfg),
+                                           ctypes.byref(nbytes)), 'MPNEncoder workspace')
+    ws = torch.empty(max(nbytes.value, 256), dtype=torch.uint8, device=device)
+    out = torch.empty((gstruct.n_mols, hidden_out), dtype=torch.float32, device=device)
+    _native.check(L.wdmpnn_forward(ctypes.byref(gstruct), ctypes.byref(pstruct), ctypes.byref(cfg), ws.data_ptr(),
+                                   nbytes.value, out.data_ptr(), _native.current_stream(device)),
+                  'MPNEncoder forward')
+    return out, ws, nbytes.value
+
+
 class _EncoderFunction(torch.autograd.Function):
     """Forward = wdmpnn_forward, backward = wdmpnn_backward (parameter gradients only: the graph
     features are inputs without gradient, as in the reference training loop)."""
@@ -36,18 +50,10 @@ class _EncoderFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, enc, gstruct, cfg, pstruct, keep, hidden_out, device, W_i, b_i, W_h, b_h, W_o, b_o, W_d, b_d,
                 prelu):
-        L = _native.lib()
-        nbytes = ctypes.c_size_t()
-        _native.check(L.wdmpnn_workspace_bytes(ctypes.byref(gstruct), ctypes.byref(pstruct), ctypes.byref(cfg),
-                                               ctypes.byref(nbytes)), 'MPNEncoder workspace')
-        ws = torch.empty(max(nbytes.value, 256), dtype=torch.uint8, device=device)
-        out = torch.empty((gstruct.n_mols, hidden_out), dtype=torch.float32, device=device)
-        _native.check(L.wdmpnn_forward(ctypes.byref(gstruct), ctypes.byref(pstruct), ctypes.byref(cfg), ws.data_ptr(),
-                                       nbytes.value, out.data_ptr(), _native.current_stream(device)),
-                      'MPNEncoder forward')
+        out, ws, ws_bytes = _forward_call(gstruct, cfg, pstruct, hidden_out, device)
         if cfg.save_for_backward:
             ctx.save_for_backward(W_i, b_i, W_h, b_h, W_o, b_o, W_d, b_d, prelu)
-            ctx.ws, ctx.ws_bytes, ctx.gstruct, ctx.cfg, ctx.p, ctx.keep = ws, nbytes.value, gstruct, cfg, pstruct, keep
+            ctx.ws, ctx.ws_bytes, ctx.gstruct, ctx.cfg, ctx.p, ctx.keep = ws, ws_bytes, gstruct, cfg, pstruct, keep
         return out
 
     @staticmethod
@@ -149,14 +155,18 @@ class MPNEncoder(nn.Module):
             raise RuntimeError('chemprop_amd.MPNEncoder runs on the MI355X HIP path only: move the model to a '
                                'GPU (model.to("cuda"))')
         dg = mol_graph.device_graph(device, self.atom_messages, self.bond_fdim)
-        gs = _native.WdGraph.from_buffer_copy(dg.struct)
-        fa_expect = self.atom_fdim
-        fb_expect = self.bond_fdim
-        if gs.n_atoms > 1 and gs.atom_fdim != fa_expect:
-            raise ValueError(f'atom feature size {gs.atom_fdim} != encoder atom_fdim {fa_expect}')
-        if gs.n_bonds > 1 and gs.bond_fdim != fb_expect:
-            raise ValueError(f'bond feature size {gs.bond_fdim} != encoder bond_fdim {fb_expect}')
-        gs.atom_fdim, gs.bond_fdim = fa_expect, fb_expect
+        gs = dg.encoder_structs.get((self.atom_fdim, self.bond_fdim)) if atom_descriptors_batch is None else None
+        if gs is None:
+            gs = _native.WdGraph.from_buffer_copy(dg.struct)
+            fa_expect = self.atom_fdim
+            fb_expect = self.bond_fdim
+            if gs.n_atoms > 1 and gs.atom_fdim != fa_expect:
+                raise ValueError(f'atom feature size {gs.atom_fdim} != encoder atom_fdim {fa_expect}')
+            if gs.n_bonds > 1 and gs.bond_fdim != fb_expect:
+                raise ValueError(f'bond feature size {gs.bond_fdim} != encoder bond_fdim {fb_expect}')
+            gs.atom_fdim, gs.bond_fdim = fa_expect, fb_expect
+            if atom_descriptors_batch is None:  # (descriptors are per call: never cached)
+                dg.encoder_structs[(self.atom_fdim, self.bond_fdim)] = gs
         desc = None
         hidden_out = self.hidden_size
         if atom_descriptors_batch is not None:  # mpn.py:77-79, 136-143
@@ -187,28 +197,31 @@ class MPNEncoder(nn.Module):
         save = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in params)
         cfg = self._config(save)
         pstruct, packed = self._packed_params(gs, cfg, params, device)
+        if not save:  # inference: the same C-ABI call without the autograd.Function wrapper
+            return _forward_call(gs, cfg, pstruct, hidden_out, device)[0]
         return _EncoderFunction.apply(self, gs, cfg, pstruct, (packed, desc), hidden_out, device, *params)
 
     def _packed_params(self, gs, cfg, params, device):
         """WdParams + the padded weight copies (wdmpnn_pack_params), cached per parameter version."""
+        key = (tuple((t.data_ptr(), t._version) if t is not None else None for t in params),
+               self.cached_zero_vector.data_ptr(), gs.atom_fdim, gs.bond_fdim, gs.desc_dim, gs.atom_messages,
+               device)
+        cached = self._pack_cache
+        if cached is not None and cached[0] == key:
+            return cached[2], cached[1]
         p = _native.WdParams()
         p.hidden = self.hidden_size
         p.W_i, p.b_i, p.W_h, p.b_h, p.W_o, p.b_o, p.W_d, p.b_d, p.prelu = map(_native.ptr, params)
         p.zero_vec = _native.ptr(_f32(self.cached_zero_vector))
-        key = (tuple((t.data_ptr(), t._version) if t is not None else None for t in params),
-               gs.atom_fdim, gs.bond_fdim, gs.desc_dim, gs.atom_messages, str(device))
-        cached = self._pack_cache
-        if cached is None or cached[0] != key:
-            L = _native.lib()
-            nbytes = ctypes.c_size_t()
-            _native.check(L.wdmpnn_packed_params_bytes(ctypes.byref(gs), ctypes.byref(p), ctypes.byref(cfg),
-                                                       ctypes.byref(nbytes)), 'pack size')
-            buf = torch.empty(nbytes.value, dtype=torch.uint8, device=device)
-            _native.check(L.wdmpnn_pack_params(ctypes.byref(gs), ctypes.byref(p), ctypes.byref(cfg), buf.data_ptr(),
-                                               nbytes.value, _native.current_stream(device)), 'pack params')
-            cached = self._pack_cache = (key, buf)
-        buf = cached[1]
+        L = _native.lib()
+        nbytes = ctypes.c_size_t()
+        _native.check(L.wdmpnn_packed_params_bytes(ctypes.byref(gs), ctypes.byref(p), ctypes.byref(cfg),
+                                                   ctypes.byref(nbytes)), 'pack size')
+        buf = torch.empty(nbytes.value, dtype=torch.uint8, device=device)
+        _native.check(L.wdmpnn_pack_params(ctypes.byref(gs), ctypes.byref(p), ctypes.byref(cfg), buf.data_ptr(),
+                                           nbytes.value, _native.current_stream(device)), 'pack params')
         p.packed, p.packed_bytes = buf.data_ptr(), buf.numel()
+        self._pack_cache = (key, buf, p)
         return p, buf
 
 
