@@ -56,6 +56,7 @@ def _round_up(x: int, m: int) -> int:
 
 CSR_PAD = 8  # WdCsr: idx / coef readable 8 entries past the end (branch-free first-8 fetch)
 BLK_BONDS, BLK_ATOMS, BLK_MOLS = 128, 64, 64  # molecule-block capacity of the fused forward (WdGraph.blocks)
+BLK_TARGET = 64  # blocks a batch is spread over at least (x 4-5 column tiles = one workgroup per CU)
 
 
 class Csr:
@@ -296,16 +297,23 @@ class BatchMolGraph:
         keep = coef != 0.0
         return Csr.from_rows(rows[keep], src[keep], coef[keep], V1)
 
-    def molecule_blocks(self):
+    def molecule_blocks(self, target_blocks: int = BLK_TARGET):
         """Consecutive molecules grouped greedily into blocks of <= BLK_BONDS bond rows, <= BLK_ATOMS atom
         rows and <= BLK_MOLS molecules (WdGraph.blocks, int32 [n_blocks, 8]); None when a molecule alone
-        exceeds a limit."""
+        exceeds a limit.  A batch too small to give ``target_blocks`` full blocks is cut into smaller
+        ones (fill limit: the 16-row-rounded share of the bond rows, never below the largest molecule):
+        every block is one workgroup per column tile, and the kernels skip the empty 16-row groups, so
+        small batches spread over more CUs instead of a few full blocks."""
+        nb = np.array([n for _, n in self.b_scope], np.int64)
+        big = int(nb.max()) if len(nb) else 0
+        share = -(-int(nb.sum()) // max(1, target_blocks))
+        cap_b = min(BLK_BONDS, max(big, -(-share // 16) * 16))
         rows = []
         cur = None
         for i, ((as_, an), (bs, bn)) in enumerate(zip(self.a_scope, self.b_scope)):
             if bn > BLK_BONDS or an > BLK_ATOMS:
                 return None
-            if cur is not None and cur[1] + bn <= BLK_BONDS and cur[3] + an <= BLK_ATOMS and i - cur[4] < BLK_MOLS:
+            if cur is not None and cur[1] + bn <= cap_b and cur[3] + an <= BLK_ATOMS and i - cur[4] < BLK_MOLS:
                 cur[1] += bn
                 cur[3] += an
                 cur[5] = i + 1
