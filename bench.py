@@ -108,10 +108,13 @@ def forward_roofline(graphs, a, t_fwd):
             'note': 'SURVEY 8(d) formulas; combined = max(bytes/8 TB/s, flops/157.3 TF/s) / measured time'}
 
 
-def secondary_workload(a, device, enc, steps=200, warmup=20):
-    """BASELINE.json configs[1] shape (QM9-like molecules, batch 64, depth 3, hidden 300): the same
-    resident-graph forward throughput, reported beside the headline polymer number."""
-    graphs = [BatchMolGraph(synthetic.make_batch('qm9', 64, 5000 + i), device_bond_features=True) for i in range(8)]
+def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_batches=4):
+    """Other BASELINE.json configs' shapes (configs[1]: QM9-like molecules, batch 64, depth 3, hidden
+    300; configs[3]: ZINC-like molecules, batch 512, depth 5, hidden 512), timed like the headline:
+    resident graphs, eval forward, synchronised wall time over ``steps`` forwards."""
+    enc = make_encoder(TrainArgs(hidden_size=hidden, depth=depth, device=device), device)
+    graphs = [BatchMolGraph(synthetic.make_batch(kind, batch, 5000 + i), device_bond_features=True)
+              for i in range(n_batches)]
     for g in graphs:
         g.device_graph(device, False, get_bond_fdim())
     with torch.no_grad():
@@ -124,8 +127,9 @@ def secondary_workload(a, device, enc, steps=200, warmup=20):
         torch.cuda.synchronize(device)
         dt = time.perf_counter() - t0
     E = sum(graphs[i % len(graphs)].n_bonds - 1 for i in range(steps))
-    return {'workload': 'QM9-like synthetic batches of 64 molecules (5-9 heavy atoms), depth 3, hidden 300',
-            'value': E / dt, 'unit': 'edges/s', 'ms_per_step': dt / steps * 1e3, 'steps': steps}
+    return {'workload': f'{kind}-like synthetic batches of {batch} molecules, depth {depth}, hidden {hidden}',
+            'value': E / dt, 'unit': 'edges/s', 'ms_per_step': dt / steps * 1e3, 'steps': steps,
+            'avg_edges': E / steps}
 
 
 def packing_report(a, device, t_fwd):
@@ -171,6 +175,7 @@ def main():
     ap.add_argument('--n-batches', type=int, default=8, help='distinct resident batches cycled per rank')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--no-secondary', action='store_true', help='skip the QM9 / ZINC-shaped secondary workloads')
     ap.add_argument('--fuse-gather', action='store_true', help='experimental fused gather->GEMM (WdConfig.fuse_gather)')
     ap.add_argument('--variant', type=int, default=0, help='WdConfig.gemm_variant (0 = default path; 9 = f32 MFMA)')
     a = ap.parse_args()
@@ -255,7 +260,7 @@ def main():
         flops_launch = 2.0 * E_avg * H * H + 2.0 * E_avg * d_avg * H
         bytes_launch = 4.0 * (3 * E_avg * H + H * H + H) + 8.0 * E_avg * d_avg + 4.0 * E_avg
         avg_launch_s = (kernel_ms.value / 1e3 / n_launch) if n_launch else float('nan')
-        traffic, traffic_src = pmc_traffic('mp_layer_kernel')
+        traffic, traffic_src = pmc_traffic('mp_layer_kernel<80')
         achieved = flops_launch / avg_launch_s / 1e12 if n_launch else None
         hbm = bytes_launch / avg_launch_s / 1e9 if n_launch else None
         line = {
@@ -293,8 +298,9 @@ def main():
         }
         line['forward'] = forward_roofline(graphs, a, elapsed / a.steps)
         line['packing'] = packing_report(a, device, elapsed / a.steps)
-        if world == 1 and a.kind == 'polymer':
-            line['secondary'] = secondary_workload(a, device, enc)
+        if world == 1 and a.kind == 'polymer' and not a.no_secondary:
+            line['secondary'] = [secondary_workload(device, 'qm9', 64, 3, 300, 200),
+                                 secondary_workload(device, 'zinc', 512, 5, 512, 30)]
         if not a.no_cpu:
             cpu = cpu_baseline(TrainArgs(hidden_size=H, depth=a.depth, device=torch.device('cpu')), graphs[0],
                                a.cpu_seconds)
