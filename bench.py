@@ -132,6 +132,40 @@ def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_b
             'avg_edges': E / steps}
 
 
+def training_workload(device, batch=128, steps=20, warmup=3):
+    """BASELINE.json configs[2] shape (copolymer batches of 128 with weighted edges, full training
+    step): MoleculeModel (encoder + FFN, regression, one task) forward + loss + backward (the
+    deterministic HIP backward) + Adam step per batch, resident graphs, synchronised wall time."""
+    from chemprop_amd.model import MoleculeModel
+    from chemprop_amd.train import build_optimizer, get_loss_func, train_step
+    args = TrainArgs(hidden_size=300, depth=3, device=device)
+    torch.manual_seed(0)
+    model = MoleculeModel(args)
+    initialize_weights(model)
+    model = model.to(device)
+    opt = build_optimizer(model, 1e-4)
+    loss_func = get_loss_func('regression')
+    rng = torch.Generator().manual_seed(0)
+    batches = []
+    for i in range(4):
+        g = BatchMolGraph(synthetic.make_batch('polymer', batch, 7000 + i), device_bond_features=True)
+        g.device_graph(device, False, get_bond_fdim())
+        batches.append(([g], torch.randn(batch, 1, generator=rng).tolist()))
+    for i in range(warmup):
+        train_step(model, *batches[i % 4], loss_func, opt)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        train_step(model, *batches[i % 4], loss_func, opt)
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    E = sum(batches[i % 4][0][0].n_bonds - 1 for i in range(steps))
+    return {'workload': f'training step: MoleculeModel on synthetic polymer batches of {batch}, depth 3, hidden 300, '
+                        'MSE + Adam (forward, backward, optimizer step)',
+            'value': E / dt, 'unit': 'edges/s', 'ms_per_step': dt / steps * 1e3, 'graphs_per_s': batch * steps / dt,
+            'steps': steps}
+
+
 def packing_report(a, device, t_fwd):
     """Host side of one batch, outside the timed region (pack + H2D reported separately,
     and end to end): native packer time, device_graph() time (gather lists, blocks, one pinned H2D,
@@ -300,7 +334,8 @@ def main():
         line['packing'] = packing_report(a, device, elapsed / a.steps)
         if world == 1 and a.kind == 'polymer' and not a.no_secondary:
             line['secondary'] = [secondary_workload(device, 'qm9', 64, 3, 300, 200),
-                                 secondary_workload(device, 'zinc', 512, 5, 512, 30)]
+                                 secondary_workload(device, 'zinc', 512, 5, 512, 30),
+                                 training_workload(device)]
         if not a.no_cpu:
             cpu = cpu_baseline(TrainArgs(hidden_size=H, depth=a.depth, device=torch.device('cpu')), graphs[0],
                                a.cpu_seconds)
