@@ -258,20 +258,20 @@ def main():
         # second pass: HIP events around the dominant launches (the message-passing layers) on the
         # stream they run on
         L = _native.lib()
-        pairs = a.steps * max(a.depth - 1, 1)
+        pairs = a.steps  # one pair per forward around its depth - 1 layer launches (WdConfig.prof_pool)
         pool = ctypes.c_void_p()
         _native.check(L.wdmpnn_event_pool_create(pairs, ctypes.byref(pool)), 'event pool')
         barrier()
         t1 = time.perf_counter()
         for i in range(a.steps):
-            step(i, (pool.value, i * (a.depth - 1)))
+            step(i, (pool.value, i))
         barrier()
         elapsed_prof = time.perf_counter() - t1
         enc._prof = None
         kernel_ms = ctypes.c_float()
         n_launch = a.steps * (a.depth - 1)
-        if n_launch:
-            _native.check(L.wdmpnn_event_pool_elapsed_ms(pool, 0, n_launch, ctypes.byref(kernel_ms)), 'events')
+        if n_launch:  # (the span of each pair also holds the ~0.1 us gaps between the layer launches)
+            _native.check(L.wdmpnn_event_pool_elapsed_ms(pool, 0, a.steps, ctypes.byref(kernel_ms)), 'events')
         L.wdmpnn_event_pool_destroy(pool)
 
     t = torch.tensor([elapsed, elapsed_prof], dtype=torch.float64, device=device)

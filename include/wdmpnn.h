@@ -153,8 +153,9 @@ typedef struct WdConfig {
     uint64_t seed;          /* dropout RNG stream (counter based, re-derivable in backward) */
     int32_t save_for_backward; /* 1: keep pre-activations + every message layer in the workspace */
     int32_t prof_slot;      /* first event pair used when prof_pool != NULL                      */
-    void   *prof_pool;      /* optional WdEventPool: an event pair is recorded around each message-
-                               passing launch (the dominant kernel), pairs prof_slot + t - 1       */
+    void   *prof_pool;      /* optional WdEventPool: one event pair (pair prof_slot) is recorded around
+                               the depth - 1 message-passing launches (the dominant kernel) of this
+                               forward: before the first, after the last                          */
     int32_t gemm_variant;   /* 0 = default = 10: bf16x6 split-plane GEMMs (fp32-accurate) with the
                                molecule-blocked fused inference forward when WdGraph.blocks allow it;
                                9 = f32-MFMA GEMMs; 11..14 = bf16x6 with in-kernel operand split;

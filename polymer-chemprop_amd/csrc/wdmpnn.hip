@@ -718,7 +718,7 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
             M.n_tiles = Hk / BNf;
             const dim3 grid(D.nblk * M.n_tiles);
             const bool last = t == D.T - 1;
-            WD_TRY(record_prof(c, t - 1, 0, st));
+            if (t == 1) WD_TRY(record_prof(c, 0, 0, st));  // one pair around all the layers
             if (bn80) {
                 const dim3 blk(64 * MpWaves<80>::WM * MpWaves<80>::WN);
                 if (last) hipLaunchKernelGGL((mp_layer_kernel<80, true>), grid, blk, 0, st, M);
@@ -729,7 +729,7 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
                 else hipLaunchKernelGGL((mp_layer_kernel<64, false>), grid, blk, 0, st, M);
             }
             WD_CHECK_LAUNCH("mp_layer");
-            WD_TRY(record_prof(c, t - 1, 1, st));
+            if (t == D.T - 1) WD_TRY(record_prof(c, 0, 1, st));
         }
         if (D.B > 0) {
             WoReadoutP R{};
@@ -773,7 +773,7 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
         float *Zt = D.save ? F(L.Z[t]) : nullptr;
         const Epi e = epi_act(c->activation, p->prelu, W(PL.bh), F(L.Z[0]), Zt, F(L.M[next]), Hk, c, t);
         const int32_t *sym = D.undirected ? g->b2revb : nullptr;
-        WD_TRY(record_prof(c, t - 1, 0, st));
+        if (t == 1) WD_TRY(record_prof(c, 0, 0, st));  // one pair around all the layers
         if (fuse && fused_eligible(D.ldx, Hk, D.ldx, e)) {
             const FSeg s0 = fseg_gather(F(L.M[prev]), Hk, Hk, g->msg_gather, sym, D.save ? Xt : nullptr, D.ldx);
             if (D.atom) {
@@ -795,7 +795,7 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
                                0, D.R, D.Rp, st));
             WD_TRY(gemm_nt(Xt, D.ldx, D.ldx, nullptr, 0, 0, W(PL.Wh), D.ldx, D.Rp, Hk, e, st, var_split));
         }
-        WD_TRY(record_prof(c, t - 1, 1, st));
+        if (t == D.T - 1) WD_TRY(record_prof(c, 0, 1, st));
         cur = next;
     }
     const float *M_last = F(L.M[D.save ? D.T - 1 : cur]);
