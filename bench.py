@@ -210,6 +210,7 @@ def main():
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--no-secondary', action='store_true', help='skip the QM9 / ZINC-shaped secondary workloads')
+    ap.add_argument('--streams', type=int, default=2, help='batches in flight per GPU (one HIP stream each)')
     ap.add_argument('--fuse-gather', action='store_true', help='experimental fused gather->GEMM (WdConfig.fuse_gather)')
     ap.add_argument('--variant', type=int, default=0, help='WdConfig.gemm_variant (0 = default path; 9 = f32 MFMA)')
     a = ap.parse_args()
@@ -235,9 +236,16 @@ def main():
     enc._gemm_variant = a.variant
     edges = [g.n_bonds - 1 for g in graphs]
 
+    # independent batches in flight on a.streams HIP streams (round-robin): the kernels of one batch's
+    # forward overlap another's ramp / drain / epilogue on the same GPU (graphs are independent units)
+    streams = [torch.cuda.current_stream(device)] + [torch.cuda.Stream(device) for _ in range(a.streams - 1)]
+
     def step(i, prof=None):
         enc._prof = prof
-        return enc(graphs[i % len(graphs)])
+        if prof is not None or len(streams) == 1:
+            return enc(graphs[i % len(graphs)])
+        with torch.cuda.stream(streams[i % len(streams)]):
+            return enc(graphs[i % len(graphs)])
 
     def barrier():
         torch.cuda.synchronize(device)
@@ -245,7 +253,9 @@ def main():
             dist.barrier()
 
     with torch.no_grad():
-        for i in range(a.warmup):
+        step(0)  # packs the weights on the default stream; the other streams wait on its event
+        barrier()
+        for i in range(1, a.warmup):
             step(i)
         barrier()
         t0 = time.perf_counter()
@@ -254,6 +264,17 @@ def main():
         barrier()
         elapsed = time.perf_counter() - t0
         my_edges = sum(edges[i % len(edges)] for i in range(a.steps))
+
+        # the same K steps with one batch in flight (latency-bound: each forward waits for the last)
+        single = None
+        if len(streams) > 1:
+            barrier()
+            t2 = time.perf_counter()
+            for i in range(a.steps):
+                enc._prof = None
+                enc(graphs[i % len(graphs)])
+            barrier()
+            single = time.perf_counter() - t2
 
         # second pass: HIP events around the dominant launches (the message-passing layers) on the
         # stream they run on
@@ -274,12 +295,13 @@ def main():
             _native.check(L.wdmpnn_event_pool_elapsed_ms(pool, 0, a.steps, ctypes.byref(kernel_ms)), 'events')
         L.wdmpnn_event_pool_destroy(pool)
 
-    t = torch.tensor([elapsed, elapsed_prof], dtype=torch.float64, device=device)
+    t = torch.tensor([elapsed, elapsed_prof, single or 0.0], dtype=torch.float64, device=device)
     e = torch.tensor([my_edges], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(e, op=dist.ReduceOp.SUM)
     elapsed, elapsed_prof = float(t[0]), float(t[1])
+    single = float(t[2]) if single is not None else None
     total_edges = float(e[0])
 
     if rank == 0:
@@ -316,7 +338,13 @@ def main():
                                    f'(avg E={E_avg:.0f} directed edges), depth={a.depth}, hidden={H}, '
                                    f'{a.n_batches} resident batches cycled per rank',
                        'global_batch': a.batch * world, 'depth': a.depth, 'hidden': H,
-                       'parallelism': f'dp{world} (independent graphs, no collective in the forward)'},
+                       'parallelism': f'dp{world} (independent graphs, no collective in the forward)',
+                       'streams': a.streams,
+                       'in_flight': f'{a.streams} independent batches in flight per GPU (round-robin over '
+                                    f'{a.streams} HIP streams); every step is a full B={a.batch} forward'},
+            'single_stream': ({'value': total_edges / single, 'ms_per_step': single / a.steps * 1e3,
+                               'note': 'same steps, one batch in flight (each forward waits for the previous)'}
+                              if single else None),
             'roofline': {'bound': 'mfma',
                          'kernel': 'mp_layer_kernel: one message-passing layer, W_h split-plane GEMM + in-block CSR '
                                    'gather + residual/activation (mpn.py:110-124)',

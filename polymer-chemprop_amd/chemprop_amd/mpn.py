@@ -208,6 +208,8 @@ class MPNEncoder(nn.Module):
                device)
         cached = self._pack_cache
         if cached is not None and cached[0] == key:
+            if cached[3] is not None and cached[4] != torch.cuda.current_stream(device).cuda_stream:
+                torch.cuda.current_stream(device).wait_event(cached[3])  # packed on another stream
             return cached[2], cached[1]
         p = _native.WdParams()
         p.hidden = self.hidden_size
@@ -221,7 +223,9 @@ class MPNEncoder(nn.Module):
         _native.check(L.wdmpnn_pack_params(ctypes.byref(gs), ctypes.byref(p), ctypes.byref(cfg), buf.data_ptr(),
                                            nbytes.value, _native.current_stream(device)), 'pack params')
         p.packed, p.packed_bytes = buf.data_ptr(), buf.numel()
-        self._pack_cache = (key, buf, p)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        self._pack_cache = (key, buf, p, ev, torch.cuda.current_stream(device).cuda_stream)
         return p, buf
 
 

@@ -183,6 +183,27 @@ def test_repeat_runs_are_bitwise_deterministic():
     assert torch.equal(grads[0], grads[1])
 
 
+def test_batches_in_flight_on_streams_match_serial():
+    """bench.py's --streams: independent batches round-robin over HIP streams, the first call on a
+    side stream (the weight pack happens there, other streams wait on its event)."""
+    args = TrainArgs(hidden_size=300, depth=3)
+    graphs = [BatchMolGraph(synthetic.make_batch('polymer', 64, 40 + i), device_bond_features=True)
+              for i in range(6)]
+    enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim())
+    synthetic.fill_parameters(enc, 4)
+    enc = enc.to(DEV).eval()
+    streams = [torch.cuda.Stream(DEV) for _ in range(3)]
+    with torch.no_grad():
+        outs = [None] * len(graphs)
+        for i, g in enumerate(graphs):
+            with torch.cuda.stream(streams[i % 3]):
+                outs[i] = enc(g)
+        torch.cuda.synchronize(DEV)
+        serial = [enc(g) for g in graphs]
+    for a, b in zip(outs, serial):
+        assert torch.equal(a.cpu(), b.cpu())
+
+
 def test_dropout_training_mode():
     args = TrainArgs(hidden_size=64, depth=3, dropout=0.3)
     g = BatchMolGraph(synthetic.make_batch('polymer', 16, 6))

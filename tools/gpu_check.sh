@@ -20,7 +20,7 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     benchq) step bench_quick 300 python bench.py --steps 100 --warmup 10 --cpu-seconds 5 ;;
-    prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu --no-secondary ;;
+    prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu --no-secondary --streams 1 ;;
     tune) step tune 600 python tools/tune_gemm.py ;;
     lab) step gemm_lab 300 ./tools/gemm_lab 200 ;;
     stream) step stream 120 ./tools/gemm_lab 50 stream ;;
@@ -28,7 +28,7 @@ for s in "$@"; do
     host) step host 300 python tools/host_overhead.py ;;
     ab) step ab_x6 300 python bench.py --steps 200 --warmup 20 --no-cpu --variant 10 && step ab_f32 300 python bench.py --steps 200 --warmup 20 --no-cpu --variant 9 ;;
     x6prec) step x6prec 300 python tools/x6_precision.py ;;
-    profx6) step rocprof_x6 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof_x6 -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu --no-secondary --variant ${VARIANT:-10} ;;
+    profx6) step rocprof_x6 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof_x6 -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu --no-secondary --streams 1 --variant ${VARIANT:-10} ;;
     counters) step counters 120 rocprofv3 -L ;;
     pmc) step pmc 1500 bash tools/pmc.sh ;;
     sweep) step sweep 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/sweep -o run -- python tools/size_sweep.py ;;
