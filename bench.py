@@ -364,7 +364,7 @@ def main():
             line['secondary'] = [secondary_workload(device, 'qm9', 64, 3, 300, 200),
                                  secondary_workload(device, 'zinc', 512, 5, 512, 30),
                                  training_workload(device)]
-        if not a.no_cpu:
+        if not a.no_cpu and world == 1:  # the CPU leg is timed at N=1 only
             cpu = cpu_baseline(TrainArgs(hidden_size=H, depth=a.depth, device=torch.device('cpu')), graphs[0],
                                a.cpu_seconds)
             line['cpu_baseline'] = cpu

@@ -43,6 +43,10 @@ class TrainArgs:
     freeze_first_only: bool = False
     frzn_ffn_layers: int = 0
     polymer: bool = False
+    # optimizer (args.py:397-407, utils.py:295-310)
+    init_lr: float = 1e-4
+    optimizer: str = 'adam'
+    weight_decay: float = 0.0
 
     def __post_init__(self):
         if self.ffn_hidden_size is None:  # args.py:584-585

@@ -15,10 +15,22 @@ from typing import List, Union
 import numpy as np
 import torch
 import torch.nn as nn
+from torch.optim.optimizer import register_optimizer_step_post_hook
 
 from . import _native
 from .featurization import BatchMolGraph, get_atom_fdim, get_bond_fdim, mol2graph
 from .nn_utils import get_activation_function
+
+# optimizer steps taken in this process (any torch.optim optimizer): part of the packed-weight cache
+# key, since fused / capturable optimizers write the parameters without bumping their version counters
+_OPT_STEPS = [0]
+
+
+def _count_optimizer_step(optimizer, args, kwargs):
+    _OPT_STEPS[0] += 1
+
+
+register_optimizer_step_post_hook(_count_optimizer_step)
 
 
 def _f32(t):
@@ -196,17 +208,25 @@ class MPNEncoder(nn.Module):
         params = [_f32(t) for t in params]
         save = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in params)
         cfg = self._config(save)
-        pstruct, packed = self._packed_params(gs, cfg, params, device)
+        pstruct, packed = self._packed_params(gs, cfg, params, device, cache=not save)
         if not save:  # inference: the same C-ABI call without the autograd.Function wrapper
             return _forward_call(gs, cfg, pstruct, hidden_out, device)[0]
         return _EncoderFunction.apply(self, gs, cfg, pstruct, (packed, desc), hidden_out, device, *params)
 
-    def _packed_params(self, gs, cfg, params, device):
-        """WdParams + the padded weight copies (wdmpnn_pack_params), cached per parameter version."""
-        key = (tuple((t.data_ptr(), t._version) if t is not None else None for t in params),
+    def invalidate_packed_params(self) -> None:
+        """Drop the cached padded weights.  Needed only after writing the parameters in a way that
+        bypasses both their version counters and ``torch.optim`` (e.g. ``p.data.copy_(...)``)."""
+        self._pack_cache = None
+
+    def _packed_params(self, gs, cfg, params, device, cache=True):
+        """WdParams + the padded weight copies (wdmpnn_pack_params).  Inference caches them per
+        (parameter pointer, version counter, optimizer-step generation): fused optimizers update the
+        weights without bumping version counters, so every ``Optimizer.step`` also bumps
+        ``_OPT_STEPS``.  A training forward always repacks and leaves no cache behind."""
+        key = (tuple((t.data_ptr(), t._version) if t is not None else None for t in params), _OPT_STEPS[0],
                self.cached_zero_vector.data_ptr(), gs.atom_fdim, gs.bond_fdim, gs.desc_dim, gs.atom_messages,
                device)
-        cached = self._pack_cache
+        cached = self._pack_cache if cache else None
         if cached is not None and cached[0] == key:
             if cached[3] is not None and cached[4] != torch.cuda.current_stream(device).cuda_stream:
                 torch.cuda.current_stream(device).wait_event(cached[3])  # packed on another stream
@@ -225,7 +245,7 @@ class MPNEncoder(nn.Module):
         p.packed, p.packed_bytes = buf.data_ptr(), buf.numel()
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(device))
-        self._pack_cache = (key, buf, p, ev, torch.cuda.current_stream(device).cuda_stream)
+        self._pack_cache = (key, buf, p, ev, torch.cuda.current_stream(device).cuda_stream) if cache else None
         return p, buf
 
 

@@ -71,9 +71,21 @@ def get_loss_func(dataset_type: str) -> nn.Module:
     raise ValueError(f'Dataset type "{dataset_type}" not supported.')
 
 
-def build_optimizer(model: nn.Module, init_lr: float = 1e-4, weight_decay: float = 0.0) -> Optimizer:
-    """utils.py:295-310 (Adam)."""
-    return Adam([{'params': model.parameters(), 'lr': init_lr, 'weight_decay': weight_decay}])
+def build_optimizer(model: nn.Module, args=1e-4, weight_decay: float = 0.0) -> Optimizer:
+    """utils.py:295-310: Adam (or AdamW when ``args.optimizer == 'adamw'``) over all parameters.
+    ``args`` is a TrainArgs-like object (``init_lr``, optional ``weight_decay`` / ``optimizer``) as in
+    the reference, or a plain learning rate.  On a GPU the update runs as torch's fused
+    single-kernel Adam (same update rule; the multi-tensor version issues ~7 launches per step)."""
+    if isinstance(args, (int, float)):
+        lr, wd, kind = float(args), weight_decay, 'adam'
+    else:
+        lr, wd, kind = args.init_lr, getattr(args, 'weight_decay', 0.0), getattr(args, 'optimizer', 'adam')
+    params = list(model.parameters())
+    fused = bool(params) and all(p.device.type == 'cuda' for p in params)
+    groups = [{'params': params, 'lr': lr, 'weight_decay': wd}]
+    if kind == 'adamw':
+        return torch.optim.AdamW(groups, fused=fused or None)
+    return Adam(groups, fused=fused or None)
 
 
 def batch_loss(preds: torch.Tensor, target_batch: Sequence[Sequence[Optional[float]]], loss_func: Callable,
@@ -81,10 +93,17 @@ def batch_loss(preds: torch.Tensor, target_batch: Sequence[Sequence[Optional[flo
                data_weights: Sequence[float] = None) -> torch.Tensor:
     """train.py:46-74: masked, weighted loss averaged over the present targets."""
     dev = preds.device
-    mask = torch.tensor([[x is not None for x in tb] for tb in target_batch], dtype=torch.bool, device=dev)
-    targets = torch.tensor([[0 if x is None else x for x in tb] for tb in target_batch], device=dev)
+    # targets, mask and data weights travel as one host table: on a GPU one pinned, asynchronous copy
+    # (three pageable copies would each stall the host until the forward has drained)
+    n_t = len(target_batch[0]) if len(target_batch) else 0
+    rows = [[0.0 if x is None else float(x) for x in tb] + [float(x is not None) for x in tb]
+            + [1.0 if data_weights is None else float(data_weights[i])] for i, tb in enumerate(target_batch)]
+    host = torch.tensor(rows, dtype=torch.float32).reshape(len(target_batch), 2 * n_t + 1)
+    if dev.type == 'cuda':
+        host = host.pin_memory()
+    table = host.to(dev, non_blocking=True)
+    targets, mask, dw = table[:, :n_t], table[:, n_t:2 * n_t] > 0, table[:, 2 * n_t:]
     tw = torch.Tensor(target_weights).to(dev) if target_weights is not None else torch.ones_like(targets)
-    dw = torch.Tensor(data_weights if data_weights is not None else [1.0] * len(target_batch)).unsqueeze(1).to(dev)
     if dataset_type == 'multiclass':
         targets = targets.long()
         loss = torch.cat([loss_func(preds[:, j, :], targets[:, j]).unsqueeze(1) for j in range(preds.size(1))],

@@ -131,7 +131,8 @@ template <> struct MpWaves<80> { static constexpr int WM = 2, WN = 5; };
 #endif
 
 // grid = nblk * n_tiles (XCD-grouped: the column tiles of a block share an XCD), 64 WM WN threads.
-// LDS: two GEMM stages, reused by the epilogue as P [128][BN + 4] and M [128][BN + 4] fp32.
+// LDS: two GEMM stages, reused by the epilogue as P [128][BN + 4] fp32; the last layer then
+// overwrites P with M_t (held in registers across a barrier) for the atom aggregate.
 template <int BN, bool LAST>
 __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_layer_kernel(MpLayerP P) {
     constexpr int BM = BLK_BONDS, LDC = BN + 4, WM = MpWaves<BN>::WM, WN = MpWaves<BN>::WN, NT = 64 * WM * WN;
@@ -139,9 +140,12 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
     // two stages of one chunk (measured: 3 stages slower; two-chunk stages, one barrier per two
     // chunks, no faster: the chunk time is not bound by load latency or barriers)
     constexpr int S = 2, CPS = 1;
-    constexpr int LDS_BYTES = 2 * BM * LDC * 4 > S * CPS * x6_stage_bytes<BM, BN>()
-                                  ? 2 * BM * LDC * 4
+    // (<= 80 KB: two workgroups fit one CU's 160 KB, so layers of batches in flight on other
+    // streams co-reside)
+    constexpr int LDS_BYTES = BM * LDC * 4 > S * CPS * x6_stage_bytes<BM, BN>()
+                                  ? BM * LDC * 4
                                   : S * CPS * x6_stage_bytes<BM, BN>();
+    static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU");
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
     const int tile = xcd_tile(blockIdx.x, gridDim.x);
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
@@ -197,12 +201,12 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
     }
     __syncthreads();
     float *Pt = reinterpret_cast<float *>(lds);
-    float *Mt = Pt + BM * LDC;
     x6_acc_to_lds<BM, BN, WM, WN>(acc, Pt);
     __syncthreads();
 
     const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
     const __amdgpu_buffer_rsrc_t mrs = x6_block_rsrc<BM>(LAST ? P.aplanes : P.mnext, P.kp, blk);
+    float4 ym[LAST ? UPT : 1][2];  // LAST: this thread's M_t units until P is dead
 #pragma unroll
     for (int i = 0; i < UPT; ++i) {
         const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
@@ -240,13 +244,22 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
             y1 = make_float4(z[4], z[5], z[6], z[7]);
         }
         if constexpr (LAST) {
-            st4(Mt + lr * LDC + c, y0);
-            st4(Mt + lr * LDC + c + 4, y1);
+            ym[i][0] = y0;
+            ym[i][1] = y1;
         } else if (lr < B.bn && WD_EXP != 2) {  // rows past the block's bonds are never loaded by the next layer
             x6_store8_blk<BM>(mrs, lr, n0 + c, y0, y1);
         }
     }
     if constexpr (LAST) {
+        __syncthreads();  // every read of P done: M_t replaces it
+        float *Mt = Pt;
+#pragma unroll
+        for (int i = 0; i < UPT; ++i) {
+            const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
+            if (v >= UNITS) break;
+            st4(Mt + lr * LDC + c, ym[i][0]);
+            st4(Mt + lr * LDC + c + 4, ym[i][1]);
+        }
         __syncthreads();
         // atom aggregate of this column tile: A[a] = Σ_{b into a} w_b M_t[b] (mpn.py:126-131)
         const __amdgpu_buffer_rsrc_t ars = x6_block_rsrc<BLK_ATOMS>(P.aplanes, P.kp, blk);

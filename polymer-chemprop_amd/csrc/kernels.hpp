@@ -189,37 +189,51 @@ struct ActBwd {
     int rows, rows_p, cols, ld;  // cols: padded width (zero columns stay zero)
 };
 
+// V consecutive columns per thread (V = 4 when cols, ld, ldg are multiples of 4: 16-byte loads and
+// stores); 32-bit index math (rows_p * cols < 2^31 is checked by the launcher).  The CSR sum runs in
+// entry order per element, so V does not change any result bit.
+template <int V>
 __global__ __launch_bounds__(256) void act_bwd_kernel(ActBwd P) {
+    typedef float __attribute__((ext_vector_type(V))) fv;
     __shared__ float red[256];
     const float slope = (P.Z && P.act == ACT_PRELU) ? P.slope[0] : 0.f;
     float ppart = 0.f;
-    const size_t total = (size_t)P.rows_p * P.cols;
-    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
-        const int r = (int)(t / P.cols), c = (int)(t % P.cols);
+    const int cv = P.cols / V;
+    const int total = P.rows_p * cv;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        const int r = t / cv, c = (t - r * cv) * V;
         const size_t o = (size_t)r * P.ld + c;
-        float dz = 0.f;
+        fv dz = (fv)0.f;
         if (r < P.rows) {
-            float g;
+            fv g;
             if (P.ptr) {
-                g = 0.f;
-                for (int e = P.ptr[r]; e < P.ptr[r + 1]; ++e)
-                    g = fmaf(P.coef ? P.coef[e] : 1.f, P.G[(size_t)P.idx[e] * P.ldg + c], g);
+                g = (fv)0.f;
+                const int e1 = P.ptr[r + 1];
+                for (int e = P.ptr[r]; e < e1; ++e) {
+                    const float w = P.coef ? P.coef[e] : 1.f;
+                    const fv x = *(const fv *)(P.G + (size_t)P.idx[e] * P.ldg + c);
+                    for (int q = 0; q < V; ++q) g[q] = fmaf(w, x[q], g[q]);
+                }
             } else if (P.sym_rev) {
-                g = (P.G[(size_t)r * P.ldg + c] + P.G[(size_t)P.sym_rev[r] * P.ldg + c]) * 0.5f;
+                const fv a = *(const fv *)(P.G + (size_t)r * P.ldg + c);
+                const fv b = *(const fv *)(P.G + (size_t)P.sym_rev[r] * P.ldg + c);
+                for (int q = 0; q < V; ++q) g[q] = (a[q] + b[q]) * 0.5f;
             } else {
-                g = P.G[(size_t)r * P.ldg + c];
+                g = *(const fv *)(P.G + (size_t)r * P.ldg + c);
             }
             dz = g;
             if (P.Z) {
-                const float z = P.Z[o];
-                const float s = P.p_drop > 0.f ? dropout_scale(P.seed, P.layer, r, c, P.p_drop) : 1.f;
-                dz = g * s * act_grad(P.act, z, slope);
-                if (P.act == ACT_PRELU && !(z > 0.f)) ppart += z * g * s;
+                const fv z = *(const fv *)(P.Z + o);
+                for (int q = 0; q < V; ++q) {
+                    const float s = P.p_drop > 0.f ? dropout_scale(P.seed, P.layer, r, c + q, P.p_drop) : 1.f;
+                    dz[q] = g[q] * s * act_grad(P.act, z[q], slope);
+                    if (P.act == ACT_PRELU && !(z[q] > 0.f)) ppart += z[q] * g[q] * s;
+                }
             }
-            if (P.add_in) dz += P.add_in[o];
+            if (P.add_in) dz += *(const fv *)(P.add_in + o);
         }
-        if (P.res_out) P.res_out[o] = P.res_init ? dz : P.res_out[o] + dz;
-        P.out[o] = dz;
+        if (P.res_out) *(fv *)(P.res_out + o) = P.res_init ? dz : *(const fv *)(P.res_out + o) + dz;
+        *(fv *)(P.out + o) = dz;
     }
     if (P.prelu_part) {
         red[threadIdx.x] = ppart;

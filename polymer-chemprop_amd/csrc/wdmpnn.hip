@@ -866,9 +866,14 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
 
     auto act_bwd = [&](ActBwd P) -> int {
         const size_t total = (size_t)P.rows_p * P.cols;
-        const int nb = ew_blocks(total);
+        if (total >= (size_t)1 << 31) return fail(WD_ERR_SHAPE, "act_bwd: %zu elements exceed the 32-bit index", total);
+        auto al = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
+        const bool v4 = P.cols % 4 == 0 && P.ld % 4 == 0 && P.ldg % 4 == 0 && al(P.G) && al(P.out) &&
+                        (!P.Z || al(P.Z)) && (!P.add_in || al(P.add_in)) && (!P.res_out || al(P.res_out));
+        const int nb = ew_blocks(v4 ? total / 4 : total);
         if (prelu && P.Z) { P.prelu_part = prelu_part + prelu_used; prelu_used += nb; }
-        hipLaunchKernelGGL(act_bwd_kernel, dim3(nb), dim3(256), 0, st, P);
+        if (v4) hipLaunchKernelGGL(act_bwd_kernel<4>, dim3(nb), dim3(256), 0, st, P);
+        else hipLaunchKernelGGL(act_bwd_kernel<1>, dim3(nb), dim3(256), 0, st, P);
         WD_CHECK_LAUNCH("act_bwd");
         return 0;
     };

@@ -369,3 +369,30 @@ def test_dropout_masks_agree_across_paths(extra):
     enc._seed_counter = 0
     b = enc(g)
     assert golden_io.normwise(a.cpu().numpy(), b.detach().cpu().numpy()) <= TOL
+
+
+def test_training_step_fused_adam_and_pinned_targets():
+    """train_step on the GPU (pinned target table, fused Adam from build_optimizer) agrees with the
+    same steps through torch's plain per-parameter Adam (the reference's optimizer)."""
+    from chemprop_amd.nn_utils import initialize_weights
+    from chemprop_amd.train import build_optimizer, get_loss_func, train_step
+    args = TrainArgs(hidden_size=64, depth=3, device=DEV)
+    g = BatchMolGraph(synthetic.make_batch('polymer', 16, 9), device_bond_features=True)
+    targets = [[0.1 * i - 0.5, None if i % 5 == 0 else float(i % 3)] for i in range(16)]
+    args.num_tasks = 2
+    models, opts = [], []
+    for fused in (True, False):
+        torch.manual_seed(0)
+        m = MoleculeModel(args)
+        initialize_weights(m)
+        m = m.to(DEV)
+        opt = build_optimizer(m, 1e-3) if fused else torch.optim.Adam(m.parameters(), lr=1e-3, foreach=False)
+        assert opt.param_groups[0]['fused'] == (True if fused else None)
+        models.append(m)
+        opts.append(opt)
+    for _ in range(3):
+        losses = [train_step(m, [g], targets, get_loss_func('regression'), o) for m, o in zip(models, opts)]
+        assert abs(float(losses[0]) - float(losses[1])) <= 1e-6 * max(1.0, abs(float(losses[1])))
+    for (n, a), b in zip(models[0].named_parameters(), models[1].parameters()):
+        d = float((a - b).detach().abs().max())
+        assert d <= 1e-6, (n, d)

@@ -29,3 +29,29 @@ def test_masked_weighted_loss():
     loss = batch_loss(preds, targets, get_loss_func('regression'), data_weights=[1.0, 2.0])
     expect = (0.25 * 1 + (1.0 * 2 + 1.0 * 2)) / 3  # train.py:73-74
     assert math.isclose(float(loss), expect, rel_tol=1e-6)
+
+
+def test_loss_classification_and_multiclass():
+    preds = torch.tensor([[0.5, -1.0], [2.0, 0.0]])
+    targets = [[1, None], [0, 1]]
+    loss = batch_loss(preds, targets, get_loss_func('classification'), dataset_type='classification')
+    bce = torch.nn.functional.binary_cross_entropy_with_logits
+    expect = (bce(preds[0, 0], torch.tensor(1.)) + bce(preds[1, 0], torch.tensor(0.))
+              + bce(preds[1, 1], torch.tensor(1.))) / 3
+    assert math.isclose(float(loss), float(expect), rel_tol=1e-6)
+    logits = torch.randn(3, 1, 4, generator=torch.Generator().manual_seed(0))
+    loss = batch_loss(logits, [[2], [0], [3]], get_loss_func('multiclass'), dataset_type='multiclass')
+    expect = torch.nn.functional.cross_entropy(logits[:, 0, :], torch.tensor([2, 0, 3]))
+    assert math.isclose(float(loss), float(expect), rel_tol=1e-6)
+
+
+def test_build_optimizer_follows_reference_args():
+    from chemprop_amd import TrainArgs
+    from chemprop_amd.train import build_optimizer
+    m = torch.nn.Linear(4, 2)
+    opt = build_optimizer(m, TrainArgs(init_lr=3e-4, weight_decay=0.01, device=torch.device('cpu')))
+    assert type(opt) is torch.optim.Adam
+    assert opt.param_groups[0]['lr'] == 3e-4 and opt.param_groups[0]['weight_decay'] == 0.01
+    opt = build_optimizer(m, TrainArgs(optimizer='adamw', device=torch.device('cpu')))
+    assert type(opt) is torch.optim.AdamW and opt.param_groups[0]['lr'] == 1e-4
+    assert build_optimizer(m, 2e-3).param_groups[0]['lr'] == 2e-3

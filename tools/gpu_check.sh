@@ -25,6 +25,8 @@ for s in "$@"; do
     lab) step gemm_lab 300 ./tools/gemm_lab 200 ;;
     stream) step stream 120 ./tools/gemm_lab 50 stream ;;
     mainloop) step mainloop 120 ./tools/gemm_lab 200 mainloop ;;
+    train) step train 300 python tools/train_bench.py ;;
+    proftrain) step rocprof_train 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof_train -o run --output-format csv -- python tools/train_bench.py ;;
     host) step host 300 python tools/host_overhead.py ;;
     ab) step ab_x6 300 python bench.py --steps 200 --warmup 20 --no-cpu --variant 10 && step ab_f32 300 python bench.py --steps 200 --warmup 20 --no-cpu --variant 9 ;;
     x6prec) step x6prec 300 python tools/x6_precision.py ;;
