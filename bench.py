@@ -108,28 +108,43 @@ def forward_roofline(graphs, a, t_fwd):
             'note': 'SURVEY 8(d) formulas; combined = max(bytes/8 TB/s, flops/157.3 TF/s) / measured time'}
 
 
-def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_batches=4):
+def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_batches=4, streams=1):
     """Other BASELINE.json configs' shapes (configs[1]: QM9-like molecules, batch 64, depth 3, hidden
     300; configs[3]: ZINC-like molecules, batch 512, depth 5, hidden 512), timed like the headline:
-    resident graphs, eval forward, synchronised wall time over ``steps`` forwards."""
+    resident graphs, eval forward, synchronised wall time over ``steps`` forwards, with ``streams``
+    independent batches in flight (as the headline) and with one."""
     enc = make_encoder(TrainArgs(hidden_size=hidden, depth=depth, device=device), device)
     graphs = [BatchMolGraph(synthetic.make_batch(kind, batch, 5000 + i), device_bond_features=True)
               for i in range(n_batches)]
     for g in graphs:
         g.device_graph(device, False, get_bond_fdim())
-    with torch.no_grad():
+    ss = [torch.cuda.current_stream(device)] + [torch.cuda.Stream(device) for _ in range(streams - 1)]
+
+    def timed(n_streams):
+        def fwd(i):
+            if n_streams == 1:
+                return enc(graphs[i % len(graphs)])
+            with torch.cuda.stream(ss[i % n_streams]):
+                return enc(graphs[i % len(graphs)])
         for i in range(warmup):
-            enc(graphs[i % len(graphs)])
+            fwd(i)
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
         for i in range(steps):
-            enc(graphs[i % len(graphs)])
+            fwd(i)
         torch.cuda.synchronize(device)
-        dt = time.perf_counter() - t0
+        return time.perf_counter() - t0
+
+    with torch.no_grad():
+        enc(graphs[0])  # weights packed once, on the default stream
+        torch.cuda.synchronize(device)
+        dt = timed(len(ss))
+        dt1 = timed(1) if len(ss) > 1 else dt
     E = sum(graphs[i % len(graphs)].n_bonds - 1 for i in range(steps))
     return {'workload': f'{kind}-like synthetic batches of {batch} molecules, depth {depth}, hidden {hidden}',
             'value': E / dt, 'unit': 'edges/s', 'ms_per_step': dt / steps * 1e3, 'steps': steps,
-            'avg_edges': E / steps}
+            'avg_edges': E / steps, 'streams': len(ss),
+            'single_stream': {'value': E / dt1, 'ms_per_step': dt1 / steps * 1e3}}
 
 
 def training_workload(device, batch=128, steps=20, warmup=3):
@@ -361,8 +376,8 @@ def main():
         line['forward'] = forward_roofline(graphs, a, elapsed / a.steps)
         line['packing'] = packing_report(a, device, elapsed / a.steps)
         if world == 1 and a.kind == 'polymer' and not a.no_secondary:
-            line['secondary'] = [secondary_workload(device, 'qm9', 64, 3, 300, 200),
-                                 secondary_workload(device, 'zinc', 512, 5, 512, 30),
+            line['secondary'] = [secondary_workload(device, 'qm9', 64, 3, 300, 200, streams=a.streams),
+                                 secondary_workload(device, 'zinc', 512, 5, 512, 30, streams=a.streams),
                                  training_workload(device)]
         if not a.no_cpu and world == 1:  # the CPU leg is timed at N=1 only
             cpu = cpu_baseline(TrainArgs(hidden_size=H, depth=a.depth, device=torch.device('cpu')), graphs[0],
