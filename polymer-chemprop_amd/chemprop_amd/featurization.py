@@ -125,6 +125,7 @@ class DeviceGraph:
         self.struct = struct
         self.device = buffer.device
         self.encoder_structs = {}  # (atom_fdim, bond_fdim) -> the WdGraph copy an encoder passes (mpn.py)
+        self.encoder_plans = {}  # (encoder token, encoder config) -> cached inference call (MPNEncoder._infer)
 
 
 class BatchMolGraph:

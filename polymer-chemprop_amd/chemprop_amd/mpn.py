@@ -140,6 +140,7 @@ class MPNEncoder(nn.Module):
         self._pack_cache = None  # (parameter-version key, packed weight buffer)
         self._gemm_variant = 0  # WdConfig.gemm_variant (tuning knob; 0 = automatic)
         self._fuse_gather = 0  # WdConfig.fuse_gather (1 = experimental fused gather->GEMM kernel)
+        self._plan_token = object()  # this encoder's key in DeviceGraph.encoder_plans
 
     def _config(self, save: bool) -> _native.WdConfig:
         c = _native.WdConfig()
@@ -160,25 +161,84 @@ class MPNEncoder(nn.Module):
         c.fuse_gather = self._fuse_gather
         return c
 
+    def _param_tuple(self):
+        """(W_i, b_i, W_h, b_h, W_o, b_o, W_d, b_d, prelu) read straight from the submodules' parameter
+        dicts: the same tensors as ``self.W_i.weight`` ..., without nn.Module.__getattr__ (≈ 8 µs of host
+        time per forward for the nine lookups)."""
+        m = self._modules
+        wi, wh, wo = m['W_i']._parameters, m['W_h']._parameters, m['W_o']._parameters
+        act = m['act_func']
+        return (wi['weight'], wi.get('bias'), wh['weight'], wh.get('bias'), wo['weight'], wo.get('bias'), None,
+                None, act._parameters['weight'] if isinstance(act, nn.PReLU) else None)
+
+    def _infer(self, mol_graph: BatchMolGraph):
+        """Inference call path (no autograd, no dropout, no descriptors, no profiling hook): the graph
+        struct, config and workspace size are cached per (graph, encoder configuration) in a plan on the
+        DeviceGraph, so a repeated forward costs two allocations and one C-ABI call.  Returns None when
+        the call needs the general path."""
+        d = self.__dict__
+        if d['_prof'] is not None or (self.training and self.dropout > 0):
+            return None
+        params = self._param_tuple()
+        device = params[0].device
+        if device.type != 'cuda':
+            return None  # the general path raises
+        if params[8] is not None and params[8].numel() != 1:
+            return None
+        dg = mol_graph.device_graph(device, d['atom_messages'], d['bond_fdim'])
+        ckey = (self._plan_token, d['atom_fdim'], d['bond_fdim'], d['hidden_size'], d['depth'], d['undirected'],
+                d['activation'], d['aggregation'], d['aggregation_norm'], d['_gemm_variant'], d['_fuse_gather'])
+        plan = dg.encoder_plans.get(ckey)
+        stream = torch.cuda.current_stream(device)
+        if plan is None:
+            gs = self._graph_struct(dg)
+            cfg = self._config(False)
+            params = tuple(_f32(t) for t in params)
+            pstruct, _ = self._packed_params(gs, cfg, params, device, stream=stream)
+            nbytes = ctypes.c_size_t()
+            _native.check(_native.lib().wdmpnn_workspace_bytes(ctypes.byref(gs), ctypes.byref(pstruct),
+                                                               ctypes.byref(cfg), ctypes.byref(nbytes)),
+                          'MPNEncoder workspace')
+            plan = (ctypes.byref(gs), ctypes.byref(cfg), max(nbytes.value, 256), gs.n_mols, gs, cfg)
+            dg.encoder_plans[ckey] = plan
+        pstruct, _ = self._packed_params(plan[4], plan[5], params, device, stream=stream)
+        ws = torch.empty(plan[2], dtype=torch.uint8, device=device)
+        out = torch.empty((plan[3], d['hidden_size']), dtype=torch.float32, device=device)
+        _native.check(_native.lib().wdmpnn_forward(plan[0], ctypes.byref(pstruct), plan[1], ws.data_ptr(), plan[2],
+                                                   out.data_ptr(), stream.cuda_stream), 'MPNEncoder forward')
+        return out
+
+    def _graph_struct(self, dg):
+        """The WdGraph copy this encoder passes (feature sizes checked against the encoder's), cached on
+        the DeviceGraph per (atom_fdim, bond_fdim)."""
+        gs = dg.encoder_structs.get((self.atom_fdim, self.bond_fdim))
+        if gs is None:
+            gs = self._new_graph_struct(dg)
+            dg.encoder_structs[(self.atom_fdim, self.bond_fdim)] = gs
+        return gs
+
+    def _new_graph_struct(self, dg):
+        gs = _native.WdGraph.from_buffer_copy(dg.struct)
+        if gs.n_atoms > 1 and gs.atom_fdim != self.atom_fdim:
+            raise ValueError(f'atom feature size {gs.atom_fdim} != encoder atom_fdim {self.atom_fdim}')
+        if gs.n_bonds > 1 and gs.bond_fdim != self.bond_fdim:
+            raise ValueError(f'bond feature size {gs.bond_fdim} != encoder bond_fdim {self.bond_fdim}')
+        gs.atom_fdim, gs.bond_fdim = self.atom_fdim, self.bond_fdim
+        return gs
+
     def forward(self, mol_graph: BatchMolGraph, atom_descriptors_batch: List[np.ndarray] = None) -> torch.FloatTensor:
         """mpn.py:66-173 -> [num_molecules, hidden_size (+ atom_descriptors_size)]."""
+        if atom_descriptors_batch is None and not torch.is_grad_enabled():
+            out = self._infer(mol_graph)
+            if out is not None:
+                return out
         device = self.W_i.weight.device
         if device.type != 'cuda':
             raise RuntimeError('chemprop_amd.MPNEncoder runs on the MI355X HIP path only: move the model to a '
                                'GPU (model.to("cuda"))')
         dg = mol_graph.device_graph(device, self.atom_messages, self.bond_fdim)
-        gs = dg.encoder_structs.get((self.atom_fdim, self.bond_fdim)) if atom_descriptors_batch is None else None
-        if gs is None:
-            gs = _native.WdGraph.from_buffer_copy(dg.struct)
-            fa_expect = self.atom_fdim
-            fb_expect = self.bond_fdim
-            if gs.n_atoms > 1 and gs.atom_fdim != fa_expect:
-                raise ValueError(f'atom feature size {gs.atom_fdim} != encoder atom_fdim {fa_expect}')
-            if gs.n_bonds > 1 and gs.bond_fdim != fb_expect:
-                raise ValueError(f'bond feature size {gs.bond_fdim} != encoder bond_fdim {fb_expect}')
-            gs.atom_fdim, gs.bond_fdim = fa_expect, fb_expect
-            if atom_descriptors_batch is None:  # (descriptors are per call: never cached)
-                dg.encoder_structs[(self.atom_fdim, self.bond_fdim)] = gs
+        # descriptors are per call: their struct is never cached
+        gs = self._graph_struct(dg) if atom_descriptors_batch is None else self._new_graph_struct(dg)
         desc = None
         hidden_out = self.hidden_size
         if atom_descriptors_batch is not None:  # mpn.py:77-79, 136-143
@@ -218,18 +278,20 @@ class MPNEncoder(nn.Module):
         bypasses both their version counters and ``torch.optim`` (e.g. ``p.data.copy_(...)``)."""
         self._pack_cache = None
 
-    def _packed_params(self, gs, cfg, params, device, cache=True):
+    def _packed_params(self, gs, cfg, params, device, cache=True, stream=None):
         """WdParams + the padded weight copies (wdmpnn_pack_params).  Inference caches them per
         (parameter pointer, version counter, optimizer-step generation): fused optimizers update the
         weights without bumping version counters, so every ``Optimizer.step`` also bumps
         ``_OPT_STEPS``.  A training forward always repacks and leaves no cache behind."""
         key = (tuple((t.data_ptr(), t._version) if t is not None else None for t in params), _OPT_STEPS[0],
-               self.cached_zero_vector.data_ptr(), gs.atom_fdim, gs.bond_fdim, gs.desc_dim, gs.atom_messages,
-               device)
+               self._parameters['cached_zero_vector'].data_ptr(), gs.atom_fdim, gs.bond_fdim, gs.desc_dim,
+               gs.atom_messages, device)
         cached = self._pack_cache if cache else None
         if cached is not None and cached[0] == key:
-            if cached[3] is not None and cached[4] != torch.cuda.current_stream(device).cuda_stream:
-                torch.cuda.current_stream(device).wait_event(cached[3])  # packed on another stream
+            if stream is None:
+                stream = torch.cuda.current_stream(device)
+            if cached[3] is not None and cached[4] != stream.cuda_stream:
+                stream.wait_event(cached[3])  # packed on another stream
             return cached[2], cached[1]
         p = _native.WdParams()
         p.hidden = self.hidden_size

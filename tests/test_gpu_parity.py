@@ -396,3 +396,33 @@ def test_training_step_fused_adam_and_pinned_targets():
     for (n, a), b in zip(models[0].named_parameters(), models[1].parameters()):
         d = float((a - b).detach().abs().max())
         assert d <= 1e-6, (n, d)
+
+
+def test_inference_plan_cache_follows_config_and_weights():
+    """The cached inference call (MPNEncoder._infer: per-graph plan + packed weights) picks up a changed
+    aggregation and in-place weight updates, and agrees with the
+    autograd path of the same encoder."""
+    args = TrainArgs(hidden_size=48, depth=3, bias=True)
+    g = BatchMolGraph(synthetic.make_batch('polymer', 8, 77))
+    enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim())
+    synthetic.fill_parameters(enc, 3)
+    cpu = {n: t.detach().clone() for n, t in enc.named_parameters()}
+    enc = enc.to(DEV).eval()
+    for agg in ('mean', 'sum', 'norm', 'mean'):
+        enc.aggregation = agg
+        args.aggregation = agg
+        with torch.no_grad():
+            out = enc(g)
+            again = enc(g)
+        ref = mpn_ref.encoder_forward(cpu, g, args)
+        assert golden_io.normwise(out.cpu().numpy(), ref.numpy()) <= TOL, agg
+        assert torch.equal(out, again)
+        assert len(g.device_graph(DEV, False, get_bond_fdim()).encoder_plans) <= 3
+    with torch.no_grad():
+        enc.W_h.weight.mul_(0.5)  # in-place: bumps the version counter
+        cpu['W_h.weight'].mul_(0.5)
+        out = enc(g)
+    ref = mpn_ref.encoder_forward(cpu, g, args)
+    assert golden_io.normwise(out.cpu().numpy(), ref.numpy()) <= TOL
+    grad_path = enc(g)  # grad enabled: the autograd.Function path
+    assert golden_io.normwise(grad_path.detach().cpu().numpy(), ref.numpy()) <= TOL
