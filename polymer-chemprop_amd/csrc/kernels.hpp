@@ -301,21 +301,43 @@ struct SlabReduce {
     float *db; int bias_col;
 };
 
+// grid (column groups of 64, row groups of 4), 256 threads: one output element per thread (the
+// bias is the extra column after the segments).  Every thread sums its column over the splits in
+// split order z = 0, 1, ... (eight independent loads in flight, then eight ordered adds), so the
+// result does not depend on the launch shape.
 __global__ __launch_bounds__(256) void slab_reduce_kernel(SlabReduce P) {
-    const int n = blockIdx.x;
-    const float *row = P.slab + (size_t)n * P.ld_slab;
-    if (P.dW)
-        for (int s = 0; s < P.nseg; ++s)
-            for (int kk = threadIdx.x; kk < P.K[s]; kk += blockDim.x) {
-                float acc = 0.f;
-                for (int z = 0; z < P.nsplit; ++z) acc += row[(size_t)z * P.slab_stride + P.c0[s] + kk];
-                P.dW[(size_t)n * P.ldw + P.w0[s] + kk] = acc;
+    const int n = blockIdx.y * 4 + (threadIdx.x >> 6);
+    int j = blockIdx.x * 64 + (threadIdx.x & 63);
+    if (n >= P.rows) return;
+    int src = -1;
+    float *dst = nullptr;
+    if (P.dW) {
+        for (int s = 0; s < P.nseg; ++s) {
+            if (j < P.K[s]) {
+                src = P.c0[s] + j;
+                dst = P.dW + (size_t)n * P.ldw + P.w0[s] + j;
+                break;
             }
-    if (P.db && threadIdx.x == 0) {
-        float acc = 0.f;
-        for (int z = 0; z < P.nsplit; ++z) acc += row[(size_t)z * P.slab_stride + P.bias_col];
-        P.db[n] = acc;
+            j -= P.K[s];
+        }
     }
+    if (!dst && P.db && j == 0) {
+        src = P.bias_col;
+        dst = P.db + n;
+    }
+    if (!dst) return;
+    const float *col = P.slab + (size_t)n * P.ld_slab + src;
+    float acc = 0.f;
+    int z = 0;
+    for (; z + 8 <= P.nsplit; z += 8) {
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = col[(size_t)(z + q) * P.slab_stride];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc += v[q];
+    }
+    for (; z < P.nsplit; ++z) acc += col[(size_t)z * P.slab_stride];
+    *dst = acc;
 }
 
 __global__ void sum_kernel(const float *__restrict__ x, int n, float *__restrict__ out) {

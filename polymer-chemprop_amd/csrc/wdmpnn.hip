@@ -422,7 +422,7 @@ TnPlan tn_plan(int n_out, int cols_p, int m_rows) {
     TnPlan t{};
     const int tiles = ((n_out + NBM - 1) / NBM) * ((cols_p + NBN - 1) / NBN);
     const int chunks = (m_rows + BK - 1) / BK;
-    int ns = (1024 + tiles - 1) / tiles;
+    int ns = (2048 + tiles - 1) / tiles;
     if (ns > chunks) ns = chunks;
     if (ns < 1) ns = 1;
     const int cps = (chunks + ns - 1) / ns;
@@ -459,7 +459,11 @@ int slab_reduce(const TnPlan &tp, const float *slab, int n_rows, std::initialize
         ++R.nseg;
     }
     R.dW = dW; R.ldw = ldw; R.db = db; R.bias_col = bias_col;
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3(n_rows), dim3(256), 0, st, R);
+    int cols = 0;
+    if (dW)
+        for (int q = 0; q < R.nseg; ++q) cols += R.K[q];
+    if (db) cols += 1;  // the bias column after the segments
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((cols + 63) / 64, (n_rows + 3) / 4), dim3(256), 0, st, R);
     WD_CHECK_LAUNCH("slab_reduce");
     return 0;
 }
