@@ -60,7 +60,7 @@ __device__ __forceinline__ bool ell_more(const EllRow &e) { return e.ix[ELLW / 4
 
 // WD_EXP (timing experiments only, never set in the product build): 1 = skip the layer GEMM,
 // 2 = skip the layer's plane stores, 3 = skip the in-block gather, 4 = skip the residual prefetch,
-// 6 = skip residual and ELL prefetch
+// 6 = skip residual and ELL prefetch; wo_readout: 20 = skip the molecule readout
 #ifndef WD_EXP
 #define WD_EXP 0
 #endif
@@ -302,8 +302,11 @@ template <> struct WoWaves<80> { static constexpr int WM = 2, WN = 5; };
 template <int BN>
 __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_readout_kernel(WoReadoutP P) {
     constexpr int BM = BLK_ATOMS, LDC = BN + 4, WM = WoWaves<BN>::WM, WN = WoWaves<BN>::WN, NT = 64 * WM * WN;
-    constexpr int CPS = 1;  // chunks per barrier (see mp_layer_kernel)
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * CPS * x6_stage_bytes<BM, BN>()];
+    // two chunks per barrier: W_o's 64-row chunks are short, and one barrier per chunk cost 0.6 us
+    // (12.5 vs 13.1 us at the benchmark size; three single-chunk stages measured 15.1 us)
+    constexpr int CPS = 2;
+    constexpr int WS = 2;  // LDS stages
+    __shared__ __attribute__((aligned(16))) uint8_t lds[WS * CPS * x6_stage_bytes<BM, BN>()];
     const int tile = xcd_tile(blockIdx.x, gridDim.x);
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
@@ -332,7 +335,7 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
         }
     };
     floatx4 acc[BM / WM / 16][BN / WN / 16];
-    x6_mainloop<BM, BN, WM, WN, 2, CPS>(O, lds, acc, prefetch);
+    x6_mainloop<BM, BN, WM, WN, WS, CPS>(O, lds, acc, prefetch);
     __syncthreads();
     float *H = reinterpret_cast<float *>(lds);
     float *Wl = H + BM * LDC;           // [BM] atom weights of the block
@@ -364,23 +367,31 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
         }
     }
     __syncthreads();
-    // readout (mpn.py:145-171) of this block's molecules, columns n0 .. n0 + BN - 1: thread -> (molecule,
-    // column); the atom weights and molecule scopes come from LDS, summed in atom order
-    for (int t = tid; t < nm * BN; t += NT) {
-        const int im = t / BN, i = B.ml + im, cc = t % BN, col = n0 + cc;
-        if (col >= P.ncols) continue;
+    // readout (mpn.py:145-171) of this block's molecules, columns n0 .. n0 + BN - 1: eight lanes per
+    // (molecule, column), lane j summing the molecule's atoms j, j + 8, ... from LDS, then a fixed xor
+    // butterfly over the eight lanes (deterministic; every lane ends with the same sum)
+    constexpr int RP = 8;
+    static_assert(NT % RP == 0 && 64 % RP == 0, "lane groups stay inside a wave");
+    for (int t = tid; t < (WD_EXP == 20 ? 0 : nm * BN * RP); t += NT) {
+        const int part = t % RP, u = t / RP, im = u / BN, i = B.ml + im, cc = u % BN, col = n0 + cc;
         const int n = __float_as_int(Ml[BLK_MOLS + im]);
+        float s = 0.f, wsum = 0.f;
+        const int a0 = __float_as_int(Ml[im]) - B.as;
+        for (int a = part; a < n; a += RP) {
+            const float w = Wl[a0 + a];
+            s = fmaf(w, H[(a0 + a) * LDC + cc], s);
+            wsum += w;
+        }
+#pragma unroll
+        for (int off = 1; off < RP; off <<= 1) {
+            s += __shfl_xor(s, off, 64);
+            wsum += __shfl_xor(wsum, off, 64);
+        }
+        if (part != 0 || col >= P.ncols) continue;
         float v;
         if (n == 0) {
             v = P.zero_vec[col];  // cached_zero_vector, no Xn factor (mpn.py:148-149)
         } else {
-            const int a0 = __float_as_int(Ml[im]) - B.as;
-            float s = 0.f, wsum = 0.f;
-            for (int a = 0; a < n; ++a) {
-                const float w = Wl[a0 + a];
-                s = fmaf(w, H[(a0 + a) * LDC + cc], s);
-                wsum += w;
-            }
             const float m = P.agg == 0 ? s / wsum : (P.agg == 2 ? s / P.norm : s);
             v = Ml[2 * BLK_MOLS + im] * m;
         }
