@@ -302,9 +302,11 @@ template <> struct WoWaves<80> { static constexpr int WM = 2, WN = 5; };
 template <int BN>
 __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_readout_kernel(WoReadoutP P) {
     constexpr int BM = BLK_ATOMS, LDC = BN + 4, WM = WoWaves<BN>::WM, WN = WoWaves<BN>::WN, NT = 64 * WM * WN;
-    // two chunks per barrier: W_o's 64-row chunks are short, and one barrier per chunk cost 0.6 us
-    // (12.5 vs 13.1 us at the benchmark size; three single-chunk stages measured 15.1 us)
-    constexpr int CPS = 2;
+    // 80-column tiles (one workgroup per CU at the benchmark size): two chunks per barrier, since W_o's
+    // 64-row chunks are short and one barrier per chunk cost 0.6 us (12.5 vs 13.1 us; three
+    // single-chunk stages measured 15.1 us).  64-column tiles (large batches, several workgroups per
+    // CU) keep one chunk per barrier and half the LDS
+    constexpr int CPS = BN == 80 ? 2 : 1;
     constexpr int WS = 2;  // LDS stages
     __shared__ __attribute__((aligned(16))) uint8_t lds[WS * CPS * x6_stage_bytes<BM, BN>()];
     const int tile = xcd_tile(blockIdx.x, gridDim.x);

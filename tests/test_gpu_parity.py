@@ -279,6 +279,9 @@ def test_fused_and_unfused_paths_agree_in_training(extra):
     ('zinc', 64, 512, 5, dict(activation='LeakyReLU')),                 # 64-column tiles
     ('qm9', 96, 128, 3, dict(activation='SELU', bias=True)),           # many molecules per block
     ('polymer', 16, 70, 2, dict(activation='PReLU', bias=True)),       # Hk = 128, T = 2 (single layer)
+    ('qm9', 64, 300, 3, {}),                                            # bench secondary (configs[1] shape)
+    ('polymer', 128, 300, 3, {}),                                       # configs[2] batch size
+    ('zinc', 512, 512, 5, {}),                                          # bench secondary (configs[3] shape)
 ])
 def test_blocked_fused_forward(kind, b, hidden, depth, extra):
     """The molecule-blocked fused inference forward (WdConfig.gemm_variant 10, no grad) matches the
