@@ -147,7 +147,7 @@ def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_b
             'single_stream': {'value': E / dt1, 'ms_per_step': dt1 / steps * 1e3}}
 
 
-def training_workload(device, batch=128, steps=20, warmup=3):
+def training_workload(device, batch=128, steps=100, warmup=10):
     """BASELINE.json configs[2] shape (copolymer batches of 128 with weighted edges, full training
     step): MoleculeModel (encoder + FFN, regression, one task) forward + loss + backward (the
     deterministic HIP backward) + Adam step per batch, resident graphs, synchronised wall time."""

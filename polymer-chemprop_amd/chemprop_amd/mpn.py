@@ -285,7 +285,7 @@ class MPNEncoder(nn.Module):
         ``_OPT_STEPS``.  A training forward always repacks and leaves no cache behind."""
         key = (tuple((t.data_ptr(), t._version) if t is not None else None for t in params), _OPT_STEPS[0],
                self._parameters['cached_zero_vector'].data_ptr(), gs.atom_fdim, gs.bond_fdim, gs.desc_dim,
-               gs.atom_messages, device)
+               gs.atom_messages, device) if cache else None
         cached = self._pack_cache if cache else None
         if cached is not None and cached[0] == key:
             if stream is None:
@@ -303,11 +303,17 @@ class MPNEncoder(nn.Module):
                                                    ctypes.byref(nbytes)), 'pack size')
         buf = torch.empty(nbytes.value, dtype=torch.uint8, device=device)
         _native.check(L.wdmpnn_pack_params(ctypes.byref(gs), ctypes.byref(p), ctypes.byref(cfg), buf.data_ptr(),
-                                           nbytes.value, _native.current_stream(device)), 'pack params')
+                                           nbytes.value, stream.cuda_stream if stream is not None
+                                           else _native.current_stream(device)), 'pack params')
         p.packed, p.packed_bytes = buf.data_ptr(), buf.numel()
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(device))
-        self._pack_cache = (key, buf, p, ev, torch.cuda.current_stream(device).cuda_stream) if cache else None
+        if cache:  # (a training forward uses its packed weights on this stream only: no event)
+            if stream is None:
+                stream = torch.cuda.current_stream(device)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            self._pack_cache = (key, buf, p, ev, stream.cuda_stream)
+        else:
+            self._pack_cache = None
         return p, buf
 
 

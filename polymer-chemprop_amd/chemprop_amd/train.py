@@ -91,26 +91,33 @@ def build_optimizer(model: nn.Module, args=1e-4, weight_decay: float = 0.0) -> O
 def batch_loss(preds: torch.Tensor, target_batch: Sequence[Sequence[Optional[float]]], loss_func: Callable,
                dataset_type: str = 'regression', target_weights: Sequence[float] = None,
                data_weights: Sequence[float] = None) -> torch.Tensor:
-    """train.py:46-74: masked, weighted loss averaged over the present targets."""
+    """train.py:46-74: ``(loss_func(preds, targets) * target_weights * data_weights * mask).sum() /
+    mask.sum()``.  The three weight factors are multiplied on the host into one weight table W, and
+    ``mask.sum()`` is a host count: two fewer device ops forward and backward, the same loss (W is
+    rounded once to fp32 instead of twice)."""
     dev = preds.device
-    # targets, mask and data weights travel as one host table: on a GPU one pinned, asynchronous copy
-    # (three pageable copies would each stall the host until the forward has drained)
     n_t = len(target_batch[0]) if len(target_batch) else 0
-    rows = [[0.0 if x is None else float(x) for x in tb] + [float(x is not None) for x in tb]
-            + [1.0 if data_weights is None else float(data_weights[i])] for i, tb in enumerate(target_batch)]
-    host = torch.tensor(rows, dtype=torch.float32).reshape(len(target_batch), 2 * n_t + 1)
+    tw = [1.0] * n_t if target_weights is None else [float(x) for x in target_weights]
+    # targets and W travel as one host table: on a GPU one pinned, asynchronous copy (pageable copies
+    # would each stall the host until the forward has drained)
+    rows, n_mask = [], 0
+    for i, tb in enumerate(target_batch):
+        dw = 1.0 if data_weights is None else float(data_weights[i])
+        rows.append([0.0 if x is None else float(x) for x in tb]
+                    + [0.0 if x is None else tw[j] * dw for j, x in enumerate(tb)])
+        n_mask += sum(x is not None for x in tb)
+    host = torch.tensor(rows, dtype=torch.float32).reshape(len(target_batch), 2 * n_t)
     if dev.type == 'cuda':
         host = host.pin_memory()
     table = host.to(dev, non_blocking=True)
-    targets, mask, dw = table[:, :n_t], table[:, n_t:2 * n_t] > 0, table[:, 2 * n_t:]
-    tw = torch.Tensor(target_weights).to(dev) if target_weights is not None else torch.ones_like(targets)
+    targets, w = table[:, :n_t], table[:, n_t:]
     if dataset_type == 'multiclass':
         targets = targets.long()
         loss = torch.cat([loss_func(preds[:, j, :], targets[:, j]).unsqueeze(1) for j in range(preds.size(1))],
-                         dim=1) * tw * dw * mask
+                         dim=1) * w
     else:
-        loss = loss_func(preds, targets) * tw * dw * mask
-    return loss.sum() / mask.sum()
+        loss = loss_func(preds, targets) * w
+    return loss.sum() / float(n_mask)
 
 
 def train_step(model: nn.Module, mol_batch, target_batch, loss_func: Callable, optimizer: Optimizer,

@@ -31,6 +31,27 @@ def test_masked_weighted_loss():
     assert math.isclose(float(loss), expect, rel_tol=1e-6)
 
 
+def test_loss_matches_reference_formula_with_all_weights():
+    """train.py:46-74 restated literally (mask / targets / target_weights / data_weights tensors, the
+    product, loss.sum() / mask.sum()) against batch_loss's host-combined weight table: values and
+    gradients."""
+    g = torch.Generator().manual_seed(1)
+    preds = torch.randn(6, 3, generator=g, requires_grad=True)
+    tb = [[0.3, None, 1.2], [None, None, -0.4], [2.0, 0.1, 0.0], [0.5, -1.0, None], [1.0, 1.0, 1.0],
+          [None, 0.7, 0.2]]
+    tw, dw = [0.5, 2.0, 1.5], [1.0, 0.3, 2.5, 1.0, 0.7, 1.2]
+    mask = torch.Tensor([[x is not None for x in r] for r in tb])
+    targets = torch.Tensor([[0 if x is None else x for x in r] for r in tb])
+    ref = (torch.nn.MSELoss(reduction='none')(preds, targets) * torch.Tensor(tw).unsqueeze(0)
+           * torch.Tensor(dw).unsqueeze(1) * mask)
+    ref = ref.sum() / mask.sum()
+    g_ref, = torch.autograd.grad(ref, preds)
+    out = batch_loss(preds, tb, get_loss_func('regression'), target_weights=tw, data_weights=dw)
+    g_out, = torch.autograd.grad(out, preds)
+    assert math.isclose(out.item(), ref.item(), rel_tol=1e-6)
+    assert torch.allclose(g_out, g_ref, rtol=1e-6, atol=1e-8)
+
+
 def test_loss_classification_and_multiclass():
     preds = torch.tensor([[0.5, -1.0], [2.0, 0.0]])
     targets = [[1, None], [0, 1]]

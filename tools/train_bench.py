@@ -9,4 +9,4 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-print(json.dumps(bench.training_workload(torch.device('cuda:0'), steps=int(os.environ.get('STEPS', '20')))))
+print(json.dumps(bench.training_workload(torch.device('cuda:0'), steps=int(os.environ.get('STEPS', '100')))))
