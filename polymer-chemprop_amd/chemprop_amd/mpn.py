@@ -177,7 +177,7 @@ class MPNEncoder(nn.Module):
         DeviceGraph, so a repeated forward costs two allocations and one C-ABI call.  Returns None when
         the call needs the general path."""
         d = self.__dict__
-        if d['_prof'] is not None or (self.training and self.dropout > 0):
+        if d.get('_prof') is not None or '_plan_token' not in d or (self.training and self.dropout > 0):
             return None
         params = self._param_tuple()
         device = params[0].device
