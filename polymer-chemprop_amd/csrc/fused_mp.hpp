@@ -306,6 +306,9 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     // 64-row chunks are short and one barrier per chunk cost 0.6 us (12.5 vs 13.1 us; three
     // single-chunk stages measured 15.1 us).  64-column tiles (large batches, several workgroups per
     // CU) keep one chunk per barrier and half the LDS
+    // (deeper single-chunk pipelines, with the mainloop hook's loads ordered ahead of the partial vmcnt
+    // waits, measured slower: three / four stages 15.1 / 14.8 us here, 12.8 / 11.8 against 9.7 us on
+    // QM9-shaped batches)
     constexpr int CPS = BN == 80 ? 2 : 1;
     constexpr int WS = 2;  // LDS stages
     __shared__ __attribute__((aligned(16))) uint8_t lds[WS * CPS * x6_stage_bytes<BM, BN>()];
