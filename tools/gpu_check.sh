@@ -28,6 +28,8 @@ for s in "$@"; do
     train) step train 300 python tools/train_bench.py ;;
     proftrain) step rocprof_train 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof_train -o run --output-format csv -- python tools/train_bench.py ;;
     host) step host 300 python tools/host_overhead.py ;;
+    hiptrace) step hiptrace 300 rocprofv3 --hip-trace --stats --output-format csv -d gpurun_out/hiptrace -o run -- python tools/host_overhead.py ;;
+    packprof) step pack_profile 200 python tools/pack_profile.py ;;
     ab) step ab_x6 300 python bench.py --steps 200 --warmup 20 --no-cpu --variant 10 && step ab_f32 300 python bench.py --steps 200 --warmup 20 --no-cpu --variant 9 ;;
     x6prec) step x6prec 300 python tools/x6_precision.py ;;
     profx6) step rocprof_x6 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof_x6 -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu --no-secondary --streams 1 --variant ${VARIANT:-10} ;;
