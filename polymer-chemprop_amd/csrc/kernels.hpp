@@ -159,14 +159,44 @@ __global__ __launch_bounds__(256) void readout_bwd_kernel(ReadoutP P, const floa
     const int i = blockIdx.x;
     const int a0 = P.mol_start[i], n = P.mol_size[i];
     if (n == 0) return;
-    float wsum = 0.f;
-    for (int a = 0; a < n; ++a) wsum += P.w_atoms[a0 + a];
+    // Σ w_a as a fixed-shape tree over the block (deterministic), the atom weights staged in LDS, and
+    // each thread's column gradient kept in registers: the store loop issues no global loads (the
+    // previous element-per-iteration form waited on two dependent loads per element, ~19 us per call)
+    constexpr int NT = 256, MAXC = 4;  // columns per thread: ncols <= NT * MAXC (checked by the launcher)
+    __shared__ float red[NT];
+    __shared__ float wl[NT];
+    const int tid = threadIdx.x;
+    float w = 0.f;
+    for (int a = tid; a < n; a += NT) w += P.w_atoms[a0 + a];
+    red[tid] = w;
+    __syncthreads();
+    for (int k = NT / 2; k > 0; k >>= 1) {
+        if (tid < k) red[tid] += red[tid + k];
+        __syncthreads();
+    }
+    const float wsum = red[0];
     const float x = P.xn[i];
-    for (int t = threadIdx.x; t < n * P.ncols; t += blockDim.x) {
-        const int a = t / P.ncols, c = t % P.ncols;
-        const float g = dout[(size_t)i * P.ncols + c] * x;
-        const float gs = P.agg == 0 ? g / wsum : (P.agg == 2 ? g / P.norm : g);
-        dh[(size_t)(a0 + a) * P.ldh + c] = gs * P.w_atoms[a0 + a];
+    float gs[MAXC];
+#pragma unroll
+    for (int q = 0; q < MAXC; ++q) {
+        const int c = tid + NT * q;
+        const float g = c < P.ncols ? dout[(size_t)i * P.ncols + c] * x : 0.f;
+        gs[q] = P.agg == 0 ? g / wsum : (P.agg == 2 ? g / P.norm : g);
+    }
+    for (int base = 0; base < n; base += NT) {
+        const int m = min(NT, n - base);
+        __syncthreads();
+        if (tid < m) wl[tid] = P.w_atoms[a0 + base + tid];
+        __syncthreads();
+        float *row = dh + (size_t)(a0 + base) * P.ldh;
+        for (int a = 0; a < m; ++a, row += P.ldh) {
+            const float wa = wl[a];
+#pragma unroll
+            for (int q = 0; q < MAXC; ++q) {
+                const int c = tid + NT * q;
+                if (c < P.ncols) row[c] = gs[q] * wa;
+            }
+        }
     }
 }
 

@@ -894,6 +894,7 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
     float *dH = S(Bl.dH);
     if (hipMemsetAsync(dH, 0, (size_t)D.Vap * ldH * 4, st) != hipSuccess) return fail(WD_ERR_ARG, "memset failed");
     if (D.B > 0) {
+        if (D.Hd > 4 * 256) return fail(WD_ERR_UNSUPPORTED, "readout backward: hidden + descriptors > 1024");
         hipLaunchKernelGGL(readout_bwd_kernel, dim3(D.B), dim3(256), 0, st,
                            readout_params(g, p, c, nullptr, ldH, D.Hd, nullptr), dout, dH);
         WD_CHECK_LAUNCH("readout_bwd");
