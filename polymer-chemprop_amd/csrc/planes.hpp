@@ -152,4 +152,21 @@ __global__ __launch_bounds__(256) void split_tiles_kernel(const float *__restric
     }
 }
 
+// Several dense splits in one launch (blockIdx.y = job; BR 64 or 80 per job): the weight packing of
+// a training forward splits five small matrices, and five launches cost more than the work.
+struct SplitJob { const float *src; uint8_t *dst; int ld, rows, kp, br; };
+struct SplitJobs { SplitJob j[5]; int n; };
+
+__global__ __launch_bounds__(256) void split_tiles_batch_kernel(SplitJobs J) {
+    const SplitJob S = J.j[blockIdx.y];
+    const int q8 = S.kp >> 3;
+    const size_t total = (size_t)S.rows * q8;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+        const int r = (int)(t / q8), k = (int)(t % q8) * 8;
+        const float *s = S.src + (size_t)r * S.ld + k;
+        if (S.br == 80) x6_store8<80>(S.dst, S.kp, r, k, ld4(s), ld4(s + 4));
+        else x6_store8<64>(S.dst, S.kp, r, k, ld4(s), ld4(s + 4));
+    }
+}
+
 }  // namespace wd

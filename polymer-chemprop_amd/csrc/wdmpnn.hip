@@ -215,20 +215,21 @@ int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
     }
     hipLaunchKernelGGL(pack_kernel, dim3(64, J.n), dim3(256), 0, st, J);
     WD_CHECK_LAUNCH("pack_params");
-    // bf16x3 plane tiles of the padded W_i / W_h / W_o copies (B operands of gemm_x6g_kernel)
-    const std::array<std::array<size_t, 3>, 3> xs = {{{L.Wi, L.WiX, (size_t)D.Kink}, {L.Wh, L.WhX, (size_t)D.ldx},
-                                                      {L.Wo, L.WoX, (size_t)D.Ko}}};
-    for (const auto &x : xs) {
-        const int kp = (int)x[2];
-        hipLaunchKernelGGL(split_tiles_kernel<64>, dim3(ew_blocks((size_t)D.Hk * kp / 8)), dim3(256), 0, st,
-                           (const float *)(base + x[0]), kp, D.Hk, kp, (uint8_t *)(base + x[1]));
-    }
+    // bf16x3 plane tiles of the padded W_i / W_h / W_o copies (B operands of gemm_x6g_kernel; BR 80
+    // copies of W_h / W_o for the fused layer and W_o kernels), one launch
+    SplitJobs X{};
+    auto split = [&](size_t from, size_t to, int kp, int br) {
+        X.j[X.n++] = SplitJob{(const float *)(base + from), (uint8_t *)(base + to), kp, D.Hk, kp, br};
+    };
+    split(L.Wi, L.WiX, D.Kink, 64);
+    split(L.Wh, L.WhX, D.ldx, 64);
+    split(L.Wo, L.WoX, D.Ko, 64);
     if (D.Hk % 80 == 0) {
-        hipLaunchKernelGGL(split_tiles_kernel<80>, dim3(ew_blocks((size_t)D.Hk * D.ldx / 8)), dim3(256), 0, st,
-                           (const float *)(base + L.Wh), D.ldx, D.Hk, D.ldx, (uint8_t *)(base + L.WhX80));
-        hipLaunchKernelGGL(split_tiles_kernel<80>, dim3(ew_blocks((size_t)D.Hk * D.Ko / 8)), dim3(256), 0, st,
-                           (const float *)(base + L.Wo), D.Ko, D.Hk, D.Ko, (uint8_t *)(base + L.WoX80));
+        split(L.Wh, L.WhX80, D.ldx, 80);
+        split(L.Wo, L.WoX80, D.Ko, 80);
     }
+    const int kmax = std::max(D.Kink, std::max(D.ldx, D.Ko));
+    hipLaunchKernelGGL(split_tiles_batch_kernel, dim3(ew_blocks((size_t)D.Hk * kmax / 8), X.n), dim3(256), 0, st, X);
     WD_CHECK_LAUNCH("pack_params planes");
     return 0;
 }
