@@ -232,7 +232,8 @@ class MPNEncoder(nn.Module):
             out = self._infer(mol_graph)
             if out is not None:
                 return out
-        device = self.W_i.weight.device
+        base = self._param_tuple()
+        device = base[0].device
         if device.type != 'cuda':
             raise RuntimeError('chemprop_amd.MPNEncoder runs on the MI355X HIP path only: move the model to a '
                                'GPU (model.to("cuda"))')
@@ -256,10 +257,10 @@ class MPNEncoder(nn.Module):
             desc = torch.from_numpy(padded).to(device)
             gs.atom_desc, gs.desc_dim = desc.data_ptr(), d
             hidden_out += d
-        act_w = self.act_func.weight if isinstance(self.act_func, nn.PReLU) else None
+        act_w = base[8]
         if act_w is not None and act_w.numel() != 1:
             raise NotImplementedError('PReLU with num_parameters > 1')
-        params = [self.W_i.weight, self.W_i.bias, self.W_h.weight, self.W_h.bias, self.W_o.weight, self.W_o.bias]
+        params = list(base[:6])
         if desc is not None:
             params += [self.atom_descriptors_layer.weight, self.atom_descriptors_layer.bias]
         else:
