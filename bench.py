@@ -226,7 +226,6 @@ def main():
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--no-secondary', action='store_true', help='skip the QM9 / ZINC-shaped secondary workloads')
     ap.add_argument('--streams', type=int, default=2, help='batches in flight per GPU (one HIP stream each)')
-    ap.add_argument('--fuse-gather', action='store_true', help='experimental fused gather->GEMM (WdConfig.fuse_gather)')
     ap.add_argument('--variant', type=int, default=0, help='WdConfig.gemm_variant (0 = default path; 9 = f32 MFMA)')
     a = ap.parse_args()
 
@@ -247,7 +246,6 @@ def main():
         g.device_graph(device, False, get_bond_fdim())
     torch.cuda.synchronize(device)
     enc = make_encoder(args, device)
-    enc._fuse_gather = int(a.fuse_gather)
     enc._gemm_variant = a.variant
     edges = [g.n_bonds - 1 for g in graphs]
 

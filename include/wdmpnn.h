@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define WDMPNN_ABI_VERSION 2
+#define WDMPNN_ABI_VERSION 3
 #define WDMPNN_ELL_WIDTH 8
 
 enum WdActivation {     /* nn_utils.py:70-99 get_activation_function */
@@ -156,14 +156,10 @@ typedef struct WdConfig {
     void   *prof_pool;      /* optional WdEventPool: one event pair (pair prof_slot) is recorded around
                                the depth - 1 message-passing launches (the dominant kernel) of this
                                forward: before the first, after the last                          */
-    int32_t gemm_variant;   /* 0 = default = 10: bf16x6 split-plane GEMMs (fp32-accurate) with the
+    int32_t gemm_variant;   /* 0 (default): bf16x6 split-plane GEMMs (fp32-accurate), with the
                                molecule-blocked fused inference forward when WdGraph.blocks allow it;
-                               9 = f32-MFMA GEMMs; 11..14 = bf16x6 with in-kernel operand split;
-                               1..8 = older f32 tile variants (tuning only).  The
-                               backward always runs the deterministic f32-MFMA kernels.             */
-    int32_t fuse_gather;    /* 0 = separate gather + GEMM kernels (default, fastest measured);
-                               1 = gather fused into the GEMM's A-panel build (gemm_fused_kernel,
-                               experimental: DESIGN.md §4)                                          */
+                               9: f32-MFMA GEMMs on the unblocked path (precision A/B).  The backward
+                               always runs the deterministic f32-MFMA kernels.                       */
 } WdConfig;
 
 /* Gradients (device, caller-zeroed NOT required: every pointer is fully overwritten). NULL = skip. */
@@ -194,6 +190,18 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c,
 int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c,
                     const void *workspace, size_t workspace_bytes, const float *dout,
                     void *scratch, size_t scratch_bytes, const WdGrads *grads, void *stream);
+
+/* Introspection of a save_for_backward forward's workspace (tests, debugging): byte offsets of the
+ * saved fp32 pre-activations.  Z_t (t = 0 .. depth-1) = the input of the activation of message layer t
+ * (t = 0: W_i, mpn.py:96-97; t >= 1: mpn.py:123), [rows][ld] in natural row order; zo = the W_o
+ * pre-activation (mpn.py:133), [atom_rows][ld].  Padding rows / columns hold 0. */
+#define WDMPNN_MAX_SAVED_DEPTH 32
+typedef struct WdSaved {
+    int32_t depth, rows, atom_rows, ld;
+    size_t z[WDMPNN_MAX_SAVED_DEPTH];
+    size_t zo;
+} WdSaved;
+int wdmpnn_saved_layout(const WdGraph *g, const WdParams *p, const WdConfig *c, WdSaved *out);
 
 /* Measurement hook (bench.py): a pool of hipEvent pairs recorded by wdmpnn_forward around its
  * dominant launches (see WdConfig.prof_pool).  elapsed_ms synchronises on the events it reads. */
@@ -226,6 +234,12 @@ int wdmpnn_build_bond_features(const float *f_atoms, int32_t ld_atoms, int32_t a
  * the caller (the kernel clamps nothing and reads src[index]). */
 int wdmpnn_index_select_rows(const float *src, int64_t n_src_rows, int64_t row_len,
                              const int64_t *index, int64_t n_index, float *out, void *stream);
+/* Its gradient (the backward of nn_utils.py:64's index_select under autograd): dsrc[j, :] = sum of
+ * grad[p, :] over the positions p with index[p] == j, in increasing p (deterministic, no atomics).
+ * perm [n_index] = the positions sorted stably by index value, ptr [n_src_rows + 1] = the CSR bounds of
+ * each source row in perm.  Every dsrc row is written (0 for rows never selected). */
+int wdmpnn_index_select_rows_backward(const float *grad, int64_t n_index, int64_t row_len, const int64_t *perm,
+                                      const int64_t *ptr, int64_t n_src_rows, float *dsrc, void *stream);
 
 #ifdef __cplusplus
 }

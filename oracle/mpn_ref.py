@@ -30,8 +30,25 @@ def index_select_ND(source: torch.Tensor, index: torch.Tensor) -> torch.Tensor:
     return target.view(index.size() + source.size()[1:])
 
 
-def activation(name: str, x: torch.Tensor, prelu_weight: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """nn_utils.py:70-99 (functional form)."""
+KINKED = ('ReLU', 'LeakyReLU', 'PReLU', 'SELU')  # derivative jumps at 0
+
+
+def activation(name: str, x: torch.Tensor, prelu_weight: Optional[torch.Tensor] = None,
+               mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """nn_utils.py:70-99 (functional form).  ``mask`` (parity tests only): for the kinked activations,
+    take the branch of each element from ``mask`` (True = the z > 0 branch) instead of from the sign of
+    ``x``; same function away from 0, so an fp64 evaluation shares the kink decisions of an fp32 run
+    whose pre-activations gave the mask (sub-ulp sign flips at 0 are then not compared)."""
+    if mask is not None and name in KINKED:
+        m = mask.to(x.device)
+        if name == 'ReLU':
+            return torch.where(m, x, torch.zeros_like(x))
+        if name == 'LeakyReLU':
+            return torch.where(m, x, 0.1 * x)
+        if name == 'PReLU':
+            return torch.where(m, x, prelu_weight * x)
+        return torch.where(m, 1.0507009873554804934193349852946 * x,
+                           1.0507009873554804934193349852946 * 1.6732632423543772848170429916717 * torch.expm1(x))
     if name == 'ReLU':
         return F.relu(x)
     if name == 'LeakyReLU':
@@ -53,12 +70,16 @@ def _linear(p: Dict[str, torch.Tensor], name: str, x: torch.Tensor) -> torch.Ten
 
 
 def encoder_forward(p: Dict[str, torch.Tensor], graph, args,
-                    atom_descriptors_batch: Optional[List[np.ndarray]] = None, dtype=None) -> torch.Tensor:
+                    atom_descriptors_batch: Optional[List[np.ndarray]] = None, dtype=None,
+                    masks: Optional[dict] = None) -> torch.Tensor:
     """mpn.py:66-173 with dropout = 0.  ``p`` keys: W_i.weight, [W_i.bias], W_h.weight, [W_h.bias],
     W_o.weight, W_o.bias, cached_zero_vector, [act_func.weight], [atom_descriptors_layer.*].
     ``dtype=torch.float64`` evaluates the same op sequence in double precision (conditioning
-    reference for the parity tests); the default keeps the reference's float32."""
-    act = lambda x: activation(args.activation, x, p.get('act_func.weight'))  # noqa: E731
+    reference for the parity tests); the default keeps the reference's float32.  ``masks`` = {'Z':
+    [one bool tensor per message activation, mpn.py:97 then each mpn.py:123], 'Zo': bool tensor for
+    mpn.py:133}: kink branches taken from another evaluation (``activation``'s ``mask``)."""
+    calls = iter((masks['Z'] + [masks['Zo']]) if masks is not None else [])
+    act = lambda x: activation(args.activation, x, p.get('act_func.weight'), next(calls, None))  # noqa: E731
     if atom_descriptors_batch is not None:  # mpn.py:77-79
         atom_descriptors_batch = [np.zeros([1, atom_descriptors_batch[0].shape[1]])] + list(atom_descriptors_batch)
         atom_descriptors_batch = torch.from_numpy(np.concatenate(atom_descriptors_batch, axis=0)).float()

@@ -21,14 +21,15 @@ LIB_PATH = os.environ.get('WDMPNN_LIB', os.path.join(HERE, 'libwdmpnn.so'))
 ACTIVATIONS = {'ReLU': 0, 'LeakyReLU': 1, 'PReLU': 2, 'tanh': 3, 'SELU': 4, 'ELU': 5}
 ACT_IDENTITY = 6
 AGGREGATIONS = {'mean': 0, 'sum': 1, 'norm': 2}
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace_bytes',
                     'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
                     'wdmpnn_index_select_rows', 'wdmpnn_event_pool_create', 'wdmpnn_event_pool_destroy',
                     'wdmpnn_event_pool_elapsed_ms', 'wdmpnn_packed_params_bytes', 'wdmpnn_pack_params',
                     'wdmpnn_plane_bytes', 'wdmpnn_split_planes', 'wdmpnn_split_planes_rows',
-                    'wdmpnn_build_bond_features')
+                    'wdmpnn_build_bond_features', 'wdmpnn_index_select_rows_backward',
+                    'wdmpnn_saved_layout')
 
 
 class WdCsr(Structure):
@@ -59,7 +60,12 @@ class WdConfig(Structure):
     _fields_ = [('depth', c_int32), ('undirected', c_int32), ('activation', c_int32), ('aggregation', c_int32),
                 ('aggregation_norm', c_float), ('dropout', c_float), ('seed', c_uint64),
                 ('save_for_backward', c_int32), ('prof_slot', c_int32), ('prof_pool', c_void_p),
-                ('gemm_variant', c_int32), ('fuse_gather', c_int32)]
+                ('gemm_variant', c_int32)]
+
+
+class WdSaved(Structure):
+    _fields_ = [('depth', c_int32), ('rows', c_int32), ('atom_rows', c_int32), ('ld', c_int32),
+                ('z', c_size_t * 32), ('zo', c_size_t)]
 
 
 class WdGrads(Structure):
@@ -92,10 +98,13 @@ def lib() -> ctypes.CDLL:
     L.wdmpnn_backward.argtypes = [POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig), c_void_p, c_size_t,
                                   c_void_p, c_void_p, c_size_t, POINTER(WdGrads), c_void_p]
     L.wdmpnn_index_select_rows.argtypes = [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p]
+    L.wdmpnn_index_select_rows_backward.argtypes = [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int64, c_void_p,
+                                                    c_void_p]
     L.wdmpnn_packed_params_bytes.argtypes = [POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig),
                                              POINTER(c_size_t)]
     L.wdmpnn_pack_params.argtypes = [POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig), c_void_p, c_size_t,
                                      c_void_p]
+    L.wdmpnn_saved_layout.argtypes = [POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig), POINTER(WdSaved)]
     L.wdmpnn_plane_bytes.argtypes = [c_int32, c_int32, POINTER(c_size_t)]
     L.wdmpnn_split_planes.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_size_t, c_void_p]
     L.wdmpnn_split_planes_rows.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_void_p, c_size_t,

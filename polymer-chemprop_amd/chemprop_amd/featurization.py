@@ -117,7 +117,12 @@ def _packer():
 
 
 class DeviceGraph:
-    """Device-resident packed graph + the ctypes ``WdGraph`` pointing into it."""
+    """Device-resident packed graph + the ctypes ``WdGraph`` pointing into it.
+
+    Its uploads and device-side builds run on the stream current at ``device_graph()`` time (the home
+    stream) and end with an event.  ``use_on(stream)`` makes another stream wait for that event and
+    records the graph's allocations as used by that stream (``record_stream``), so a graph may be
+    encoded on any stream and freed while another stream still reads it."""
 
     def __init__(self, buffer: torch.Tensor, views: Dict[str, torch.Tensor], struct: '_native.WdGraph'):
         self.buffer = buffer
@@ -126,6 +131,32 @@ class DeviceGraph:
         self.device = buffer.device
         self.encoder_structs = {}  # (atom_fdim, bond_fdim) -> the WdGraph copy an encoder passes (mpn.py)
         self.encoder_plans = {}  # (encoder token, encoder config) -> cached inference call (MPNEncoder._infer)
+        self.ready = None  # event after the uploads / builds on the home stream
+        self.home_stream = None
+        self._streams = set()
+
+    def finish(self) -> None:
+        """Record the ready event on the current (home) stream; called once the graph is built."""
+        if self.device.type == 'cuda':
+            st = torch.cuda.current_stream(self.device)
+            self.ready = torch.cuda.Event()
+            self.ready.record(st)
+            self.home_stream = st.cuda_stream
+            self._streams.add(st.cuda_stream)
+
+    def use_on(self, stream) -> None:
+        """Order ``stream`` after the graph's build and keep its memory alive for that stream's work."""
+        sid = stream.cuda_stream
+        if sid in self._streams:
+            return
+        stream.wait_event(self.ready)
+        seen = set()
+        for t in [self.buffer] + list(self.views.values()):
+            base = t.untyped_storage().data_ptr()
+            if base not in seen:
+                seen.add(base)
+                t.record_stream(stream)
+        self._streams.add(sid)
 
 
 class BatchMolGraph:
@@ -479,6 +510,7 @@ class BatchMolGraph:
                 s.atom_ell_idx, s.atom_ell_coef = P('agg_ell_idx'), P('agg_ell_coef')
                 s.f_atoms_blk_x6 = planes.data_ptr()
         dg = DeviceGraph(buf, views, s)
+        dg.finish()
         dg.host_csr = dict(csrs)
         dg.n_edges = self.n_bonds - 1
         dg.h2d_bytes = total

@@ -33,6 +33,16 @@ def _count_optimizer_step(optimizer, args, kwargs):
 register_optimizer_step_post_hook(_count_optimizer_step)
 
 
+def _dropout_seed() -> int:
+    """64-bit counter-hash seed for one training forward's dropout masks, drawn from torch's default
+    CPU generator (so ``torch.manual_seed`` reproduces the masks) and mixed with the data-parallel
+    rank (ranks with the same seed still draw different masks).  No device sync."""
+    s = int(torch.randint(0, 2 ** 62, (1,)).item())
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        s ^= (torch.distributed.get_rank() + 1) * 0x9E3779B97F4A7C15
+    return s & 0xFFFFFFFFFFFFFFFF
+
+
 def _f32(t):
     if t is None:
         return None
@@ -94,9 +104,31 @@ class _EncoderFunction(torch.autograd.Function):
                                         ctx.ws.data_ptr(), ctx.ws_bytes, dout.data_ptr(), scratch.data_ptr(),
                                         nbytes.value, ctypes.byref(g), _native.current_stream(dev)),
                       'MPNEncoder backward')
-        ctx.ws = ctx.keep = None
+        # ctx.ws stays alive until autograd frees ctx: a second backward through the same graph
+        # (retain_graph=True) reads the same saved forward state
         return (None,) * 7 + tuple(grads.get(n) for n in ('W_i', 'b_i', 'W_h', 'b_h', 'W_o', 'b_o', 'W_d', 'b_d',
                                                            'prelu'))
+
+
+def saved_preactivations(out: torch.Tensor):
+    """The fp32 pre-activations a training forward saved for its backward (introspection for tests and
+    debugging; ``wdmpnn_saved_layout``): ``{'Z': [Z_0 .. Z_{depth-1}] ([rows, H] each, natural row order
+    with the pad row 0: Z_0 = W_i output mpn.py:96, Z_t = input + W_h(message) mpn.py:123), 'Zo': the
+    W_o pre-activation [n_atoms, H] (mpn.py:133)}``.  ``out`` must come from ``MPNEncoder.forward``
+    with gradients enabled."""
+    ctx = out.grad_fn
+    if ctx is None or not hasattr(ctx, 'ws'):
+        raise ValueError('not the output of a training-mode MPNEncoder forward')
+    lay = _native.WdSaved()
+    _native.check(_native.lib().wdmpnn_saved_layout(ctypes.byref(ctx.gstruct), ctypes.byref(ctx.p),
+                                                    ctypes.byref(ctx.cfg), ctypes.byref(lay)), 'saved layout')
+    H = ctx.p.hidden
+    ws = ctx.ws
+
+    def view(off, rows):
+        return ws[off:off + rows * lay.ld * 4].view(torch.float32).view(rows, lay.ld)[:, :H]
+
+    return {'Z': [view(lay.z[t], lay.rows) for t in range(lay.depth)], 'Zo': view(lay.zo, lay.atom_rows)}
 
 
 class MPNEncoder(nn.Module):
@@ -135,11 +167,9 @@ class MPNEncoder(nn.Module):
         if self.atom_messages and self.undirected:
             raise NotImplementedError('undirected=True with atom_messages=True indexes atom messages with bond '
                                       'indices in the reference (mpn.py:101-102) and is not supported')
-        self._seed_counter = 0
         self._prof = None  # (event pool, first pair): bench.py measurement hook, see WdConfig.prof_pool
         self._pack_cache = None  # (parameter-version key, packed weight buffer)
-        self._gemm_variant = 0  # WdConfig.gemm_variant (tuning knob; 0 = automatic)
-        self._fuse_gather = 0  # WdConfig.fuse_gather (1 = experimental fused gather->GEMM kernel)
+        self._gemm_variant = 0  # WdConfig.gemm_variant (0 = split-plane default; 9 = f32-MFMA A/B)
         self._plan_token = object()  # this encoder's key in DeviceGraph.encoder_plans
 
     def _config(self, save: bool) -> _native.WdConfig:
@@ -152,13 +182,11 @@ class MPNEncoder(nn.Module):
         p = float(self.dropout) if self.training else 0.0
         c.dropout = p
         if p > 0.0:
-            self._seed_counter += 1
-            c.seed = (int(torch.initial_seed()) * 1000003 + self._seed_counter) & 0xFFFFFFFFFFFFFFFF
+            c.seed = _dropout_seed()
         c.save_for_backward = int(bool(save))
         if self._prof is not None:
             c.prof_pool, c.prof_slot = self._prof
         c.gemm_variant = self._gemm_variant
-        c.fuse_gather = self._fuse_gather
         return c
 
     def _param_tuple(self):
@@ -186,10 +214,11 @@ class MPNEncoder(nn.Module):
         if params[8] is not None and params[8].numel() != 1:
             return None
         dg = mol_graph.device_graph(device, d['atom_messages'], d['bond_fdim'])
-        ckey = (self._plan_token, d['atom_fdim'], d['bond_fdim'], d['hidden_size'], d['depth'], d['undirected'],
-                d['activation'], d['aggregation'], d['aggregation_norm'], d['_gemm_variant'], d['_fuse_gather'])
-        plan = dg.encoder_plans.get(ckey)
         stream = torch.cuda.current_stream(device)
+        dg.use_on(stream)
+        ckey = (self._plan_token, d['atom_fdim'], d['bond_fdim'], d['hidden_size'], d['depth'], d['undirected'],
+                d['activation'], d['aggregation'], d['aggregation_norm'], d['_gemm_variant'])
+        plan = dg.encoder_plans.get(ckey)
         if plan is None:
             gs = self._graph_struct(dg)
             cfg = self._config(False)
@@ -238,6 +267,7 @@ class MPNEncoder(nn.Module):
             raise RuntimeError('chemprop_amd.MPNEncoder runs on the MI355X HIP path only: move the model to a '
                                'GPU (model.to("cuda"))')
         dg = mol_graph.device_graph(device, self.atom_messages, self.bond_fdim)
+        dg.use_on(torch.cuda.current_stream(device))
         # descriptors are per call: their struct is never cached
         gs = self._graph_struct(dg) if atom_descriptors_batch is None else self._new_graph_struct(dg)
         desc = None
@@ -291,9 +321,12 @@ class MPNEncoder(nn.Module):
         if cached is not None and cached[0] == key:
             if stream is None:
                 stream = torch.cuda.current_stream(device)
-            if cached[3] is not None and cached[4] != stream.cuda_stream:
-                stream.wait_event(cached[3])  # packed on another stream
+            if stream.cuda_stream not in cached[4]:  # packed on another stream: order after the pack and
+                stream.wait_event(cached[3])         # keep the buffer alive for this stream's kernels
+                cached[1].record_stream(stream)
+                cached[4].add(stream.cuda_stream)
             return cached[2], cached[1]
+        params = [_f32(t) for t in params]  # also after model.half() / .double(): never pack other dtypes
         p = _native.WdParams()
         p.hidden = self.hidden_size
         p.W_i, p.b_i, p.W_h, p.b_h, p.W_o, p.b_o, p.W_d, p.b_d, p.prelu = map(_native.ptr, params)
@@ -312,7 +345,7 @@ class MPNEncoder(nn.Module):
                 stream = torch.cuda.current_stream(device)
             ev = torch.cuda.Event()
             ev.record(stream)
-            self._pack_cache = (key, buf, p, ev, stream.cuda_stream)
+            self._pack_cache = (key, buf, p, ev, {stream.cuda_stream})
         else:
             self._pack_cache = None
         return p, buf

@@ -37,9 +37,22 @@ class _IndexSelectND(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad):
+        """Transposed gather on the HIP path (wdmpnn_index_select_rows_backward): every source row sums
+        its selected positions' gradients in position order, deterministic and atomics-free (autograd
+        of the reference's index_select scatter-adds them)."""
         (index,) = ctx.saved_tensors
-        g = torch.zeros((ctx.n_src,) + tuple(grad.shape[index.dim():]), dtype=grad.dtype, device=grad.device)
-        g.index_add_(0, index.reshape(-1), grad.reshape((-1,) + tuple(grad.shape[index.dim():])))
+        tail = tuple(grad.shape[index.dim():])
+        g = torch.empty((ctx.n_src,) + tail, dtype=grad.dtype, device=grad.device)
+        idx = index.reshape(-1).to(torch.int64)
+        _, perm = torch.sort(idx, stable=True)
+        ptr = torch.searchsorted(idx[perm], torch.arange(ctx.n_src + 1, device=idx.device, dtype=torch.int64))
+        gr = grad.contiguous()
+        row_len = 1
+        for s in tail:
+            row_len *= s
+        _native.check(_native.lib().wdmpnn_index_select_rows_backward(
+            gr.data_ptr(), idx.numel(), row_len, perm.data_ptr(), ptr.data_ptr(), ctx.n_src, g.data_ptr(),
+            _native.current_stream(grad.device)), 'index_select_ND backward')
         return g, None
 
 

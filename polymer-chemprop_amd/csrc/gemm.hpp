@@ -1,7 +1,8 @@
 // gemm.hpp — fp32 MFMA GEMMs of the wD-MPNN encoder (v_mfma_f32_32x32x2_f32, exact f32 fma chain,
 // 64 FLOP/clk/SIMD = the fp32 dense peak of MI355X).
 //
-// gemm_nt_kernel  C[m][n] = epi( sum_k A(m,k) * B[n][k] )        forward layers + data gradients
+// gemm_nt16_kernel  C[m][n] = epi( sum_k A(m,k) * B[n][k] )      unblocked forward layers (f32 A/B
+//                                                                 variant) + backward data gradients
 //     A = one or two dense row-major segments laid side by side along k (mpn.py:132's concat without a
 //     copy), B = a packed weight [Np][Kp].  Every buffer is padded (rows to the 64-row tile, columns
 //     and K to the 32-wide chunk, padding zero), so the loads are unconditional float4 and the
@@ -11,11 +12,9 @@
 //     reduction over rows m (thousands of bonds) split across workgroups into slabs that a second
 //     kernel reduces in a fixed order (deterministic, no atomics).
 //
-// Tile: BM x BN per workgroup of WM x WN waves, each wave a (BM/WM) x (BN/WN) block of 32x32 MFMA
-// accumulators; K in chunks of 32 staged through LDS with a one-chunk register prefetch.  At MFMA
-// step s of a chunk, lane l supplies k = 16*(l>>5) + s, so a row-major LDS tile (row stride 36
+// Tiles: BM x BN per workgroup of WM x WN waves; K in chunks of 32 staged through LDS (row stride 36
 // floats, conflict-free for ds_read_b128 and ds_write_b128: checked by brute force over the lane
-// groups of MI355X_MICROARCH.md §LDS) feeds 16 MFMAs with four ds_read_b128 per operand.
+// groups of MI355X_MICROARCH.md §LDS).
 #pragma once
 #include "common.hpp"
 #include "planes.hpp"
@@ -88,143 +87,9 @@ struct NtParams {
     Epi epi;
 };
 
-// KC = K-chunk (32 or 64 floats) consumed per LDS stage / barrier: 16 * KC / 32 MFMAs per wave and
-// accumulator between two barriers.  DEPTH = global-load prefetch distance in chunks.  DEPTH 1:
-// chunk k+1 is loaded while chunk k is multiplied.  DEPTH 2: two register sets alternate (loop
-// unrolled by two so every register index is static, §5.4 rule 20) and chunk k+2 is loaded while
-// chunk k is multiplied.  Two LDS stages, one barrier per chunk.  LDS row stride KC + 4 floats
-// (36 or 68: conflict-free for the b128 reads and writes).
-template <int BM, int BN, int WM, int WN, int DEPTH, int KC>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_nt_kernel(NtParams P) {
-    constexpr int NT = 64 * WM * WN;
-    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-    constexpr int LD = KC + 4;
-    constexpr int Q4 = KC / 4;  // float4 per tile row
-    constexpr int A_V4 = BM * Q4, B_V4 = BN * Q4;
-    constexpr int PA = A_V4 / NT, PB = B_V4 / NT;
-    constexpr int STAGE = (BM + BN) * LD;
-    static_assert(A_V4 % NT == 0 && B_V4 % NT == 0, "tile must divide evenly over threads");
-    __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wi = wave / WN, wj = wave % WN, h = lane >> 5, l32 = lane & 31;
-    const int tile = xcd_tile(blockIdx.x, P.tiles_m * P.tiles_n);
-    const int mt = tile / P.tiles_n, nt = tile % P.tiles_n;
-    const int m0 = mt * BM, n0 = nt * BN;
-    const int K = P.ka0 + P.ka1;
-
-    floatx16 acc[TM][TN];
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-
-    const float *pb[PB];
-#pragma unroll
-    for (int p = 0; p < PB; ++p) {
-        const int q = tid + p * NT, r = q / Q4, c = (q % Q4) * 4;
-        pb[p] = P.b + (size_t)(n0 + r) * P.ldb + c;
-    }
-    struct Regs { float4 a[PA], b[PB]; };
-    auto load_chunk = [&](Regs &R, int k0) {
-        const bool seg1 = k0 >= P.ka0;  // workgroup-uniform (segments are KC-aligned)
-        const float *base = seg1 ? P.a1 : P.a0;
-        const int ld = seg1 ? P.lda1 : P.lda0;
-        const int kk = seg1 ? k0 - P.ka0 : k0;
-#pragma unroll
-        for (int p = 0; p < PA; ++p) {
-            const int q = tid + p * NT, r = q / Q4, c = (q % Q4) * 4;
-            R.a[p] = ld4(base + (size_t)(m0 + r) * ld + kk + c);
-        }
-#pragma unroll
-        for (int p = 0; p < PB; ++p) R.b[p] = ld4(pb[p] + k0);
-    };
-    auto store_chunk = [&](const Regs &R, float *st) {
-#pragma unroll
-        for (int p = 0; p < PA; ++p) {
-            const int q = tid + p * NT, r = q / Q4, c = (q % Q4) * 4;
-            st4(st + r * LD + c, R.a[p]);
-        }
-#pragma unroll
-        for (int p = 0; p < PB; ++p) {
-            const int q = tid + p * NT, r = q / Q4, c = (q % Q4) * 4;
-            st4(st + BM * LD + r * LD + c, R.b[p]);
-        }
-    };
-    auto compute = [&](const float *As) {
-        const float *Bs = As + BM * LD;
-#pragma unroll
-        for (int sub = 0; sub < KC / 32; ++sub) {
-            float af[TM][16], bf[TN][16];
-#pragma unroll
-            for (int a = 0; a < TM; ++a) {
-                const float *src = As + (wi * (BM / WM) + a * 32 + l32) * LD + 32 * sub + 16 * h;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 v = ld4(src + 4 * q);
-                    af[a][4 * q] = v.x; af[a][4 * q + 1] = v.y; af[a][4 * q + 2] = v.z; af[a][4 * q + 3] = v.w;
-                }
-            }
-#pragma unroll
-            for (int b = 0; b < TN; ++b) {
-                const float *src = Bs + (wj * (BN / WN) + b * 32 + l32) * LD + 32 * sub + 16 * h;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 v = ld4(src + 4 * q);
-                    bf[b][4 * q] = v.x; bf[b][4 * q + 1] = v.y; bf[b][4 * q + 2] = v.z; bf[b][4 * q + 3] = v.w;
-                }
-            }
-#pragma unroll
-            for (int s = 0; s < 16; ++s)
-#pragma unroll
-                for (int a = 0; a < TM; ++a)
-#pragma unroll
-                    for (int b = 0; b < TN; ++b)
-                        acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
-        }
-    };
-
-    const int nchunks = K / KC;
-    if constexpr (DEPTH == 1) {
-        Regs R;
-        load_chunk(R, 0);
-        store_chunk(R, lds);
-        __syncthreads();
-        for (int kc = 0; kc < nchunks; ++kc) {
-            const bool more = kc + 1 < nchunks;
-            if (more) load_chunk(R, (kc + 1) * KC);
-            compute(lds + (kc & 1) * STAGE);
-            if (more) store_chunk(R, lds + ((kc + 1) & 1) * STAGE);
-            __syncthreads();
-        }
-    } else {
-        Regs R0, R1;
-        load_chunk(R0, 0);
-        if (nchunks > 1) load_chunk(R1, KC);
-        store_chunk(R0, lds);
-        __syncthreads();
-        // step(kc, Rnext, Rfree): Rnext holds chunk kc+1 (in flight), Rfree receives chunk kc+2
-        auto step = [&](int kc, Regs &Rnext, Regs &Rfree) {
-            if (kc + 2 < nchunks) load_chunk(Rfree, (kc + 2) * KC);
-            compute(lds + (kc & 1) * STAGE);
-            if (kc + 1 < nchunks) store_chunk(Rnext, lds + ((kc + 1) & 1) * STAGE);
-            __syncthreads();
-        };
-        int kc = 0;
-        for (; kc + 1 < nchunks; kc += 2) {
-            step(kc, R1, R0);
-            step(kc + 1, R0, R1);
-        }
-        if (kc < nchunks) step(kc, R1, R0);
-    }
-    epilogue<TM, TN>(P.epi, acc, m0 + wi * (BM / WM), n0 + wj * (BN / WN), h, l32, P.M, P.N, P.epi.Y);
-}
-
 // ---------------------------------------------------------------------------------------------
-// 16x16x4 variant of gemm_nt_kernel: the wave's 32x32 block is 2x2 v_mfma_f32_16x16x4_f32 tiles (4
-// independent accumulator chains instead of one), same LDS staging / prefetch.  Lane l = (i = l&15,
+// NT GEMM on f32 MFMA: the wave's 32x32 block is 2x2 v_mfma_f32_16x16x4_f32 tiles (4 independent
+// accumulator chains), two-chunk register prefetch, two LDS stages.  Lane l = (i = l&15,
 // g = l>>4) supplies k = 8g + s at step s (0..7 per 32-chunk): two ds_read_b128 per operand tile.
 // C/D map of 16x16: col = l&15, row = 4*(l>>4) + reg.
 // ---------------------------------------------------------------------------------------------
@@ -423,91 +288,6 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_nt16_kernel(NtParams P) {
                 lds[(wi * (BM / WM) + a * 16 + 4 * g + r) * LDC + wj * (BN / WN) + b * 16 + i16] = acc[a][b][r];
     __syncthreads();
     epilogue_v4<BM, BN, NT>(P.epi, lds, LDC, m0, n0, P.M, P.N, ep);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Panel kernel (forward NT layers with a narrow output): the workgroup's whole B panel
-// [BN][K] is loaded into LDS once; every wave then streams its own A rows straight from global
-// memory into the MFMA A-operand registers (lane l holds row l&31, 16 consecutive k of the chunk
-// = four float4 loads, prefetched two chunks ahead), reads B fragments from the resident panel
-// and runs 2 independent 32x32 accumulator chains.  The K loop has no barrier and no LDS write.
-// Workgroup = NW waves stacked along M (NW*32 rows) x BN = 64 columns.  LDS row stride K + 4
-// (K a multiple of 32 => stride = 4 mod 32... conflict-free ds_read_b128 needs stride = 4 mod 64,
-// which the launcher pads to).
-// ---------------------------------------------------------------------------------------------
-template <int NW>
-__global__ __launch_bounds__(64 * NW) void gemm_panel_kernel(NtParams P, int ldp) {
-    constexpr int BN = 64, TN = 2, BM = 32 * NW;
-    extern __shared__ __attribute__((aligned(16))) float panel[];  // [BN][ldp]
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, l32 = lane & 31;
-    const int tile = xcd_tile(blockIdx.x, P.tiles_m * P.tiles_n);
-    const int mt = tile / P.tiles_n, nt = tile % P.tiles_n;
-    const int m0 = mt * BM, n0 = nt * BN;
-    const int K = P.ka0 + P.ka1;
-    const int kq = K / 4;
-
-    // B panel -> LDS (all threads, float4)
-    for (int q = tid; q < BN * kq; q += 64 * NW) {
-        const int r = q / kq, c = (q % kq) * 4;
-        st4(panel + r * ldp + c, ld4(P.b + (size_t)(n0 + r) * P.ldb + c));
-    }
-
-    // this lane's A row and the chunk -> (segment base, column) map
-    const int row = m0 + wave * 32 + l32;
-    const float *rowA0 = P.a0 + (size_t)row * P.lda0 + 16 * h;
-    const float *rowA1 = P.ka1 ? P.a1 + (size_t)row * P.lda1 + 16 * h - P.ka0 : nullptr;
-    struct Frag { float4 v[4]; };
-    auto load_a = [&](Frag &F, int k0) {
-        const float *p = (k0 < P.ka0 ? rowA0 : rowA1) + k0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) F.v[q] = ld4(p + 4 * q);
-    };
-
-    floatx16 acc[TN];
-#pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
-
-    const int nchunks = K / BK;
-    Frag F0, F1;
-    load_a(F0, 0);
-    load_a(F1, min(1, nchunks - 1) * BK);
-    __syncthreads();  // panel resident
-
-    auto step = [&](int kc, Frag &F, Frag &Fnext2) {
-        float bf[TN][16];
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-            const float *src = panel + (b * 32 + l32) * ldp + kc * BK + 16 * h;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float4 v = ld4(src + 4 * q);
-                bf[b][4 * q] = v.x; bf[b][4 * q + 1] = v.y; bf[b][4 * q + 2] = v.z; bf[b][4 * q + 3] = v.w;
-            }
-        }
-        const float af[16] = {F.v[0].x, F.v[0].y, F.v[0].z, F.v[0].w, F.v[1].x, F.v[1].y, F.v[1].z, F.v[1].w,
-                              F.v[2].x, F.v[2].y, F.v[2].z, F.v[2].w, F.v[3].x, F.v[3].y, F.v[3].z, F.v[3].w};
-#pragma unroll
-        for (int s = 0; s < 16; ++s)
-#pragma unroll
-            for (int b = 0; b < TN; ++b)
-                acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[b][s], acc[b], 0, 0, 0);
-        // F's registers are free again: prefetch chunk kc+2 (clamped: branch-free, so the compiler
-        // keeps counted vmcnt waits instead of draining every load at the loop head)
-        load_a(Fnext2, min(kc + 2, nchunks - 1) * BK);
-        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch here (hipcc otherwise sinks it a step)
-    };
-    int kc = 0;
-    for (; kc + 1 < nchunks; kc += 2) {
-        step(kc, F0, F0);
-        step(kc + 1, F1, F1);
-    }
-    if (kc < nchunks) step(kc, F0, F0);
-    floatx16 acc2[1][TN];
-#pragma unroll
-    for (int b = 0; b < TN; ++b) acc2[0][b] = acc[b];
-    epilogue<1, TN>(P.epi, acc2, m0 + wave * 32, n0, h, l32, P.M, P.N, P.epi.Y);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -1,6 +1,6 @@
 // kernels.hpp — bandwidth-bound kernels of the wD-MPNN encoder: CSR row gathers (the padded
 // index_select_ND + weighted sum of mpn.py:112-131), the molecule readout (mpn.py:145-171), the
-// fused activation/gather backward, weight packing and the deterministic slab reduction.
+// activation/gather backward, weight packing and the deterministic slab reduction.
 #pragma once
 #include "common.hpp"
 #include "planes.hpp"
@@ -97,6 +97,8 @@ __global__ __launch_bounds__(256) void gather8_kernel(Gather8P P) {
     if (P.planes) x6_store8(P.planes, P.kp, r, P.pcol0 + c, lo, hi);
 }
 
+constexpr int RO_BWD_COLS = 1024;  // columns per workgroup of readout_bwd_kernel (256 threads x 4)
+
 // ---------------------------------------------------------------------------------------------
 // Readout (mpn.py:145-171): out_i = Xn_i * (sum_a w_a h_a) / sum_a w_a  (mean) | sum | / norm.
 // One workgroup per molecule; lanes = (atom slot, float4 column); atom slots reduced through LDS
@@ -153,7 +155,8 @@ __global__ __launch_bounds__(RO_THREADS) void readout_kernel(ReadoutP P) {
 }
 
 // d readout / d h: dh[a] = dout[i] * Xn_i * w_a * (1/sum w | 1 | 1/norm); rows outside every scope
-// stay 0 (caller memsets).
+// stay 0 (caller memsets).  grid = (molecules, ceil(ncols / (NT * MAXC))): blockIdx.y picks a chunk of
+// RO_BWD_COLS columns (any hidden + descriptor width).
 __global__ __launch_bounds__(256) void readout_bwd_kernel(ReadoutP P, const float *__restrict__ dout,
                                                           float *__restrict__ dh) {
     const int i = blockIdx.x;
@@ -162,7 +165,7 @@ __global__ __launch_bounds__(256) void readout_bwd_kernel(ReadoutP P, const floa
     // Σ w_a as a fixed-shape tree over the block (deterministic), the atom weights staged in LDS, and
     // each thread's column gradient kept in registers: the store loop issues no global loads (the
     // previous element-per-iteration form waited on two dependent loads per element, ~19 us per call)
-    constexpr int NT = 256, MAXC = 4;  // columns per thread: ncols <= NT * MAXC (checked by the launcher)
+    constexpr int NT = 256, MAXC = 4;  // columns per thread in this workgroup's chunk
     __shared__ float red[NT];
     __shared__ float wl[NT];
     const int tid = threadIdx.x;
@@ -177,9 +180,10 @@ __global__ __launch_bounds__(256) void readout_bwd_kernel(ReadoutP P, const floa
     const float wsum = red[0];
     const float x = P.xn[i];
     float gs[MAXC];
+    const int c0 = blockIdx.y * NT * MAXC;
 #pragma unroll
     for (int q = 0; q < MAXC; ++q) {
-        const int c = tid + NT * q;
+        const int c = c0 + tid + NT * q;
         const float g = c < P.ncols ? dout[(size_t)i * P.ncols + c] * x : 0.f;
         gs[q] = P.agg == 0 ? g / wsum : (P.agg == 2 ? g / P.norm : g);
     }
@@ -193,7 +197,7 @@ __global__ __launch_bounds__(256) void readout_bwd_kernel(ReadoutP P, const floa
             const float wa = wl[a];
 #pragma unroll
             for (int q = 0; q < MAXC; ++q) {
-                const int c = tid + NT * q;
+                const int c = c0 + tid + NT * q;
                 if (c < P.ncols) row[c] = gs[q] * wa;
             }
         }
@@ -282,14 +286,10 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(ActBwd P) {
 //   plain:      segment s with dst cols [dc0_s, dc0_s + K_s): src[r][sc0_s + c - dc0_s]  (r < nrows)
 //   transpose:  src[c][sc0_0 + r]  for r < nrows (= K_0 source cols), c < K_0 (source rows)
 // ---------------------------------------------------------------------------------------------
-//   frag:       same values as plain, stored in the MFMA-fragment order of gemm_fused_kernel:
-//               [rows_p/64][cols_p/32][4 tiles][2 halves][64 lanes][4], lane (i, g) of tile b,
-//               half h holding row 64w + 16b + i, cols 32kc + 8g + 4h .. +3 (one 1 KB contiguous
-//               global_load_dwordx4 per wave per tile-half)
 struct PackJob {
     float *dst; int rows_p, cols_p;
     const float *src; int ld_src;
-    int transpose, frag, nrows, nseg;
+    int transpose, nrows, nseg;
     int dc0[2], sc0[2], K[2];
 };
 struct PackJobs { PackJob j[16]; int n; };
@@ -298,14 +298,7 @@ __global__ __launch_bounds__(256) void pack_kernel(PackJobs J) {
     const PackJob &P = J.j[blockIdx.y];
     const size_t total = (size_t)P.rows_p * P.cols_p;
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
-        int r = (int)(t / P.cols_p), c = (int)(t % P.cols_p);
-        if (P.frag) {
-            const int lane = (int)(t >> 2) & 63, h = (int)(t >> 8) & 1, b = (int)(t >> 9) & 3;
-            const size_t rest = t >> 11;
-            const int nck = P.cols_p / 32, kc = (int)(rest % nck), w = (int)(rest / nck);
-            r = 64 * w + 16 * b + (lane & 15);
-            c = 32 * kc + 8 * (lane >> 4) + 4 * h + (int)(t & 3);
-        }
+        const int r = (int)(t / P.cols_p), c = (int)(t % P.cols_p);
         float v = 0.f;
         if (P.src && r < P.nrows) {
             if (P.transpose) {
@@ -391,6 +384,22 @@ __global__ __launch_bounds__(256) void index_select_rows_kernel(const float *__r
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = t / row_len, c = t % row_len;
         out[t] = src[index[i] * row_len + c];
+    }
+}
+
+// Gradient of index_select_rows: dsrc[j] = sum over positions p with index[p] == j of grad[p], added in
+// increasing p (deterministic, no atomics).  perm = positions sorted stably by index, ptr[j] .. ptr[j+1]
+// the positions of row j in perm; one thread per output value.
+__global__ __launch_bounds__(256) void index_select_rows_bwd_kernel(const float *__restrict__ grad, int64_t row_len,
+                                                                    const int64_t *__restrict__ perm,
+                                                                    const int64_t *__restrict__ ptr, int64_t n_src,
+                                                                    float *__restrict__ dsrc) {
+    const int64_t total = n_src * row_len;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = t / row_len, c = t % row_len;
+        float s = 0.f;
+        for (int64_t e = ptr[j]; e < ptr[j + 1]; ++e) s += grad[perm[e] * row_len + c];
+        dsrc[t] = s;
     }
 }
 

@@ -26,7 +26,6 @@
 #include <string>
 #include <vector>
 
-#include "fused.hpp"
 #include "fused_mp.hpp"
 #include "gemm.hpp"
 #include "gemm_x6.hpp"
@@ -78,7 +77,8 @@ struct Dims {
     int H, Hk, T, R, Rp, Va, Vap, B, Fa, Fak, Fb, Fbk, d, dk, Hd, Hdk, Kin, Kink;
     int ldx, Ko, Kd;
     bool atom, undirected, save, desc;
-    bool x6;  // plane-tile pipeline: gathers emit bf16x3 plane tiles, GEMMs run gemm_x6g_kernel
+    bool f32;  // WdConfig.gemm_variant 9: f32-MFMA GEMMs (gemm_nt16_kernel) on the unblocked path
+    bool x6;   // plane-tile pipeline: gathers emit bf16x3 plane tiles, GEMMs run gemm_x6g_kernel
     bool blocked;  // molecule-blocked fused inference forward (fused_mp.hpp)
     int nblk;
 };
@@ -105,7 +105,8 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     D.Ko = D.Fak + D.Hk;
     D.Kd = D.Hk + D.dk;
     // default (0) = 10: bf16x6 split-plane GEMMs (fp32-accurate)
-    D.x6 = (c->gemm_variant == 10 || c->gemm_variant == 0) && !D.atom && !c->fuse_gather;
+    D.f32 = c->gemm_variant == 9;
+    D.x6 = !D.f32 && !D.atom;
     D.blocked = D.x6 && !D.save && !D.desc && D.T >= 2 && g->n_blocks > 0 && g->blocks && g->bond_blk_row &&
                 g->f_atoms_blk_x6 && g->f_bonds_x6 && g->msg_ell_idx && g->msg_ell_coef && g->atom_ell_idx &&
                 g->atom_ell_coef;
@@ -128,7 +129,6 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
 // ------------------------------------------------------------------------------------------------
 struct PackLayout {
     size_t Wi = 0, bi = 0, Wh = 0, bh = 0, Wo = 0, bo = 0, Wd = 0, bd = 0, WhT = 0, WoT = 0, WdT = 0, total = 0;
-    size_t WiF = 0, WhF = 0, WoF = 0;  // fragment-order copies for gemm_fused_kernel
     size_t WiX = 0, WhX = 0, WoX = 0;  // bf16x3 plane tiles (64-row blocks) of W_i / W_h / W_o
     size_t WhX80 = 0, WoX80 = 0;       // the same with 80-row blocks (fused forward, Hk % 80 == 0)
 };
@@ -145,9 +145,6 @@ PackLayout pack_layout(const Dims &D) {
     L.bo = take(D.Hk);
     L.WhT = take((size_t)D.Hk * D.Hk);
     L.WoT = take((size_t)D.Hk * D.Hk);
-    L.WiF = take((size_t)D.Hk * D.Kink);
-    L.WhF = take((size_t)D.Hk * D.ldx);
-    L.WoF = take((size_t)D.Hk * D.Ko);
     L.WiX = take((size_t)D.Hk * D.Kink * 3 / 2);  // 3 bf16 planes = 1.5 floats per value
     L.WhX = take((size_t)D.Hk * D.ldx * 3 / 2);
     L.WoX = take((size_t)D.Hk * D.Ko * 3 / 2);
@@ -201,13 +198,6 @@ int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
     // transposes for dX = dZ W_h[:, :H] and dA = dZo W_o[:, Fa:]
     add(job_transpose(F(L.WhT), D.Hk, D.Hk, p->W_h, D.atom ? H + D.Fb : H, 0, H, H));
     add(job_transpose(F(L.WoT), D.Hk, D.Hk, p->W_o, D.Fa + H, D.Fa, H, H));
-    // fragment-order copies of W_i / W_h / W_o (gemm_fused_kernel's B stream)
-    for (int f = 0; f < 3; ++f) {
-        PackJob j = J.j[f == 0 ? 0 : f == 1 ? 2 : 4];
-        j.dst = F(f == 0 ? L.WiF : f == 1 ? L.WhF : L.WoF);
-        j.frag = 1;
-        add(j);
-    }
     if (D.desc) {
         add(job_plain(F(L.Wd), D.Hdk, D.Kd, p->W_d, D.Hd, D.Hd, {{0, 0, H}, {D.Hk, H, D.d}}));
         add(job_plain(F(L.bd), 1, D.Hdk, p->b_d, D.Hd, 1, {{0, 0, D.Hd}}));
@@ -255,110 +245,45 @@ Epi epi_store(float *Y, int ld, long long slab_stride = 0, int accumulate = 0) {
 
 constexpr int NBM = 64, NBN = 64, NWM = 2, NWN = 2;
 
-// C[Mp][Np] = epi([A0 | A1] B^T); A segments [Mp][lda], K extents multiples of 32; B [Np][ldb].
-// Tile 64x64 (4 waves) or 32x64 (2 waves), global-load prefetch depth 1 or 2; WdConfig.gemm_variant
-// selects one for tuning (0 = default = 9, 64x64 tile of 16x16x4 MFMAs, measured fastest at every size).
+bool epi_aligned(const Epi &epi) {
+    const uintptr_t al = (uintptr_t)epi.Y | (uintptr_t)epi.Z | (uintptr_t)epi.resid | (uintptr_t)epi.bias;
+    return epi.ld % 4 == 0 && al % 16 == 0;
+}
+
+// C[Mp][Np] = epi([A0 | A1] B^T) on fp32 operands; A segments [Mp][lda], K extents multiples of 32, B
+// [Np][ldb].  split: bf16x6 GEMM with the operands split into planes in the kernel (gemm_x6_kernel,
+// 128- or 64-row tiles; fp32-accurate), else f32 MFMA (gemm_nt16_kernel, 64x64 tiles).
 int gemm_nt(const float *a0, int lda0, int ka0, const float *a1, int lda1, int ka1, const float *b, int ldb, int Mp,
-            int Np, const Epi &epi, hipStream_t st, int variant = 0) {
+            int Np, const Epi &epi, hipStream_t st, bool split = false) {
     if (Mp <= 0 || Np <= 0) return 0;
-    if (Mp % NBM || Np % NBN || ka0 % BK || ka1 % BK || ka0 <= 0 || lda0 % 4 || (ka1 && lda1 % 4) || ldb % 4)
-        return fail(WD_ERR_SHAPE, "gemm_nt: unpadded operand (Mp %d Np %d ka %d/%d)", Mp, Np, ka0, ka1);
-    // 11-14 = bf16x6 split GEMM with fp32 operands split in the kernel (gemm_x6.hpp):
-    // 11 = 64x64 tile, 12 = 128x64, 13 = 64x64 with 64-wide K chunks, 14 = 128x64 with 64-wide chunks
-    if (variant >= 11 && variant <= 14) {
-        const uintptr_t al = (uintptr_t)epi.Y | (uintptr_t)epi.Z | (uintptr_t)epi.resid | (uintptr_t)epi.bias;
-        if (epi.ld % 4 || al % 16) variant = 9;
-        else if ((variant == 12 || variant == 14) && Mp % 128) variant -= 1;
-        if ((variant == 13 || variant == 14) && (ka0 % 64 || ka1 % 64)) variant -= 2;
-    }
-    if (variant >= 11 && variant <= 14) {
+    if (Mp % NBM || Np % NBN || ka0 % BK || ka1 % BK || ka0 <= 0 || lda0 % 4 || (ka1 && lda1 % 4) || ldb % 4 ||
+        !epi_aligned(epi))
+        return fail(WD_ERR_SHAPE, "gemm_nt: unpadded or unaligned operand (Mp %d Np %d ka %d/%d)", Mp, Np, ka0, ka1);
+    if (split) {
         X6Params X{};
         X.a0 = a0; X.lda0 = lda0; X.ka0 = ka0; X.a1 = a1; X.lda1 = lda1; X.ka1 = ka1;
         X.bf = b; X.ldb = ldb;
         X.M = Mp; X.N = Np; X.epi = epi; X.tiles_n = Np / X6_BN;
-        const int bm = (variant == 12 || variant == 14) ? 128 : 64;
+        const int bm = Mp % 128 == 0 ? 128 : 64;
         X.tiles_m = Mp / bm;
         const dim3 grid(X.tiles_m * X.tiles_n), blk(4 * bm);
-        if (variant == 11) hipLaunchKernelGGL((gemm_x6_kernel<64, 32>), grid, blk, 0, st, X);
-        else if (variant == 12) hipLaunchKernelGGL((gemm_x6_kernel<128, 32>), grid, blk, 0, st, X);
-        else if (variant == 13) hipLaunchKernelGGL((gemm_x6_kernel<64, 64>), grid, blk, 0, st, X);
-        else hipLaunchKernelGGL((gemm_x6_kernel<128, 64>), grid, blk, 0, st, X);
+        if (bm == 128) hipLaunchKernelGGL((gemm_x6_kernel<128, 32>), grid, blk, 0, st, X);
+        else hipLaunchKernelGGL((gemm_x6_kernel<64, 32>), grid, blk, 0, st, X);
         WD_CHECK_LAUNCH("gemm_x6");
         return 0;
     }
     NtParams P{};
     P.a0 = a0; P.lda0 = lda0; P.ka0 = ka0; P.a1 = a1; P.lda1 = lda1; P.ka1 = ka1; P.b = b; P.ldb = ldb;
     P.M = Mp; P.N = Np; P.epi = epi;
-    // variants (tuning): 1 = 64x64 depth 1, 2 = 32x64 depth 1, 3 = 64x64 depth 2, 4 = 32x64 depth 2,
-    // 5 = 64x64 depth 2 with 64-wide K chunks (needs K segments aligned to 64, else falls back to 3)
-    const bool k64 = ka0 % 64 == 0 && ka1 % 64 == 0;
-    // 6 = B-panel-resident kernel (128x64 tiles, A streamed to registers; experimental, slower)
-    const int K = ka0 + ka1;
-    const int ldp = K + ((68 - K % 64) % 64);  // stride = 4 (mod 64): conflict-free ds_read_b128
-    const size_t panel_bytes = (size_t)64 * ldp * 4;
-    if (variant == 0) variant = 9;
-    if (variant == 6 && (panel_bytes > 160 * 1024 || Mp % 128)) variant = 3;
-    if (variant == 6) {
-        P.tiles_m = Mp / 128; P.tiles_n = Np / 64;
-        static bool lds_attr = false;  // idempotent: allow up to 160 KiB of dynamic LDS
-        if (!lds_attr) {
-            if (hipFuncSetAttribute((const void *)&gemm_panel_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024) != hipSuccess)
-                return fail(WD_ERR_ARG, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-            lds_attr = true;
-        }
-        hipLaunchKernelGGL((gemm_panel_kernel<4>), dim3(P.tiles_m * P.tiles_n), dim3(256), panel_bytes, st, P, ldp);
-        WD_CHECK_LAUNCH("gemm_panel");
-        return 0;
-    }
-    if (variant == 5 && !k64) variant = 3;
-    const dim3 blk64(64 * NWM * NWN);
-    // 9 = 64x64 with 16x16x4 MFMA (4 independent accumulators per wave)
-    if (variant == 9) {  // float4 epilogue: ld and the resid / Z / Y bases must be 16-byte aligned
-        const uintptr_t al = (uintptr_t)epi.Y | (uintptr_t)epi.Z | (uintptr_t)epi.resid | (uintptr_t)epi.bias;
-        if (epi.ld % 4 || al % 16) variant = 3;
-    }
-    if (variant == 9) {
-        P.tiles_m = Mp / 64; P.tiles_n = Np / 64;
-        hipLaunchKernelGGL((gemm_nt16_kernel<64, 64, 2, 2>), dim3(P.tiles_m * P.tiles_n), dim3(256), 0, st, P);
-        WD_CHECK_LAUNCH("gemm_nt16");
-        return 0;
-    }
-    // 7 = 128x64 (4 waves x 32x64, two accumulators per wave), 8 = 64x64 (2 waves x 32x64)
-    if (variant == 7 && Mp % 128 == 0) {
-        P.tiles_m = Mp / 128; P.tiles_n = Np / 64;
-        hipLaunchKernelGGL((gemm_nt_kernel<128, 64, 4, 1, 2, 32>), dim3(P.tiles_m * P.tiles_n), dim3(256), 0, st, P);
-        WD_CHECK_LAUNCH("gemm_nt 128x64");
-        return 0;
-    }
-    if (variant == 8 || variant == 7) {
-        P.tiles_m = Mp / 64; P.tiles_n = Np / 64;
-        hipLaunchKernelGGL((gemm_nt_kernel<64, 64, 2, 1, 2, 32>), dim3(P.tiles_m * P.tiles_n), dim3(128), 0, st, P);
-        WD_CHECK_LAUNCH("gemm_nt 64x64x2w");
-        return 0;
-    }
-    if (variant == 2 || variant == 4) {
-        P.tiles_m = Mp / 32; P.tiles_n = Np / 64;
-        const dim3 grid(P.tiles_m * P.tiles_n);
-        if (variant == 2) hipLaunchKernelGGL((gemm_nt_kernel<32, 64, 1, 2, 1, 32>), grid, dim3(128), 0, st, P);
-        else hipLaunchKernelGGL((gemm_nt_kernel<32, 64, 1, 2, 2, 32>), grid, dim3(128), 0, st, P);
-    } else {
-        P.tiles_m = Mp / NBM; P.tiles_n = Np / NBN;
-        const dim3 grid(P.tiles_m * P.tiles_n);
-        if (variant == 1) hipLaunchKernelGGL((gemm_nt_kernel<NBM, NBN, NWM, NWN, 1, 32>), grid, blk64, 0, st, P);
-        else if (variant == 5) hipLaunchKernelGGL((gemm_nt_kernel<NBM, NBN, NWM, NWN, 2, 64>), grid, blk64, 0, st, P);
-        else hipLaunchKernelGGL((gemm_nt_kernel<NBM, NBN, NWM, NWN, 2, 32>), grid, blk64, 0, st, P);
-    }
-    WD_CHECK_LAUNCH("gemm_nt");
+    P.tiles_m = Mp / 64; P.tiles_n = Np / 64;
+    hipLaunchKernelGGL((gemm_nt16_kernel<64, 64, 2, 2>), dim3(P.tiles_m * P.tiles_n), dim3(256), 0, st, P);
+    WD_CHECK_LAUNCH("gemm_nt16");
     return 0;
 }
 
 // C[Mp][Np] = epi([A0 | A1] B^T) with every operand in plane tiles (planes.hpp): A segment i is the
 // first ka_i columns of a [Mp][kp_i] plane-tile matrix, B a [Np][ka0 + ka1] one.
-bool x6g_eligible(const Epi &epi) {
-    const uintptr_t al = (uintptr_t)epi.Y | (uintptr_t)epi.Z | (uintptr_t)epi.resid | (uintptr_t)epi.bias;
-    return epi.ld % 4 == 0 && al % 16 == 0;
-}
+bool x6g_eligible(const Epi &epi) { return epi_aligned(epi); }
 
 int gemm_x6g(const void *a0, int kp0, int ka0, const void *a1, int kp1, int ka1, const void *b, int Mp, int Np,
              const Epi &epi, hipStream_t st) {
@@ -466,56 +391,6 @@ int slab_reduce(const TnPlan &tp, const float *slab, int n_rows, std::initialize
     if (db) cols += 1;  // the bias column after the segments
     hipLaunchKernelGGL(slab_reduce_kernel, dim3((cols + 63) / 64, (n_rows + 3) / 4), dim3(256), 0, st, R);
     WD_CHECK_LAUNCH("slab_reduce");
-    return 0;
-}
-
-FSeg fseg_dense(const float *src, int ld, int K, float *xout = nullptr, int ld_xout = 0) {
-    FSeg s{};
-    s.src = src; s.ld = ld; s.K = K; s.xout = xout; s.ld_xout = ld_xout;
-    return s;
-}
-
-FSeg fseg_gather(const float *src, int ld, int K, const WdCsr &csr, const int32_t *sym_rev, float *xout, int ld_xout) {
-    FSeg s{};
-    s.src = src; s.ld = ld; s.K = K; s.ptr = csr.ptr; s.idx = csr.idx; s.coef = csr.coef; s.sym_rev = sym_rev;
-    s.xout = xout; s.ld_xout = ld_xout;
-    return s;
-}
-
-constexpr size_t FUSED_LDS_MAX = 160 * 1024;
-
-size_t fused_lds_bytes(int K, int Np) { return (size_t)FP_ROWS * (std::max(K, Np) + 4) * 4; }
-
-// Can gemm_fused take this layer?  N = one wave per 64 columns (<= 512 threads), the panel fits
-// in LDS, float4-aligned epilogue.
-bool fused_eligible(int K, int Np, int ldb, const Epi &epi) {
-    const uintptr_t al = (uintptr_t)epi.Y | (uintptr_t)epi.Z | (uintptr_t)epi.resid | (uintptr_t)epi.bias;
-    return Np % 64 == 0 && Np <= 512 && K % BK == 0 && fused_lds_bytes(K, Np) <= FUSED_LDS_MAX && ldb % 4 == 0 &&
-           ldb == K && epi.ld % 4 == 0 && al % 16 == 0;
-}
-
-int gemm_fused(const FSeg &s0, const FSeg *s1, int rows, const float *b, int ldb, int Mp, int Np, const Epi &epi,
-               hipStream_t st) {
-    if (Mp <= 0) return 0;
-    FusedP P{};
-    P.seg[0] = s0; P.nseg = 1;
-    if (s1) { P.seg[1] = *s1; P.nseg = 2; }
-    const int K = s0.K + (s1 ? s1->K : 0);
-    if (Mp % FP_ROWS || !fused_eligible(K, Np, ldb, epi))
-        return fail(WD_ERR_SHAPE, "gemm_fused: ineligible shape (Mp %d Np %d K %d)", Mp, Np, K);
-    for (int i = 0; i < P.nseg; ++i)
-        if (P.seg[i].K % BK || P.seg[i].ld % 4 || (P.seg[i].xout && P.seg[i].ld_xout % 4))
-            return fail(WD_ERR_SHAPE, "gemm_fused: unaligned segment %d", i);
-    P.rows = rows; P.b = b; P.ldb = ldb; P.M = Mp; P.N = Np; P.epi = epi;
-    static bool lds_attr = false;
-    if (!lds_attr) {
-        if (hipFuncSetAttribute((const void *)gemm_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)FUSED_LDS_MAX) != hipSuccess)
-            return fail(WD_ERR_ARG, "hipFuncSetAttribute(gemm_fused_kernel) failed");
-        lds_attr = true;
-    }
-    hipLaunchKernelGGL(gemm_fused_kernel, dim3(Mp / FP_ROWS), dim3(Np), fused_lds_bytes(K, Np), st, P);
-    WD_CHECK_LAUNCH("gemm_fused");
     return 0;
 }
 
@@ -691,10 +566,8 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
     auto W = [&](size_t off) { return (const float *)(pk + off); };
     const int Hk = D.Hk;
 
-    const bool fuse = c->fuse_gather != 0;
-    const int var = c->gemm_variant ? c->gemm_variant : 10;
-    // plane-tile pipeline (D.x6): a GEMM without a plane copy of its A operand splits in the kernel
-    const int var_split = var == 10 ? 12 : var;
+    // without plane copies of its A operand a split-plane GEMM splits in the kernel (gemm_x6_kernel)
+    const bool split = !D.f32;
     const char *pkb = pk;
 
     if (D.blocked) {
@@ -761,12 +634,10 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
         const float *a = D.atom ? g->f_atoms : g->f_bonds;
         const int lda = D.atom ? g->ld_atoms : g->ld_bonds;
         const Epi e = epi_act(c->activation, p->prelu, W(PL.bi), nullptr, F(L.Z[0]), F(L.M[0]), Hk, c, 0);
-        if (fuse && fused_eligible(D.Kink, Hk, D.Kink, e))
-            WD_TRY(gemm_fused(fseg_dense(a, lda, D.Kink), nullptr, D.R, W(PL.WiF), D.Kink, D.Rp, Hk, e, st));
-        else if (D.x6 && g->f_bonds_x6 && x6g_eligible(e))
+        if (D.x6 && g->f_bonds_x6 && x6g_eligible(e))
             WD_TRY(gemm_x6g(g->f_bonds_x6, g->ld_bonds, D.Kink, nullptr, 0, 0, pkb + PL.WiX, D.Rp, Hk, e, st));
         else
-            WD_TRY(gemm_nt(a, lda, D.Kink, nullptr, 0, 0, W(PL.Wi), D.Kink, D.Rp, Hk, e, st, var_split));
+            WD_TRY(gemm_nt(a, lda, D.Kink, nullptr, 0, 0, W(PL.Wi), D.Kink, D.Rp, Hk, e, st, split));
     }
     // L1..T-1: message passing (mpn.py:100-124): X_t = gather(M_{t-1}) [| bond features], then
     // M_t = act(inp + X_t W_h^T (+ b_h))
@@ -779,16 +650,7 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
         const Epi e = epi_act(c->activation, p->prelu, W(PL.bh), F(L.Z[0]), Zt, F(L.M[next]), Hk, c, t);
         const int32_t *sym = D.undirected ? g->b2revb : nullptr;
         if (t == 1) WD_TRY(record_prof(c, 0, 0, st));  // one pair around all the layers
-        if (fuse && fused_eligible(D.ldx, Hk, D.ldx, e)) {
-            const FSeg s0 = fseg_gather(F(L.M[prev]), Hk, Hk, g->msg_gather, sym, D.save ? Xt : nullptr, D.ldx);
-            if (D.atom) {
-                const FSeg s1 = fseg_gather(g->f_bonds, g->ld_bonds, D.Fbk, g->bond_feat_gather, nullptr,
-                                           D.save ? Xt + Hk : nullptr, D.ldx);
-                WD_TRY(gemm_fused(s0, &s1, D.R, W(PL.WhF), D.ldx, D.Rp, Hk, e, st));
-            } else {
-                WD_TRY(gemm_fused(s0, nullptr, D.R, W(PL.WhF), D.ldx, D.Rp, Hk, e, st));
-            }
-        } else if (D.x6 && x6g_eligible(e)) {
+        if (D.x6 && x6g_eligible(e)) {
             // X_t as plane tiles (+ fp32 for the weight gradient when training)
             WD_TRY(gather8(F(L.M[prev]), Hk, Hk, g->msg_gather, sym, D.save ? Xt : nullptr, D.ldx, ws + L.Xp, Hk, 0,
                            D.R, D.Rp, st));
@@ -798,7 +660,7 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
             if (D.atom)
                 WD_TRY(gather8(g->f_bonds, g->ld_bonds, D.Fbk, g->bond_feat_gather, nullptr, Xt + Hk, D.ldx, nullptr, 0,
                                0, D.R, D.Rp, st));
-            WD_TRY(gemm_nt(Xt, D.ldx, D.ldx, nullptr, 0, 0, W(PL.Wh), D.ldx, D.Rp, Hk, e, st, var_split));
+            WD_TRY(gemm_nt(Xt, D.ldx, D.ldx, nullptr, 0, 0, W(PL.Wh), D.ldx, D.Rp, Hk, e, st, split));
         }
         if (t == D.T - 1) WD_TRY(record_prof(c, 0, 1, st));
         cur = next;
@@ -808,18 +670,14 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
     {
         const Epi e = epi_act(c->activation, p->prelu, W(PL.bo), nullptr, D.save ? F(L.Zo) : nullptr, F(L.h), Hk, c,
                               D.T);
-        if (fuse && fused_eligible(D.Ko, Hk, D.Ko, e)) {
-            const FSeg s0 = fseg_dense(g->f_atoms, g->ld_atoms, D.Fak);
-            const FSeg s1 = fseg_gather(M_last, Hk, Hk, g->atom_gather, nullptr, D.save ? F(L.A) : nullptr, Hk);
-            WD_TRY(gemm_fused(s0, &s1, D.Va, W(PL.WoF), D.Ko, D.Vap, Hk, e, st));
-        } else if (D.x6 && g->f_atoms_x6 && x6g_eligible(e)) {
+        if (D.x6 && g->f_atoms_x6 && x6g_eligible(e)) {
             WD_TRY(gather8(M_last, Hk, Hk, g->atom_gather, nullptr, D.save ? F(L.A) : nullptr, Hk, ws + L.Ap, Hk, 0,
                            D.Va, D.Vap, st));
             WD_TRY(gemm_x6g(g->f_atoms_x6, g->ld_atoms, D.Fak, ws + L.Ap, Hk, Hk, pkb + PL.WoX, D.Vap, Hk, e, st));
         } else {
             WD_TRY(gather8(M_last, Hk, Hk, g->atom_gather, nullptr, F(L.A), Hk, nullptr, 0, 0, D.Va, D.Vap, st));
             WD_TRY(gemm_nt(g->f_atoms, g->ld_atoms, D.Fak, F(L.A), Hk, Hk, W(PL.Wo), D.Ko, D.Vap, Hk, e, st,
-                           var_split));
+                           split));
         }
     }
     const float *hfin = F(L.h);
@@ -895,8 +753,7 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
     float *dH = S(Bl.dH);
     if (hipMemsetAsync(dH, 0, (size_t)D.Vap * ldH * 4, st) != hipSuccess) return fail(WD_ERR_ARG, "memset failed");
     if (D.B > 0) {
-        if (D.Hd > 4 * 256) return fail(WD_ERR_UNSUPPORTED, "readout backward: hidden + descriptors > 1024");
-        hipLaunchKernelGGL(readout_bwd_kernel, dim3(D.B), dim3(256), 0, st,
+        hipLaunchKernelGGL(readout_bwd_kernel, dim3(D.B, (D.Hd + RO_BWD_COLS - 1) / RO_BWD_COLS), dim3(256), 0, st,
                            readout_params(g, p, c, nullptr, ldH, D.Hd, nullptr), dout, dH);
         WD_CHECK_LAUNCH("readout_bwd");
     }
@@ -987,6 +844,20 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
         hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(256), 0, st, prelu_part, prelu_used, grads->prelu);
         WD_CHECK_LAUNCH("prelu sum");
     }
+    return 0;
+}
+
+int wdmpnn_saved_layout(const WdGraph *g, const WdParams *p, const WdConfig *c, WdSaved *out) {
+    Dims D;
+    WD_TRY(get_dims(g, p, c, D));
+    if (!out) return fail(WD_ERR_ARG, "null out");
+    if (!D.save) return fail(WD_ERR_ARG, "saved_layout needs save_for_backward = 1");
+    if (D.T > WDMPNN_MAX_SAVED_DEPTH) return fail(WD_ERR_UNSUPPORTED, "depth %d > %d", D.T, WDMPNN_MAX_SAVED_DEPTH);
+    const FwdLayout L = fwd_layout(D, p->packed == nullptr);
+    *out = WdSaved{};
+    out->depth = D.T; out->rows = D.R; out->atom_rows = D.Va; out->ld = D.Hk;
+    for (int t = 0; t < D.T; ++t) out->z[t] = L.Z[t];
+    out->zo = L.Zo;
     return 0;
 }
 
@@ -1088,6 +959,18 @@ int wdmpnn_index_select_rows(const float *src, int64_t n_src_rows, int64_t row_l
     hipLaunchKernelGGL(index_select_rows_kernel, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, src,
                        row_len, index, n_index, out);
     WD_CHECK_LAUNCH("index_select_rows");
+    return 0;
+}
+
+int wdmpnn_index_select_rows_backward(const float *grad, int64_t n_index, int64_t row_len, const int64_t *perm,
+                                      const int64_t *ptr, int64_t n_src_rows, float *dsrc, void *stream) {
+    if (n_index < 0 || row_len < 0 || n_src_rows < 0) return fail(WD_ERR_ARG, "negative size");
+    if (n_src_rows == 0 || row_len == 0) return 0;
+    if (!dsrc || !ptr || (n_index && (!grad || !perm))) return fail(WD_ERR_ARG, "null pointer");
+    const size_t total = (size_t)n_src_rows * row_len;
+    hipLaunchKernelGGL(index_select_rows_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, grad,
+                       row_len, perm, ptr, n_src_rows, dsrc);
+    WD_CHECK_LAUNCH("index_select_rows_backward");
     return 0;
 }
 

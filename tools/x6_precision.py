@@ -3,8 +3,8 @@
 For each configuration, prints max|out - ref64| / max|ref64| of the encoder output for
   ref32  the fp32 oracle (the reference's own arithmetic, CPU),
   f32    the HIP path with the f32-MFMA GEMM (WdConfig.gemm_variant 9),
-  x6g    the HIP path with the bf16x6 plane-tile pipeline (gemm_variant 10),
-  x6split  bf16x6 GEMMs splitting fp32 operands in the kernel (gemm_variant 12),
+  x6     the default HIP path: bf16x6 split-plane GEMMs (gemm_variant 0; molecule-blocked when the
+         batch allows it, operands split in the kernel in atom-message mode),
 so the split GEMM can be judged against the fp32 arithmetic it replaces."""
 import os
 import sys
@@ -43,7 +43,7 @@ for kind, b, H, T, extra in (('polymer', 64, 300, 3, {}), ('polymer', 64, 300, 3
             refs[dt] = mpn_ref.encoder_forward(p, g, args, dtype=dt).numpy()
     enc = enc.to(dev).eval()
     res = {'ref32': nw(refs[torch.float32], refs[torch.float64])}
-    for name, v in (('f32', 9), ('x6g', 10), ('x6split', 12)):
+    for name, v in (('f32', 9), ('x6', 0)):
         enc._gemm_variant = v
         with torch.no_grad():
             res[name] = nw(enc(g).cpu().numpy(), refs[torch.float64])
