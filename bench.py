@@ -324,7 +324,7 @@ def main():
         # Algorithmic FLOPs 2 E H^2 (W_h) + 2 E d H (weighted in-edge sums, d = CSR entries / row);
         # algorithmic bytes (fp32, each tensor once): read M_{t-1}, inp, W_h, CSR; write M_t.
         g0 = graphs[0]
-        nnz = float(g0.device_graph(device, False, get_bond_fdim()).host_csr["msg"].idx.shape[0])
+        nnz = float(g0.device_graph(device, False, get_bond_fdim()).nnz_msg)
         d_avg = nnz / max(g0.n_bonds - 1, 1)
         flops_launch = 2.0 * E_avg * H * H + 2.0 * E_avg * d_avg * H
         bytes_launch = 4.0 * (3 * E_avg * H + H * H + H) + 8.0 * E_avg * d_avg + 4.0 * E_avg

@@ -229,6 +229,60 @@ int wdmpnn_build_bond_features(const float *f_atoms, int32_t ld_atoms, int32_t a
                                const int32_t *b2a, const float *bond_tail, int32_t ld_tail, int32_t tail_dim,
                                int32_t rows, float *f_bonds, int32_t ld_bonds, void *stream);
 
+/* ------------------------------------------------------------------------------------------------
+ * Compact graphs: categorical codes on the wire, the whole WdGraph built on the device
+ * (SURVEY §8(f) row 2).
+ *
+ * The reference featurises every atom as six one-hot blocks + an aromatic bit + mass * 0.01
+ * (featurization.py:190-211, 133 columns) and every bond as 14 binary columns (featurization.py:229-250);
+ * each directed bond row is its source atom's row followed by the bond's (featurization.py:467-468,
+ * 545-546, 616-617), and MolGraph appends bonds in pairs b1 = a1 -> a2, b2 = a2 -> a1 = b2revb[b1]
+ * (featurization.py:469-480, 621-630), a2b[a] listing the bonds INTO a in creation order.  A batch in
+ * that form travels as
+ *   WdAtomCode [n_atoms]  the columns holding 1.0 (ascending, 0xFF = none) + the last column's value
+ *                         (mass * 0.01) + the atom weight (w_atoms, featurization.py:507);
+ *   WdBondPair [pairs]    molecule-local endpoints a1, a2, the 14 bond columns as a bit mask (bit k =
+ *                         column atom_fdim + k) and the two directed weights (w_bonds, :628);
+ *   mols [n_mols][4]      {atom_start, n_atoms, bond_start, n_bonds} (natural ids, pad row 0 included
+ *                         in the numbering like BatchMolGraph.a_scope / b_scope) + xn [n_mols];
+ *   blocks [n_blocks][8]  the molecule blocks of the fused forward (WdGraph.blocks) + block_nnz
+ *                         [n_blocks][2] = {first msg_gather entry, first atom_gather entry} of the block;
+ * about 14 bytes per directed edge, against ~450 for the fp32 rows + gather lists.  wdmpnn_build_graph
+ * expands it on the device into every WdGraph array (fp32 feature rows, plane tiles, gather lists and
+ * their transposes, ELL rows, block maps) with the same values and entry order as the host packer
+ * (chemprop_amd.featurization.BatchMolGraph.device_graph): one launch.  Requires every molecule to fit
+ * one block (<= 128 directed bonds, <= 64 atoms); atom_fdim <= 255 with the code's columns < atom_fdim - 1.
+ * ------------------------------------------------------------------------------------------------ */
+typedef struct WdAtomCode {
+    uint8_t col[8];         /* columns of f_atoms holding 1.0, ascending; 0xFF = unused slot     */
+    float last;             /* f_atoms[atom_fdim - 1] (mass * 0.01)                              */
+    float w;                /* w_atoms                                                           */
+} WdAtomCode;
+typedef struct WdBondPair {
+    uint16_t a1, a2;        /* molecule-local atom ids: b1 = a1 -> a2, b2 = a2 -> a1             */
+    uint16_t tail;          /* bond feature columns as bits (bit k = column atom_fdim + k)       */
+    uint16_t reserved;
+    float w12, w21;         /* w_bonds[b1], w_bonds[b2]                                          */
+} WdBondPair;
+typedef struct WdCompact {
+    int32_t n_mols, n_atoms, n_bonds, n_blocks;   /* n_atoms / n_bonds include the pad row        */
+    int32_t atom_fdim, bond_fdim;                 /* 133 / 147 by default (bond_fdim - atom_fdim <= 16) */
+    int32_t nnz_msg, nnz_agg;                     /* total entries of msg_gather / atom_gather    */
+    const int32_t *mols;                          /* [n_mols][4]                                  */
+    const float *xn;                              /* [n_mols] degree_of_polym                     */
+    const WdAtomCode *atoms;                      /* [n_atoms], row 0 = pad (no columns, 0, 0)    */
+    const WdBondPair *pairs;                      /* [(n_bonds - 1) / 2]                          */
+    const int32_t *blocks;                        /* [n_blocks][8]                                */
+    const int32_t *block_nnz;                     /* [n_blocks][2]                                */
+} WdCompact;
+
+/* Device bytes of the graph wdmpnn_build_graph writes (one buffer, caller-allocated). */
+int wdmpnn_graph_bytes(const WdCompact *c, size_t *bytes);
+/* Build the WdGraph of a compact batch into `buffer` (device, >= wdmpnn_graph_bytes, 256-byte aligned)
+ * on `stream`; *g receives the struct (bond-message mode, blocks set, no descriptors) whose pointers
+ * point into `buffer`.  All arrays of c are device pointers. */
+int wdmpnn_build_graph(const WdCompact *c, void *buffer, size_t bytes, WdGraph *g, void *stream);
+
 /* index_select_ND (nn_utils.py:50-67): out[i, :] = src[index[i], :], row_len floats per row.
  * Indices are int64 like the reference's LongTensor; out-of-range indices are an error checked by
  * the caller (the kernel clamps nothing and reads src[index]). */

@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace
                     'wdmpnn_event_pool_elapsed_ms', 'wdmpnn_packed_params_bytes', 'wdmpnn_pack_params',
                     'wdmpnn_plane_bytes', 'wdmpnn_split_planes', 'wdmpnn_split_planes_rows',
                     'wdmpnn_build_bond_features', 'wdmpnn_index_select_rows_backward',
-                    'wdmpnn_saved_layout')
+                    'wdmpnn_saved_layout', 'wdmpnn_graph_bytes', 'wdmpnn_build_graph')
 
 
 class WdCsr(Structure):
@@ -61,6 +61,13 @@ class WdConfig(Structure):
                 ('aggregation_norm', c_float), ('dropout', c_float), ('seed', c_uint64),
                 ('save_for_backward', c_int32), ('prof_slot', c_int32), ('prof_pool', c_void_p),
                 ('gemm_variant', c_int32)]
+
+
+class WdCompact(Structure):
+    _fields_ = [('n_mols', c_int32), ('n_atoms', c_int32), ('n_bonds', c_int32), ('n_blocks', c_int32),
+                ('atom_fdim', c_int32), ('bond_fdim', c_int32), ('nnz_msg', c_int32), ('nnz_agg', c_int32),
+                ('mols', c_void_p), ('xn', c_void_p), ('atoms', c_void_p), ('pairs', c_void_p), ('blocks', c_void_p),
+                ('block_nnz', c_void_p)]
 
 
 class WdSaved(Structure):
@@ -105,6 +112,8 @@ def lib() -> ctypes.CDLL:
     L.wdmpnn_pack_params.argtypes = [POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig), c_void_p, c_size_t,
                                      c_void_p]
     L.wdmpnn_saved_layout.argtypes = [POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig), POINTER(WdSaved)]
+    L.wdmpnn_graph_bytes.argtypes = [POINTER(WdCompact), POINTER(c_size_t)]
+    L.wdmpnn_build_graph.argtypes = [POINTER(WdCompact), c_void_p, c_size_t, POINTER(WdGraph), c_void_p]
     L.wdmpnn_plane_bytes.argtypes = [c_int32, c_int32, POINTER(c_size_t)]
     L.wdmpnn_split_planes.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_size_t, c_void_p]
     L.wdmpnn_split_planes_rows.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_void_p, c_size_t,

@@ -1,0 +1,285 @@
+// graph_build.hpp — the whole device graph (WdGraph) of a compact batch, built on the GPU in one launch
+// (format: include/wdmpnn.h "Compact graphs").
+//
+// One workgroup per molecule block (<= 128 directed bonds, <= 64 atoms, <= 64 molecules: every index of
+// the block is block-local, so the in-lists are built in LDS) plus one workgroup for the pad rows.
+// It reproduces, value for value and entry for entry, what the host path builds:
+//   * feature rows: f_atoms[a] = one-hot columns from the atom code + the last column's value
+//     (featurization.py:190-211), f_bonds[b] = f_atoms[src(b)] ‖ bond columns (featurization.py:467-468,
+//     545-546, 616-617), fp32 with 16-byte aligned rows, and their bf16x3 plane tiles (planes.hpp):
+//     natural rows (BR 64) and, for atoms, the molecule-blocked layout of the fused W_o;
+//   * in(a) = the bonds into a in creation order (= a2b[a], featurization.py:471-476, 624-627);
+//   * msg_gather row b (mpn.py:112-120): j in in(src(b)), coefficient w_j - [j == rev(b)] (w - 1 is a
+//     single fp32 rounding, as the host's double-then-float), zero coefficients dropped;
+//     atom_gather row a (mpn.py:126-131): j in in(a), coefficient w_j != 0;
+//     their transposes (the backward's gathers): msg_gather_t row j = the rows b with src(b) = dst(j) in
+//     increasing b, atom_gather_t row j = (dst(j), w_j);
+//   * the ELL-8 rows, the block maps, b2revb, w_atoms and the molecule scope arrays.
+// Pair structure: bond ids 1 + 2p and 2 + 2p are pair p's b1 = a1 -> a2 and b2 = a2 -> a1 (pad bond 0),
+// so every molecule's first bond id is odd and a block-local bond index lb has rev(lb) = lb ^ 1.
+#pragma once
+#include "planes.hpp"
+#include "wdmpnn.h"
+
+namespace wd {
+
+constexpr int GB_BONDS = 128, GB_ATOMS = 64, GB_MOLS = 64, GB_ELLW = 8, GB_CSR_PAD = 8;
+
+struct GraphBuildP {
+    WdCompact c;
+    int Fa, Fb, lda, ldb, Vap, Rbp;
+    float *f_atoms, *f_bonds;
+    uint8_t *fa_x6, *fb_x6, *fa_blk_x6;
+    float *w_atoms, *xn;
+    int32_t *mol_start, *mol_size, *b2revb, *blocks, *bond_blk_row, *atom_blk_row;
+    uint8_t *msg_ell_idx, *agg_ell_idx;
+    float *msg_ell_coef, *agg_ell_coef;
+    int32_t *msg_ptr, *msg_idx, *agg_ptr, *agg_idx, *msgt_ptr, *msgt_idx, *aggt_ptr, *aggt_idx;
+    float *msg_coef, *agg_coef, *msgt_coef, *aggt_coef;
+};
+
+// value of f_atoms column c for an atom code (c < Fa)
+__device__ __forceinline__ float code_value(const WdAtomCode &a, int c, int Fa) {
+    if (c == Fa - 1) return a.last;
+    bool hit = false;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) hit |= a.col[k] == c;
+    return hit ? 1.f : 0.f;
+}
+
+// 8 consecutive columns c0 .. c0 + 7 of a natural fp32 row + its plane tiles (BR 64)
+__device__ __forceinline__ void put_row8(float *row_f32, uint8_t *planes, int ld, int r, int c0, const float (&v)[8]) {
+    const float4 lo = make_float4(v[0], v[1], v[2], v[3]), hi = make_float4(v[4], v[5], v[6], v[7]);
+    st4(row_f32 + c0, lo);
+    st4(row_f32 + c0 + 4, hi);
+    x6_store8<64>(planes, ld, r, c0, lo, hi);
+}
+
+__global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
+    const int tid = threadIdx.x, k = blockIdx.x;
+    const WdCompact &C = P.c;
+    const int Fa = P.Fa, Fb = P.Fb, UA = P.lda / 8, UB = P.ldb / 8;
+    if (k == C.n_blocks) {  // pad rows: atom / bond row 0, the rows up to the padded extents, CSR heads and tails
+        const int V1 = C.n_atoms, E1 = C.n_bonds;
+        const int na_pad = 1 + (P.Vap - V1), nb_pad = 1 + (P.Rbp - E1);
+        const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int u = tid; u < na_pad * UA; u += 256) {
+            const int i = u / UA, r = i == 0 ? 0 : V1 + i - 1, c0 = (u % UA) * 8;
+            put_row8(P.f_atoms + (size_t)r * P.lda, P.fa_x6, P.lda, r, c0, z);
+        }
+        for (int u = tid; u < nb_pad * UB; u += 256) {
+            const int i = u / UB, r = i == 0 ? 0 : E1 + i - 1, c0 = (u % UB) * 8;
+            put_row8(P.f_bonds + (size_t)r * P.ldb, P.fb_x6, P.ldb, r, c0, z);
+        }
+        for (int i = tid; i < na_pad; i += 256) {
+            const int r = i == 0 ? 0 : V1 + i - 1;
+            P.atom_blk_row[r] = -1;
+            for (int s = 0; s < GB_ELLW; ++s) { P.agg_ell_idx[GB_ELLW * r + s] = 0; P.agg_ell_coef[GB_ELLW * r + s] = 0.f; }
+        }
+        for (int i = tid; i < nb_pad; i += 256) {
+            const int r = i == 0 ? 0 : E1 + i - 1;
+            P.bond_blk_row[r] = -1;
+            for (int s = 0; s < GB_ELLW; ++s) { P.msg_ell_idx[GB_ELLW * r + s] = 0; P.msg_ell_coef[GB_ELLW * r + s] = 0.f; }
+        }
+        if (tid < 2) {  // row 0 (pad atom / bond) has no entries
+            P.msg_ptr[tid] = 0; P.msgt_ptr[tid] = 0; P.aggt_ptr[tid] = 0; P.agg_ptr[tid] = 0;
+        }
+        if (tid == 0) { P.w_atoms[0] = 0.f; P.b2revb[0] = 0; }
+        if (tid < GB_CSR_PAD) {  // readable dummy entries past the end (WdCsr)
+            P.msg_idx[C.nnz_msg + tid] = 0; P.msg_coef[C.nnz_msg + tid] = 0.f;
+            P.msgt_idx[C.nnz_msg + tid] = 0; P.msgt_coef[C.nnz_msg + tid] = 0.f;
+            P.agg_idx[C.nnz_agg + tid] = 0; P.agg_coef[C.nnz_agg + tid] = 0.f;
+            P.aggt_idx[C.nnz_agg + tid] = 0; P.aggt_coef[C.nnz_agg + tid] = 0.f;
+        }
+        return;
+    }
+
+    __shared__ int s_blk[8];
+    __shared__ int s_mas[GB_MOLS], s_mbs[GB_MOLS];
+    __shared__ WdAtomCode s_code[GB_ATOMS];
+    __shared__ uint8_t s_src[GB_BONDS], s_dst[GB_BONDS], s_in[GB_BONDS];
+    __shared__ uint16_t s_tail[GB_BONDS];
+    __shared__ float s_w[GB_BONDS];
+    __shared__ int s_deg[GB_ATOMS], s_start[GB_ATOMS + 1];
+    __shared__ int s_pm[GB_BONDS + 1], s_pt[GB_BONDS + 1], s_pg[GB_BONDS + 1], s_pa[GB_ATOMS + 1];
+    __shared__ int s_off[2];
+    if (tid < 8) s_blk[tid] = C.blocks[8 * k + tid];
+    if (tid < 2) s_off[tid] = C.block_nnz[2 * k + tid];
+    __syncthreads();
+    const int bs = s_blk[0], bn = s_blk[1], as = s_blk[2], an = s_blk[3], ml = s_blk[4], nm = s_blk[5] - s_blk[4];
+    if (bn > GB_BONDS || an > GB_ATOMS || nm > GB_MOLS || nm < 0) return;  // the host plan never does this
+    if (tid < nm) {
+        s_mas[tid] = C.mols[4 * (ml + tid)];
+        s_mbs[tid] = C.mols[4 * (ml + tid) + 2];
+        P.mol_start[ml + tid] = C.mols[4 * (ml + tid)];
+        P.mol_size[ml + tid] = C.mols[4 * (ml + tid) + 1];
+        P.xn[ml + tid] = C.xn[ml + tid];
+    }
+    if (tid < an) {
+        s_code[tid] = C.atoms[as + tid];
+        P.w_atoms[as + tid] = s_code[tid].w;
+        P.atom_blk_row[as + tid] = GB_ATOMS * k + tid;
+    }
+    if (tid < 8) P.blocks[8 * k + tid] = s_blk[tid];
+    __syncthreads();
+    if (tid < bn) {  // endpoints of bond b = bs + tid
+        const int b = bs + tid;
+        int lo = 0, hi = nm - 1;  // the molecule: last one whose first bond is <= b
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_mbs[mid] <= b) lo = mid; else hi = mid - 1;
+        }
+        const int p = (b - 1) >> 1, dir = (b - 1) & 1;
+        const WdBondPair q = C.pairs[p];
+        const int l1 = s_mas[lo] + q.a1 - as, l2 = s_mas[lo] + q.a2 - as;
+        s_src[tid] = (uint8_t)(dir ? l2 : l1);
+        s_dst[tid] = (uint8_t)(dir ? l1 : l2);
+        s_w[tid] = dir ? q.w21 : q.w12;
+        s_tail[tid] = q.tail;
+        P.b2revb[b] = dir ? b - 1 : b + 1;
+        P.bond_blk_row[b] = GB_BONDS * k + tid;
+    }
+    __syncthreads();
+    if (tid < an) {  // in(a): bonds into a in creation order
+        int d = 0;
+        for (int lb = 0; lb < bn; ++lb) d += s_dst[lb] == tid;
+        s_deg[tid] = d;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int s = 0;
+        for (int a = 0; a < an; ++a) { s_start[a] = s; s += s_deg[a]; }
+        s_start[an] = s;
+    }
+    __syncthreads();
+    if (tid < an) {
+        int o = s_start[tid];
+        for (int lb = 0; lb < bn; ++lb)
+            if (s_dst[lb] == tid) s_in[o++] = (uint8_t)lb;
+    }
+    __syncthreads();
+    // entry counts: msg row, msg_t row, agg_t row (bonds); agg row (atoms)
+    if (tid < bn) {
+        const int s = s_src[tid], rev = tid ^ 1;
+        int cm = 0;
+        for (int e = s_start[s]; e < s_start[s + 1]; ++e) {
+            const int j = s_in[e];
+            cm += (j == rev ? s_w[j] - 1.0f : s_w[j]) != 0.f;
+        }
+        int ct = 0;
+        for (int lb = 0; lb < bn; ++lb)
+            if (s_src[lb] == s_dst[tid]) ct += (tid == (lb ^ 1) ? s_w[tid] - 1.0f : s_w[tid]) != 0.f;
+        s_pm[tid + 1] = cm;
+        s_pt[tid + 1] = ct;
+        s_pg[tid + 1] = s_w[tid] != 0.f;
+    }
+    if (tid < an) {
+        int ca = 0;
+        for (int e = s_start[tid]; e < s_start[tid + 1]; ++e) ca += s_w[s_in[e]] != 0.f;
+        s_pa[tid + 1] = ca;
+    }
+    __syncthreads();
+    if (tid == 0) { s_pm[0] = 0; for (int i = 0; i < bn; ++i) s_pm[i + 1] += s_pm[i]; }
+    if (tid == 64) { s_pt[0] = 0; for (int i = 0; i < bn; ++i) s_pt[i + 1] += s_pt[i]; }
+    if (tid == 128) { s_pg[0] = 0; for (int i = 0; i < bn; ++i) s_pg[i + 1] += s_pg[i]; }
+    if (tid == 192) { s_pa[0] = 0; for (int i = 0; i < an; ++i) s_pa[i + 1] += s_pa[i]; }
+    __syncthreads();
+    const int om = s_off[0], oa = s_off[1];
+    if (tid < bn) {
+        const int b = bs + tid, s = s_src[tid], rev = tid ^ 1;
+        // msg_gather row b + its ELL-8 row
+        int o = om + s_pm[tid], n = 0;
+        uint8_t eidx[GB_ELLW];
+        float ecoef[GB_ELLW];
+#pragma unroll
+        for (int q = 0; q < GB_ELLW; ++q) { eidx[q] = 0; ecoef[q] = 0.f; }
+        for (int e = s_start[s]; e < s_start[s + 1]; ++e) {
+            const int j = s_in[e];
+            const float c = j == rev ? s_w[j] - 1.0f : s_w[j];
+            if (c == 0.f) continue;
+            P.msg_idx[o] = bs + j;
+            P.msg_coef[o] = c;
+            ++o;
+            if (n < GB_ELLW) { eidx[n] = (uint8_t)j; ecoef[n] = c; }
+            ++n;
+        }
+        P.msg_ptr[b + 1] = om + s_pm[tid + 1];
+        if (n > GB_ELLW) eidx[GB_ELLW - 1] |= 0x80;
+#pragma unroll
+        for (int q = 0; q < GB_ELLW; ++q) {
+            P.msg_ell_idx[(size_t)GB_ELLW * b + q] = eidx[q];
+            P.msg_ell_coef[(size_t)GB_ELLW * b + q] = ecoef[q];
+        }
+        // msg_gather_t row b: rows lb with src(lb) = dst(b), in increasing lb
+        o = om + s_pt[tid];
+        for (int lb = 0; lb < bn; ++lb) {
+            if (s_src[lb] != s_dst[tid]) continue;
+            const float c = tid == (lb ^ 1) ? s_w[tid] - 1.0f : s_w[tid];
+            if (c == 0.f) continue;
+            P.msgt_idx[o] = bs + lb;
+            P.msgt_coef[o] = c;
+            ++o;
+        }
+        P.msgt_ptr[b + 1] = om + s_pt[tid + 1];
+        // atom_gather_t row b: (dst(b), w_b)
+        if (s_w[tid] != 0.f) {
+            P.aggt_idx[oa + s_pg[tid]] = as + s_dst[tid];
+            P.aggt_coef[oa + s_pg[tid]] = s_w[tid];
+        }
+        P.aggt_ptr[b + 1] = oa + s_pg[tid + 1];
+    }
+    if (tid < an) {  // atom_gather row a + its ELL-8 row
+        const int a = as + tid;
+        int o = oa + s_pa[tid], n = 0;
+        uint8_t eidx[GB_ELLW];
+        float ecoef[GB_ELLW];
+#pragma unroll
+        for (int q = 0; q < GB_ELLW; ++q) { eidx[q] = 0; ecoef[q] = 0.f; }
+        for (int e = s_start[tid]; e < s_start[tid + 1]; ++e) {
+            const int j = s_in[e];
+            if (s_w[j] == 0.f) continue;
+            P.agg_idx[o] = bs + j;
+            P.agg_coef[o] = s_w[j];
+            ++o;
+            if (n < GB_ELLW) { eidx[n] = (uint8_t)j; ecoef[n] = s_w[j]; }
+            ++n;
+        }
+        P.agg_ptr[a + 1] = oa + s_pa[tid + 1];
+        if (n > GB_ELLW) eidx[GB_ELLW - 1] |= 0x80;
+#pragma unroll
+        for (int q = 0; q < GB_ELLW; ++q) {
+            P.agg_ell_idx[(size_t)GB_ELLW * a + q] = eidx[q];
+            P.agg_ell_coef[(size_t)GB_ELLW * a + q] = ecoef[q];
+        }
+    }
+    // feature rows (8 columns per thread-step): atoms natural + blocked (zero rows past an), bonds natural
+    for (int u = tid; u < GB_ATOMS * UA; u += 256) {
+        const int la = u / UA, c0 = (u % UA) * 8;
+        float v[8];
+        if (la < an) {
+            const WdAtomCode &cd = s_code[la];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = c0 + q < Fa ? code_value(cd, c0 + q, Fa) : 0.f;
+            put_row8(P.f_atoms + (size_t)(as + la) * P.lda, P.fa_x6, P.lda, as + la, c0, v);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = 0.f;
+        }
+        x6_store8<64>(P.fa_blk_x6, P.lda, GB_ATOMS * k + la, c0, make_float4(v[0], v[1], v[2], v[3]),
+                      make_float4(v[4], v[5], v[6], v[7]));
+    }
+    for (int u = tid; u < bn * UB; u += 256) {
+        const int lb = u / UB, c0 = (u % UB) * 8;
+        const WdAtomCode &cd = s_code[s_src[lb]];
+        const int tail = s_tail[lb];
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int c = c0 + q;
+            v[q] = c < Fa ? code_value(cd, c, Fa) : (c < Fb ? (float)((tail >> (c - Fa)) & 1) : 0.f);
+        }
+        put_row8(P.f_bonds + (size_t)(bs + lb) * P.ldb, P.fb_x6, P.ldb, bs + lb, c0, v);
+    }
+}
+
+}  // namespace wd

@@ -24,6 +24,8 @@
 #include <type_traits>
 #include <vector>
 
+#include "compact.hpp"
+
 namespace {
 
 struct PyErrAlready {};  // a Python exception is set; unwind to the entry point
@@ -504,6 +506,236 @@ PyObject *ell(PyObject *, PyObject *args) {
     return nullptr;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Compact graphs (compact.hpp, include/wdmpnn.h): encode / decode / plan / generate / stage
+// ---------------------------------------------------------------------------------------------
+PyObject *bytes_of(const void *d, size_t n) {
+    PyObject *b = PyByteArray_FromStringAndSize(static_cast<const char *>(d), (Py_ssize_t)n);
+    if (!b) throw PyErrAlready{};
+    return b;
+}
+
+PyObject *batch_tuple(const compact::Batch &c) {
+    PyObject *t = PyTuple_New(4);
+    if (!t) throw PyErrAlready{};
+    const void *d[4] = {c.mols.data(), c.xn.data(), c.atoms.data(), c.pairs.data()};
+    const size_t n[4] = {c.mols.size() * 4, c.xn.size() * 4, c.atoms.size() * sizeof(WdAtomCode),
+                         c.pairs.size() * sizeof(WdBondPair)};
+    for (int k = 0; k < 4; ++k) {
+        PyObject *b;
+        try { b = bytes_of(d[k], n[k]); } catch (...) { Py_DECREF(t); throw; }
+        PyTuple_SET_ITEM(t, k, b);
+    }
+    return t;
+}
+
+// (mols, xn, atoms, pairs) buffers -> Batch
+void batch_from(PyObject *o_mols, PyObject *o_xn, PyObject *o_atoms, PyObject *o_pairs, int fa, int fb,
+                compact::Batch &c) {
+    Buf m(o_mols), x(o_xn), a(o_atoms), q(o_pairs);
+    if (!m.ok || !x.ok || !a.ok || !q.ok) fail(PyExc_TypeError, "compact arrays must support the buffer protocol");
+    if (m.b.len % 16 || x.b.len % 4 || a.b.len % (Py_ssize_t)sizeof(WdAtomCode) ||
+        q.b.len % (Py_ssize_t)sizeof(WdBondPair) || m.b.len / 16 != x.b.len / 4 || a.b.len == 0)
+        fail(PyExc_ValueError, "compact arrays have inconsistent sizes");
+    c = compact::Batch{};
+    c.fa = fa; c.fb = fb;
+    c.mols.resize((size_t)m.b.len / 4);
+    std::memcpy(c.mols.data(), m.b.buf, (size_t)m.b.len);
+    c.xn.resize((size_t)x.b.len / 4);
+    std::memcpy(c.xn.data(), x.b.buf, (size_t)x.b.len);
+    c.atoms.resize((size_t)a.b.len / sizeof(WdAtomCode));
+    std::memcpy(c.atoms.data(), a.b.buf, (size_t)a.b.len);
+    c.pairs.resize((size_t)q.b.len / sizeof(WdBondPair));
+    std::memcpy(c.pairs.data(), q.b.buf, (size_t)q.b.len);
+    // structural checks (the device build trusts these)
+    int64_t ao = 1, bo = 1;
+    for (int i = 0; i < c.n_mols(); ++i) {
+        const int32_t *r = &c.mols[(size_t)4 * i];
+        if (r[0] != ao || r[2] != bo || r[1] < 0 || r[3] < 0 || r[3] % 2)
+            fail(PyExc_ValueError, "compact molecules are not contiguous in the reference's numbering");
+        for (int64_t lb = 0; lb < r[3]; lb += 2) {
+            const WdBondPair &p = c.pairs[(size_t)((bo + lb - 1) / 2)];
+            if (p.a1 >= r[1] || p.a2 >= r[1]) fail(PyExc_ValueError, "compact bond endpoint outside its molecule");
+        }
+        ao += r[1];
+        bo += r[3];
+    }
+    if (ao != c.n_atoms() || bo != c.n_bonds()) fail(PyExc_ValueError, "compact molecules do not cover the tables");
+}
+
+// compact_encode(f_atoms, tail, w_atoms, w_bonds, b2a, b2revb, deg, in_idx, na, nb, xn(float64), fa, tail_w)
+// -> (mols, xn, atoms, pairs) or (None, reason); tail = the bond columns [E+1][tail_w] or whole f_bonds rows
+// [E+1][fa + tail_w] (then checked to start with their source atom's row)
+PyObject *compact_encode(PyObject *, PyObject *args) {
+    PyObject *o[11];
+    int fa, tw;
+    if (!PyArg_ParseTuple(args, "OOOOOOOOOOOii", &o[0], &o[1], &o[2], &o[3], &o[4], &o[5], &o[6], &o[7], &o[8], &o[9],
+                          &o[10], &fa, &tw))
+        return nullptr;
+    try {
+        In<float> f_atoms(o[0], "f", "f_atoms"), tail(o[1], "f", "tail"), w_atoms(o[2], "f", "w_atoms"),
+            w_bonds(o[3], "f", "w_bonds");
+        In<int64_t> b2a(o[4], "i", "b2a"), rev(o[5], "i", "b2revb"), deg(o[6], "i", "deg"), in(o[7], "i", "in_idx"),
+            na(o[8], "i", "na"), nb(o[9], "i", "nb");
+        Buf xb(o[10]);
+        if (!xb.ok || xb.b.itemsize != 8) fail(PyExc_TypeError, "xn must be a float64 buffer");
+        const int64_t B = na.n;
+        if (nb.n != B || xb.b.len / 8 != B) fail(PyExc_ValueError, "per-molecule arrays differ in length");
+        int64_t V = 0, E = 0;
+        for (int64_t i = 0; i < B; ++i) { V += na.p[i]; E += nb.p[i]; }
+        const int64_t row_w = E + 1 > 0 ? tail.n / (E + 1) : tw;
+        if (f_atoms.n != (V + 1) * fa || tail.n != (E + 1) * row_w || w_atoms.n != V + 1 || w_bonds.n != E + 1 ||
+            b2a.n != E + 1 || rev.n != E + 1 || deg.n != V + 1 || in.n != E)
+            fail(PyExc_ValueError, "compact_encode: array sizes do not match the molecule counts");
+        compact::Batch c;
+        std::string why;
+        if (!compact::encode(fa, tw, (int)row_w, f_atoms.p, tail.p, w_atoms.p, w_bonds.p, b2a.p, rev.p, deg.p, in.p, na.p, nb.p,
+                             static_cast<const double *>(xb.b.buf), B, c, why)) {
+            PyObject *s = PyUnicode_FromString(why.c_str());
+            if (!s) throw PyErrAlready{};
+            PyObject *r = PyTuple_Pack(2, Py_None, s);
+            Py_DECREF(s);
+            return r;
+        }
+        return batch_tuple(c);
+    } catch (const PyErrAlready &) {
+    } catch (const std::exception &e) {
+        PyErr_SetString(PyExc_RuntimeError, e.what());
+    }
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_RuntimeError, "compact_encode failed");
+    return nullptr;
+}
+
+// compact_decode(mols, xn, atoms, pairs, fa, fb) -> pack()'s 10 outputs in tail mode
+PyObject *compact_decode(PyObject *, PyObject *args) {
+    PyObject *o[4];
+    int fa, fb;
+    if (!PyArg_ParseTuple(args, "OOOOii", &o[0], &o[1], &o[2], &o[3], &fa, &fb)) return nullptr;
+    try {
+        compact::Batch c;
+        batch_from(o[0], o[1], o[2], o[3], fa, fb, c);
+        compact::Dense d;
+        compact::decode(c, d);
+        PyObject *t = PyTuple_New(10);
+        if (!t) throw PyErrAlready{};
+        const void *ptr[10] = {d.f_atoms.data(), d.tail.data(), d.w_atoms.data(), d.w_bonds.data(), d.b2a.data(),
+                               d.b2revb.data(), d.deg.data(), d.in_idx.data(), d.na.data(), d.nb.data()};
+        const size_t n[10] = {d.f_atoms.size() * 4, d.tail.size() * 4, d.w_atoms.size() * 4, d.w_bonds.size() * 4,
+                              d.b2a.size() * 8, d.b2revb.size() * 8, d.deg.size() * 8, d.in_idx.size() * 8,
+                              d.na.size() * 8, d.nb.size() * 8};
+        for (int k = 0; k < 10; ++k) {
+            PyObject *b;
+            try { b = bytes_of(ptr[k], n[k]); } catch (...) { Py_DECREF(t); throw; }
+            PyTuple_SET_ITEM(t, k, b);
+        }
+        return t;
+    } catch (const PyErrAlready &) {
+    } catch (const std::exception &e) {
+        PyErr_SetString(PyExc_RuntimeError, e.what());
+    }
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_RuntimeError, "compact_decode failed");
+    return nullptr;
+}
+
+// compact_generate(kind, B, seed) -> (mols, xn, atoms, pairs); kind 0 polymer, 1 qm9, 2 zinc
+PyObject *compact_generate(PyObject *, PyObject *args) {
+    int kind, B;
+    unsigned long long seed;
+    if (!PyArg_ParseTuple(args, "iiK", &kind, &B, &seed)) return nullptr;
+    if (kind < 0 || kind > 2 || B < 0) {
+        PyErr_SetString(PyExc_ValueError, "kind in {0, 1, 2}, B >= 0");
+        return nullptr;
+    }
+    try {
+        compact::Batch c;
+        Py_BEGIN_ALLOW_THREADS
+        compact::generate(kind, B, seed, c);
+        Py_END_ALLOW_THREADS
+        return batch_tuple(c);
+    } catch (const PyErrAlready &) {
+    } catch (const std::exception &e) {
+        PyErr_SetString(PyExc_RuntimeError, e.what());
+    }
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_RuntimeError, "compact_generate failed");
+    return nullptr;
+}
+
+PyObject *stage_result(const compact::Batch &c, const compact::Plan &p, const compact::Staged &s, bool copied) {
+    return Py_BuildValue("(O(iiiiLL)(nnnnnn)n)", copied ? Py_True : Py_False, c.n_mols(), c.n_atoms(), c.n_bonds(),
+                         p.n_blocks(), (long long)p.nnz_msg, (long long)p.nnz_agg, (Py_ssize_t)s.off[0],
+                         (Py_ssize_t)s.off[1], (Py_ssize_t)s.off[2], (Py_ssize_t)s.off[3], (Py_ssize_t)s.off[4],
+                         (Py_ssize_t)s.off[5], (Py_ssize_t)s.total);
+}
+
+// compact_stage(mols, xn, atoms, pairs, fa, fb, target_blocks, dst_address, capacity)
+// -> None (a molecule exceeds a block) | (copied, (n_mols, n_atoms, n_bonds, n_blocks, nnz_msg, nnz_agg),
+//    offsets[6], total): the plan and the upload image written to dst (host memory, e.g. pinned) when it fits
+PyObject *compact_stage(PyObject *, PyObject *args) {
+    PyObject *o[4];
+    int fa, fb, target;
+    unsigned long long dst;
+    Py_ssize_t cap;
+    if (!PyArg_ParseTuple(args, "OOOOiiiKn", &o[0], &o[1], &o[2], &o[3], &fa, &fb, &target, &dst, &cap)) return nullptr;
+    try {
+        compact::Batch c;
+        batch_from(o[0], o[1], o[2], o[3], fa, fb, c);
+        compact::Plan p;
+        if (!compact::plan(c, target, p)) Py_RETURN_NONE;
+        const compact::Staged s = compact::stage_layout(c, p);
+        const bool fits = dst && (Py_ssize_t)s.total <= cap;
+        if (fits) compact::stage_copy(c, p, s, reinterpret_cast<uint8_t *>(dst));
+        return stage_result(c, p, s, fits);
+    } catch (const PyErrAlready &) {
+    } catch (const std::exception &e) {
+        PyErr_SetString(PyExc_RuntimeError, e.what());
+    }
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_RuntimeError, "compact_stage failed");
+    return nullptr;
+}
+
+// generate_stage(kind, B, seed, target_blocks, dst_address, capacity) -> as compact_stage, plus the
+// generated (mols, xn, atoms, pairs) when keep is set; generation, plan and copy run without the GIL
+// (the streaming producer thread, bench.py / chemprop_amd.stream)
+PyObject *generate_stage(PyObject *, PyObject *args) {
+    int kind, B, target, keep = 0;
+    unsigned long long seed, dst;
+    Py_ssize_t cap;
+    if (!PyArg_ParseTuple(args, "iiKiKn|p", &kind, &B, &seed, &target, &dst, &cap, &keep)) return nullptr;
+    if (kind < 0 || kind > 2 || B < 0) {
+        PyErr_SetString(PyExc_ValueError, "kind in {0, 1, 2}, B >= 0");
+        return nullptr;
+    }
+    try {
+        compact::Batch c;
+        compact::Plan p;
+        compact::Staged s;
+        bool ok = false, fits = false;
+        Py_BEGIN_ALLOW_THREADS
+        compact::generate(kind, B, seed, c);
+        ok = compact::plan(c, target, p);
+        if (ok) {
+            s = compact::stage_layout(c, p);
+            fits = dst && (Py_ssize_t)s.total <= cap;
+            if (fits) compact::stage_copy(c, p, s, reinterpret_cast<uint8_t *>(dst));
+        }
+        Py_END_ALLOW_THREADS
+        if (!ok) Py_RETURN_NONE;
+        PyObject *r = stage_result(c, p, s, fits);
+        if (!r || !keep) return r;
+        PyObject *arrays;
+        try { arrays = batch_tuple(c); } catch (...) { Py_DECREF(r); throw; }
+        PyObject *both = PyTuple_Pack(2, r, arrays);
+        Py_DECREF(r);
+        Py_DECREF(arrays);
+        return both;
+    } catch (const PyErrAlready &) {
+    } catch (const std::exception &e) {
+        PyErr_SetString(PyExc_RuntimeError, e.what());
+    }
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_RuntimeError, "generate_stage failed");
+    return nullptr;
+}
+
 PyMethodDef methods[] = {
     {"pack", pack, METH_VARARGS,
      "pack(mol_graphs, fa_w, fb_w, tail_from=0, check=False) -> 10 bytearrays: the concatenated BatchMolGraph tables "
@@ -511,6 +743,16 @@ PyMethodDef methods[] = {
     {"gathers", gathers, METH_VARARGS,
      "gathers(b2a, b2revb, w_bonds, deg, in_idx) -> (msg, agg, msg_t, agg_t) CSR gather lists (mpn.py:112-131)"},
     {"ell", ell, METH_VARARGS, "ell(ptr, idx, coef, rows_p, row_base, width) -> block-local ELL rows"},
+    {"compact_encode", compact_encode, METH_VARARGS,
+     "compact_encode(f_atoms, tail, w_atoms, w_bonds, b2a, b2revb, deg, in_idx, na, nb, xn, fa, tail_w) -> "
+     "(mols, xn, atoms, pairs) | (None, reason)"},
+    {"compact_decode", compact_decode, METH_VARARGS,
+     "compact_decode(mols, xn, atoms, pairs, fa, fb) -> pack()'s outputs in tail mode"},
+    {"compact_generate", compact_generate, METH_VARARGS, "compact_generate(kind, B, seed) -> (mols, xn, atoms, pairs)"},
+    {"compact_stage", compact_stage, METH_VARARGS,
+     "compact_stage(mols, xn, atoms, pairs, fa, fb, target_blocks, dst, capacity) -> plan + upload image"},
+    {"generate_stage", generate_stage, METH_VARARGS,
+     "generate_stage(kind, B, seed, target_blocks, dst, capacity[, keep]) -> generated batch's plan + upload image"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef module = {PyModuleDef_HEAD_INIT, "_wdpack", "native BatchMolGraph packer", -1, methods,

@@ -29,6 +29,7 @@
 #include "fused_mp.hpp"
 #include "gemm.hpp"
 #include "gemm_x6.hpp"
+#include "graph_build.hpp"
 #include "kernels.hpp"
 #include "wdmpnn.h"
 
@@ -505,6 +506,57 @@ int record_prof(const WdConfig *c, int pair, int which, hipStream_t st) {
     return 0;
 }
 
+// ------------------------------------------------------------------------------------------------
+// device graph of a compact batch (graph_build.hpp)
+// ------------------------------------------------------------------------------------------------
+struct GraphLayout {
+    int lda = 0, ldb = 0, Vap = 0, Rbp = 0;
+    size_t f_atoms = 0, f_bonds = 0, fa_x6 = 0, fb_x6 = 0, fa_blk_x6 = 0, w_atoms = 0, mol_start = 0, mol_size = 0,
+           xn = 0, b2revb = 0, blocks = 0, bond_blk_row = 0, atom_blk_row = 0, msg_ell_idx = 0, msg_ell_coef = 0,
+           agg_ell_idx = 0, agg_ell_coef = 0, csr[4][3] = {}, total = 0;
+};
+
+int graph_layout(const WdCompact *c, GraphLayout &L) {
+    if (!c) return fail(WD_ERR_ARG, "null compact graph");
+    if (c->n_atoms < 1 || c->n_bonds < 1 || c->n_mols < 0 || c->n_blocks < 0 || (c->n_bonds - 1) % 2 ||
+        c->nnz_msg < 0 || c->nnz_agg < 0)
+        return fail(WD_ERR_SHAPE, "compact graph: bad counts (atoms %d bonds %d mols %d blocks %d)", c->n_atoms,
+                    c->n_bonds, c->n_mols, c->n_blocks);
+    if (c->atom_fdim < 2 || c->atom_fdim > 255 || c->bond_fdim < c->atom_fdim || c->bond_fdim - c->atom_fdim > 16)
+        return fail(WD_ERR_SHAPE, "compact graph: atom_fdim %d / bond_fdim %d out of range", c->atom_fdim, c->bond_fdim);
+    L.lda = rup(c->atom_fdim, 32); L.ldb = rup(c->bond_fdim, 32);
+    L.Vap = rup(c->n_atoms, 128); L.Rbp = rup(c->n_bonds, 128);
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off = align256(off + bytes); return o; };
+    L.f_atoms = take((size_t)L.Vap * L.lda * 4);
+    L.f_bonds = take((size_t)L.Rbp * L.ldb * 4);
+    L.fa_x6 = take((size_t)L.Vap * L.lda * 6);
+    L.fb_x6 = take((size_t)L.Rbp * L.ldb * 6);
+    L.fa_blk_x6 = take((size_t)std::max(c->n_blocks, 1) * BLK_ATOMS * L.lda * 6);
+    L.w_atoms = take((size_t)c->n_atoms * 4);
+    L.mol_start = take((size_t)c->n_mols * 4 + 4);
+    L.mol_size = take((size_t)c->n_mols * 4 + 4);
+    L.xn = take((size_t)c->n_mols * 4 + 4);
+    L.b2revb = take((size_t)c->n_bonds * 4);
+    L.blocks = take((size_t)c->n_blocks * 32 + 32);
+    L.bond_blk_row = take((size_t)L.Rbp * 4);
+    L.atom_blk_row = take((size_t)L.Vap * 4);
+    L.msg_ell_idx = take((size_t)L.Rbp * GB_ELLW);
+    L.msg_ell_coef = take((size_t)L.Rbp * GB_ELLW * 4);
+    L.agg_ell_idx = take((size_t)L.Vap * GB_ELLW);
+    L.agg_ell_coef = take((size_t)L.Vap * GB_ELLW * 4);
+    // msg, agg, msg_t, agg_t: {ptr, idx, coef}
+    const int rows[4] = {c->n_bonds, c->n_atoms, c->n_bonds, c->n_bonds};
+    const int nnz[4] = {c->nnz_msg, c->nnz_agg, c->nnz_msg, c->nnz_agg};
+    for (int q = 0; q < 4; ++q) {
+        L.csr[q][0] = take((size_t)(rows[q] + 1) * 4);
+        L.csr[q][1] = take((size_t)(nnz[q] + GB_CSR_PAD) * 4);
+        L.csr[q][2] = take((size_t)(nnz[q] + GB_CSR_PAD) * 4);
+    }
+    L.total = off;
+    return 0;
+}
+
 }  // namespace
 
 // ================================================================================================
@@ -959,6 +1011,64 @@ int wdmpnn_index_select_rows(const float *src, int64_t n_src_rows, int64_t row_l
     hipLaunchKernelGGL(index_select_rows_kernel, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, src,
                        row_len, index, n_index, out);
     WD_CHECK_LAUNCH("index_select_rows");
+    return 0;
+}
+
+int wdmpnn_graph_bytes(const WdCompact *c, size_t *bytes) {
+    GraphLayout L;
+    WD_TRY(graph_layout(c, L));
+    if (!bytes) return fail(WD_ERR_ARG, "null bytes");
+    *bytes = L.total;
+    return 0;
+}
+
+int wdmpnn_build_graph(const WdCompact *c, void *buffer, size_t bytes, WdGraph *g, void *stream) {
+    GraphLayout L;
+    WD_TRY(graph_layout(c, L));
+    if (!buffer || !g) return fail(WD_ERR_ARG, "null buffer / graph");
+    if (bytes < L.total) return fail(WD_ERR_WORKSPACE, "graph buffer too small: need %zu bytes, got %zu", L.total, bytes);
+    if ((uintptr_t)buffer % 256) return fail(WD_ERR_ARG, "graph buffer must be 256-byte aligned");
+    if (c->n_mols && (!c->mols || !c->xn)) return fail(WD_ERR_ARG, "null molecule arrays");
+    if (!c->atoms || (c->n_bonds > 1 && !c->pairs) || (c->n_blocks && (!c->blocks || !c->block_nnz)))
+        return fail(WD_ERR_ARG, "null compact arrays");
+    char *base = (char *)buffer;
+    auto F = [&](size_t o) { return (float *)(base + o); };
+    auto I = [&](size_t o) { return (int32_t *)(base + o); };
+    auto U = [&](size_t o) { return (uint8_t *)(base + o); };
+    GraphBuildP P{};
+    P.c = *c;
+    P.Fa = c->atom_fdim; P.Fb = c->bond_fdim; P.lda = L.lda; P.ldb = L.ldb; P.Vap = L.Vap; P.Rbp = L.Rbp;
+    P.f_atoms = F(L.f_atoms); P.f_bonds = F(L.f_bonds);
+    P.fa_x6 = U(L.fa_x6); P.fb_x6 = U(L.fb_x6); P.fa_blk_x6 = U(L.fa_blk_x6);
+    P.w_atoms = F(L.w_atoms); P.xn = F(L.xn); P.mol_start = I(L.mol_start); P.mol_size = I(L.mol_size);
+    P.b2revb = I(L.b2revb); P.blocks = I(L.blocks); P.bond_blk_row = I(L.bond_blk_row);
+    P.atom_blk_row = I(L.atom_blk_row);
+    P.msg_ell_idx = U(L.msg_ell_idx); P.msg_ell_coef = F(L.msg_ell_coef);
+    P.agg_ell_idx = U(L.agg_ell_idx); P.agg_ell_coef = F(L.agg_ell_coef);
+    P.msg_ptr = I(L.csr[0][0]); P.msg_idx = I(L.csr[0][1]); P.msg_coef = F(L.csr[0][2]);
+    P.agg_ptr = I(L.csr[1][0]); P.agg_idx = I(L.csr[1][1]); P.agg_coef = F(L.csr[1][2]);
+    P.msgt_ptr = I(L.csr[2][0]); P.msgt_idx = I(L.csr[2][1]); P.msgt_coef = F(L.csr[2][2]);
+    P.aggt_ptr = I(L.csr[3][0]); P.aggt_idx = I(L.csr[3][1]); P.aggt_coef = F(L.csr[3][2]);
+    hipLaunchKernelGGL(graph_build_kernel, dim3(c->n_blocks + 1), dim3(256), 0, (hipStream_t)stream, P);
+    WD_CHECK_LAUNCH("graph_build");
+    WdGraph G{};
+    G.n_atoms = c->n_atoms; G.n_bonds = c->n_bonds; G.n_mols = c->n_mols;
+    G.atom_fdim = c->atom_fdim; G.bond_fdim = c->bond_fdim; G.ld_atoms = L.lda; G.ld_bonds = L.ldb; G.bond_col0 = 0;
+    G.f_atoms = P.f_atoms; G.f_bonds = P.f_bonds; G.w_atoms = P.w_atoms;
+    G.mol_start = P.mol_start; G.mol_size = P.mol_size; G.degree_of_polym = P.xn;
+    G.msg_gather = WdCsr{P.msg_ptr, P.msg_idx, P.msg_coef};
+    G.atom_gather = WdCsr{P.agg_ptr, P.agg_idx, P.agg_coef};
+    G.msg_gather_t = WdCsr{P.msgt_ptr, P.msgt_idx, P.msgt_coef};
+    G.atom_gather_t = WdCsr{P.aggt_ptr, P.aggt_idx, P.aggt_coef};
+    G.bond_feat_gather = WdCsr{nullptr, nullptr, nullptr};
+    G.bond_feat_gather_t = WdCsr{nullptr, nullptr, nullptr};
+    G.b2revb = P.b2revb;
+    G.atom_desc = nullptr; G.desc_dim = 0; G.atom_messages = 0;
+    G.f_atoms_x6 = P.fa_x6; G.f_bonds_x6 = P.fb_x6;
+    G.n_blocks = c->n_blocks; G.blocks = P.blocks; G.bond_blk_row = P.bond_blk_row; G.f_atoms_blk_x6 = P.fa_blk_x6;
+    G.msg_ell_idx = P.msg_ell_idx; G.msg_ell_coef = P.msg_ell_coef;
+    G.atom_ell_idx = P.agg_ell_idx; G.atom_ell_coef = P.agg_ell_coef;
+    *g = G;
     return 0;
 }
 

@@ -329,8 +329,8 @@ def test_device_bond_features(kind, b, extra):
     (wdmpnn_build_bond_features) equals the host-packed f_bonds bit for bit, and the encoder's output
     (forward and gradients) is bitwise identical to the host-featurised graph's."""
     mols = synthetic.make_batch(kind, b, 77) if kind != 'edge' else synthetic.edge_case_batch(b, star_leaves=30)
-    g_host = BatchMolGraph(mols)
-    g_dev = BatchMolGraph(mols, device_bond_features=True, check_bond_features=True)
+    g_host = BatchMolGraph(mols, compact=False)
+    g_dev = BatchMolGraph(mols, device_bond_features=True, check_bond_features=True, compact=False)
     am = bool(extra.get('atom_messages'))
     fdim = get_bond_fdim(atom_messages=am)
     d_host = g_host.device_graph(DEV, am, fdim)
