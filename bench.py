@@ -181,6 +181,66 @@ def training_workload(device, batch=128, steps=100, warmup=10):
             'steps': steps}
 
 
+def streamed_workload(device, args, rank, world, graphs_per_rank, batch=64, producers=4, barrier=None):
+    """BASELINE.json configs[4]: synthetic polymer graphs streamed per rank (10 M over 8 GPUs = 1.25 M per
+    rank by default: weak scaling), generated on the fly by native producer threads, staged in compact
+    form (~14 B per edge), uploaded and expanded on the GPU (wdmpnn_build_graph) while the previous batch
+    is encoded (chemprop_amd.stream).  Everything is inside the timed region: generation, block plan,
+    H2D, device graph build and the B=64 forward.  Disjoint seeds per rank, no collective on the data
+    path; value = edges of all ranks / max-over-ranks time."""
+    from chemprop_amd.stream import StreamedBatches
+    enc = make_encoder(args, device)
+    n = -(-graphs_per_rank // batch)
+    warm = 32
+    with torch.no_grad():
+        for g in StreamedBatches('polymer', batch, warm, seed=99, device=device, rank=rank, producers=producers):
+            enc(g)
+        barrier()
+        t0 = time.perf_counter()
+        edges = 0
+        h2d = 0
+        for g in StreamedBatches('polymer', batch, n, seed=2024, device=device, rank=rank, producers=producers):
+            enc(g)
+            edges += g.n_bonds - 1
+            h2d += g.device_graph(device, False, get_bond_fdim()).h2d_bytes
+        barrier()
+        dt = time.perf_counter() - t0
+    return dt, edges, n * batch, h2d
+
+
+def streamed_training(device, rank, world, graphs_per_rank, batch=128, producers=4, barrier=None):
+    """configs[4] as data-parallel training: each rank trains MoleculeModel (depth 3, hidden 300, one
+    regression task, Adam) on its own streamed batches of ``batch`` graphs; one flat fp32 gradient
+    all-reduce per step (chemprop_amd.dp.GradBucket: RCCL over xGMI when world > 1)."""
+    from chemprop_amd.dp import GradBucket, broadcast_parameters
+    from chemprop_amd.model import MoleculeModel
+    from chemprop_amd.stream import StreamedBatches
+    from chemprop_amd.train import build_optimizer, get_loss_func, train_step
+    args = TrainArgs(hidden_size=300, depth=3, device=device)
+    torch.manual_seed(0)
+    model = MoleculeModel(args)
+    initialize_weights(model)
+    model = model.to(device)
+    broadcast_parameters(model)
+    bucket = GradBucket(model)
+    opt = build_optimizer(model, 1e-4)
+    loss_func = get_loss_func('regression')
+    gen = torch.Generator().manual_seed(rank)
+    targets = [torch.randn(batch, 1, generator=gen).tolist() for _ in range(8)]
+    steps = -(-graphs_per_rank // batch)
+    for i, g in enumerate(StreamedBatches('polymer', batch, 10, seed=77, device=device, rank=rank, producers=producers)):
+        train_step(model, [g], targets[i % 8], loss_func, opt, bucket=bucket)
+    barrier()
+    t0 = time.perf_counter()
+    edges = 0
+    for i, g in enumerate(StreamedBatches('polymer', batch, steps, seed=4048, device=device, rank=rank,
+                                          producers=producers)):
+        train_step(model, [g], targets[i % 8], loss_func, opt, bucket=bucket)
+        edges += g.n_bonds - 1
+    barrier()
+    return time.perf_counter() - t0, edges, steps
+
+
 def packing_report(a, device, t_fwd):
     """Host side of one batch, outside the timed region (pack + H2D reported separately,
     and end to end): native packer time, device_graph() time (gather lists, blocks, one pinned H2D,
@@ -227,14 +287,25 @@ def main():
     ap.add_argument('--no-secondary', action='store_true', help='skip the QM9 / ZINC-shaped secondary workloads')
     ap.add_argument('--streams', type=int, default=2, help='batches in flight per GPU (one HIP stream each)')
     ap.add_argument('--variant', type=int, default=0, help='WdConfig.gemm_variant (0 = default path; 9 = f32 MFMA)')
+    ap.add_argument('--stream-graphs', type=int, default=10_000_000 // 8,
+                    help='configs[4]: polymer graphs streamed per rank (default 10 M / 8 GPUs); 0 = skip')
+    ap.add_argument('--stream-train-graphs', type=int, default=131_072,
+                    help='configs[4] as DP training: streamed graphs per rank (batches of 128); 0 = skip')
     a = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # one process per GPU over RCCL (backend "nccl"); BENCH_BACKEND=gloo rehearses the multi-rank path
+    # with several ranks on one GPU (device = local rank modulo the visible GPUs)
+    backend = os.environ.get('BENCH_BACKEND', 'nccl')
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device('cuda', local)
     args = TrainArgs(hidden_size=a.hidden, depth=a.depth, device=device)
 
@@ -308,14 +379,25 @@ def main():
             _native.check(L.wdmpnn_event_pool_elapsed_ms(pool, 0, a.steps, ctypes.byref(kernel_ms)), 'events')
         L.wdmpnn_event_pool_destroy(pool)
 
-    t = torch.tensor([elapsed, elapsed_prof, single or 0.0], dtype=torch.float64, device=device)
-    e = torch.tensor([my_edges], dtype=torch.float64, device=device)
+    # configs[4]: streamed graphs (generation + upload + device build + forward, all timed), then the
+    # same stream as data-parallel training with one gradient all-reduce per step
+    st_dt = st_edges = st_graphs = st_h2d = tr_dt = tr_edges = tr_steps = 0
+    if a.stream_graphs > 0:
+        st_dt, st_edges, st_graphs, st_h2d = streamed_workload(device, args, rank, world, a.stream_graphs,
+                                                               barrier=barrier)
+    if a.stream_train_graphs > 0:
+        tr_dt, tr_edges, tr_steps = streamed_training(device, rank, world, a.stream_train_graphs, barrier=barrier)
+
+    t = torch.tensor([elapsed, elapsed_prof, single or 0.0, st_dt, tr_dt], dtype=torch.float64, device=device)
+    e = torch.tensor([my_edges, st_edges, st_graphs, st_h2d, tr_edges], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(e, op=dist.ReduceOp.SUM)
     elapsed, elapsed_prof = float(t[0]), float(t[1])
     single = float(t[2]) if single is not None else None
     total_edges = float(e[0])
+    st_dt, tr_dt = float(t[3]), float(t[4])
+    st_edges, st_graphs, st_h2d, tr_edges = float(e[1]), float(e[2]), float(e[3]), float(e[4])
 
     if rank == 0:
         H = a.hidden
@@ -372,6 +454,22 @@ def main():
                          'launches_timed': n_launch},
         }
         line['forward'] = forward_roofline(graphs, a, elapsed / a.steps)
+        if st_dt > 0:
+            line['streamed'] = {
+                'workload': 'configs[4]: synthetic polymer graphs streamed per rank in batches of 64 (native '
+                            'generation on producer threads, compact upload, device graph build, forward; all '
+                            'inside the timed region), disjoint seeds per rank, no data-path collective',
+                'graphs': st_graphs, 'graphs_per_rank': a.stream_graphs, 'n_gpus': world,
+                'value': st_edges / st_dt, 'unit': 'edges/s', 'graphs_per_s': st_graphs / st_dt, 'seconds': st_dt,
+                'h2d_bytes_per_edge': st_h2d / st_edges, 'scaling': 'weak'}
+        if tr_dt > 0:
+            line['streamed_training'] = {
+                'workload': 'configs[4] as DP training: MoleculeModel (depth 3, hidden 300, regression, Adam) on '
+                            'streamed polymer batches of 128 per rank, one flat fp32 gradient all-reduce per step '
+                            f'({"RCCL" if world > 1 else "none at N=1"})',
+                'steps_per_rank': tr_steps, 'n_gpus': world, 'value': tr_edges / tr_dt, 'unit': 'edges/s',
+                'ms_per_step': tr_dt / tr_steps * 1e3, 'graphs_per_s': tr_steps * 128 * world / tr_dt,
+                'scaling': 'weak'}
         line['packing'] = packing_report(a, device, elapsed / a.steps)
         if world == 1 and a.kind == 'polymer' and not a.no_secondary:
             line['secondary'] = [secondary_workload(device, 'qm9', 64, 3, 300, 200, streams=a.streams),

@@ -108,6 +108,11 @@ class GradBucket:
                 v.copy_(p.grad)  # autograd created a fresh tensor: fold it into the bucket
                 p.grad = v
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            if self.buffer.is_cuda and dist.get_backend() == 'gloo':
+                # gloo stages CUDA tensors through host memory; measured on ROCm: without draining the
+                # producing stream first it can read the bucket before the backward kernels have written
+                # it (RCCL orders the collective after the stream's work by itself)
+                torch.cuda.current_stream(self.buffer.device).synchronize()
             dist.all_reduce(self.buffer, op=dist.ReduceOp.SUM)
             self.buffer.div_(dist.get_world_size())
 

@@ -279,7 +279,7 @@ class BatchMolGraph:
 
     def __getattr__(self, name):
         # only reached for attributes not set yet: a from_compact batch decodes its tables once
-        if name in BatchMolGraph._LAZY and '_compact' in self.__dict__ and '_np' not in self.__dict__:
+        if name in BatchMolGraph._LAZY and self.__dict__.get('_compact') is not None and '_np' not in self.__dict__:
             self._decode_compact()
             return self.__dict__[name]
         raise AttributeError(name)

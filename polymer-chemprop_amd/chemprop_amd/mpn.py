@@ -302,7 +302,10 @@ class MPNEncoder(nn.Module):
         pstruct, packed = self._packed_params(gs, cfg, params, device, cache=not save)
         if not save:  # inference: the same C-ABI call without the autograd.Function wrapper
             return _forward_call(gs, cfg, pstruct, hidden_out, device)[0]
-        return _EncoderFunction.apply(self, gs, cfg, pstruct, (packed, desc), hidden_out, device, *params)
+        # the autograd context keeps the device graph alive with the packed weights and descriptors: the
+        # backward reads its buffers through raw pointers (gs), and the caller may drop the BatchMolGraph
+        # before calling backward (``model([BatchMolGraph(mols)]).sum().backward()``)
+        return _EncoderFunction.apply(self, gs, cfg, pstruct, (packed, desc, dg), hidden_out, device, *params)
 
     def invalidate_packed_params(self) -> None:
         """Drop the cached padded weights.  Needed only after writing the parameters in a way that

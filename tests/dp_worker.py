@@ -51,3 +51,43 @@ def run(rank, world, port, out_path):
         torch.save({'params': [g for g in gathered], 'nbytes': bucket.nbytes}, out_path)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def run_gpu(rank, world, port, out_path):
+    """Two ranks on cuda:0 (gloo process group): MoleculeModel with the HIP encoder, DP training with the
+    flat GradBucket all-reduce, fused Adam, on disjoint synthetic polymer shards."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from chemprop_amd import TrainArgs, synthetic
+    from chemprop_amd.featurization import BatchMolGraph
+    from chemprop_amd.model import MoleculeModel
+    from chemprop_amd.nn_utils import initialize_weights
+    from chemprop_amd.train import build_optimizer
+    env = dp.init_distributed('gloo')
+    dev = torch.device('cuda:0')
+    args = TrainArgs(hidden_size=64, depth=3, device=dev)
+    torch.manual_seed(200 + rank)  # deliberately different init per rank: the broadcast must fix it
+    model = MoleculeModel(args)
+    initialize_weights(model)
+    model = model.to(dev)
+    dp.broadcast_parameters(model)
+    bucket = dp.GradBucket(model)
+    opt = build_optimizer(model, 1e-3)
+    shards = dp.shard([gpu_data(s) for s in range(4)], env.rank, env.world_size)
+    loss_func = get_loss_func('regression')
+    for mols, y in shards:
+        train_step(model, [BatchMolGraph(mols)], y, loss_func, opt, bucket=bucket)
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu()
+    gathered = [torch.zeros_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    if rank == 0:
+        torch.save({'params': gathered}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def gpu_data(seed, n=16):
+    from chemprop_amd import synthetic
+    g = torch.Generator().manual_seed(seed)
+    y = [[float(v)] for v in torch.randn(n, generator=g)]
+    return synthetic.make_batch('polymer', n, 300 + seed), y

@@ -28,7 +28,8 @@ def test_forward_roofline_matches_survey_numbers():
 @pytest.mark.gpu
 def test_bench_prints_one_contract_line():
     p = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--steps', '5', '--warmup', '1', '--no-cpu',
-                        '--no-secondary'], cwd=ROOT, capture_output=True, text=True, timeout=240)
+                        '--no-secondary', '--stream-graphs', '6400', '--stream-train-graphs', '1280'], cwd=ROOT,
+                       capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, p.stdout
@@ -42,3 +43,6 @@ def test_bench_prints_one_contract_line():
     for k in ('bound', 'achieved', 'peak', 'unit', 'frac', 'traffic'):
         assert k in rf, k
     assert abs(rf['frac'] - rf['achieved'] / rf['peak']) < 1e-9
+    st, tr = d['streamed'], d['streamed_training']  # configs[4]: streamed forward and DP training
+    assert st['graphs'] == 6400 and st['value'] > 0 and st['h2d_bytes_per_edge'] <= 16
+    assert tr['steps_per_rank'] == 10 and tr['value'] > 0

@@ -5,6 +5,7 @@ a single-process run that averages the two shards' gradients."""
 import os
 import socket
 
+import pytest
 import torch
 import torch.multiprocessing as mp
 
@@ -53,3 +54,45 @@ def test_two_rank_gradient_allreduce_matches_single_process(tmp_path):
     ref = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
     assert torch.allclose(p0, ref, atol=1e-6, rtol=1e-5)
     assert res['nbytes'] == 4 * sum(p.numel() for p in model.parameters())
+
+
+@pytest.mark.gpu
+def test_two_rank_molecule_model_on_gpu_matches_single_process(tmp_path):
+    """World size 2 on cuda:0 (gloo): the real MoleculeModel with the HIP encoder (its autograd.Function
+    returns fresh gradient tensors that must land in the GradBucket views), fused Adam, two DP steps on
+    disjoint shards = one process taking the same steps on the averaged gradients."""
+    from chemprop_amd import TrainArgs
+    from chemprop_amd.featurization import BatchMolGraph
+    from chemprop_amd.model import MoleculeModel
+    from chemprop_amd.nn_utils import initialize_weights
+    from chemprop_amd.train import build_optimizer
+    out = str(tmp_path / 'dp_gpu.pt')
+    mp.spawn(dp_worker.run_gpu, args=(2, free_port(), out), nprocs=2, join=True)
+    p0, p1 = torch.load(out, weights_only=True)['params']
+    assert torch.equal(p0, p1), 'ranks diverged'
+    dev = torch.device('cuda:0')
+    torch.manual_seed(200)  # rank 0's init (broadcast)
+    model = MoleculeModel(TrainArgs(hidden_size=64, depth=3, device=dev))
+    initialize_weights(model)
+    model = model.to(dev)
+    opt = build_optimizer(model, 1e-3)
+    lf = get_loss_func('regression')
+    shards = [dp.shard([dp_worker.gpu_data(s) for s in range(4)], r, 2) for r in range(2)]
+    for step in range(2):
+        grads = []
+        for r in range(2):
+            model.zero_grad()
+            mols, y = shards[r][step]
+            batch_loss(model([BatchMolGraph(mols)]), y, lf).backward()
+            grads.append([p.grad.clone() for p in model.parameters() if p.requires_grad])
+        for p, g0, g1 in zip([q for q in model.parameters() if q.requires_grad], *grads):
+            p.grad = (g0 + g1) / 2
+        opt.step()
+    ref = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu()
+    names, off, bad = [n for n, _ in model.named_parameters()], 0, {}
+    for n, p in zip(names, model.parameters()):
+        d = float((p0[off:off + p.numel()] - ref[off:off + p.numel()]).abs().max()) if p.numel() else 0.0
+        if d > 1e-6:
+            bad[n] = d
+        off += p.numel()
+    assert not bad, bad

@@ -429,3 +429,25 @@ def test_inference_plan_cache_follows_config_and_weights():
     assert golden_io.normwise(out.cpu().numpy(), ref.numpy()) <= TOL
     grad_path = enc(g)  # grad enabled: the autograd.Function path
     assert golden_io.normwise(grad_path.detach().cpu().numpy(), ref.numpy()) <= TOL
+
+
+def test_backward_after_the_batch_graph_is_dropped():
+    """The graph may be dropped between forward and backward (a temporary BatchMolGraph inside the call):
+    the autograd context keeps its device buffers alive, so the gradients equal those of a run that
+    keeps the graph (regression: the context held only raw pointers)."""
+    mols = synthetic.make_batch('polymer', 16, 0)
+    args = TrainArgs(hidden_size=64, depth=3)
+    grads = []
+    for keep in (True, False):
+        enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim())
+        synthetic.fill_parameters(enc, 1)
+        enc = enc.to(DEV)
+        g = BatchMolGraph(mols)
+        out = enc(g) if keep else enc(BatchMolGraph(mols))
+        if not keep:
+            del g
+        junk = [torch.randn(1 << 20, device=DEV) for _ in range(8)]  # reuse any freed device memory
+        out.square().sum().backward()
+        del junk
+        grads.append([p.grad.cpu() for p in enc.parameters() if p.grad is not None])
+    assert all(torch.equal(a, b) for a, b in zip(*grads))

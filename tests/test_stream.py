@@ -1,0 +1,91 @@
+"""Streamed synthetic batches (chemprop_amd.stream, BASELINE.json configs[4]): generation + staging on
+producer threads, H2D + device graph build on a feed stream, overlapped with the encoder on the
+compute stream.  Every batch is a full polymer batch; sampled batches are checked against the oracle
+on their decoded tables, the whole stream against a second pass (bitwise), and the training step on
+streamed batches against the same step on host-packed copies."""
+import numpy as np
+import pytest
+import torch
+
+import golden_io
+from chemprop_amd import TrainArgs, synthetic
+from chemprop_amd.featurization import BatchMolGraph, get_atom_fdim, get_bond_fdim
+from chemprop_amd.mpn import MPNEncoder
+from chemprop_amd.stream import StreamedBatches, stage_capacity
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda:0')
+
+
+def _encoder(hidden=300, depth=3, seed=3, **kw):
+    enc = MPNEncoder(TrainArgs(hidden_size=hidden, depth=depth, **kw), get_atom_fdim(), get_bond_fdim())
+    synthetic.fill_parameters(enc, seed)
+    return enc.to(DEV).eval()
+
+
+def test_stream_60_batches_vs_oracle_and_replay():
+    from oracle import mpn_ref
+    enc = _encoder()
+    p = {n: t.detach().cpu().clone() for n, t in enc.named_parameters()}
+    args = TrainArgs(hidden_size=300, depth=3)
+    outs, checked = [], 0
+    with torch.no_grad():
+        for i, g in enumerate(StreamedBatches('polymer', 64, 60, seed=11, device=DEV, keep_host=True, producers=3)):
+            out = enc(g)
+            outs.append(out)
+            assert g.device_graph(DEV, False, get_bond_fdim()).built_on_device
+            if i % 10 == 3:  # sampled batches against the oracle on the decoded reference tables
+                ref = mpn_ref.encoder_forward(p, g, args)
+                assert golden_io.normwise(out.cpu().numpy(), ref.numpy()) <= 1e-5
+                checked += 1
+        torch.cuda.synchronize()
+        again = [enc(g) for g in StreamedBatches('polymer', 64, 60, seed=11, device=DEV, producers=1, slots=3)]
+    assert checked == 6
+    assert all(torch.equal(a, b) for a, b in zip(outs, again))  # same seeds, any producer count: same batches
+    assert not torch.equal(outs[0], outs[1])
+
+
+def test_streams_of_two_ranks_are_disjoint():
+    a = next(iter(StreamedBatches('polymer', 8, 1, seed=5, device=DEV, rank=0, keep_host=True)))
+    b = next(iter(StreamedBatches('polymer', 8, 1, seed=5, device=DEV, rank=1, keep_host=True)))
+    assert bytes(a._compact[2]) != bytes(b._compact[2])
+
+
+@pytest.mark.parametrize('kind', ['qm9', 'zinc'])
+def test_stream_other_kinds_fit_their_slots(kind):
+    enc = _encoder(hidden=64)
+    n = 0
+    with torch.no_grad():
+        for g in StreamedBatches(kind, 128, 5, seed=2, device=DEV):
+            assert torch.isfinite(enc(g)).all()
+            n += 1
+    assert n == 5 and stage_capacity(kind, 128) > 0
+
+
+def test_training_on_streamed_batches_matches_host_packed():
+    """train_step on streamed (device-built) batches = the same steps on BatchMolGraphs packed on the host
+    from the decoded tables (compact=False): identical losses and parameters."""
+    from chemprop_amd.model import MoleculeModel
+    from chemprop_amd.nn_utils import initialize_weights
+    from chemprop_amd.train import build_optimizer, get_loss_func, train_step
+    args = TrainArgs(hidden_size=96, depth=3, device=DEV)
+    stream = list(StreamedBatches('polymer', 32, 4, seed=9, device=DEV, keep_host=True))
+    host = [BatchMolGraph(_molgraphs(g), compact=False) for g in stream]
+    rng = np.random.default_rng(0)
+    targets = [[[float(x)] for x in rng.standard_normal(32)] for _ in stream]
+    res = []
+    for batches in (stream, host):
+        torch.manual_seed(0)
+        m = MoleculeModel(args)
+        initialize_weights(m)
+        m = m.to(DEV)
+        opt = build_optimizer(m, 1e-3)
+        losses = [float(train_step(m, [g], t, get_loss_func('regression'), opt)) for g, t in zip(batches, targets)]
+        res.append((losses, [q.detach().cpu() for q in m.parameters()]))
+    assert res[0][0] == res[1][0]
+    assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+
+
+def _molgraphs(g):
+    from test_compact import _as_molgraphs
+    return _as_molgraphs(g)
