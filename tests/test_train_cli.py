@@ -21,8 +21,8 @@ from chemprop_amd.train import NoamLR
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = json.load(open(os.path.join(HERE, 'golden', 'host_plumbing.json')))
-CSV = os.path.join(HERE, 'golden', 'polymer10.csv')
-NPZ = os.path.join(HERE, 'golden', 'polymer10_graphs.npz')
+CSV = os.path.join(HERE, 'data', 'polymer10.csv')
+NPZ = os.path.join(HERE, 'data', 'polymer10_graphs.npz')
 
 
 @pytest.mark.parametrize('case', range(len(GOLD['polymer_rules'])))

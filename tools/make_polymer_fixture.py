@@ -5,7 +5,7 @@ Monomer pairs with two attachment points each, monomer fractions, the 10 stochas
 attachment points (incl. self loops) with random weights (the reference's sum-to-1 check never fires,
 featurization.py:362), and a degree of polymerisation; graphs from ``chemprop_amd.polymer.synthetic_polymer_graph`` (structure from the string,
 synthetic atom / bond features: RDKit is not available).  Targets: a smooth function of the fractions
-and Xn plus noise (seeded).  Writes tests/golden/polymer10.csv and tests/golden/polymer10_graphs.npz.
+and Xn plus noise (seeded).  Writes tests/data/polymer10.csv and tests/data/polymer10_graphs.npz.
 """
 import csv
 import os
@@ -44,7 +44,7 @@ def main():
         y = 1.5 * fa - 0.3 * np.log10(xn) + 0.1 * rng.standard_normal()
         rows.append([s, f'{y:.6f}'])
         graphs.append(synthetic_polymer_graph(s, seed=k))
-    out = os.path.join(ROOT, 'tests', 'golden')
+    out = os.path.join(ROOT, 'tests', 'data')
     with open(os.path.join(out, 'polymer10.csv'), 'w', newline='') as f:
         w = csv.writer(f)
         w.writerow(['poly_chemprop_input', 'EA vs SHE (eV)'])
