@@ -51,23 +51,49 @@ def make_encoder(args, device):
     return enc.to(device).eval()
 
 
+def _cpu_model():
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
 def cpu_baseline(args, graph, seconds):
-    """The oracle (op-for-op restatement of the reference forward, oracle/mpn_ref.py) on host cores."""
+    """The oracle (op-for-op restatement of the reference forward, oracle/mpn_ref.py; within +-10 % of
+    the real reference at 8 threads, profiles/round2_cpu_port_check.txt) on the GPU box's host cores:
+    median over ~``seconds`` of forwards with torch's thread count, then a shorter 1-thread sample."""
     from oracle import mpn_ref
     enc = make_encoder(args, torch.device('cpu'))
     p = {n: t.detach() for n, t in enc.named_parameters()}
-    times = []
-    t_end = time.perf_counter() + seconds
-    with torch.no_grad():
-        mpn_ref.encoder_forward(p, graph, args)  # warm-up
-        while len(times) < 5 or time.perf_counter() < t_end:
-            t0 = time.perf_counter()
-            mpn_ref.encoder_forward(p, graph, args)
-            times.append(time.perf_counter() - t0)
-    med = statistics.median(times)
-    return {'value': (graph.n_bonds - 1) / med, 'unit': 'edges/s', 'cores': torch.get_num_threads(), 'kind': 'port',
-            'sample': f'{len(times)} forwards of one polymer B={len(graph.a_scope)} batch (E={graph.n_bonds - 1} '
-                      f'directed edges), median {med * 1e3:.2f} ms, torch {torch.__version__} CPU, eval/no_grad'}
+
+    def sample(secs, min_n):
+        times = []
+        t_end = time.perf_counter() + secs
+        with torch.no_grad():
+            mpn_ref.encoder_forward(p, graph, args)  # warm-up
+            while len(times) < min_n or time.perf_counter() < t_end:
+                t0 = time.perf_counter()
+                mpn_ref.encoder_forward(p, graph, args)
+                times.append(time.perf_counter() - t0)
+        return statistics.median(times), len(times)
+
+    threads = torch.get_num_threads()
+    med, n = sample(seconds, 5)
+    torch.set_num_threads(1)
+    med1, n1 = sample(seconds / 3, 3)
+    torch.set_num_threads(threads)
+    E = graph.n_bonds - 1
+    return {'value': E / med, 'unit': 'edges/s', 'cores': threads, 'kind': 'port',
+            'sample': f'{n} forwards of one polymer B={len(graph.a_scope)} batch (E={E} directed edges), median '
+                      f'{med * 1e3:.2f} ms at {threads} threads, eval/no_grad',
+            'single_thread': {'value': E / med1, 'ms': med1 * 1e3, 'forwards': n1},
+            'host': {'cpu_model': _cpu_model(), 'logical_cpus': os.cpu_count(), 'torch': torch.__version__,
+                     'mkl': bool(torch.backends.mkl.is_available()),
+                     'mkldnn': bool(torch.backends.mkldnn.is_available())}}
 
 
 def pmc_traffic(prefix):

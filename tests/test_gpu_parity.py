@@ -123,6 +123,8 @@ def _check(res):
     ('polymer', 32, 96, 4, dict(undirected=True, aggregation='sum')),
     ('polymer', 32, 64, 3, dict(atom_messages=True, bias=True)),
     ('polymer', 16, 70, 3, dict(activation='PReLU', bias=True, aggregation='norm')),
+    ('polymer', 8, 1100, 2, dict(activation='ELU')),                 # hidden > 1024 (readout backward chunks)
+    ('polymer', 6, 2400, 3, dict(bias=True)),                        # the reference hyperopt's largest hidden
 ])
 def test_random_graphs_vs_oracle(kind, b, hidden, depth, extra):
     args = TrainArgs(hidden_size=hidden, depth=depth, **extra)
