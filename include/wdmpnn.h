@@ -66,6 +66,18 @@ typedef struct WdCsr {
     const float   *coef;  /* [ptr[rows]] coefficients, NULL = all ones */
 } WdCsr;
 
+/* Categorical codes of one atom / one bond pair (see "Compact graphs" below). */
+typedef struct WdAtomCode {
+    uint8_t col[8];         /* columns of f_atoms holding 1.0, ascending; 0xFF = unused slot     */
+    float last;             /* f_atoms[atom_fdim - 1] (mass * 0.01)                              */
+    float w;                /* w_atoms                                                           */
+} WdAtomCode;
+typedef struct WdBondPair {
+    uint16_t a1, a2;        /* molecule-local atom ids: b1 = a1 -> a2, b2 = a2 -> a1             */
+    uint16_t tail;          /* bond feature columns as bits (bit k = column atom_fdim + k)       */
+    uint16_t reserved;
+    float w12, w21;         /* w_bonds[b1], w_bonds[b2]                                          */
+} WdBondPair;
 /*
  * Device-resident packed BatchMolGraph (featurization.py:757-813) plus the gather lists derived
  * from it by the host packer (chemprop_amd/featurization.py, BatchMolGraph.device_graph()).
@@ -123,6 +135,14 @@ typedef struct WdGraph {
     const float *msg_ell_coef;
     const uint8_t *atom_ell_idx;
     const float *atom_ell_coef;
+    /* Optional categorical codes (compact graphs, wdmpnn_build_graph; NULL otherwise).  With blocks, the
+     * fused forward then replaces the W_i GEMM and the f_atoms half of the W_o GEMM by sums of weight
+     * columns (one-hot rows: f W^T = sum of the columns holding 1.0 + last * the last column):
+     * atom_codes [n_atoms] natural rows; bond_src_blk [rows of f_bonds] = the block-local index of the
+     * bond's source atom (b2a); bond_tail [rows of f_bonds] = its bond columns as bits. */
+    const WdAtomCode *atom_codes;
+    const uint8_t *bond_src_blk;
+    const uint16_t *bond_tail;
 } WdGraph;
 
 /* nn.Module parameters of MPNEncoder (mpn.py:17-64); all device pointers, row-major like nn.Linear. */
@@ -253,17 +273,6 @@ int wdmpnn_build_bond_features(const float *f_atoms, int32_t ld_atoms, int32_t a
  * (chemprop_amd.featurization.BatchMolGraph.device_graph): one launch.  Requires every molecule to fit
  * one block (<= 128 directed bonds, <= 64 atoms); atom_fdim <= 255 with the code's columns < atom_fdim - 1.
  * ------------------------------------------------------------------------------------------------ */
-typedef struct WdAtomCode {
-    uint8_t col[8];         /* columns of f_atoms holding 1.0, ascending; 0xFF = unused slot     */
-    float last;             /* f_atoms[atom_fdim - 1] (mass * 0.01)                              */
-    float w;                /* w_atoms                                                           */
-} WdAtomCode;
-typedef struct WdBondPair {
-    uint16_t a1, a2;        /* molecule-local atom ids: b1 = a1 -> a2, b2 = a2 -> a1             */
-    uint16_t tail;          /* bond feature columns as bits (bit k = column atom_fdim + k)       */
-    uint16_t reserved;
-    float w12, w21;         /* w_bonds[b1], w_bonds[b2]                                          */
-} WdBondPair;
 typedef struct WdCompact {
     int32_t n_mols, n_atoms, n_bonds, n_blocks;   /* n_atoms / n_bonds include the pad row        */
     int32_t atom_fdim, bond_fdim;                 /* 133 / 147 by default (bond_fdim - atom_fdim <= 16) */

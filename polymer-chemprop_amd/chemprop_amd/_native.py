@@ -47,7 +47,8 @@ class WdGraph(Structure):
                 ('f_atoms_x6', c_void_p), ('f_bonds_x6', c_void_p),
                 ('n_blocks', c_int32), ('blocks', c_void_p), ('bond_blk_row', c_void_p), ('f_atoms_blk_x6', c_void_p),
                 ('msg_ell_idx', c_void_p), ('msg_ell_coef', c_void_p), ('atom_ell_idx', c_void_p),
-                ('atom_ell_coef', c_void_p)]
+                ('atom_ell_coef', c_void_p), ('atom_codes', c_void_p), ('bond_src_blk', c_void_p),
+                ('bond_tail', c_void_p)]
 
 
 class WdParams(Structure):

@@ -21,6 +21,7 @@
 #pragma once
 #include "gemm_x6.hpp"
 #include "kernels.hpp"
+#include "wdmpnn.h"
 
 namespace wd {
 
@@ -277,8 +278,120 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// embed_kernel: the input layer (mpn.py:92-97) of a compact batch without a GEMM.  Every f_bonds row is
+// its source atom's one-hot row + the bond's binary columns (+ mass * 0.01 in the atom's last column,
+// featurization.py:190-250, 467-468), so f_bonds[b] W_i^T is a sum of W_i columns:
+//     Ea[a]  = sum_{c in code(a)} W_i[:, c] + last(a) W_i[:, Fa-1]          (per atom of the block)
+//     inp[b] = Ea[src(b)] + sum_{k in tail(b)} W_i[:, Fa + k] (+ b_i)       (per bond)
+//     M0[b]  = act(inp[b])
+//     Eo[a]  = sum_{c in code(a)} W_o[:, c] + last(a) W_o[:, Fa-1]          (the f_atoms half of W_o)
+// One workgroup per (block, BN-column tile), the tile's W_i^T and W_o[:, :Fa]^T rows staged in LDS.
+// Writes inp (fp32, natural rows: the residual of every layer), M0 (plane tiles, blocked rows) like
+// gemm_x6g's epilogue, and Eo (fp32, blocked atom rows) for wo_readout_kernel's epilogue.
+// ------------------------------------------------------------------------------------------------
+struct EmbedP {
+    const WdAtomCode *codes;     // natural atom rows
+    const uint8_t *src_blk;      // per natural bond row: block-local source atom
+    const uint16_t *tail;        // per natural bond row: bond columns as bits
+    const float *wt;             // W_i^T [>= Fb][Hk] (fp32, packed)
+    const float *woat;           // W_o[:, :Fa]^T [>= Fa][Hk] (fp32, packed)
+    float *eo;                   // [nblk * 64][Hk]
+    const float *bias;           // b_i (padded) or null
+    const int32_t *blocks;
+    int Fa, Fb, Hk, n_tiles;
+    int act; const float *slope;
+    float *inp;                  // [Rp][Hk]
+    uint8_t *mplanes;            // M0 plane tiles, blocked bond rows (BR 128)
+};
+
+// Stage rows [0, rows0) of src0 and [0, rows1) of src1 (BN columns from n0, row stride ld, fp32) into
+// LDS dst0 / dst1 [rows][BN]: every load of the thread issued before the first LDS store (one latency,
+// not one per row group); rows <= MAXK.
+template <int BN, int NT, int MAXK>
+__device__ __forceinline__ void stage_rows2(float *dst0, const float *src0, int rows0, float *dst1,
+                                            const float *src1, int rows1, int ld, int n0) {
+    constexpr int C4 = BN / 4, PER = (MAXK * C4 + NT - 1) / NT;
+    float4 r0[PER], r1[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int v = threadIdx.x + NT * j, k = v / C4, c = 4 * (v % C4);
+        r0[j] = k < rows0 ? ld4(src0 + (size_t)k * ld + n0 + c) : f4zero();
+        r1[j] = k < rows1 ? ld4(src1 + (size_t)k * ld + n0 + c) : f4zero();
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int v = threadIdx.x + NT * j, k = v / C4, c = 4 * (v % C4);
+        if (k < rows0) st4(dst0 + k * BN + c, r0[j]);
+        if (k < rows1) st4(dst1 + k * BN + c, r1[j]);
+    }
+}
+
+template <int BN>
+__global__ __launch_bounds__(512) void embed_kernel(EmbedP P) {
+    constexpr int NT = 512, LDC = BN + 4, C4 = BN / 4, U8 = BN / 8, MAXK = 160;
+    __shared__ __attribute__((aligned(16))) float wt[MAXK * BN];        // W_i^T rows of the tile
+    __shared__ __attribute__((aligned(16))) float wo[MAXK * BN];        // W_o[:, :Fa]^T rows of the tile
+    __shared__ __attribute__((aligned(16))) float ea[BLK_ATOMS * LDC];  // Ea of the block's atoms
+    __shared__ __attribute__((aligned(16))) float bb[BN];
+    __shared__ WdAtomCode code[BLK_ATOMS];
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
+    const BlockRow B = load_block(P.blocks, blk);
+    const int tid = threadIdx.x;
+    if (tid < B.an) code[tid] = P.codes[B.as + tid];
+    if (tid >= NT - C4) st4(bb + 4 * (tid - (NT - C4)), P.bias ? ld4(P.bias + n0 + 4 * (tid - (NT - C4))) : f4zero());
+    stage_rows2<BN, NT, MAXK>(wt, P.wt, P.Fb, wo, P.woat, P.Fa, P.Hk, n0);
+    __syncthreads();
+    for (int v = tid; v < B.an * C4; v += NT) {
+        const int la = v / C4, c = 4 * (v % C4);
+        const WdAtomCode &cd = code[la];
+        float4 s = f4zero(), so = f4zero();
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (cd.col[q] == 0xFF) continue;
+            const float4 w = ld4(wt + cd.col[q] * BN + c), u = ld4(wo + cd.col[q] * BN + c);
+            s.x += w.x; s.y += w.y; s.z += w.z; s.w += w.w;
+            so.x += u.x; so.y += u.y; so.z += u.z; so.w += u.w;
+        }
+        fma4(s, cd.last, ld4(wt + (P.Fa - 1) * BN + c));
+        fma4(so, cd.last, ld4(wo + (P.Fa - 1) * BN + c));
+        st4(ea + la * LDC + c, s);
+        st4(P.eo + ((size_t)blk * BLK_ATOMS + la) * P.Hk + n0 + c, so);
+    }
+    __syncthreads();
+    const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
+    const __amdgpu_buffer_rsrc_t mrs = x6_block_rsrc<BLK_BONDS>(P.mplanes, P.Hk, blk);
+    for (int v = tid; v < B.bn * U8; v += NT) {
+        const int lb = v / U8, c = 8 * (v % U8), b = B.bs + lb;
+        const int sa = P.src_blk[b];
+        const uint32_t tl = P.tail[b];
+        float4 z0 = ld4(ea + sa * LDC + c), z1 = ld4(ea + sa * LDC + c + 4);
+        for (uint32_t m = tl; m; m &= m - 1) {
+            const float *w = wt + (P.Fa + __builtin_ctz(m)) * BN + c;
+            const float4 w0 = ld4(w), w1 = ld4(w + 4);
+            z0.x += w0.x; z0.y += w0.y; z0.z += w0.z; z0.w += w0.w;
+            z1.x += w1.x; z1.y += w1.y; z1.z += w1.z; z1.w += w1.w;
+        }
+        const float4 b0 = ld4(bb + c), b1 = ld4(bb + c + 4);
+        z0.x += b0.x; z0.y += b0.y; z0.z += b0.z; z0.w += b0.w;
+        z1.x += b1.x; z1.y += b1.y; z1.z += b1.z; z1.w += b1.w;
+        float *zr = P.inp + (size_t)b * P.Hk + n0 + c;
+        st4(zr, z0);
+        st4(zr + 4, z1);
+        const float4 y0 = make_float4(act_fwd(P.act, z0.x, slope), act_fwd(P.act, z0.y, slope),
+                                      act_fwd(P.act, z0.z, slope), act_fwd(P.act, z0.w, slope));
+        const float4 y1 = make_float4(act_fwd(P.act, z1.x, slope), act_fwd(P.act, z1.y, slope),
+                                      act_fwd(P.act, z1.z, slope), act_fwd(P.act, z1.w, slope));
+        x6_store8_blk<BLK_BONDS>(mrs, lb, n0 + c, y0, y1);
+    }
+}
+
+constexpr int WO_MAXK = 160;  // f_atoms / f_bonds columns embed_kernel stages (Fa, Fb <= 160)
+
 struct WoReadoutP {
     const uint8_t *fa; int kpa; int kca;     // f_atoms: blocked atom plane tiles [nblk * 64][kpa], kca chunks used
+    int kcw;                                 // f_atoms chunks in the W_o plane tiles (Fak / 32; kca = 0 or kcw)
     const uint8_t *ag; int kp;               // A: blocked atom plane tiles [nblk * 64][kp = Hk]
     const uint8_t *wo;                       // W_o plane tiles [Hk][Fak + Hk] with BN-row blocks
     const float *bias;                       // b_o (padded)
@@ -288,6 +401,10 @@ struct WoReadoutP {
     int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;
     float *out; int ncols;                   // out [B][ncols] (ncols = H)
     int n_tiles;
+    // categorical codes (kca = 0): the f_atoms half of [f_atoms | A] W_o^T, precomputed per atom by
+    // embed_kernel as sums of W_o columns: fp32 [nblk * 64][Hk], blocked atom rows (null: GEMM segment)
+    const float *eo;
+    int Hk;
 };
 
 template <int BN> struct WoWaves;
@@ -311,7 +428,8 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     // QM9-shaped batches)
     constexpr int CPS = BN == 80 ? 2 : 1;
     constexpr int WS = 2;  // LDS stages
-    __shared__ __attribute__((aligned(16))) uint8_t lds[WS * CPS * x6_stage_bytes<BM, BN>()];
+    constexpr int LDS_BYTES = WS * CPS * x6_stage_bytes<BM, BN>();
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
     const int tile = xcd_tile(blockIdx.x, gridDim.x);
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
@@ -321,7 +439,9 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     O.a1 = P.ag; O.nkc1 = P.kp >> 5; O.kc1 = P.kp >> 5;
     O.rb = blk;
     O.a_rows = B.an;
-    O.b = P.wo + (size_t)nt * (P.kca + (P.kp >> 5)) * (3 * BN * 64);
+    // W_o planes: per BN-row block, kcw f_atoms chunks then kp / 32 A chunks; the f_atoms chunks are
+    // skipped when the codes path adds that half in the epilogue (kca = 0)
+    O.b = P.wo + ((size_t)nt * (P.kcw + (P.kp >> 5)) + (P.kcw - P.kca)) * (3 * BN * 64);
     // prefetched during the GEMM (mainloop hook): this thread's bias columns, the block's atom weights
     // (thread a < an: w_atoms[as + a]) and its molecules' scope / Xn (thread i < nm)
     constexpr int C4 = BN / 4;
@@ -330,9 +450,17 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     float4 bb = f4zero();
     float watom = 0.f, mxn = 0.f;
     int mstart = 0, msize = 0;
+    // codes path: this thread's rows of the precomputed f_atoms W_o[:, :Fa]^T (the epilogue units below)
+    constexpr int EPU = (BM * C4 + NT - 1) / NT;
+    float4 eo[EPU];
     auto prefetch = [&]() {
         bb = ld4(P.bias + n0 + 4 * (tid % C4));
         if (tid < B.an) watom = P.w_atoms[B.as + tid];
+#pragma unroll
+        for (int j = 0; j < EPU; ++j) {
+            const int v = tid + NT * j, la = v / C4, c = 4 * (v % C4);
+            eo[j] = P.eo && v < BM * C4 && la < B.an ? ld4(P.eo + ((size_t)blk * BM + la) * P.Hk + n0 + c) : f4zero();
+        }
         if (tid < nm) {
             mstart = P.mol_start[B.ml + tid];
             msize = P.mol_size[B.ml + tid];
@@ -345,7 +473,7 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     float *H = reinterpret_cast<float *>(lds);
     float *Wl = H + BM * LDC;           // [BM] atom weights of the block
     float *Ml = Wl + BM;                // [3][BLK_MOLS] per molecule: start (as float bits), size, Xn
-    static_assert((BM * LDC + BM + 3 * BLK_MOLS) * 4 <= 2 * CPS * x6_stage_bytes<BM, BN>(), "readout staging fits");
+    static_assert((BM * LDC + BM + 3 * BLK_MOLS) * 4 <= LDS_BYTES, "readout staging fits");
     static_assert(BLK_MOLS <= NT, "one molecule per thread in the prefetch");
     x6_acc_to_lds<BM, BN, WM, WN>(acc, H);
     if (tid < BM) Wl[tid] = watom;
@@ -358,9 +486,13 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     // h = act(. + b_o) (* dropout), in place (mpn.py:133-134)
     {
         const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
-        for (int v = tid; v < BM * C4; v += NT) {
+#pragma unroll
+        for (int j = 0; j < EPU; ++j) {
+            const int v = tid + NT * j;
+            if (v >= BM * C4) break;
             const int la = v / C4, c = 4 * (v % C4);
-            const float4 hv = ld4(H + la * LDC + c);
+            float4 hv = ld4(H + la * LDC + c);
+            hv.x += eo[j].x; hv.y += eo[j].y; hv.z += eo[j].z; hv.w += eo[j].w;  // (0 without codes)
             float z[4] = {hv.x + bb.x, hv.y + bb.y, hv.z + bb.z, hv.w + bb.w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {

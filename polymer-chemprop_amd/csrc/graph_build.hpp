@@ -32,6 +32,8 @@ struct GraphBuildP {
     uint8_t *fa_x6, *fb_x6, *fa_blk_x6;
     float *w_atoms, *xn;
     int32_t *mol_start, *mol_size, *b2revb, *blocks, *bond_blk_row, *atom_blk_row;
+    uint8_t *bond_src_blk;
+    uint16_t *bond_tail;
     uint8_t *msg_ell_idx, *agg_ell_idx;
     float *msg_ell_coef, *agg_ell_coef;
     int32_t *msg_ptr, *msg_idx, *agg_ptr, *agg_idx, *msgt_ptr, *msgt_idx, *aggt_ptr, *aggt_idx;
@@ -79,6 +81,8 @@ __global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
         for (int i = tid; i < nb_pad; i += 256) {
             const int r = i == 0 ? 0 : E1 + i - 1;
             P.bond_blk_row[r] = -1;
+            P.bond_src_blk[r] = 0;
+            P.bond_tail[r] = 0;
             for (int s = 0; s < GB_ELLW; ++s) { P.msg_ell_idx[GB_ELLW * r + s] = 0; P.msg_ell_coef[GB_ELLW * r + s] = 0.f; }
         }
         if (tid < 2) {  // row 0 (pad atom / bond) has no entries
@@ -97,10 +101,11 @@ __global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
     __shared__ int s_blk[8];
     __shared__ int s_mas[GB_MOLS], s_mbs[GB_MOLS];
     __shared__ WdAtomCode s_code[GB_ATOMS];
-    __shared__ uint8_t s_src[GB_BONDS], s_dst[GB_BONDS], s_in[GB_BONDS];
+    __shared__ __attribute__((aligned(16))) uint8_t s_src[GB_BONDS], s_dst[GB_BONDS];
+    __shared__ uint8_t s_in[GB_BONDS], s_out[GB_BONDS];
     __shared__ uint16_t s_tail[GB_BONDS];
     __shared__ float s_w[GB_BONDS];
-    __shared__ int s_deg[GB_ATOMS], s_start[GB_ATOMS + 1];
+    __shared__ int s_start[GB_ATOMS + 1];  // in(a) = s_in[s_start[a] ..), out(a) = s_out[s_start[a] ..)
     __shared__ int s_pm[GB_BONDS + 1], s_pt[GB_BONDS + 1], s_pg[GB_BONDS + 1], s_pa[GB_ATOMS + 1];
     __shared__ int s_off[2];
     if (tid < 8) s_blk[tid] = C.blocks[8 * k + tid];
@@ -108,6 +113,7 @@ __global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
     __syncthreads();
     const int bs = s_blk[0], bn = s_blk[1], as = s_blk[2], an = s_blk[3], ml = s_blk[4], nm = s_blk[5] - s_blk[4];
     if (bn > GB_BONDS || an > GB_ATOMS || nm > GB_MOLS || nm < 0) return;  // the host plan never does this
+    const int lane = tid & 63, wave = tid >> 6;
     if (tid < nm) {
         s_mas[tid] = C.mols[4 * (ml + tid)];
         s_mbs[tid] = C.mols[4 * (ml + tid) + 2];
@@ -121,6 +127,7 @@ __global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
         P.atom_blk_row[as + tid] = GB_ATOMS * k + tid;
     }
     if (tid < 8) P.blocks[8 * k + tid] = s_blk[tid];
+    if (tid >= bn && tid < GB_BONDS) s_src[tid] = s_dst[tid] = 0xFF;  // never equal to an atom of the block
     __syncthreads();
     if (tid < bn) {  // endpoints of bond b = bs + tid
         const int b = bs + tid;
@@ -138,24 +145,39 @@ __global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
         s_tail[tid] = q.tail;
         P.b2revb[b] = dir ? b - 1 : b + 1;
         P.bond_blk_row[b] = GB_BONDS * k + tid;
+        P.bond_src_blk[b] = (uint8_t)(dir ? l2 : l1);
+        P.bond_tail[b] = q.tail;
     }
     __syncthreads();
-    if (tid < an) {  // in(a): bonds into a in creation order
-        int d = 0;
-        for (int lb = 0; lb < bn; ++lb) d += s_dst[lb] == tid;
-        s_deg[tid] = d;
+    // in(a) / out(a) in creation order by counting sort: a bond's slot = start of its atom + the number of
+    // earlier bonds with the same endpoint (16-byte broadcast reads of the endpoint arrays: no serial
+    // loops over the block's bonds); every pair gives each endpoint one in- and one out-bond, so
+    // |in(a)| = |out(a)| = deg(a)
+    auto count_eq = [](const uint8_t *arr, int v, int below) {
+        int n = 0;
+        for (int q = 0; q < GB_BONDS / 16 && 16 * q < below; ++q) {
+            const uint4 w = *reinterpret_cast<const uint4 *>(arr + 16 * q);
+            const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                n += ((wd[u >> 2] >> (8 * (u & 3))) & 0xFF) == (uint32_t)v && 16 * q + u < below;
+        }
+        return n;
+    };
+    if (wave == 0) {  // deg + exclusive prefix over the atoms (one wave)
+        const int d = lane < an ? count_eq(s_dst, lane, bn) : 0;
+        int incl = d;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += t;
+        }
+        if (lane < an) s_start[lane] = incl - d;
+        if (lane == 63) s_start[an] = incl;  // (an <= 64: lanes >= an add 0)
     }
     __syncthreads();
-    if (tid == 0) {
-        int s = 0;
-        for (int a = 0; a < an; ++a) { s_start[a] = s; s += s_deg[a]; }
-        s_start[an] = s;
-    }
-    __syncthreads();
-    if (tid < an) {
-        int o = s_start[tid];
-        for (int lb = 0; lb < bn; ++lb)
-            if (s_dst[lb] == tid) s_in[o++] = (uint8_t)lb;
+    if (tid < bn) {
+        s_in[s_start[s_dst[tid]] + count_eq(s_dst, s_dst[tid], tid)] = (uint8_t)tid;
+        s_out[s_start[s_src[tid]] + count_eq(s_src, s_src[tid], tid)] = (uint8_t)tid;
     }
     __syncthreads();
     // entry counts: msg row, msg_t row, agg_t row (bonds); agg row (atoms)
@@ -166,11 +188,11 @@ __global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
             const int j = s_in[e];
             cm += (j == rev ? s_w[j] - 1.0f : s_w[j]) != 0.f;
         }
-        int ct = 0;
-        for (int lb = 0; lb < bn; ++lb)
-            if (s_src[lb] == s_dst[tid]) ct += (tid == (lb ^ 1) ? s_w[tid] - 1.0f : s_w[tid]) != 0.f;
+        // msg_t row: the rows lb in out(dst(tid)); every one has coefficient w - [lb == rev(tid)], and
+        // rev(tid) is among them (src(rev) = dst(tid))
+        const int nout = s_start[s_dst[tid] + 1] - s_start[s_dst[tid]];
         s_pm[tid + 1] = cm;
-        s_pt[tid + 1] = ct;
+        s_pt[tid + 1] = (nout - 1) * (s_w[tid] != 0.f) + (s_w[tid] - 1.0f != 0.f);
         s_pg[tid + 1] = s_w[tid] != 0.f;
     }
     if (tid < an) {
@@ -179,10 +201,21 @@ __global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
         s_pa[tid + 1] = ca;
     }
     __syncthreads();
-    if (tid == 0) { s_pm[0] = 0; for (int i = 0; i < bn; ++i) s_pm[i + 1] += s_pm[i]; }
-    if (tid == 64) { s_pt[0] = 0; for (int i = 0; i < bn; ++i) s_pt[i + 1] += s_pt[i]; }
-    if (tid == 128) { s_pg[0] = 0; for (int i = 0; i < bn; ++i) s_pg[i + 1] += s_pg[i]; }
-    if (tid == 192) { s_pa[0] = 0; for (int i = 0; i < an; ++i) s_pa[i + 1] += s_pa[i]; }
+    if (wave < 4) {  // four exclusive prefix sums, one wave each (two elements per lane)
+        int *pre = wave == 0 ? s_pm : wave == 1 ? s_pt : wave == 2 ? s_pg : s_pa;
+        const int n = wave == 3 ? an : bn;
+        const int e0 = 2 * lane + 1, e1 = 2 * lane + 2;
+        const int a = e0 <= n ? pre[e0] : 0, c = e1 <= n ? pre[e1] : 0;
+        int incl = a + c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += t;
+        }
+        const int base = incl - a - c;
+        if (e0 <= n) pre[e0] = base + a;
+        if (e1 <= n) pre[e1] = base + a + c;
+        if (lane == 0) pre[0] = 0;
+    }
     __syncthreads();
     const int om = s_off[0], oa = s_off[1];
     if (tid < bn) {
@@ -210,10 +243,11 @@ __global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
             P.msg_ell_idx[(size_t)GB_ELLW * b + q] = eidx[q];
             P.msg_ell_coef[(size_t)GB_ELLW * b + q] = ecoef[q];
         }
-        // msg_gather_t row b: rows lb with src(lb) = dst(b), in increasing lb
+        // msg_gather_t row b: the rows lb in out(dst(b)), increasing lb
         o = om + s_pt[tid];
-        for (int lb = 0; lb < bn; ++lb) {
-            if (s_src[lb] != s_dst[tid]) continue;
+        const int d = s_dst[tid];
+        for (int e = s_start[d]; e < s_start[d + 1]; ++e) {
+            const int lb = s_out[e];
             const float c = tid == (lb ^ 1) ? s_w[tid] - 1.0f : s_w[tid];
             if (c == 0.f) continue;
             P.msgt_idx[o] = bs + lb;

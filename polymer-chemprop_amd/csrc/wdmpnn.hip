@@ -132,6 +132,8 @@ struct PackLayout {
     size_t Wi = 0, bi = 0, Wh = 0, bh = 0, Wo = 0, bo = 0, Wd = 0, bd = 0, WhT = 0, WoT = 0, WdT = 0, total = 0;
     size_t WiX = 0, WhX = 0, WoX = 0;  // bf16x3 plane tiles (64-row blocks) of W_i / W_h / W_o
     size_t WhX80 = 0, WoX80 = 0;       // the same with 80-row blocks (fused forward, Hk % 80 == 0)
+    size_t WiT = 0, WoaT = 0;          // W_i^T [Kink][Hk] and W_o[:, :Fa]^T [Fak][Hk]: weight columns as rows
+                                       // (the categorical-code embedding of the fused forward)
 };
 
 PackLayout pack_layout(const Dims &D) {
@@ -146,6 +148,8 @@ PackLayout pack_layout(const Dims &D) {
     L.bo = take(D.Hk);
     L.WhT = take((size_t)D.Hk * D.Hk);
     L.WoT = take((size_t)D.Hk * D.Hk);
+    L.WiT = take((size_t)D.Kink * D.Hk);
+    L.WoaT = take((size_t)D.Fak * D.Hk);
     L.WiX = take((size_t)D.Hk * D.Kink * 3 / 2);  // 3 bf16 planes = 1.5 floats per value
     L.WhX = take((size_t)D.Hk * D.ldx * 3 / 2);
     L.WoX = take((size_t)D.Hk * D.Ko * 3 / 2);
@@ -199,6 +203,9 @@ int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
     // transposes for dX = dZ W_h[:, :H] and dA = dZo W_o[:, Fa:]
     add(job_transpose(F(L.WhT), D.Hk, D.Hk, p->W_h, D.atom ? H + D.Fb : H, 0, H, H));
     add(job_transpose(F(L.WoT), D.Hk, D.Hk, p->W_o, D.Fa + H, D.Fa, H, H));
+    // weight columns as rows for the categorical-code embedding (fused_mp.hpp embed_kernel / wo_readout)
+    add(job_transpose(F(L.WiT), D.Kink, D.Hk, p->W_i, D.Kin, 0, D.Kin, H));
+    add(job_transpose(F(L.WoaT), D.Fak, D.Hk, p->W_o, D.Fa + H, 0, D.Fa, H));
     if (D.desc) {
         add(job_plain(F(L.Wd), D.Hdk, D.Kd, p->W_d, D.Hd, D.Hd, {{0, 0, H}, {D.Hk, H, D.d}}));
         add(job_plain(F(L.bd), 1, D.Hdk, p->b_d, D.Hd, 1, {{0, 0, D.Hd}}));
@@ -412,6 +419,7 @@ struct FwdLayout {
     size_t packed = 0, A = 0, Zo = 0, h = 0, Zd = 0, hd = 0, total = 0;
     size_t Xp = 0, Ap = 0;  // plane tiles of X_t and A (D.x6)
     size_t Mb[2] = {0, 0}, Ab = 0;  // molecule-blocked plane tiles of M_t (ping-pong) and A (D.blocked)
+    size_t Eo = 0;                  // D.blocked: f_atoms W_o[:, :Fa]^T per blocked atom row (compact codes)
     bool own_pack = false;
 };
 
@@ -430,6 +438,7 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
     if (D.blocked) {
         for (int i = 0; i < 2; ++i) L.Mb[i] = take((size_t)D.nblk * BLK_BONDS * D.Hk * 6);
         L.Ab = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 6);
+        L.Eo = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 4);
     } else if (D.x6) {
         if (D.T > 1) L.Xp = take((size_t)D.Rp * D.Hk * 6);
         L.Ap = take((size_t)D.Vap * D.Hk * 6);
@@ -512,7 +521,8 @@ int record_prof(const WdConfig *c, int pair, int which, hipStream_t st) {
 struct GraphLayout {
     int lda = 0, ldb = 0, Vap = 0, Rbp = 0;
     size_t f_atoms = 0, f_bonds = 0, fa_x6 = 0, fb_x6 = 0, fa_blk_x6 = 0, w_atoms = 0, mol_start = 0, mol_size = 0,
-           xn = 0, b2revb = 0, blocks = 0, bond_blk_row = 0, atom_blk_row = 0, msg_ell_idx = 0, msg_ell_coef = 0,
+           xn = 0, b2revb = 0, blocks = 0, bond_blk_row = 0, atom_blk_row = 0, bond_src_blk = 0, bond_tail = 0,
+           msg_ell_idx = 0, msg_ell_coef = 0,
            agg_ell_idx = 0, agg_ell_coef = 0, csr[4][3] = {}, total = 0;
 };
 
@@ -541,6 +551,8 @@ int graph_layout(const WdCompact *c, GraphLayout &L) {
     L.blocks = take((size_t)c->n_blocks * 32 + 32);
     L.bond_blk_row = take((size_t)L.Rbp * 4);
     L.atom_blk_row = take((size_t)L.Vap * 4);
+    L.bond_src_blk = take((size_t)L.Rbp);
+    L.bond_tail = take((size_t)L.Rbp * 2);
     L.msg_ell_idx = take((size_t)L.Rbp * GB_ELLW);
     L.msg_ell_coef = take((size_t)L.Rbp * GB_ELLW * 4);
     L.agg_ell_idx = take((size_t)L.Vap * GB_ELLW);
@@ -624,14 +636,29 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
 
     if (D.blocked) {
         // molecule-blocked fused forward (fused_mp.hpp): W_i -> (T-1) x mp_layer -> wo_readout
-        Epi e = epi_act(c->activation, p->prelu, W(PL.bi), nullptr, F(L.Z[0]), nullptr, Hk, c, 0);
-        e.planes = (uint8_t *)(ws + L.Mb[0]); e.plane_row = g->bond_blk_row; e.planes_kp = Hk;
-        if (!x6g_eligible(e)) return fail(WD_ERR_SHAPE, "fused forward: unaligned buffers");
-        WD_TRY(gemm_x6g(g->f_bonds_x6, g->ld_bonds, D.Kink, nullptr, 0, 0, pkb + PL.WiX, D.Rp, Hk, e, st));
         // 80-column tiles when they divide Hk (Hk = 320: 4 tiles, one workgroup per CU at the benchmark
         // size), else 64
         const bool bn80 = Hk % 80 == 0;
         const int BNf = bn80 ? 80 : 64;
+        // categorical codes (compact graphs): the input layer and the f_atoms half of W_o as sums of
+        // weight columns instead of GEMMs over the one-hot rows (fused_mp.hpp embed_kernel)
+        const bool codes = g->atom_codes && g->bond_src_blk && g->bond_tail && D.Fb <= WO_MAXK && D.Fa <= WO_MAXK;
+        if (codes) {
+            EmbedP E{};
+            E.codes = g->atom_codes; E.src_blk = g->bond_src_blk; E.tail = g->bond_tail;
+            E.wt = W(PL.WiT); E.woat = W(PL.WoaT); E.eo = F(L.Eo); E.bias = p->b_i ? W(PL.bi) : nullptr; E.blocks = g->blocks;
+            E.Fa = D.Fa; E.Fb = D.Fb; E.Hk = Hk; E.n_tiles = Hk / BNf;
+            E.act = c->activation; E.slope = p->prelu;
+            E.inp = F(L.Z[0]); E.mplanes = (uint8_t *)(ws + L.Mb[0]);
+            if (bn80) hipLaunchKernelGGL(embed_kernel<80>, dim3(D.nblk * E.n_tiles), dim3(512), 0, st, E);
+            else hipLaunchKernelGGL(embed_kernel<64>, dim3(D.nblk * E.n_tiles), dim3(512), 0, st, E);
+            WD_CHECK_LAUNCH("embed");
+        } else {
+            Epi e = epi_act(c->activation, p->prelu, W(PL.bi), nullptr, F(L.Z[0]), nullptr, Hk, c, 0);
+            e.planes = (uint8_t *)(ws + L.Mb[0]); e.plane_row = g->bond_blk_row; e.planes_kp = Hk;
+            if (!x6g_eligible(e)) return fail(WD_ERR_SHAPE, "fused forward: unaligned buffers");
+            WD_TRY(gemm_x6g(g->f_bonds_x6, g->ld_bonds, D.Kink, nullptr, 0, 0, pkb + PL.WiX, D.Rp, Hk, e, st));
+        }
         for (int t = 1; t < D.T; ++t) {
             MpLayerP M{};
             M.mprev = (const uint8_t *)(ws + L.Mb[(t - 1) & 1]); M.mnext = (uint8_t *)(ws + L.Mb[t & 1]); M.kp = Hk;
@@ -663,7 +690,9 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
         }
         if (D.B > 0) {
             WoReadoutP R{};
-            R.fa = (const uint8_t *)g->f_atoms_blk_x6; R.kpa = g->ld_atoms; R.kca = D.Fak / 32;
+            R.fa = (const uint8_t *)g->f_atoms_blk_x6; R.kpa = g->ld_atoms; R.kcw = D.Fak / 32;
+            R.kca = codes ? 0 : R.kcw;
+            R.eo = codes ? F(L.Eo) : nullptr; R.Hk = Hk;
             R.ag = (const uint8_t *)(ws + L.Ab); R.kp = Hk;
             R.wo = (const uint8_t *)(pkb + (bn80 ? PL.WoX80 : PL.WoX)); R.bias = W(PL.bo);
             R.blocks = g->blocks;
@@ -1043,6 +1072,7 @@ int wdmpnn_build_graph(const WdCompact *c, void *buffer, size_t bytes, WdGraph *
     P.w_atoms = F(L.w_atoms); P.xn = F(L.xn); P.mol_start = I(L.mol_start); P.mol_size = I(L.mol_size);
     P.b2revb = I(L.b2revb); P.blocks = I(L.blocks); P.bond_blk_row = I(L.bond_blk_row);
     P.atom_blk_row = I(L.atom_blk_row);
+    P.bond_src_blk = U(L.bond_src_blk); P.bond_tail = (uint16_t *)(base + L.bond_tail);
     P.msg_ell_idx = U(L.msg_ell_idx); P.msg_ell_coef = F(L.msg_ell_coef);
     P.agg_ell_idx = U(L.agg_ell_idx); P.agg_ell_coef = F(L.agg_ell_coef);
     P.msg_ptr = I(L.csr[0][0]); P.msg_idx = I(L.csr[0][1]); P.msg_coef = F(L.csr[0][2]);
@@ -1068,6 +1098,7 @@ int wdmpnn_build_graph(const WdCompact *c, void *buffer, size_t bytes, WdGraph *
     G.n_blocks = c->n_blocks; G.blocks = P.blocks; G.bond_blk_row = P.bond_blk_row; G.f_atoms_blk_x6 = P.fa_blk_x6;
     G.msg_ell_idx = P.msg_ell_idx; G.msg_ell_coef = P.msg_ell_coef;
     G.atom_ell_idx = P.agg_ell_idx; G.atom_ell_coef = P.agg_ell_coef;
+    G.atom_codes = c->atoms; G.bond_src_blk = P.bond_src_blk; G.bond_tail = P.bond_tail;
     *g = G;
     return 0;
 }

@@ -211,7 +211,10 @@ def test_generated_batches_forward_and_backward_vs_oracle(kind, b, hidden, depth
 
 
 @pytest.mark.gpu
-def test_compact_and_host_paths_encode_bitwise_equal():
+def test_compact_and_host_paths_agree():
+    """Training path (unblocked kernels on the device-built arrays): bitwise equal to the host-packed
+    graph.  Inference: the compact graph's input layer and W_o atom half are sums of weight columns
+    (embed_kernel) instead of GEMMs over the one-hot rows, so only rounding differs."""
     from chemprop_amd.mpn import MPNEncoder
     mols = synthetic.make_batch('polymer', 64, 13)
     args = TrainArgs(hidden_size=300, depth=3)
@@ -227,4 +230,6 @@ def test_compact_and_host_paths_encode_bitwise_equal():
         o2 = enc.train()(g)
         o2.square().sum().backward()
         outs.append([o1.cpu(), o2.detach().cpu()] + [q.grad.cpu().clone() for q in enc.parameters() if q.grad is not None])
-    assert all(torch.equal(x, y) for x, y in zip(*outs))
+    (a, *ra), (b, *rb) = outs
+    assert all(torch.equal(x, y) for x, y in zip(ra, rb))
+    assert golden_io.normwise(a.numpy(), b.numpy()) <= 1e-6

@@ -20,7 +20,7 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     benchq) step bench_quick 300 python bench.py --steps 100 --warmup 10 --cpu-seconds 5 ;;
-    prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu --no-secondary --streams 1 ;;
+    prof) step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu --no-secondary --streams 1 --stream-graphs 0 --stream-train-graphs 0 ;;
     lab) step gemm_lab 300 ./tools/gemm_lab 200 ;;
     stream) step stream 120 ./tools/gemm_lab 50 stream ;;
     mainloop) step mainloop 120 ./tools/gemm_lab 200 mainloop ;;
