@@ -115,6 +115,8 @@ struct MpLayerP {
     const uint8_t *aell_idx; const float *aell_coef;
     uint8_t *aplanes;           // A: blocked atom plane tiles [nblk * 64][kp]
     int n_tiles;                // Hk / BN
+    int xp;                     // TEMP experiment bits
+    uint64_t *dbg;              // TEMP timestamps
 };
 
 // Wave layout of the fused kernels per column-tile width: BN = 64 -> 4 x 2 waves, BN = 80 -> 2 x 5.
@@ -131,36 +133,25 @@ template <> struct MpWaves<80> { static constexpr int WM = 4, WN = 1; };
 template <> struct MpWaves<80> { static constexpr int WM = 2, WN = 5; };
 #endif
 
-// grid = nblk * n_tiles (XCD-grouped: the column tiles of a block share an XCD), 64 WM WN threads.
-// LDS: two GEMM stages, reused by the epilogue as P [128][BN + 4] fp32; the last layer then
-// overwrites P with M_t (held in registers across a barrier) for the atom aggregate.
-template <int BN, bool LAST>
-__global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_layer_kernel(MpLayerP P) {
-    constexpr int BM = BLK_BONDS, LDC = BN + 4, WM = MpWaves<BN>::WM, WN = MpWaves<BN>::WN, NT = 64 * WM * WN;
-    constexpr int UPR = BN / 8, UNITS = BM * UPR, UPT = (UNITS + NT - 1) / NT;  // 8-column epilogue units
-    // two stages of one chunk (measured: 3 stages slower; two-chunk stages, one barrier per two
-    // chunks, no faster: the chunk time is not bound by load latency or barriers)
-    constexpr int S = 2, CPS = 1;
-    // (<= 80 KB: two workgroups fit one CU's 160 KB, so layers of batches in flight on other
-    // streams co-reside)
-    constexpr int LDS_BYTES = BM * LDC * 4 > S * CPS * x6_stage_bytes<BM, BN>()
-                                  ? BM * LDC * 4
-                                  : S * CPS * x6_stage_bytes<BM, BN>();
-    static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU");
-    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
-    const int tile = xcd_tile(blockIdx.x, gridDim.x);
-    const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
-    const BlockRow B = load_block(P.blocks, blk);
-    const int tid = threadIdx.x;
-    // residual rows and the rows' gather lists (ELL) prefetched during the GEMM (unit v = tid + NT i:
-    // row v / UPR, columns 8 (v % UPR) ..); the last layer also prefetches the atom gather rows of its
-    // atom-aggregate units (unit v = tid: atom v / UPR)
-    constexpr int AUNITS = BLK_ATOMS * UPR;
-    static_assert(!LAST || AUNITS <= NT, "one atom-aggregate unit per thread");
+// mp_layer epilogue, shared by both layer kernels: residual rows and gather lists prefetched during the
+// GEMM, then (P tile in LDS) the in-block gather, bias, residual, activation, dropout and the plane
+// stores of M_t -- or, in the last layer, the atom aggregate of M_t.
+template <int BN, int NT, bool LAST>
+struct MpEpilogue {
+    static constexpr int BM = BLK_BONDS, LDC = BN + 4;
+    static constexpr int UPR = BN / 8, UNITS = BM * UPR, UPT = (UNITS + NT - 1) / NT;  // 8-column units
+    static constexpr int AUNITS = BLK_ATOMS * UPR, AUPT = LAST ? (AUNITS + NT - 1) / NT : 1;
     float4 res[UPT][2];
     EllRow ell[UPT];
-    EllRow aell = ell_zero();
-    auto prefetch = [&]() {
+    EllRow aell[AUPT];
+
+    // residual rows and the rows' gather lists (ELL) (unit v = tid + NT i: row v / UPR, columns 8 (v %
+    // UPR) ..); the last layer also prefetches the atom gather rows of its atom-aggregate units (unit v =
+    // tid + NT i: atom v / UPR)
+    __device__ __forceinline__ void prefetch(const MpLayerP &P, const BlockRow &B, int n0) {
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < AUPT; ++i) aell[i] = ell_zero();
 #pragma unroll
         for (int i = 0; i < UPT; ++i) {
             const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
@@ -177,11 +168,122 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
             }
         }
         if constexpr (LAST)
-            if (tid / UPR < B.an) aell = ell_load(P.aell_idx, P.aell_coef, (size_t)B.as + tid / UPR);
-    };
-#if WD_EXP == 13
-    prefetch();
-#endif
+#pragma unroll
+            for (int i = 0; i < AUPT; ++i) {
+                const int v = tid + NT * i;
+                if (v / UPR < B.an) aell[i] = ell_load(P.aell_idx, P.aell_coef, (size_t)B.as + v / UPR);
+            }
+    }
+
+    // Pt: the P = M_{t-1} W_hᵀ tile [BM][LDC] fp32 in LDS (every write of it done and synchronised)
+    __device__ __forceinline__ void run(const MpLayerP &P, const BlockRow &B, int blk, int n0, float *Pt) {
+        if (P.xp & 2048) return;
+        with_act(P.act, [&](auto act_c) { run_act<decltype(act_c)::value>(P, B, blk, n0, Pt); });
+    }
+
+    template <int ACT>
+    __device__ __forceinline__ void run_act(const MpLayerP &P, const BlockRow &B, int blk, int n0, float *Pt) {
+        const int tid = threadIdx.x;
+        const float slope = ACT == ACT_PRELU ? P.slope[0] : 0.f;
+        float4 b0 = f4zero(), b1 = f4zero();
+        const __amdgpu_buffer_rsrc_t mrs = x6_block_rsrc<BM>(LAST ? P.aplanes : P.mnext, P.kp, blk);
+        float4 ym[LAST ? UPT : 1][2];  // LAST: this thread's M_t units until P is dead
+#pragma unroll
+        for (int i = 0; i < UPT; ++i) {
+            const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
+            if (v >= UNITS) break;
+            float4 y0 = f4zero(), y1 = f4zero();
+            if (lr < B.bn) {
+                const int b = B.bs + lr;
+                float4 s0 = f4zero(), s1 = f4zero();
+                // the first ELLW entries from the prefetched ELL row, in CSR order (the reference's slot
+                // order); unused slots have weight 0 and are skipped (the CSR lists hold no zero weights)
+                const EllRow &E = ell[i];
+                if (P.sym_rev) {
+#pragma unroll
+                    for (int k = 0; k < ELLW; ++k)
+                        if (E.w[k] != 0.f) msg_term<LDC>(Pt, B.bs + ell_idx(E, k), B.bs, P.sym_rev, c, E.w[k], s0, s1);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < ELLW; ++k)
+                        if (E.w[k] != 0.f) lds_term<LDC>(Pt, ell_idx(E, k), c, E.w[k], s0, s1);
+                }
+                if (ell_more(E))  // more than ELLW entries: the rest from the CSR list
+                    for (int e = P.ptr[b] + ELLW; e < P.ptr[b + 1]; ++e)
+                        msg_term<LDC>(Pt, P.idx[e], B.bs, P.sym_rev, c, P.coef ? P.coef[e] : 1.0f, s0, s1);
+                if (P.bias) { b0 = ld4(P.bias + n0 + c); b1 = ld4(P.bias + n0 + c + 4); }
+                float z[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+                const float r8[8] = {res[i][0].x, res[i][0].y, res[i][0].z, res[i][0].w,
+                                     res[i][1].x, res[i][1].y, res[i][1].z, res[i][1].w};
+                const float b8[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+                for (int q = 0; q < 8; ++q) z[q] = act_fwd(ACT, r8[q] + (z[q] + b8[q]), slope);  // mpn.py:123
+                if (P.p_drop > 0.f)
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) z[q] *= dropout_scale(P.seed, P.layer, b, n0 + c + q, P.p_drop);
+                y0 = make_float4(z[0], z[1], z[2], z[3]);
+                y1 = make_float4(z[4], z[5], z[6], z[7]);
+            }
+            if constexpr (LAST) {
+                ym[i][0] = y0;
+                ym[i][1] = y1;
+            } else if (lr < B.bn) {  // rows past the block's bonds are never loaded by the next layer
+                x6_store8_blk<BM>(mrs, lr, n0 + c, y0, y1);
+            }
+        }
+        if constexpr (LAST) {
+            __syncthreads();  // every read of P done: M_t replaces it
+            float *Mt = Pt;
+#pragma unroll
+            for (int i = 0; i < UPT; ++i) {
+                const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
+                if (v >= UNITS) break;
+                st4(Mt + lr * LDC + c, ym[i][0]);
+                st4(Mt + lr * LDC + c + 4, ym[i][1]);
+            }
+            __syncthreads();
+            // atom aggregate of this column tile: A[a] = Σ_{b into a} w_b M_t[b] (mpn.py:126-131)
+            const __amdgpu_buffer_rsrc_t ars = x6_block_rsrc<BLK_ATOMS>(P.aplanes, P.kp, blk);
+#pragma unroll
+            for (int i = 0; i < AUPT; ++i) {
+                const int v = tid + NT * i;
+                if (v >= B.an * UPR) break;  // rows past the block's atoms are never loaded
+                const int la = v / UPR, c = 8 * (v % UPR), a = B.as + la;
+                const EllRow &E = aell[i];
+                float4 s0 = f4zero(), s1 = f4zero();
+#pragma unroll
+                for (int k = 0; k < ELLW; ++k)
+                    if (E.w[k] != 0.f) lds_term<LDC>(Mt, ell_idx(E, k), c, E.w[k], s0, s1);
+                if (ell_more(E))
+                    for (int q = P.aptr[a] + ELLW; q < P.aptr[a + 1]; ++q)
+                        lds_term<LDC>(Mt, P.aidx[q] - B.bs, c, P.acoef ? P.acoef[q] : 1.0f, s0, s1);
+                x6_store8_blk<BLK_ATOMS>(ars, la, n0 + c, s0, s1);
+            }
+        }
+    }
+};
+
+// grid = nblk * n_tiles (XCD-grouped: the column tiles of a block share an XCD), 64 WM WN threads.
+// LDS: two GEMM stages, reused by the epilogue as P [128][BN + 4] fp32; the last layer then
+// overwrites P with M_t (held in registers across a barrier) for the atom aggregate.
+template <int BN, bool LAST>
+__global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_layer_kernel(MpLayerP P) {
+    constexpr int BM = BLK_BONDS, LDC = BN + 4, WM = MpWaves<BN>::WM, WN = MpWaves<BN>::WN, NT = 64 * WM * WN;
+    // two stages of one chunk (measured: 3 stages slower; two-chunk stages, one barrier per two
+    // chunks, no faster: the chunk time is not bound by load latency or barriers)
+    constexpr int S = 2, CPS = 1;
+    // (<= 80 KB: two workgroups fit one CU's 160 KB, so layers of batches in flight on other
+    // streams co-reside)
+    constexpr int LDS_BYTES = BM * LDC * 4 > S * CPS * x6_stage_bytes<BM, BN>()
+                                  ? BM * LDC * 4
+                                  : S * CPS * x6_stage_bytes<BM, BN>();
+    static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
+    const BlockRow B = load_block(P.blocks, blk);
+    MpEpilogue<BN, NT, LAST> E;
+    auto prefetch = [&]() { E.prefetch(P, B, n0); };
     X6Operands O{};
     O.a0 = P.mprev; O.nkc0 = P.kp >> 5; O.kc0 = P.kp >> 5;
     O.a1 = P.mprev; O.nkc1 = P.kp >> 5; O.kc1 = 0;  // no second segment (a non-null alias: no null arithmetic)
@@ -194,88 +296,176 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
             for (auto &x : r) x = floatx4{0.f, 0.f, 0.f, 0.f};
         prefetch();
     } else {
-#if WD_EXP == 13
-        x6_mainloop<BM, BN, WM, WN, S, CPS>(O, lds, acc);
-#else
         x6_mainloop<BM, BN, WM, WN, S, CPS>(O, lds, acc, prefetch);
-#endif
     }
     __syncthreads();
     float *Pt = reinterpret_cast<float *>(lds);
     x6_acc_to_lds<BM, BN, WM, WN>(acc, Pt);
     __syncthreads();
+    E.run(P, B, blk, n0, Pt);
+}
 
-    const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
-    const __amdgpu_buffer_rsrc_t mrs = x6_block_rsrc<BM>(LAST ? P.aplanes : P.mnext, P.kp, blk);
-    float4 ym[LAST ? UPT : 1][2];  // LAST: this thread's M_t units until P is dead
-#pragma unroll
-    for (int i = 0; i < UPT; ++i) {
-        const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
-        if (v >= UNITS) break;
-        float4 y0 = f4zero(), y1 = f4zero();
-        if (lr < B.bn) {
-            const int b = B.bs + lr;
-            float4 s0 = f4zero(), s1 = f4zero();
-            // the first ELLW entries from the prefetched ELL row, in CSR order (the reference's slot
-            // order); unused slots have weight 0 and are skipped (the CSR lists hold no zero weights)
-            const EllRow &E = ell[i];
-#pragma unroll
-            for (int k = 0; k < ELLW; ++k) {
-                const int j = ell_idx(E, k);
-                if (WD_EXP == 3 || (WD_EXP != 14 && E.w[k] == 0.f)) continue;
-                if (P.sym_rev) msg_term<LDC>(Pt, B.bs + j, B.bs, P.sym_rev, c, E.w[k], s0, s1);
-                else lds_term<LDC>(Pt, j, c, E.w[k], s0, s1);
-            }
-            if (ell_more(E))  // more than ELLW entries: the rest from the CSR list
-                for (int e = P.ptr[b] + ELLW; e < P.ptr[b + 1]; ++e)
-                    msg_term<LDC>(Pt, P.idx[e], B.bs, P.sym_rev, c, P.coef ? P.coef[e] : 1.0f, s0, s1);
-            float4 b0 = f4zero(), b1 = f4zero();
-            if (P.bias) { b0 = ld4(P.bias + n0 + c); b1 = ld4(P.bias + n0 + c + 4); }
-            float z[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-            const float r8[8] = {res[i][0].x, res[i][0].y, res[i][0].z, res[i][0].w,
-                                 res[i][1].x, res[i][1].y, res[i][1].z, res[i][1].w};
-            const float b8[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                float y = act_fwd(P.act, r8[q] + (z[q] + b8[q]), slope);  // mpn.py:123 input + message
-                if (P.p_drop > 0.f) y *= dropout_scale(P.seed, P.layer, b, n0 + c + q, P.p_drop);
-                z[q] = y;
-            }
-            y0 = make_float4(z[0], z[1], z[2], z[3]);
-            y1 = make_float4(z[4], z[5], z[6], z[7]);
-        }
-        if constexpr (LAST) {
-            ym[i][0] = y0;
-            ym[i][1] = y1;
-        } else if (lr < B.bn && WD_EXP != 2) {  // rows past the block's bonds are never loaded by the next layer
-            x6_store8_blk<BM>(mrs, lr, n0 + c, y0, y1);
-        }
+// f(std::integral_constant<int, i>) for i = I .. N-1
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
     }
-    if constexpr (LAST) {
-        __syncthreads();  // every read of P done: M_t replaces it
-        float *Mt = Pt;
+}
+
+// s_waitcnt vmcnt(N), N a compile-time count (0 .. 63), through the builtin so that the compiler's own
+// wait tracking sees it (after it, only the N youngest loads are pending: an LDS-DMA batch older than
+// them no longer blocks counted waits on the register loads behind it)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt field");
+    // gfx9 encoding: vmcnt[3:0] | expcnt[6:4] (7: none) | lgkmcnt[11:8] (15: none) | vmcnt[5:4] << 14
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// Fifteen bf16x8 fragments (3 planes x 5 16-column pieces) of one K-chunk of an LDS W_h image, read
+// by inline asm and complete on return (s_waitcnt lgkmcnt(0) inside): the compiler cannot tell an
+// LDS-DMA target from the chunk being read and would make every ds_read wait for the youngest DMA
+// in flight -- i.e. for the whole layer's loads.  addr = this lane's fragment base of the chunk;
+// plane p, piece b at + p * 5120 + b * 1024 (80-column images, the swizzle is the same for all b).
+__device__ __forceinline__ void rs_read_chunk(uint32_t addr, bf16x8 (&f)[5][3]) {
+    asm volatile(
+        "ds_read_b128 %0, %15\n\t"
+        "ds_read_b128 %1, %15 offset:5120\n\t"
+        "ds_read_b128 %2, %15 offset:10240\n\t"
+        "ds_read_b128 %3, %15 offset:1024\n\t"
+        "ds_read_b128 %4, %15 offset:6144\n\t"
+        "ds_read_b128 %5, %15 offset:11264\n\t"
+        "ds_read_b128 %6, %15 offset:2048\n\t"
+        "ds_read_b128 %7, %15 offset:7168\n\t"
+        "ds_read_b128 %8, %15 offset:12288\n\t"
+        "ds_read_b128 %9, %15 offset:3072\n\t"
+        "ds_read_b128 %10, %15 offset:8192\n\t"
+        "ds_read_b128 %11, %15 offset:13312\n\t"
+        "ds_read_b128 %12, %15 offset:4096\n\t"
+        "ds_read_b128 %13, %15 offset:9216\n\t"
+        "ds_read_b128 %14, %15 offset:14336\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        // early-clobber outputs: a read may land before a later read of the block has taken its address
+        : "=&v"(f[0][0]), "=&v"(f[0][1]), "=&v"(f[0][2]), "=&v"(f[1][0]), "=&v"(f[1][1]), "=&v"(f[1][2]),
+          "=&v"(f[2][0]), "=&v"(f[2][1]), "=&v"(f[2][2]), "=&v"(f[3][0]), "=&v"(f[3][1]), "=&v"(f[3][2]),
+          "=&v"(f[4][0]), "=&v"(f[4][1]), "=&v"(f[4][2])
+        : "v"(addr)
+        : "memory");
+}
+
+// mp_layer_rs_kernel: the same layer for Kp = 320 at 80-column tiles, with the GEMM operands held
+// stationary instead of streamed through recycled LDS stages:
+//   * the tile's whole W_h plane image (10 x 3 x 80 x 64 B = 150 KB) is DMA'd into LDS once;
+//   * each of the 8 waves owns 16 rows of the block and loads its A fragments (10 x 3 bf16x8 per lane,
+//     120 VGPRs) straight from the plane tiles into registers -- A never passes through LDS;
+//   * every load is issued up front, chunk by chunk (A kc, then the W_h DMA of kc); chunk kc's MFMAs
+//     wait (counted vmcnt) only for the loads of chunks <= kc plus one barrier for the other waves'
+//     DMA pieces, so the operand stream runs at the CU's request rate behind the MFMAs;
+//   * rows past the block's bonds are loaded out of bounds of a buffer resource (no memory traffic,
+//     zeros) and waves with no row of the block issue no MFMA.
+constexpr int RS_BN = 80;
+template <int NKC, bool LAST>
+__global__ __launch_bounds__(512) void mp_layer_rs_kernel(MpLayerP P) {
+    constexpr int BM = BLK_BONDS, BN = RS_BN, NT = 512, NW = 8, LDC = BN + 4, TN = BN / 16;
+    constexpr int BPL = BN * 64, BCH = 3 * BPL;   // W_h image bytes per chunk (LDS)
+    constexpr int APL = BM * 64, ACH = 3 * APL;   // A plane-tile bytes per chunk (global, BR = 128)
+    constexpr int BP = 3 * BN / 16;               // 1 KB DMA pieces per chunk (15)
+    constexpr int BPW = 2;                        // per wave: piece c = j NW + wave; c = 15 is a dummy
+    static_assert(BM == 16 * NW && BP == 15 && TN == 5 && BPL == 5120, "layout of rs_read_chunk");
+    static_assert(BM * LDC * 4 <= NKC * BCH, "P tile reuses the W_h image");
+    // the W_h image + one 1 KB landing place for the dummy 16th piece of each chunk
+    __shared__ __attribute__((aligned(16))) uint8_t lds[NKC * BCH + 1024];
+    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
+    const BlockRow B = load_block(P.blocks, blk);
+    // wave-uniform control flow (the wave index from an SGPR): the counted waits need every wave to
+    // issue the same load sequence
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int g = lane >> 4, i16 = lane & 15;
+#define WD_TS(k) if (P.dbg && threadIdx.x == 0) P.dbg[(size_t)blockIdx.x * 8 + (k)] = __builtin_readcyclecounter();
+    WD_TS(0)
+    MpEpilogue<BN, NT, LAST> E;
+    E.prefetch(P, B, n0);  // issued first: older than every operand load, so the counted waits skip them
+    const bool active = 16 * wave < B.bn;
+    // DMA pieces: lane -> (plane, row, 16-B slot) of the chunk image; the bank swizzle goes on the
+    // source address (as x6_mainloop)
+    int bsrc[BPW], bdst[BPW];
 #pragma unroll
-        for (int i = 0; i < UPT; ++i) {
-            const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
-            if (v >= UNITS) break;
-            st4(Mt + lr * LDC + c, ym[i][0]);
-            st4(Mt + lr * LDC + c + 4, ym[i][1]);
-        }
-        __syncthreads();
-        // atom aggregate of this column tile: A[a] = Σ_{b into a} w_b M_t[b] (mpn.py:126-131)
-        const __amdgpu_buffer_rsrc_t ars = x6_block_rsrc<BLK_ATOMS>(P.aplanes, P.kp, blk);
-        if (tid < B.an * UPR) {  // rows past the block's atoms are never loaded
-            const int la = tid / UPR, c = 8 * (tid % UPR), a = B.as + la;
-            float4 s0 = f4zero(), s1 = f4zero();
-#pragma unroll
-            for (int k = 0; k < ELLW; ++k)
-                if (aell.w[k] != 0.f) lds_term<LDC>(Mt, ell_idx(aell, k), c, aell.w[k], s0, s1);
-            if (ell_more(aell))
-                for (int q = P.aptr[a] + ELLW; q < P.aptr[a + 1]; ++q)
-                    lds_term<LDC>(Mt, P.aidx[q] - B.bs, c, P.acoef ? P.acoef[q] : 1.0f, s0, s1);
-            x6_store8_blk<BLK_ATOMS>(ars, la, n0 + c, s0, s1);
-        }
+    for (int j = 0; j < BPW; ++j) {
+        const int c = j * NW + wave, cs = min(c, BP - 1);
+        const int q = 64 * cs + lane, p = (q / (BN * 4)) % 3, r = (q >> 2) % BN, sl = q & 3;
+        bsrc[j] = p * BPL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
+        bdst[j] = c < BP ? 1024 * c : -1;
     }
+    // A fragments through a buffer resource over the block's plane tiles: lane (i16, g) reads row
+    // 16 wave + i16, bytes 16 g .. of each plane row; rows past the block's bonds read out of bounds
+    const int arow = 16 * wave + i16;
+    const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(P.mprev) + (size_t)blk * NKC * ACH, 0, NKC * ACH, 0x00020000);
+    const uint32_t aoff = arow < B.bn ? (uint32_t)(arow * 64 + 16 * g) : 0x80000000u;
+    const uint8_t *bblk = P.wh + (size_t)nt * NKC * BCH;
+    bf16x8 af[NKC][3];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#ifndef RS_BUF
+#define RS_BUF 1
+#endif
+            if (RS_BUF) af[kc][p] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ars, aoff + kc * ACH + p * APL, 0, 0));
+            else af[kc][p] = *reinterpret_cast<const bf16x8 *>(P.mprev + (size_t)blk * NKC * ACH + (arow * 64 + 16 * g) + kc * ACH + p * APL);
+#pragma unroll
+        for (int j = 0; j < BPW; ++j)
+            glds16(bblk + kc * BCH + bsrc[j], bdst[j] < 0 ? lds + NKC * BCH : lds + kc * BCH + bdst[j]);
+        __builtin_amdgcn_sched_barrier(0);  // issue order chunk by chunk (the counted waits rely on it)
+    }
+    WD_TS(1)
+    floatx4 acc[1][TN];
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[0][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // LDS byte address (not the generic address of the array) of this lane's fragment slot
+    const uint32_t fbase = (uint32_t)(uintptr_t)(lds_void_t *)lds + (uint32_t)x6_slot(i16, g);
+    static_for<0, NKC>([&](auto kc_c) {
+        constexpr int kc = decltype(kc_c)::value;
+#ifndef RS_SLACK
+#define RS_SLACK 0
+#endif
+        constexpr int WC = (NKC - 1 - kc) * (3 + BPW) - RS_SLACK;
+        wait_vm<(WC < 0 ? 0 : WC)>();  // this wave's loads of chunks <= kc landed ...
+        __builtin_amdgcn_s_barrier();              // ... and every wave's DMA pieces of chunk kc
+        if (kc == 0) WD_TS(2)
+        if (active && !(P.xp & 1)) {
+            bf16x8 bfr[TN][3];
+#ifndef RS_ASM
+#define RS_ASM 1
+#endif
+            if (RS_ASM) rs_read_chunk(fbase + kc * BCH, bfr);
+            else {
+                for (int b = 0; b < TN; ++b)
+                    for (int p = 0; p < 3; ++p) bfr[b][p] = *reinterpret_cast<const bf16x8 *>(lds + kc * BCH + p * BPL + x6_slot(b * 16 + i16, g));
+            }
+#pragma unroll
+            for (int b = 0; b < TN; ++b) {
+                // plane products hh, hm, mh, hl, lh, mm
+                constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};
+#pragma unroll
+                for (int t = 0; t < 6; ++t)
+                    acc[0][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kc][PA[t]], bfr[b][PB[t]], acc[0][b], 0, 0, 0);
+            }
+        }
+    });
+    WD_TS(3)
+    __syncthreads();  // every wave done reading the W_h image: the P tile replaces it
+    WD_TS(4)
+    float *Pt = reinterpret_cast<float *>(lds);
+    x6_acc_to_lds<BM, BN, NW, 1>(acc, Pt);
+    __syncthreads();
+    WD_TS(5)
+    if (!(P.xp & 8)) E.run(P, B, blk, n0, Pt);
+    WD_TS(6)
 }
 
 // ------------------------------------------------------------------------------------------------
