@@ -136,7 +136,8 @@ template <> struct MpWaves<80> { static constexpr int WM = 2, WN = 5; };
 // mp_layer epilogue, shared by both layer kernels: residual rows and gather lists prefetched during the
 // GEMM, then (P tile in LDS) the in-block gather, bias, residual, activation, dropout and the plane
 // stores of M_t -- or, in the last layer, the atom aggregate of M_t.
-template <int BN, int NT, bool LAST>
+// MF: M_t is stored as fp32 blocked rows (mp_layer_rs_kernel's A operand) instead of plane tiles
+template <int BN, int NT, bool LAST, bool MF = false>
 struct MpEpilogue {
     static constexpr int BM = BLK_BONDS, LDC = BN + 4;
     static constexpr int UPR = BN / 8, UNITS = BM * UPR, UPT = (UNITS + NT - 1) / NT;  // 8-column units
@@ -186,7 +187,8 @@ struct MpEpilogue {
         const int tid = threadIdx.x;
         const float slope = ACT == ACT_PRELU ? P.slope[0] : 0.f;
         float4 b0 = f4zero(), b1 = f4zero();
-        const __amdgpu_buffer_rsrc_t mrs = x6_block_rsrc<BM>(LAST ? P.aplanes : P.mnext, P.kp, blk);
+        const __amdgpu_buffer_rsrc_t mrs = MF && !LAST ? f32_block_rsrc<BM>(reinterpret_cast<float *>(P.mnext), P.kp, blk)
+                                                       : x6_block_rsrc<BM>(LAST ? P.aplanes : P.mnext, P.kp, blk);
         float4 ym[LAST ? UPT : 1][2];  // LAST: this thread's M_t units until P is dead
 #pragma unroll
         for (int i = 0; i < UPT; ++i) {
@@ -228,7 +230,8 @@ struct MpEpilogue {
                 ym[i][0] = y0;
                 ym[i][1] = y1;
             } else if (lr < B.bn) {  // rows past the block's bonds are never loaded by the next layer
-                x6_store8_blk<BM>(mrs, lr, n0 + c, y0, y1);
+                if constexpr (MF) f32_store8_blk(mrs, P.kp, lr, n0 + c, y0, y1);
+                else x6_store8_blk<BM>(mrs, lr, n0 + c, y0, y1);
             }
         }
         if constexpr (LAST) {
@@ -358,19 +361,21 @@ __device__ __forceinline__ void rs_read_chunk(uint32_t addr, bf16x8 (&f)[5][3]) 
 // mp_layer_rs_kernel: the same layer for Kp = 320 at 80-column tiles, with the GEMM operands held
 // stationary instead of streamed through recycled LDS stages:
 //   * the tile's whole W_h plane image (10 x 3 x 80 x 64 B = 150 KB) is DMA'd into LDS once;
-//   * each of the 8 waves owns 16 rows of the block and loads its A fragments (10 x 3 bf16x8 per lane,
-//     120 VGPRs) straight from the plane tiles into registers -- A never passes through LDS;
+//   * messages live as fp32 blocked rows (4 B per value where plane tiles take 6): each of the 8 waves
+//     owns 16 rows of the block, loads its A values (10 chunks x 8 fp32 per lane, 80 VGPRs) straight
+//     into registers and splits a chunk into its bf16x3 fragments just before that chunk's MFMAs
+//     (the same split a plane-tile producer makes: the products are bitwise those of mp_layer_kernel);
 //   * every load is issued up front, chunk by chunk (A kc, then the W_h DMA of kc); chunk kc's MFMAs
 //     wait (counted vmcnt) only for the loads of chunks <= kc plus one barrier for the other waves'
 //     DMA pieces, so the operand stream runs at the CU's request rate behind the MFMAs;
 //   * rows past the block's bonds are loaded out of bounds of a buffer resource (no memory traffic,
 //     zeros) and waves with no row of the block issue no MFMA.
+// Writes M_t as fp32 blocked rows (the last layer: A's plane tiles, as mp_layer_kernel).
 constexpr int RS_BN = 80;
 template <int NKC, bool LAST>
 __global__ __launch_bounds__(512) void mp_layer_rs_kernel(MpLayerP P) {
     constexpr int BM = BLK_BONDS, BN = RS_BN, NT = 512, NW = 8, LDC = BN + 4, TN = BN / 16;
     constexpr int BPL = BN * 64, BCH = 3 * BPL;   // W_h image bytes per chunk (LDS)
-    constexpr int APL = BM * 64, ACH = 3 * APL;   // A plane-tile bytes per chunk (global, BR = 128)
     constexpr int BP = 3 * BN / 16;               // 1 KB DMA pieces per chunk (15)
     constexpr int BPW = 2;                        // per wave: piece c = j NW + wave; c = 15 is a dummy
     static_assert(BM == 16 * NW && BP == 15 && TN == 5 && BPL == 5120, "layout of rs_read_chunk");
@@ -386,8 +391,8 @@ __global__ __launch_bounds__(512) void mp_layer_rs_kernel(MpLayerP P) {
     const int g = lane >> 4, i16 = lane & 15;
 #define WD_TS(k) if (P.dbg && threadIdx.x == 0) P.dbg[(size_t)blockIdx.x * 8 + (k)] = __builtin_readcyclecounter();
     WD_TS(0)
-    MpEpilogue<BN, NT, LAST> E;
-    E.prefetch(P, B, n0);  // issued first: older than every operand load, so the counted waits skip them
+    MpEpilogue<BN, NT, LAST, true> E;
+    if (!(P.xp & 16384)) E.prefetch(P, B, n0);  // issued first: older than every operand load, so the counted waits skip them
     const bool active = 16 * wave < B.bn;
     // DMA pieces: lane -> (plane, row, 16-B slot) of the chunk image; the bank swizzle goes on the
     // source address (as x6_mainloop)
@@ -399,29 +404,37 @@ __global__ __launch_bounds__(512) void mp_layer_rs_kernel(MpLayerP P) {
         bsrc[j] = p * BPL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
         bdst[j] = c < BP ? 1024 * c : -1;
     }
-    // A fragments through a buffer resource over the block's plane tiles: lane (i16, g) reads row
-    // 16 wave + i16, bytes 16 g .. of each plane row; rows past the block's bonds read out of bounds
+    // A values through a buffer resource over the block's fp32 rows: lane (i16, g) reads row
+    // 16 wave + i16, columns 32 kc + 8 g .. + 7 (32 bytes); rows past the block's bonds read out of bounds
     const int arow = 16 * wave + i16;
-    const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(P.mprev) + (size_t)blk * NKC * ACH, 0, NKC * ACH, 0x00020000);
-    const uint32_t aoff = arow < B.bn ? (uint32_t)(arow * 64 + 16 * g) : 0x80000000u;
+    const __amdgpu_buffer_rsrc_t ars = f32_block_rsrc<BM>(reinterpret_cast<float *>(const_cast<uint8_t *>(P.mprev)), P.kp, blk);
+    const uint32_t aoff = arow < B.bn ? (uint32_t)((arow * P.kp + 8 * g) * 4) : 0x80000000u;
     const uint8_t *bblk = P.wh + (size_t)nt * NKC * BCH;
-    bf16x8 af[NKC][3];
-    __builtin_amdgcn_sched_barrier(0);
+    constexpr int AL = 2;  // A loads per chunk
+    float4 af[NKC][AL];
+    // chunk kc's loads: this wave's A values, then its W_h DMA pieces
+    auto issue = [&](auto kc_c) {
+        constexpr int kc = decltype(kc_c)::value;
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int kc = 0; kc < NKC; ++kc) {
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-#ifndef RS_BUF
-#define RS_BUF 1
-#endif
-            if (RS_BUF) af[kc][p] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ars, aoff + kc * ACH + p * APL, 0, 0));
-            else af[kc][p] = *reinterpret_cast<const bf16x8 *>(P.mprev + (size_t)blk * NKC * ACH + (arow * 64 + 16 * g) + kc * ACH + p * APL);
+        for (int q = 0; q < AL; ++q)
+            af[kc][q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ars, aoff + kc * 128 + 16 * q, 0, 0));
 #pragma unroll
         for (int j = 0; j < BPW; ++j)
             glds16(bblk + kc * BCH + bsrc[j], bdst[j] < 0 ? lds + NKC * BCH : lds + kc * BCH + bdst[j]);
         __builtin_amdgcn_sched_barrier(0);  // issue order chunk by chunk (the counted waits rely on it)
-    }
+    };
+    // LA chunks in flight ahead of the one multiplied, issued chunk-major across the waves (a barrier
+    // between chunks): a wave issuing all its chunks back to back queues its later chunks ahead of the
+    // other waves' first ones, and the first chunk's barrier then waits for nearly every load
+#ifndef RS_LA
+#define RS_LA 3
+#endif
+    constexpr int LA = RS_LA;
+    static_for<0, LA>([&](auto c) {
+        issue(c);
+        __builtin_amdgcn_s_barrier();
+    });
     WD_TS(1)
     floatx4 acc[1][TN];
 #pragma unroll
@@ -430,33 +443,26 @@ __global__ __launch_bounds__(512) void mp_layer_rs_kernel(MpLayerP P) {
     const uint32_t fbase = (uint32_t)(uintptr_t)(lds_void_t *)lds + (uint32_t)x6_slot(i16, g);
     static_for<0, NKC>([&](auto kc_c) {
         constexpr int kc = decltype(kc_c)::value;
-#ifndef RS_SLACK
-#define RS_SLACK 0
-#endif
-        constexpr int WC = (NKC - 1 - kc) * (3 + BPW) - RS_SLACK;
-        wait_vm<(WC < 0 ? 0 : WC)>();  // this wave's loads of chunks <= kc landed ...
-        __builtin_amdgcn_s_barrier();              // ... and every wave's DMA pieces of chunk kc
+        constexpr int AHEAD = (LA - 1 < NKC - 1 - kc) ? LA - 1 : NKC - 1 - kc;  // younger chunks in flight
+        wait_vm<AHEAD * (AL + BPW)>();  // this wave's loads of chunks <= kc landed ...
+        __builtin_amdgcn_s_barrier();   // ... and every wave's DMA pieces of chunk kc
+        if constexpr (kc + LA < NKC) issue(std::integral_constant<int, kc + LA>{});
         if (kc == 0) WD_TS(2)
         if (active && !(P.xp & 1)) {
-            bf16x8 bfr[TN][3];
-#ifndef RS_ASM
-#define RS_ASM 1
-#endif
-            if (RS_ASM) rs_read_chunk(fbase + kc * BCH, bfr);
-            else {
-                for (int b = 0; b < TN; ++b)
-                    for (int p = 0; p < 3; ++p) bfr[b][p] = *reinterpret_cast<const bf16x8 *>(lds + kc * BCH + p * BPL + x6_slot(b * 16 + i16, g));
-            }
+            bf16x8 bfr[TN][3], a3[3];
+            rs_read_chunk(fbase + kc * BCH, bfr);
+            split8(af[kc][0], af[kc][1], a3[0], a3[1], a3[2]);
 #pragma unroll
             for (int b = 0; b < TN; ++b) {
                 // plane products hh, hm, mh, hl, lh, mm
                 constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};
 #pragma unroll
                 for (int t = 0; t < 6; ++t)
-                    acc[0][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kc][PA[t]], bfr[b][PB[t]], acc[0][b], 0, 0, 0);
+                    acc[0][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3[PA[t]], bfr[b][PB[t]], acc[0][b], 0, 0, 0);
             }
         }
     });
+    if (P.xp & 16384) E.prefetch(P, B, n0);
     WD_TS(3)
     __syncthreads();  // every wave done reading the W_h image: the P tile replaces it
     WD_TS(4)
@@ -492,7 +498,8 @@ struct EmbedP {
     int Fa, Fb, Hk, n_tiles;
     int act; const float *slope;
     float *inp;                  // [Rp][Hk]
-    uint8_t *mplanes;            // M0 plane tiles, blocked bond rows (BR 128)
+    uint8_t *mplanes;            // M0: plane tiles, blocked bond rows (BR 128) -- or, mf, fp32 blocked rows
+    int mf;
 };
 
 // Stage rows [0, rows0) of src0 and [0, rows1) of src1 (BN columns from n0, row stride ld, fp32) into
@@ -551,7 +558,10 @@ __global__ __launch_bounds__(512) void embed_kernel(EmbedP P) {
     }
     __syncthreads();
     const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
-    const __amdgpu_buffer_rsrc_t mrs = x6_block_rsrc<BLK_BONDS>(P.mplanes, P.Hk, blk);
+    const __amdgpu_buffer_rsrc_t mrs = P.mf ? f32_block_rsrc<BLK_BONDS>(reinterpret_cast<float *>(P.mplanes), P.Hk, blk)
+                                            : x6_block_rsrc<BLK_BONDS>(P.mplanes, P.Hk, blk);
+    with_act(P.act, [&](auto act_c) {
+    constexpr int ACT = decltype(act_c)::value;
     for (int v = tid; v < B.bn * U8; v += NT) {
         const int lb = v / U8, c = 8 * (v % U8), b = B.bs + lb;
         const int sa = P.src_blk[b];
@@ -569,12 +579,14 @@ __global__ __launch_bounds__(512) void embed_kernel(EmbedP P) {
         float *zr = P.inp + (size_t)b * P.Hk + n0 + c;
         st4(zr, z0);
         st4(zr + 4, z1);
-        const float4 y0 = make_float4(act_fwd(P.act, z0.x, slope), act_fwd(P.act, z0.y, slope),
-                                      act_fwd(P.act, z0.z, slope), act_fwd(P.act, z0.w, slope));
-        const float4 y1 = make_float4(act_fwd(P.act, z1.x, slope), act_fwd(P.act, z1.y, slope),
-                                      act_fwd(P.act, z1.z, slope), act_fwd(P.act, z1.w, slope));
-        x6_store8_blk<BLK_BONDS>(mrs, lb, n0 + c, y0, y1);
+        const float4 y0 = make_float4(act_fwd(ACT, z0.x, slope), act_fwd(ACT, z0.y, slope),
+                                      act_fwd(ACT, z0.z, slope), act_fwd(ACT, z0.w, slope));
+        const float4 y1 = make_float4(act_fwd(ACT, z1.x, slope), act_fwd(ACT, z1.y, slope),
+                                      act_fwd(ACT, z1.z, slope), act_fwd(ACT, z1.w, slope));
+        if (P.mf) f32_store8_blk(mrs, P.Hk, lb, n0 + c, y0, y1);
+        else x6_store8_blk<BLK_BONDS>(mrs, lb, n0 + c, y0, y1);
     }
+    });
 }
 
 constexpr int WO_MAXK = 160;  // f_atoms / f_bonds columns embed_kernel stages (Fa, Fb <= 160)
@@ -674,8 +686,9 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     }
     __syncthreads();
     // h = act(. + b_o) (* dropout), in place (mpn.py:133-134)
-    {
-        const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
+    with_act(P.act, [&](auto act_c) {
+        constexpr int ACT = decltype(act_c)::value;
+        const float slope = ACT == ACT_PRELU ? P.slope[0] : 0.f;
 #pragma unroll
         for (int j = 0; j < EPU; ++j) {
             const int v = tid + NT * j;
@@ -685,14 +698,13 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
             hv.x += eo[j].x; hv.y += eo[j].y; hv.z += eo[j].z; hv.w += eo[j].w;  // (0 without codes)
             float z[4] = {hv.x + bb.x, hv.y + bb.y, hv.z + bb.z, hv.w + bb.w};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                z[q] = act_fwd(P.act, z[q], slope);
-                if (P.p_drop > 0.f && la < B.an)
-                    z[q] *= dropout_scale(P.seed, P.layer, B.as + la, n0 + c + q, P.p_drop);
-            }
+            for (int q = 0; q < 4; ++q) z[q] = act_fwd(ACT, z[q], slope);
+            if (P.p_drop > 0.f && la < B.an)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) z[q] *= dropout_scale(P.seed, P.layer, B.as + la, n0 + c + q, P.p_drop);
             st4(H + la * LDC + c, make_float4(z[0], z[1], z[2], z[3]));
         }
-    }
+    });
     __syncthreads();
     // readout (mpn.py:145-171) of this block's molecules, columns n0 .. n0 + BN - 1: eight lanes per
     // (molecule, column), lane j summing the molecule's atoms j, j + 8, ... from LDS, then a fixed xor

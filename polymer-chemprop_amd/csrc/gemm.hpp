@@ -44,9 +44,9 @@ struct Epi {
     uint32_t layer;
 };
 
-template <int TM, int TN>
-__device__ __forceinline__ void epilogue(const Epi &E, floatx16 (&acc)[TM][TN], int i0, int j0, int h, int l32,
-                                         int M, int N, float *Y) {
+template <int ACT, int TM, int TN>
+__device__ __forceinline__ void epilogue_act(const Epi &E, floatx16 (&acc)[TM][TN], int i0, int j0, int h, int l32,
+                                             int M, int N, float *Y) {
     const float slope = (E.kind == EPI_ACT && E.act == ACT_PRELU) ? E.slope[0] : 0.f;
 #pragma unroll
     for (int a = 0; a < TM; ++a)
@@ -65,7 +65,7 @@ __device__ __forceinline__ void epilogue(const Epi &E, floatx16 (&acc)[TM][TN], 
                     float z = v + bias;
                     if (E.resid) z += E.resid[o];
                     if (E.Z) E.Z[o] = z;
-                    float y = act_fwd(E.act, z, slope);
+                    float y = act_fwd(ACT, z, slope);
                     if (E.p_drop > 0.f) y *= dropout_scale(E.seed, E.layer, i, j, E.p_drop);
                     Y[o] = y;
                 } else {
@@ -116,9 +116,9 @@ struct EpiPrefetch {
     }
 };
 
-template <int BM, int BN, int NT>
-__device__ __forceinline__ void epilogue_v4(const Epi &E, const float *C, int ldc, int m0, int n0, int M, int N,
-                                            const EpiPrefetch<BM, BN, NT> &ep) {
+template <int ACT, int BM, int BN, int NT>
+__device__ __forceinline__ void epilogue_v4_act(const Epi &E, const float *C, int ldc, int m0, int n0, int M, int N,
+                                                const EpiPrefetch<BM, BN, NT> &ep) {
     using EP = EpiPrefetch<BM, BN, NT>;
     const int t = threadIdx.x, cl = (t % EP::C4) * 4, j = n0 + cl;
     if (j >= N) return;
@@ -138,7 +138,7 @@ __device__ __forceinline__ void epilogue_v4(const Epi &E, const float *C, int ld
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 z[q] = vv[q] + bb[q] + rr[q];
-                float y = act_fwd(E.act, z[q], slope);
+                float y = act_fwd(ACT, z[q], slope);
                 if (E.p_drop > 0.f) y *= dropout_scale(E.seed, E.layer, i, j + q, E.p_drop);
                 out[q] = y;
             }
@@ -171,6 +171,24 @@ __device__ __forceinline__ void epilogue_v4(const Epi &E, const float *C, int ld
     }
 }
 
+
+// the epilogues with the activation dispatched once per call (common.hpp with_act)
+template <int TM, int TN>
+__device__ __forceinline__ void epilogue(const Epi &E, floatx16 (&acc)[TM][TN], int i0, int j0, int h, int l32,
+                                         int M, int N, float *Y) {
+    if (E.kind == EPI_ACT)
+        with_act(E.act, [&](auto a) { epilogue_act<decltype(a)::value>(E, acc, i0, j0, h, l32, M, N, Y); });
+    else
+        epilogue_act<ACT_IDENTITY>(E, acc, i0, j0, h, l32, M, N, Y);
+}
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void epilogue_v4(const Epi &E, const float *C, int ldc, int m0, int n0, int M, int N,
+                                            const EpiPrefetch<BM, BN, NT> &ep) {
+    if (E.kind == EPI_ACT)
+        with_act(E.act, [&](auto a) { epilogue_v4_act<decltype(a)::value>(E, C, ldc, m0, n0, M, N, ep); });
+    else
+        epilogue_v4_act<ACT_IDENTITY>(E, C, ldc, m0, n0, M, N, ep);
+}
 
 template <int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_nt16_kernel(NtParams P) {

@@ -643,8 +643,12 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
         // categorical codes (compact graphs): the input layer and the f_atoms half of W_o as sums of
         // weight columns instead of GEMMs over the one-hot rows (fused_mp.hpp embed_kernel)
         const bool codes = g->atom_codes && g->bond_src_blk && g->bond_tail && D.Fb <= WO_MAXK && D.Fa <= WO_MAXK;
+        // register-stationary layers (fused_mp.hpp mp_layer_rs_kernel): Hk = 320 at 80-column tiles, fed by
+        // embed_kernel with fp32 messages
+        const bool rs = codes && bn80 && Hk == 32 * 10 && D.T > 1;
         if (codes) {
             EmbedP E{};
+            E.mf = rs;
             E.codes = g->atom_codes; E.src_blk = g->bond_src_blk; E.tail = g->bond_tail;
             E.wt = W(PL.WiT); E.woat = W(PL.WoaT); E.eo = F(L.Eo); E.bias = p->b_i ? W(PL.bi) : nullptr; E.blocks = g->blocks;
             E.Fa = D.Fa; E.Fb = D.Fb; E.Hk = Hk; E.n_tiles = Hk / BNf;
@@ -693,7 +697,7 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
                 });
             }
             M.dbg = ts_on ? tsbuf : nullptr;
-            if (bn80 && Hk == 32 * 10 && (xpv & 1024)) {  // (in progress: not yet faster than mp_layer_kernel)
+            if (rs) {
                 // the W_h tile fits LDS whole: register-stationary layer (fused_mp.hpp mp_layer_rs_kernel)
                 if (last) hipLaunchKernelGGL((mp_layer_rs_kernel<10, true>), grid, dim3(512), 0, st, M);
                 else hipLaunchKernelGGL((mp_layer_rs_kernel<10, false>), grid, dim3(512), 0, st, M);
