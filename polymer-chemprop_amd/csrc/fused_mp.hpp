@@ -59,13 +59,6 @@ __device__ __forceinline__ EllRow ell_load(const uint8_t *idx, const float *coef
 __device__ __forceinline__ int ell_idx(const EllRow &e, int k) { return (e.ix[k >> 2] >> (8 * (k & 3))) & 0x7f; }
 __device__ __forceinline__ bool ell_more(const EllRow &e) { return e.ix[ELLW / 4 - 1] & 0x80000000u; }
 
-// WD_EXP (timing experiments only, never set in the product build): 1 = skip the layer GEMM,
-// 2 = skip the layer's plane stores, 3 = skip the in-block gather, 4 = skip the residual prefetch,
-// 6 = skip residual and ELL prefetch; wo_readout: 20 = skip the molecule readout
-#ifndef WD_EXP
-#define WD_EXP 0
-#endif
-
 // WdGraph.blocks row: {bond_start, bond_count, atom_start, atom_count, mol_lo, mol_hi, -, -}
 struct BlockRow { int bs, bn, as, an, ml, mh; };
 __device__ __forceinline__ BlockRow load_block(const int32_t *blocks, int i) {
@@ -115,8 +108,6 @@ struct MpLayerP {
     const uint8_t *aell_idx; const float *aell_coef;
     uint8_t *aplanes;           // A: blocked atom plane tiles [nblk * 64][kp]
     int n_tiles;                // Hk / BN
-    int xp;                     // TEMP experiment bits
-    uint64_t *dbg;              // TEMP timestamps
 };
 
 // Wave layout of the fused kernels per column-tile width: BN = 64 -> 4 x 2 waves, BN = 80 -> 2 x 5.
@@ -125,19 +116,12 @@ struct MpLayerP {
 // bytes to stream.
 template <int BN> struct MpWaves;
 template <> struct MpWaves<64> { static constexpr int WM = 4, WN = 2; };
-#if WD_EXP == 7
-template <> struct MpWaves<80> { static constexpr int WM = 8, WN = 1; };
-#elif WD_EXP == 8
-template <> struct MpWaves<80> { static constexpr int WM = 4, WN = 1; };
-#else
 template <> struct MpWaves<80> { static constexpr int WM = 2, WN = 5; };
-#endif
 
 // mp_layer epilogue, shared by both layer kernels: residual rows and gather lists prefetched during the
 // GEMM, then (P tile in LDS) the in-block gather, bias, residual, activation, dropout and the plane
 // stores of M_t -- or, in the last layer, the atom aggregate of M_t.
-// MF: M_t is stored as fp32 blocked rows (mp_layer_rs_kernel's A operand) instead of plane tiles
-template <int BN, int NT, bool LAST, bool MF = false>
+template <int BN, int NT, bool LAST>
 struct MpEpilogue {
     static constexpr int BM = BLK_BONDS, LDC = BN + 4;
     static constexpr int UPR = BN / 8, UNITS = BM * UPR, UPT = (UNITS + NT - 1) / NT;  // 8-column units
@@ -161,11 +145,9 @@ struct MpEpilogue {
             if (v < UNITS && lr < B.bn) {
                 const size_t b = B.bs + lr;
                 const float *s = P.inp + b * P.kp + n0 + c;
-                if (WD_EXP != 4 && WD_EXP != 6) {
-                    res[i][0] = ld4(s);
-                    res[i][1] = ld4(s + 4);
-                }
-                if (WD_EXP != 6) ell[i] = ell_load(P.ell_idx, P.ell_coef, b);
+                res[i][0] = ld4(s);
+                res[i][1] = ld4(s + 4);
+                ell[i] = ell_load(P.ell_idx, P.ell_coef, b);
             }
         }
         if constexpr (LAST)
@@ -178,7 +160,6 @@ struct MpEpilogue {
 
     // Pt: the P = M_{t-1} W_hᵀ tile [BM][LDC] fp32 in LDS (every write of it done and synchronised)
     __device__ __forceinline__ void run(const MpLayerP &P, const BlockRow &B, int blk, int n0, float *Pt) {
-        if (P.xp & 2048) return;
         with_act(P.act, [&](auto act_c) { run_act<decltype(act_c)::value>(P, B, blk, n0, Pt); });
     }
 
@@ -187,8 +168,7 @@ struct MpEpilogue {
         const int tid = threadIdx.x;
         const float slope = ACT == ACT_PRELU ? P.slope[0] : 0.f;
         float4 b0 = f4zero(), b1 = f4zero();
-        const __amdgpu_buffer_rsrc_t mrs = MF && !LAST ? f32_block_rsrc<BM>(reinterpret_cast<float *>(P.mnext), P.kp, blk)
-                                                       : x6_block_rsrc<BM>(LAST ? P.aplanes : P.mnext, P.kp, blk);
+        const __amdgpu_buffer_rsrc_t mrs = x6_block_rsrc<BM>(LAST ? P.aplanes : P.mnext, P.kp, blk);
         float4 ym[LAST ? UPT : 1][2];  // LAST: this thread's M_t units until P is dead
 #pragma unroll
         for (int i = 0; i < UPT; ++i) {
@@ -230,8 +210,7 @@ struct MpEpilogue {
                 ym[i][0] = y0;
                 ym[i][1] = y1;
             } else if (lr < B.bn) {  // rows past the block's bonds are never loaded by the next layer
-                if constexpr (MF) f32_store8_blk(mrs, P.kp, lr, n0 + c, y0, y1);
-                else x6_store8_blk<BM>(mrs, lr, n0 + c, y0, y1);
+                x6_store8_blk<BM>(mrs, lr, n0 + c, y0, y1);
             }
         }
         if constexpr (LAST) {
@@ -294,184 +273,12 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
     O.a_rows = B.bn;
     O.b = P.wh + (size_t)nt * (P.kp >> 5) * (3 * BN * 64);
     floatx4 acc[BM / WM / 16][BN / WN / 16];
-    if (WD_EXP == 1) {
-        for (auto &r : acc)
-            for (auto &x : r) x = floatx4{0.f, 0.f, 0.f, 0.f};
-        prefetch();
-    } else {
-        x6_mainloop<BM, BN, WM, WN, S, CPS>(O, lds, acc, prefetch);
-    }
+    x6_mainloop<BM, BN, WM, WN, S, CPS>(O, lds, acc, prefetch);
     __syncthreads();
     float *Pt = reinterpret_cast<float *>(lds);
     x6_acc_to_lds<BM, BN, WM, WN>(acc, Pt);
     __syncthreads();
     E.run(P, B, blk, n0, Pt);
-}
-
-// f(std::integral_constant<int, i>) for i = I .. N-1
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for(F &&f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for<I + 1, N>(f);
-    }
-}
-
-// s_waitcnt vmcnt(N), N a compile-time count (0 .. 63), through the builtin so that the compiler's own
-// wait tracking sees it (after it, only the N youngest loads are pending: an LDS-DMA batch older than
-// them no longer blocks counted waits on the register loads behind it)
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-    static_assert(N >= 0 && N < 64, "vmcnt field");
-    // gfx9 encoding: vmcnt[3:0] | expcnt[6:4] (7: none) | lgkmcnt[11:8] (15: none) | vmcnt[5:4] << 14
-    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
-
-// Fifteen bf16x8 fragments (3 planes x 5 16-column pieces) of one K-chunk of an LDS W_h image, read
-// by inline asm and complete on return (s_waitcnt lgkmcnt(0) inside): the compiler cannot tell an
-// LDS-DMA target from the chunk being read and would make every ds_read wait for the youngest DMA
-// in flight -- i.e. for the whole layer's loads.  addr = this lane's fragment base of the chunk;
-// plane p, piece b at + p * 5120 + b * 1024 (80-column images, the swizzle is the same for all b).
-__device__ __forceinline__ void rs_read_chunk(uint32_t addr, bf16x8 (&f)[5][3]) {
-    asm volatile(
-        "ds_read_b128 %0, %15\n\t"
-        "ds_read_b128 %1, %15 offset:5120\n\t"
-        "ds_read_b128 %2, %15 offset:10240\n\t"
-        "ds_read_b128 %3, %15 offset:1024\n\t"
-        "ds_read_b128 %4, %15 offset:6144\n\t"
-        "ds_read_b128 %5, %15 offset:11264\n\t"
-        "ds_read_b128 %6, %15 offset:2048\n\t"
-        "ds_read_b128 %7, %15 offset:7168\n\t"
-        "ds_read_b128 %8, %15 offset:12288\n\t"
-        "ds_read_b128 %9, %15 offset:3072\n\t"
-        "ds_read_b128 %10, %15 offset:8192\n\t"
-        "ds_read_b128 %11, %15 offset:13312\n\t"
-        "ds_read_b128 %12, %15 offset:4096\n\t"
-        "ds_read_b128 %13, %15 offset:9216\n\t"
-        "ds_read_b128 %14, %15 offset:14336\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        // early-clobber outputs: a read may land before a later read of the block has taken its address
-        : "=&v"(f[0][0]), "=&v"(f[0][1]), "=&v"(f[0][2]), "=&v"(f[1][0]), "=&v"(f[1][1]), "=&v"(f[1][2]),
-          "=&v"(f[2][0]), "=&v"(f[2][1]), "=&v"(f[2][2]), "=&v"(f[3][0]), "=&v"(f[3][1]), "=&v"(f[3][2]),
-          "=&v"(f[4][0]), "=&v"(f[4][1]), "=&v"(f[4][2])
-        : "v"(addr)
-        : "memory");
-}
-
-// mp_layer_rs_kernel: the same layer for Kp = 320 at 80-column tiles, with the GEMM operands held
-// stationary instead of streamed through recycled LDS stages:
-//   * the tile's whole W_h plane image (10 x 3 x 80 x 64 B = 150 KB) is DMA'd into LDS once;
-//   * messages live as fp32 blocked rows (4 B per value where plane tiles take 6): each of the 8 waves
-//     owns 16 rows of the block, loads its A values (10 chunks x 8 fp32 per lane, 80 VGPRs) straight
-//     into registers and splits a chunk into its bf16x3 fragments just before that chunk's MFMAs
-//     (the same split a plane-tile producer makes: the products are bitwise those of mp_layer_kernel);
-//   * every load is issued up front, chunk by chunk (A kc, then the W_h DMA of kc); chunk kc's MFMAs
-//     wait (counted vmcnt) only for the loads of chunks <= kc plus one barrier for the other waves'
-//     DMA pieces, so the operand stream runs at the CU's request rate behind the MFMAs;
-//   * rows past the block's bonds are loaded out of bounds of a buffer resource (no memory traffic,
-//     zeros) and waves with no row of the block issue no MFMA.
-// Writes M_t as fp32 blocked rows (the last layer: A's plane tiles, as mp_layer_kernel).
-constexpr int RS_BN = 80;
-template <int NKC, bool LAST>
-__global__ __launch_bounds__(512) void mp_layer_rs_kernel(MpLayerP P) {
-    constexpr int BM = BLK_BONDS, BN = RS_BN, NT = 512, NW = 8, LDC = BN + 4, TN = BN / 16;
-    constexpr int BPL = BN * 64, BCH = 3 * BPL;   // W_h image bytes per chunk (LDS)
-    constexpr int BP = 3 * BN / 16;               // 1 KB DMA pieces per chunk (15)
-    constexpr int BPW = 2;                        // per wave: piece c = j NW + wave; c = 15 is a dummy
-    static_assert(BM == 16 * NW && BP == 15 && TN == 5 && BPL == 5120, "layout of rs_read_chunk");
-    static_assert(BM * LDC * 4 <= NKC * BCH, "P tile reuses the W_h image");
-    // the W_h image + one 1 KB landing place for the dummy 16th piece of each chunk
-    __shared__ __attribute__((aligned(16))) uint8_t lds[NKC * BCH + 1024];
-    const int tile = xcd_tile(blockIdx.x, gridDim.x);
-    const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
-    const BlockRow B = load_block(P.blocks, blk);
-    // wave-uniform control flow (the wave index from an SGPR): the counted waits need every wave to
-    // issue the same load sequence
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int g = lane >> 4, i16 = lane & 15;
-#define WD_TS(k) if (P.dbg && threadIdx.x == 0) P.dbg[(size_t)blockIdx.x * 8 + (k)] = __builtin_readcyclecounter();
-    WD_TS(0)
-    MpEpilogue<BN, NT, LAST, true> E;
-    if (!(P.xp & 16384)) E.prefetch(P, B, n0);  // issued first: older than every operand load, so the counted waits skip them
-    const bool active = 16 * wave < B.bn;
-    // DMA pieces: lane -> (plane, row, 16-B slot) of the chunk image; the bank swizzle goes on the
-    // source address (as x6_mainloop)
-    int bsrc[BPW], bdst[BPW];
-#pragma unroll
-    for (int j = 0; j < BPW; ++j) {
-        const int c = j * NW + wave, cs = min(c, BP - 1);
-        const int q = 64 * cs + lane, p = (q / (BN * 4)) % 3, r = (q >> 2) % BN, sl = q & 3;
-        bsrc[j] = p * BPL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
-        bdst[j] = c < BP ? 1024 * c : -1;
-    }
-    // A values through a buffer resource over the block's fp32 rows: lane (i16, g) reads row
-    // 16 wave + i16, columns 32 kc + 8 g .. + 7 (32 bytes); rows past the block's bonds read out of bounds
-    const int arow = 16 * wave + i16;
-    const __amdgpu_buffer_rsrc_t ars = f32_block_rsrc<BM>(reinterpret_cast<float *>(const_cast<uint8_t *>(P.mprev)), P.kp, blk);
-    const uint32_t aoff = arow < B.bn ? (uint32_t)((arow * P.kp + 8 * g) * 4) : 0x80000000u;
-    const uint8_t *bblk = P.wh + (size_t)nt * NKC * BCH;
-    constexpr int AL = 2;  // A loads per chunk
-    float4 af[NKC][AL];
-    // chunk kc's loads: this wave's A values, then its W_h DMA pieces
-    auto issue = [&](auto kc_c) {
-        constexpr int kc = decltype(kc_c)::value;
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < AL; ++q)
-            af[kc][q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ars, aoff + kc * 128 + 16 * q, 0, 0));
-#pragma unroll
-        for (int j = 0; j < BPW; ++j)
-            glds16(bblk + kc * BCH + bsrc[j], bdst[j] < 0 ? lds + NKC * BCH : lds + kc * BCH + bdst[j]);
-        __builtin_amdgcn_sched_barrier(0);  // issue order chunk by chunk (the counted waits rely on it)
-    };
-    // LA chunks in flight ahead of the one multiplied, issued chunk-major across the waves (a barrier
-    // between chunks): a wave issuing all its chunks back to back queues its later chunks ahead of the
-    // other waves' first ones, and the first chunk's barrier then waits for nearly every load
-#ifndef RS_LA
-#define RS_LA 3
-#endif
-    constexpr int LA = RS_LA;
-    static_for<0, LA>([&](auto c) {
-        issue(c);
-        __builtin_amdgcn_s_barrier();
-    });
-    WD_TS(1)
-    floatx4 acc[1][TN];
-#pragma unroll
-    for (int b = 0; b < TN; ++b) acc[0][b] = floatx4{0.f, 0.f, 0.f, 0.f};
-    // LDS byte address (not the generic address of the array) of this lane's fragment slot
-    const uint32_t fbase = (uint32_t)(uintptr_t)(lds_void_t *)lds + (uint32_t)x6_slot(i16, g);
-    static_for<0, NKC>([&](auto kc_c) {
-        constexpr int kc = decltype(kc_c)::value;
-        constexpr int AHEAD = (LA - 1 < NKC - 1 - kc) ? LA - 1 : NKC - 1 - kc;  // younger chunks in flight
-        wait_vm<AHEAD * (AL + BPW)>();  // this wave's loads of chunks <= kc landed ...
-        __builtin_amdgcn_s_barrier();   // ... and every wave's DMA pieces of chunk kc
-        if constexpr (kc + LA < NKC) issue(std::integral_constant<int, kc + LA>{});
-        if (kc == 0) WD_TS(2)
-        if (active && !(P.xp & 1)) {
-            bf16x8 bfr[TN][3], a3[3];
-            rs_read_chunk(fbase + kc * BCH, bfr);
-            split8(af[kc][0], af[kc][1], a3[0], a3[1], a3[2]);
-#pragma unroll
-            for (int b = 0; b < TN; ++b) {
-                // plane products hh, hm, mh, hl, lh, mm
-                constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};
-#pragma unroll
-                for (int t = 0; t < 6; ++t)
-                    acc[0][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3[PA[t]], bfr[b][PB[t]], acc[0][b], 0, 0, 0);
-            }
-        }
-    });
-    if (P.xp & 16384) E.prefetch(P, B, n0);
-    WD_TS(3)
-    __syncthreads();  // every wave done reading the W_h image: the P tile replaces it
-    WD_TS(4)
-    float *Pt = reinterpret_cast<float *>(lds);
-    x6_acc_to_lds<BM, BN, NW, 1>(acc, Pt);
-    __syncthreads();
-    WD_TS(5)
-    if (!(P.xp & 8)) E.run(P, B, blk, n0, Pt);
-    WD_TS(6)
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -498,8 +305,7 @@ struct EmbedP {
     int Fa, Fb, Hk, n_tiles;
     int act; const float *slope;
     float *inp;                  // [Rp][Hk]
-    uint8_t *mplanes;            // M0: plane tiles, blocked bond rows (BR 128) -- or, mf, fp32 blocked rows
-    int mf;
+    uint8_t *mplanes;            // M0 plane tiles, blocked bond rows (BR 128)
 };
 
 // Stage rows [0, rows0) of src0 and [0, rows1) of src1 (BN columns from n0, row stride ld, fp32) into
@@ -558,8 +364,7 @@ __global__ __launch_bounds__(512) void embed_kernel(EmbedP P) {
     }
     __syncthreads();
     const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
-    const __amdgpu_buffer_rsrc_t mrs = P.mf ? f32_block_rsrc<BLK_BONDS>(reinterpret_cast<float *>(P.mplanes), P.Hk, blk)
-                                            : x6_block_rsrc<BLK_BONDS>(P.mplanes, P.Hk, blk);
+    const __amdgpu_buffer_rsrc_t mrs = x6_block_rsrc<BLK_BONDS>(P.mplanes, P.Hk, blk);
     with_act(P.act, [&](auto act_c) {
     constexpr int ACT = decltype(act_c)::value;
     for (int v = tid; v < B.bn * U8; v += NT) {
@@ -583,8 +388,7 @@ __global__ __launch_bounds__(512) void embed_kernel(EmbedP P) {
                                       act_fwd(ACT, z0.z, slope), act_fwd(ACT, z0.w, slope));
         const float4 y1 = make_float4(act_fwd(ACT, z1.x, slope), act_fwd(ACT, z1.y, slope),
                                       act_fwd(ACT, z1.z, slope), act_fwd(ACT, z1.w, slope));
-        if (P.mf) f32_store8_blk(mrs, P.Hk, lb, n0 + c, y0, y1);
-        else x6_store8_blk<BLK_BONDS>(mrs, lb, n0 + c, y0, y1);
+        x6_store8_blk<BLK_BONDS>(mrs, lb, n0 + c, y0, y1);
     }
     });
 }
@@ -611,11 +415,7 @@ struct WoReadoutP {
 
 template <int BN> struct WoWaves;
 template <> struct WoWaves<64> { static constexpr int WM = 4, WN = 2; };
-#if WD_EXP == 8
-template <> struct WoWaves<80> { static constexpr int WM = 4, WN = 1; };
-#else
 template <> struct WoWaves<80> { static constexpr int WM = 2, WN = 5; };
-#endif
 
 // grid = nblk * n_tiles: 64 atom rows x BN columns per workgroup.
 template <int BN>
@@ -711,7 +511,7 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     // butterfly over the eight lanes (deterministic; every lane ends with the same sum)
     constexpr int RP = 8;
     static_assert(NT % RP == 0 && 64 % RP == 0, "lane groups stay inside a wave");
-    for (int t = tid; t < (WD_EXP == 20 ? 0 : nm * BN * RP); t += NT) {
+    for (int t = tid; t < nm * BN * RP; t += NT) {
         const int part = t % RP, u = t / RP, im = u / BN, i = B.ml + im, cc = u % BN, col = n0 + cc;
         const int n = __float_as_int(Ml[BLK_MOLS + im]);
         float s = 0.f, wsum = 0.f;

@@ -121,32 +121,6 @@ __device__ __forceinline__ void x6_store8_blk(__amdgpu_buffer_rsrc_t rs, int r, 
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{l[0], l[1], l[2], l[3]}, rs, o + 2 * BR * 64, 0, POL);
 }
 
-// fp32 rows of ONE row block [BR][kp] (the register-stationary layer's message layout: fp32 in
-// molecule-blocked rows, split into planes by the consumer), same write-through policy
-template <int BR>
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t f32_block_rsrc(float *base, int kp, int blk) {
-    return __builtin_amdgcn_make_buffer_rsrc(base + (size_t)blk * BR * kp, 0, BR * kp * 4, 0x00020000);
-}
-__device__ __forceinline__ void f32_store8_blk(__amdgpu_buffer_rsrc_t rs, int kp, int r, int k, const float4 &lo,
-                                               const float4 &hi) {
-    const int o = (r * kp + k) * 4;
-    constexpr int POL = WD_WT == 1 ? 16 : WD_WT == 3 ? 2 : 0;
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), rs, o, 0, POL);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), rs, o + 16, 0, POL);
-}
-
-// eight consecutive fp32 values -> their three bf16x8 planes (the fragment a plane tile would hold)
-__device__ __forceinline__ void split8(const float4 &lo, const float4 &hi, bf16x8 &h8, bf16x8 &m8, bf16x8 &l8) {
-    uint32_t h[4], m[4], l[4];
-    split_pair(lo.x, lo.y, h[0], m[0], l[0]);
-    split_pair(lo.z, lo.w, h[1], m[1], l[1]);
-    split_pair(hi.x, hi.y, h[2], m[2], l[2]);
-    split_pair(hi.z, hi.w, h[3], m[3], l[3]);
-    h8 = __builtin_bit_cast(bf16x8, u32x4{h[0], h[1], h[2], h[3]});
-    m8 = __builtin_bit_cast(bf16x8, u32x4{m[0], m[1], m[2], m[3]});
-    l8 = __builtin_bit_cast(bf16x8, u32x4{l[0], l[1], l[2], l[3]});
-}
-
 // columns k..k+3 (k % 4 == 0): three 8-byte pieces
 template <int BR = 64>
 __device__ __forceinline__ void x6_store4(uint8_t *base, int kp, int r, int k, const float4 &v) {

@@ -643,12 +643,8 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
         // categorical codes (compact graphs): the input layer and the f_atoms half of W_o as sums of
         // weight columns instead of GEMMs over the one-hot rows (fused_mp.hpp embed_kernel)
         const bool codes = g->atom_codes && g->bond_src_blk && g->bond_tail && D.Fb <= WO_MAXK && D.Fa <= WO_MAXK;
-        // register-stationary layers (fused_mp.hpp mp_layer_rs_kernel): Hk = 320 at 80-column tiles, fed by
-        // embed_kernel with fp32 messages
-        const bool rs = codes && bn80 && Hk == 32 * 10 && D.T > 1;
         if (codes) {
             EmbedP E{};
-            E.mf = rs;
             E.codes = g->atom_codes; E.src_blk = g->bond_src_blk; E.tail = g->bond_tail;
             E.wt = W(PL.WiT); E.woat = W(PL.WoaT); E.eo = F(L.Eo); E.bias = p->b_i ? W(PL.bi) : nullptr; E.blocks = g->blocks;
             E.Fa = D.Fa; E.Fb = D.Fb; E.Hk = Hk; E.n_tiles = Hk / BNf;
@@ -680,37 +676,7 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
             const dim3 grid(D.nblk * M.n_tiles);
             const bool last = t == D.T - 1;
             if (t == 1) WD_TRY(record_prof(c, 0, 0, st));  // one pair around all the layers
-            static const int xpv = getenv("WD_XP") ? atoi(getenv("WD_XP")) : 0;  // TEMP A/B switch
-            M.xp = xpv;
-            static uint64_t *tsbuf = nullptr;
-            static double tsacc[2][8] = {};
-            static long tsn[2] = {0, 0};
-            static const bool ts_on = getenv("WD_TS") != nullptr;
-            if (ts_on && !tsbuf) {
-                hipMalloc(&tsbuf, (size_t)8192 * 8 * 8);
-                atexit([] {
-                    for (int l = 0; l < 2; ++l) {
-                        fprintf(stderr, "WD_TS layer%d n=%ld:", l, tsn[l]);
-                        for (int k = 1; k < 7; ++k) fprintf(stderr, " d%d=%.0f", k, tsacc[l][k] / (tsn[l] ? tsn[l] : 1));
-                        fprintf(stderr, "\n");
-                    }
-                });
-            }
-            M.dbg = ts_on ? tsbuf : nullptr;
-            if (rs) {
-                // the W_h tile fits LDS whole: register-stationary layer (fused_mp.hpp mp_layer_rs_kernel)
-                if (last) hipLaunchKernelGGL((mp_layer_rs_kernel<10, true>), grid, dim3(512), 0, st, M);
-                else hipLaunchKernelGGL((mp_layer_rs_kernel<10, false>), grid, dim3(512), 0, st, M);
-                if (ts_on) {
-                    std::vector<uint64_t> h((size_t)grid.x * 8);
-                    hipStreamSynchronize(st);
-                    hipMemcpy(h.data(), tsbuf, h.size() * 8, hipMemcpyDeviceToHost);
-                    const int l = last ? 1 : 0;
-                    for (unsigned w = 0; w < grid.x; ++w)
-                        for (int k = 1; k < 7; ++k) tsacc[l][k] += (double)(int64_t)(h[w * 8 + k] - h[w * 8 + k - 1]) / grid.x;
-                    tsn[l]++;
-                }
-            } else if (bn80) {
+            if (bn80) {
                 const dim3 blk(64 * MpWaves<80>::WM * MpWaves<80>::WN);
                 if (last) hipLaunchKernelGGL((mp_layer_kernel<80, true>), grid, blk, 0, st, M);
                 else hipLaunchKernelGGL((mp_layer_kernel<80, false>), grid, blk, 0, st, M);
