@@ -108,6 +108,10 @@ struct MpLayerP {
     const uint8_t *aell_idx; const float *aell_coef;
     uint8_t *aplanes;           // A: blocked atom plane tiles [nblk * 64][kp]
     int n_tiles;                // Hk / BN
+    // training forward (save_for_backward) or null: the pre-activation Z_t (mpn.py:123) as fp32 natural
+    // bond rows [Rp][kp]; the last layer also the atom aggregate A (mpn.py:126-131) as fp32 natural atom
+    // rows [Vap][kp] (the backward's operands)
+    float *zsave, *asave;
 };
 
 // Wave layout of the fused kernels per column-tile width: BN = 64 -> 4 x 2 waves, BN = 80 -> 2 x 5.
@@ -199,7 +203,14 @@ struct MpEpilogue {
                                      res[i][1].x, res[i][1].y, res[i][1].z, res[i][1].w};
                 const float b8[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-                for (int q = 0; q < 8; ++q) z[q] = act_fwd(ACT, r8[q] + (z[q] + b8[q]), slope);  // mpn.py:123
+                for (int q = 0; q < 8; ++q) z[q] = r8[q] + (z[q] + b8[q]);  // mpn.py:123
+                if (P.zsave) {
+                    float *zr = P.zsave + (size_t)b * P.kp + n0 + c;
+                    st4(zr, make_float4(z[0], z[1], z[2], z[3]));
+                    st4(zr + 4, make_float4(z[4], z[5], z[6], z[7]));
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) z[q] = act_fwd(ACT, z[q], slope);
                 if (P.p_drop > 0.f)
 #pragma unroll
                     for (int q = 0; q < 8; ++q) z[q] *= dropout_scale(P.seed, P.layer, b, n0 + c + q, P.p_drop);
@@ -240,6 +251,11 @@ struct MpEpilogue {
                     for (int q = P.aptr[a] + ELLW; q < P.aptr[a + 1]; ++q)
                         lds_term<LDC>(Mt, P.aidx[q] - B.bs, c, P.acoef ? P.acoef[q] : 1.0f, s0, s1);
                 x6_store8_blk<BLK_ATOMS>(ars, la, n0 + c, s0, s1);
+                if (P.asave) {
+                    float *ar = P.asave + (size_t)a * P.kp + n0 + c;
+                    st4(ar, s0);
+                    st4(ar + 4, s1);
+                }
             }
         }
     }
@@ -279,6 +295,12 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
     x6_acc_to_lds<BM, BN, WM, WN>(acc, Pt);
     __syncthreads();
     E.run(P, B, blk, n0, Pt);
+    // the pad row 0 (bond and atom) belongs to no block: its saved rows are written as zeros, which the
+    // backward multiplies by its zero gradients (an uninitialised NaN would poison them)
+    if (blk == 0 && threadIdx.x < BN / 4) {
+        if (P.zsave) st4(P.zsave + n0 + 4 * threadIdx.x, f4zero());
+        if (LAST && P.asave) st4(P.asave + n0 + 4 * threadIdx.x, f4zero());
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -391,6 +413,7 @@ __global__ __launch_bounds__(512) void embed_kernel(EmbedP P) {
         x6_store8_blk<BLK_BONDS>(mrs, lb, n0 + c, y0, y1);
     }
     });
+    if (blk == 0 && tid < C4) st4(P.inp + n0 + 4 * tid, f4zero());  // pad row 0 (Z_0 of the backward)
 }
 
 constexpr int WO_MAXK = 160;  // f_atoms / f_bonds columns embed_kernel stages (Fa, Fb <= 160)
@@ -411,6 +434,7 @@ struct WoReadoutP {
     // embed_kernel as sums of W_o columns: fp32 [nblk * 64][Hk], blocked atom rows (null: GEMM segment)
     const float *eo;
     int Hk;
+    float *zosave;  // training forward or null: the W_o pre-activation (mpn.py:133) as fp32 natural atom rows [Vap][Hk]
 };
 
 template <int BN> struct WoWaves;
@@ -449,6 +473,7 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     constexpr int C4 = BN / 4;
     static_assert(NT % C4 == 0 && BM <= NT, "one bias group per thread, one atom weight per thread");
     const int nm = min(B.mh - B.ml, BLK_MOLS);  // (the packer never exceeds BLK_MOLS)
+    if (P.zosave && blk == 0 && tid < BN / 4) st4(P.zosave + n0 + 4 * tid, f4zero());  // pad atom row 0
     float4 bb = f4zero();
     float watom = 0.f, mxn = 0.f;
     int mstart = 0, msize = 0;
@@ -497,6 +522,7 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
             float4 hv = ld4(H + la * LDC + c);
             hv.x += eo[j].x; hv.y += eo[j].y; hv.z += eo[j].z; hv.w += eo[j].w;  // (0 without codes)
             float z[4] = {hv.x + bb.x, hv.y + bb.y, hv.z + bb.z, hv.w + bb.w};
+            if (P.zosave && la < B.an) st4(P.zosave + (size_t)(B.as + la) * P.Hk + n0 + c, make_float4(z[0], z[1], z[2], z[3]));
 #pragma unroll
             for (int q = 0; q < 4; ++q) z[q] = act_fwd(ACT, z[q], slope);
             if (P.p_drop > 0.f && la < B.an)

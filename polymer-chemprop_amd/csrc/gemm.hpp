@@ -8,9 +8,8 @@
 //     and K to the 32-wide chunk, padding zero), so the loads are unconditional float4 and the
 //     segment of a K-chunk is uniform over the workgroup: no per-element branches or waits in the
 //     K loop.
-// gemm_tn_kernel  slab[z][n][j] (+)= sum_{m in split z} dZ[m][n] * X[m][j]   weight gradients
-//     reduction over rows m (thousands of bonds) split across workgroups into slabs that a second
-//     kernel reduces in a fixed order (deterministic, no atomics).
+// Src / Seg  the row-major operands of the weight-gradient GEMM (gemm_x6.hpp gemm_tn_x6_kernel):
+//     segments laid side by side along the columns, plus a ones column for the bias.
 //
 // Tiles: BM x BN per workgroup of WM x WN waves; K in chunks of 32 staged through LDS (row stride 36
 // floats, conflict-free for ds_read_b128 and ds_write_b128: checked by brute force over the lane
@@ -309,9 +308,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_nt16_kernel(NtParams P) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// TN kernel (weight gradients): both operands k-major (rows = m), masked at the split's row range.
+// Weight-gradient operands: both k-major (rows = m), masked at the split's row range.
 // ---------------------------------------------------------------------------------------------
-enum SegKind : int { SEG_DENSE = 0, SEG_ONES = 2 };
+// SEG_ACT: the activations M = dropout(act(Z)) recomputed from the saved pre-activations Z while
+// loading (the fused training forward keeps Z_t, not M_t: mpn.py:97, 123-124)
+enum SegKind : int { SEG_DENSE = 0, SEG_ACT = 1, SEG_ONES = 2 };
 
 struct Seg {
     const float *src;
@@ -319,6 +320,7 @@ struct Seg {
     int K;      // width (padded extent; zeros beyond the real width are fine)
     int kp0;    // first column in the operand's column space (multiple of 4)
     int kind;
+    int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;  // SEG_ACT
 };
 
 struct Src {
@@ -331,7 +333,19 @@ struct Src {
 __device__ __forceinline__ float4 seg_load4(const Seg &g, int r, int kk) {
     if (kk >= g.K) return f4zero();
     if (g.kind == SEG_ONES) return kk == 0 ? make_float4(1.f, 0.f, 0.f, 0.f) : f4zero();
-    return ld4(g.src + (size_t)r * g.ld + kk);
+    float4 v = ld4(g.src + (size_t)r * g.ld + kk);
+    if (g.kind == SEG_ACT) {
+        const float sl = g.act == ACT_PRELU ? g.slope[0] : 0.f;
+        v.x = act_fwd(g.act, v.x, sl); v.y = act_fwd(g.act, v.y, sl);
+        v.z = act_fwd(g.act, v.z, sl); v.w = act_fwd(g.act, v.w, sl);
+        if (g.p_drop > 0.f) {
+            v.x *= dropout_scale(g.seed, g.layer, r, kk, g.p_drop);
+            v.y *= dropout_scale(g.seed, g.layer, r, kk + 1, g.p_drop);
+            v.z *= dropout_scale(g.seed, g.layer, r, kk + 2, g.p_drop);
+            v.w *= dropout_scale(g.seed, g.layer, r, kk + 3, g.p_drop);
+        }
+    }
+    return v;
 }
 
 __device__ __forceinline__ float4 src_load4(const Src &S, int r, int cp, int rlim) {
@@ -343,89 +357,5 @@ __device__ __forceinline__ float4 src_load4(const Src &S, int r, int cp, int rli
     return seg_load4(g, r, cp - g.kp0);
 }
 
-struct TnParams {
-    Src A, B;        // A: rows m, cols i (=n);  B: rows m, cols j
-    int M, N;        // output rows (i) / cols (j)
-    int K;           // reduction rows
-    int k_per_split; // multiple of 32
-    int tiles_m, tiles_n;
-    Epi epi;
-};
-
-template <int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN) void gemm_tn_kernel(TnParams P) {
-    constexpr int NT = 64 * WM * WN;
-    constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-    constexpr int A_LD = BM + 4, B_LD = BN + 4;
-    constexpr int A_V4 = BK * BM / 4, B_V4 = BK * BN / 4;
-    constexpr int PA = (A_V4 + NT - 1) / NT, PB = (B_V4 + NT - 1) / NT;
-    __shared__ __attribute__((aligned(16))) float lds[BK * A_LD + BK * B_LD];
-    float *As = lds, *Bs = lds + BK * A_LD;
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wi = wave / WN, wj = wave % WN, h = lane >> 5, l32 = lane & 31;
-    const int tile = blockIdx.x;
-    const int mt = tile / P.tiles_n, nt = tile % P.tiles_n;
-    const int m0 = mt * BM, n0 = nt * BN;
-    const int kbeg = blockIdx.y * P.k_per_split;
-    const int kend = min(P.K, kbeg + P.k_per_split);
-
-    floatx16 acc[TM][TN];
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-
-    float4 ra[PA], rb[PB];
-    auto load_chunk = [&](int k0) {
-#pragma unroll
-        for (int p = 0; p < PA; ++p) {
-            const int q = tid + p * NT;
-            ra[p] = q < A_V4 ? src_load4(P.A, k0 + q / (BM / 4), m0 + (q % (BM / 4)) * 4, kend) : f4zero();
-        }
-#pragma unroll
-        for (int p = 0; p < PB; ++p) {
-            const int q = tid + p * NT;
-            rb[p] = q < B_V4 ? src_load4(P.B, k0 + q / (BN / 4), n0 + (q % (BN / 4)) * 4, kend) : f4zero();
-        }
-    };
-    const int nchunks = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-    if (nchunks > 0) load_chunk(kbeg);
-    for (int kc = 0; kc < nchunks; ++kc) {
-        __syncthreads();
-#pragma unroll
-        for (int p = 0; p < PA; ++p) {
-            const int q = tid + p * NT;
-            if (q < A_V4) st4(As + (q / (BM / 4)) * A_LD + (q % (BM / 4)) * 4, ra[p]);
-        }
-#pragma unroll
-        for (int p = 0; p < PB; ++p) {
-            const int q = tid + p * NT;
-            if (q < B_V4) st4(Bs + (q / (BN / 4)) * B_LD + (q % (BN / 4)) * 4, rb[p]);
-        }
-        __syncthreads();
-        if (kc + 1 < nchunks) load_chunk(kbeg + (kc + 1) * BK);
-        float af[TM][16], bf[TN][16];
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-            for (int s = 0; s < 16; ++s) af[a][s] = As[(16 * h + s) * A_LD + wi * (BM / WM) + a * 32 + l32];
-#pragma unroll
-        for (int b = 0; b < TN; ++b)
-#pragma unroll
-            for (int s = 0; s < 16; ++s) bf[b][s] = Bs[(16 * h + s) * B_LD + wj * (BN / WN) + b * 32 + l32];
-#pragma unroll
-        for (int s = 0; s < 16; ++s)
-#pragma unroll
-            for (int a = 0; a < TM; ++a)
-#pragma unroll
-                for (int b = 0; b < TN; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
-    }
-    float *Y = P.epi.Y + (size_t)blockIdx.y * P.epi.slab_stride;
-    epilogue<TM, TN>(P.epi, acc, m0 + wi * (BM / WM), n0 + wj * (BN / WN), h, l32, P.M, P.N, Y);
-}
 
 }  // namespace wd

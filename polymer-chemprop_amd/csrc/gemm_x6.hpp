@@ -162,6 +162,220 @@ __global__ __launch_bounds__(4 * BM) void gemm_x6_kernel(X6Params P) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// gemm_tn_x6_kernel — weight gradients as a split-plane GEMM:
+//     slab[z][i][j] (+)= sum_{m in split z} A[m][i] B[m][j]     (A = dZ, B = the layer input X)
+//     slab[z][i][bias_col] (+)= sum_{m in split z} A[m][i]      (the bias: X's ones column)
+// Both operands are row-major in the reduction index m (thousands of bond / atom rows).  A 32-row
+// chunk is loaded as 4 rows x 4 columns per thread (16 consecutive lanes read one 256-byte row
+// piece), split into bf16x3 planes in registers and written K-major: column i (or j) becomes the LDS
+// row and the four m values one 8-byte piece of it, so the 16x16x32 fragments read 8 consecutive m
+// per lane exactly as in gemm_x6_kernel (same image, same products hh hm mh hl lh mm).  Threads 0-127
+// stage A, 128-255 B.  The bias column is not a GEMM tile: the j-tile-0 workgroups sum their staged
+// A registers per column and reduce the eight row groups in a fixed order.  Deterministic: fixed
+// split ranges, fixed in-tile order, slabs reduced in split order by slab_reduce_kernel.
+// ---------------------------------------------------------------------------------------------
+struct TnX6Params {
+    Src A, B;              // A: rows m, cols i (dZ);  B: rows m, cols j (dense segments; the ones column is
+                           // the bias and is never read)
+    int M, N;              // output rows i (< A.cols_p) / dense output columns j
+    int K;                 // reduction rows
+    int k_per_split;       // multiple of 32
+    int tiles_m, tiles_n;
+    float *slab; int ld_slab; long long slab_stride; int accumulate;
+    int bias_col;          // slab column of the bias gradient, -1 = none
+    const float *bias_src; int bias_ld;  // the bias as column sums of this matrix [K][bias_ld] instead of A (or null)
+};
+
+// SACT: the activation of a SEG_ACT operand as a compile-time constant (one instantiation per activation:
+// a runtime switch over all of them in the staging path bloated the kernel past the instruction cache),
+// -1 when no operand is SEG_ACT.  BEXT: the bias sums come from P.bias_src (a compile-time switch: a runtime
+// branch around those loads left the compiler's vmcnt waits unable to skip the prefetched chunk's loads)
+template <int SACT, bool BEXT>
+__global__ __launch_bounds__(256) void gemm_tn_x6_kernel(TnX6Params P) {
+    constexpr int BM = 64, BN = 64, NT = 256, BKC = 32;
+    constexpr int PL = 64 * 64;            // one plane: 64 rows x 32 K x 2 B
+    constexpr int STAGE = 6 * PL;          // A planes, then B planes (24 KB)
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wi = wave >> 1, wj = wave & 1, g = lane >> 4, i16 = lane & 15;
+    const int tile = blockIdx.x;
+    const int mt = tile / P.tiles_n, nt = tile % P.tiles_n;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int kbeg = blockIdx.y * P.k_per_split;
+    const int kend = min(P.K, kbeg + P.k_per_split);
+    const int nchunks = kend > kbeg ? (kend - kbeg + BKC - 1) / BKC : 0;
+    // staging role: operand (A for tid < 128), column quad q (4 columns), row quad h4 (4 rows of the chunk).
+    // The thread's columns are fixed, so its operand segment is resolved once here (no per-load segment
+    // search through the kernel arguments).
+    const bool isA = tid < 128;
+    const int st = tid & 127, q = st & 15, h4 = st >> 4;
+    const int col = (isA ? m0 : n0) + 4 * q;
+    const int lim = isA ? P.M : P.N;
+    const Seg sg = [&] {
+        const Src &S = isA ? P.A : P.B;
+        int k = 0;
+        if (S.nseg > 1 && col >= S.s[1].kp0) k = 1;
+        if (S.nseg > 2 && col >= S.s[2].kp0) k = 2;
+        return S.s[k];
+    }();
+    const int kk = col - sg.kp0;
+    const bool live = col < lim && kk < sg.K && sg.kind != SEG_ONES;  // (ones columns are the bias, never tiles)
+    const bool bias = isA && nt == 0 && P.bias_col >= 0;
+    const bool bias_ext = BEXT && bias;
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    // LDS byte offset of this thread's 8-byte piece in row r (plane 0): unit h4 / 2, half h4 % 2
+    int dst[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) dst[c] = (isA ? 0 : 3 * PL) + x6_off<32>(4 * q + c, h4 >> 1) + 8 * (h4 & 1);
+    // branch-free loads: every lane loads (rows past kend clamped to the last row, dead columns from a valid
+    // dummy address) and the values are masked when staged, so the loads pipeline ahead of the MFMAs
+    const float *abase = live ? sg.src + kk : P.A.s[0].src;
+    const int ald = live ? sg.ld : 0;
+    const float *bbase = bias_ext && col < lim ? P.bias_src + col : P.A.s[0].src;
+    const int bld = bias_ext && col < lim ? P.bias_ld : 0;
+    const int rlast = kend - 1;
+    const bool base = live;
+
+    struct Regs { float4 v[4], bz[4]; };
+    auto load_chunk = [&](Regs &R, int kc) {
+        const int r0 = kbeg + kc * BKC + 4 * h4;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) R.v[s] = ld4(abase + (size_t)min(r0 + s, rlast) * ald);
+        if constexpr (BEXT)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) R.bz[s] = ld4(bbase + (size_t)min(r0 + s, rlast) * bld);
+    };
+    // rows past kend and dead columns -> 0 (after the loads have landed)
+    auto mask_rows = [&](Regs &R, int kc) {
+        const int r0 = kbeg + kc * BKC + 4 * h4;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const bool ok = r0 + s < kend;
+            if (!(ok && live)) R.v[s] = f4zero();
+            if constexpr (BEXT)
+                if (!(ok && bld)) R.bz[s] = f4zero();
+        }
+    };
+    // SEG_ACT operands: M = dropout(act(Z)) applied here, when the loads have landed
+    auto act_rows = [&](Regs &R, int kc) {
+        if constexpr (SACT >= 0) {
+            if (sg.kind != SEG_ACT || !base) return;
+            const int r0 = kbeg + kc * BKC + 4 * h4;
+            const float sl = SACT == ACT_PRELU ? sg.slope[0] : 0.f;
+            (void)base;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                float *v = reinterpret_cast<float *>(&R.v[s]);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) v[c] = act_fwd(SACT, v[c], sl);
+                if (sg.p_drop > 0.f)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) v[c] *= dropout_scale(sg.seed, sg.layer, r0 + s, kk + c, sg.p_drop);
+            }
+        }
+    };
+    auto store_chunk = [&](Regs &R, int kc, uint8_t *stg) {
+        mask_rows(R, kc);
+        act_rows(R, kc);
+        // column c of the 4x4 block: m values R.v[0..3].c -> three packed pairs per plane
+        const float a[4][4] = {{R.v[0].x, R.v[1].x, R.v[2].x, R.v[3].x}, {R.v[0].y, R.v[1].y, R.v[2].y, R.v[3].y},
+                               {R.v[0].z, R.v[1].z, R.v[2].z, R.v[3].z}, {R.v[0].w, R.v[1].w, R.v[2].w, R.v[3].w}};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            uint32_t h0, md0, l0, h1, md1, l1;
+            split_pair(a[c][0], a[c][1], h0, md0, l0);
+            split_pair(a[c][2], a[c][3], h1, md1, l1);
+            *reinterpret_cast<uint2 *>(stg + dst[c]) = make_uint2(h0, h1);
+            *reinterpret_cast<uint2 *>(stg + dst[c] + PL) = make_uint2(md0, md1);
+            *reinterpret_cast<uint2 *>(stg + dst[c] + 2 * PL) = make_uint2(l0, l1);
+        }
+        if (bias) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const float4 v = BEXT ? R.bz[s] : R.v[s];
+                bsum[0] += v.x; bsum[1] += v.y; bsum[2] += v.z; bsum[3] += v.w;
+            }
+        }
+    };
+    floatx4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](const uint8_t *stg) {
+        bf16x8 af[2][3], bfr[2][3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+                af[a][p] = *reinterpret_cast<const bf16x8 *>(stg + p * PL + x6_off<32>(wi * 32 + a * 16 + i16, g));
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+                bfr[b][p] = *reinterpret_cast<const bf16x8 *>(stg + 3 * PL + p * PL + x6_off<32>(wj * 32 + b * 16 + i16, g));
+        }
+        constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};
+#pragma unroll
+        for (int t = 0; t < 6; ++t)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][PA[t]], bfr[b][PB[t]], acc[a][b], 0, 0, 0);
+    };
+    if (nchunks > 0) {
+        Regs R0, R1;
+        load_chunk(R0, 0);
+        load_chunk(R1, min(1, nchunks - 1));
+        store_chunk(R0, 0, lds);
+        __syncthreads();
+        auto step = [&](int kc, Regs &Rnext, Regs &Rfree) {
+            // unconditional (the last chunk is reloaded past the end): a skipped load on some path made
+            // the compiler's waits for the older chunk drain the fresh prefetch too
+            load_chunk(Rfree, min(kc + 2, nchunks - 1));
+            __builtin_amdgcn_sched_barrier(0);
+            compute(lds + (kc & 1) * STAGE);
+            if (kc + 1 < nchunks) store_chunk(Rnext, kc + 1, lds + ((kc + 1) & 1) * STAGE);
+            __syncthreads();
+        };
+        int kc = 0;
+        for (; kc + 1 < nchunks; kc += 2) {
+            step(kc, R1, R0);
+            step(kc + 1, R0, R1);
+        }
+        if (kc < nchunks) step(kc, R1, R0);
+    }
+    // epilogue: C tile through LDS, coalesced float4 stores into this split's slab (accumulating over
+    // the layers of W_h when asked); the bias sums through LDS in row-group order
+    float *cl = reinterpret_cast<float *>(lds);
+    constexpr int LDC = BN + 4;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cl[(wi * 32 + a * 16 + 4 * g + r) * LDC + wj * 32 + b * 16 + i16] = acc[a][b][r];
+    float *bl = cl + BM * LDC;  // [8 row groups][64 columns]
+    if (bias) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) bl[h4 * 64 + 4 * q + c] = bsum[c];
+    }
+    __syncthreads();
+    float *Y = P.slab + (size_t)blockIdx.y * P.slab_stride;
+    Epi E{};
+    E.kind = EPI_STORE; E.Y = Y; E.ld = P.ld_slab; E.accumulate = P.accumulate;
+    EpiPrefetch<BM, BN, NT> ep;
+    ep.load(E, m0, n0, P.M, P.N);
+    epilogue_v4<BM, BN, NT>(E, cl, LDC, m0, n0, P.M, P.N, ep);
+    if (nt == 0 && P.bias_col >= 0 && tid < BM && m0 + tid < P.M) {
+        float s = 0.f;
+#pragma unroll
+        for (int h = 0; h < 8; ++h) s += bl[h * 64 + tid];
+        float *d = Y + (size_t)(m0 + tid) * P.ld_slab + P.bias_col;
+        *d = P.accumulate ? *d + s : s;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Split-plane GEMM core on LDS-DMA staged plane tiles (cdna_hip_programming.md §5 "Async
 // global->LDS copy"): no staging registers, no arithmetic in the staging path, two LDS stages (one
 // chunk in flight behind the one being multiplied), raw s_barrier (a __syncthreads would drain the DMA

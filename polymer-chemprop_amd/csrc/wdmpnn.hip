@@ -108,7 +108,9 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     // default (0) = 10: bf16x6 split-plane GEMMs (fp32-accurate)
     D.f32 = c->gemm_variant == 9;
     D.x6 = !D.f32 && !D.atom;
-    D.blocked = D.x6 && !D.save && !D.desc && D.T >= 2 && g->n_blocks > 0 && g->blocks && g->bond_blk_row &&
+    // molecule-blocked fused forward, also for training (the fused kernels then save Z_t, A and Zo in
+    // natural rows for the backward)
+    D.blocked = D.x6 && !D.desc && D.T >= 2 && g->n_blocks > 0 && g->blocks && g->bond_blk_row &&
                 g->f_atoms_blk_x6 && g->f_bonds_x6 && g->msg_ell_idx && g->msg_ell_coef && g->atom_ell_idx &&
                 g->atom_ell_coef;
     D.nblk = D.blocked ? g->n_blocks : 0;
@@ -251,7 +253,7 @@ Epi epi_store(float *Y, int ld, long long slab_stride = 0, int accumulate = 0) {
     return e;
 }
 
-constexpr int NBM = 64, NBN = 64, NWM = 2, NWN = 2;
+constexpr int NBM = 64, NBN = 64;
 
 bool epi_aligned(const Epi &epi) {
     const uintptr_t al = (uintptr_t)epi.Y | (uintptr_t)epi.Z | (uintptr_t)epi.resid | (uintptr_t)epi.bias;
@@ -350,34 +352,68 @@ Src make_src(int rows, std::initializer_list<Seg> segs) {
     return S;
 }
 
-struct TnPlan { int nsplit; int k_per_split; long long slab_stride; int ld_slab; };
+struct TnPlan { int nsplit; int k_per_split; long long slab_stride; int ld_slab; int n_dense; int bias_col; };
 
-TnPlan tn_plan(int n_out, int cols_p, int m_rows) {
+// columns of X that are GEMM tiles (its dense segments) and the slab column of the bias (its ones
+// segment, summed from dZ by gemm_tn_x6_kernel), -1 without one
+void tn_cols(const Src &X, int &n_dense, int &bias_col) {
+    const bool ones = X.nseg > 0 && X.s[X.nseg - 1].kind == SEG_ONES;
+    n_dense = ones ? X.s[X.nseg - 1].kp0 : X.cols_p;
+    bias_col = ones ? X.s[X.nseg - 1].kp0 : -1;
+}
+
+// split-K plan of the weight-gradient GEMM: about TN_TARGET workgroups over the output tiles (64 x 64
+// of [n_out][n_dense]), 32-row chunks; the slabs keep X's padded column space [n_out][cols_p]
+TnPlan tn_plan(int n_out, const Src &X, int m_rows) {
+    static const int target = [] {
+        const char *e = getenv("WDMPNN_TN_TARGET");
+        return e ? std::max(1, atoi(e)) : 512;
+    }();
     TnPlan t{};
-    const int tiles = ((n_out + NBM - 1) / NBM) * ((cols_p + NBN - 1) / NBN);
-    const int chunks = (m_rows + BK - 1) / BK;
-    int ns = (2048 + tiles - 1) / tiles;
+    tn_cols(X, t.n_dense, t.bias_col);
+    const int tiles = ((n_out + 63) / 64) * ((t.n_dense + 63) / 64);
+    const int chunks = (m_rows + 31) / 32;
+    int ns = (target + tiles - 1) / tiles;
     if (ns > chunks) ns = chunks;
     if (ns < 1) ns = 1;
     const int cps = (chunks + ns - 1) / ns;
-    t.k_per_split = cps * BK;
+    t.k_per_split = cps * 32;
     t.nsplit = (m_rows + t.k_per_split - 1) / t.k_per_split;
     if (t.nsplit < 1) t.nsplit = 1;
-    t.ld_slab = cols_p;
-    t.slab_stride = (long long)n_out * cols_p;
+    t.ld_slab = X.cols_p;
+    t.slab_stride = (long long)n_out * X.cols_p;
     return t;
 }
 
-// slab[z][n][j] (+)= sum_{m in split z} dZ[m][n] * X[m][j]
+// slab[z][n][j] (+)= sum_{m in split z} dZ[m][n] * X[m][j]  (bias column: sum_m dZ[m][n], or of bias_src
+// [m_rows][dZ's ld] when given)
 int gemm_tn(const Src &dZ, const Src &X, int n_out, int m_rows, const TnPlan &tp, float *slab, int accumulate,
-            hipStream_t st) {
+            hipStream_t st, const float *bias_src = nullptr) {
     if (n_out <= 0 || m_rows <= 0) return 0;
-    TnParams P{};
-    P.A = dZ; P.B = X; P.M = n_out; P.N = X.cols_p; P.K = m_rows; P.k_per_split = tp.k_per_split;
-    P.tiles_m = (n_out + NBM - 1) / NBM; P.tiles_n = (X.cols_p + NBN - 1) / NBN;
-    P.epi = epi_store(slab, tp.ld_slab, tp.slab_stride, accumulate);
-    hipLaunchKernelGGL((gemm_tn_kernel<NBM, NBN, NWM, NWN>), dim3(P.tiles_m * P.tiles_n, tp.nsplit),
-                       dim3(64 * NWM * NWN), 0, st, P);
+    TnX6Params P{};
+    P.A = dZ; P.B = X; P.M = n_out; P.N = tp.n_dense; P.K = m_rows; P.k_per_split = tp.k_per_split;
+    P.tiles_m = (n_out + 63) / 64; P.tiles_n = (tp.n_dense + 63) / 64;
+    P.slab = slab; P.ld_slab = tp.ld_slab; P.slab_stride = tp.slab_stride; P.accumulate = accumulate;
+    P.bias_col = tp.bias_col;
+    P.bias_src = bias_src; P.bias_ld = dZ.s[0].ld;
+    if (tp.ld_slab % 4 || tp.slab_stride % 4 || ((uintptr_t)slab & 15))
+        return fail(WD_ERR_SHAPE, "gemm_tn: unaligned slab");
+    const dim3 grid(P.tiles_m * P.tiles_n, tp.nsplit);
+    int sact = -1;
+    for (int q = 0; q < X.nseg; ++q)
+        if (X.s[q].kind == SEG_ACT) sact = X.s[q].act;
+    if (sact >= 0 && !bias_src) return fail(WD_ERR_ARG, "gemm_tn: a SEG_ACT operand needs its bias source");
+    if (bias_src && sact < 0) return fail(WD_ERR_ARG, "gemm_tn: an external bias source goes with a SEG_ACT operand");
+    switch (sact) {
+    case -1: hipLaunchKernelGGL((gemm_tn_x6_kernel<-1, false>), grid, dim3(256), 0, st, P); break;
+    case ACT_RELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_RELU, true>), grid, dim3(256), 0, st, P); break;
+    case ACT_LEAKY: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_LEAKY, true>), grid, dim3(256), 0, st, P); break;
+    case ACT_PRELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_PRELU, true>), grid, dim3(256), 0, st, P); break;
+    case ACT_TANH: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_TANH, true>), grid, dim3(256), 0, st, P); break;
+    case ACT_SELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_SELU, true>), grid, dim3(256), 0, st, P); break;
+    case ACT_ELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_ELU, true>), grid, dim3(256), 0, st, P); break;
+    default: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_IDENTITY, true>), grid, dim3(256), 0, st, P); break;
+    }
     WD_CHECK_LAUNCH("gemm_tn");
     return 0;
 }
@@ -431,9 +467,11 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
     L.own_pack = own_pack;
     if (own_pack) L.packed = take(pack_layout(D).total);
     for (int t = 0; t < (D.save ? D.T : 1); ++t) L.Z.push_back(take(msg));
-    for (int t = 0; t < (D.save ? D.T : (D.T > 1 ? 2 : 1)); ++t) L.M.push_back(take(msg));
-    if (D.T > 1)
-        for (int t = 0; t < (D.save ? D.T - 1 : 1); ++t) L.X.push_back(take((size_t)D.Rp * D.ldx * 4));
+    if (!D.blocked) {  // (the fused kernels keep M_t in plane tiles and never form X_t)
+        for (int t = 0; t < (D.save ? D.T : (D.T > 1 ? 2 : 1)); ++t) L.M.push_back(take(msg));
+        if (D.T > 1)
+            for (int t = 0; t < (D.save ? D.T - 1 : 1); ++t) L.X.push_back(take((size_t)D.Rp * D.ldx * 4));
+    }
     L.A = take(atm);
     if (D.blocked) {
         for (int i = 0; i < 2; ++i) L.Mb[i] = take((size_t)D.nblk * BLK_BONDS * D.Hk * 6);
@@ -487,7 +525,7 @@ BwdLayout bwd_layout(const WdGraph *g, const Dims &D) {
     if (D.undirected) L.dMs = take(msg);
     size_t slab = 0;
     auto upd = [&](int n_out, const Src &X, int m_rows) {
-        TnPlan tp = tn_plan(n_out, X.cols_p, m_rows);
+        TnPlan tp = tn_plan(n_out, X, m_rows);
         slab = std::max<size_t>(slab, (size_t)tp.nsplit * (size_t)tp.slab_stride);
     };
     upd(D.Hk, x_in(g, D), D.R);
@@ -673,6 +711,8 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
             M.aell_idx = g->atom_ell_idx; M.aell_coef = g->atom_ell_coef;
             M.aplanes = (uint8_t *)(ws + L.Ab);
             M.n_tiles = Hk / BNf;
+            M.zsave = D.save ? F(L.Z[t]) : nullptr;
+            M.asave = D.save && t == D.T - 1 ? F(L.A) : nullptr;
             const dim3 grid(D.nblk * M.n_tiles);
             const bool last = t == D.T - 1;
             if (t == 1) WD_TRY(record_prof(c, 0, 0, st));  // one pair around all the layers
@@ -700,6 +740,7 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
             R.agg = c->aggregation; R.norm = c->aggregation_norm; R.zero_vec = p->zero_vec;
             R.act = c->activation; R.slope = p->prelu; R.p_drop = c->dropout; R.seed = c->seed; R.layer = D.T;
             R.out = out; R.ncols = D.H; R.n_tiles = Hk / BNf;
+            R.zosave = D.save ? F(L.Zo) : nullptr;
             const dim3 grid(D.nblk * R.n_tiles);
             if (bn80)
                 hipLaunchKernelGGL(wo_readout_kernel<80>, grid, dim3(64 * WoWaves<80>::WM * WoWaves<80>::WN), 0, st, R);
@@ -845,13 +886,13 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
         WD_TRY(act_bwd(P));
         Src dZ = make_src(D.Va, {seg_dense(S(Bl.dZd), D.Hdk, D.Hdk)});
         Src X = x_d(g, D, F(L.h));
-        TnPlan tp = tn_plan(D.Hdk, X.cols_p, D.Va);
+        TnPlan tp = tn_plan(D.Hdk, X, D.Va);
         WD_TRY(gemm_tn(dZ, X, D.Hdk, D.Va, tp, S(Bl.slab), 0, st));
         WD_TRY(slab_reduce(tp, S(Bl.slab), D.Hd, {{0, 0, H}, {Hk, H, D.d}}, grads->W_d, D.Hd, grads->b_d,
                            X.s[2].kp0, st));
         // dh = dZd W_d[:, :H]
         WD_TRY(gemm_nt(S(Bl.dZd), D.Hdk, D.Hdk, nullptr, 0, 0, W(PL.WdT), D.Hdk, D.Vap, Hk,
-                       epi_store(S(Bl.dHo), Hk), st));
+                       epi_store(S(Bl.dHo), Hk), st, true));
         dh = S(Bl.dHo);
     }
     // W_o layer
@@ -861,12 +902,12 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
         WD_TRY(act_bwd(P));
         Src dZ = make_src(D.Va, {seg_dense(S(Bl.dZo), Hk, Hk)});
         Src X = x_o(g, D, F(L.A));
-        TnPlan tp = tn_plan(Hk, X.cols_p, D.Va);
+        TnPlan tp = tn_plan(Hk, X, D.Va);
         WD_TRY(gemm_tn(dZ, X, Hk, D.Va, tp, S(Bl.slab), 0, st));
         WD_TRY(slab_reduce(tp, S(Bl.slab), H, {{0, 0, D.Fa}, {D.Fak, D.Fa, H}}, grads->W_o, D.Fa + H, grads->b_o,
                            X.s[2].kp0, st));
         // dA = dZo W_o[:, Fa:]
-        WD_TRY(gemm_nt(S(Bl.dZo), Hk, Hk, nullptr, 0, 0, W(PL.WoT), Hk, D.Vap, Hk, epi_store(S(Bl.dA), Hk), st));
+        WD_TRY(gemm_nt(S(Bl.dZo), Hk, Hk, nullptr, 0, 0, W(PL.WoT), Hk, D.Vap, Hk, epi_store(S(Bl.dA), Hk), st, true));
     }
     // gradient reaching M_{T-1} through the final aggregation, then the message layers
     float *dZbuf[2] = {S(Bl.dZ0), S(Bl.dZ1)};
@@ -879,14 +920,47 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
         WD_TRY(act_bwd(P));
     }
     const Src Xh0 = x_h(D, nullptr);
-    const TnPlan tph = tn_plan(Hk, Xh0.cols_p, D.R);
-    for (int t = D.T - 1; t >= 1; --t) {
+    const TnPlan tph = tn_plan(Hk, Xh0, D.R);
+    for (int t = D.T - 1; t >= 1 && D.blocked; --t) {
+        // fused training forward: X_t = G M_{t-1} was never formed (the layer kernel computes G (M W_h^T)),
+        // so the adjoint of the gather goes first: Y_t = S G^T dZ_t, dW_h (+)= Y_t^T M_{t-1} (M recomputed
+        // from the saved Z_{t-1} while loading), db_h (+)= sum dZ_t, dM_{t-1} = Y_t W_h.
+        float *dZt = dZbuf[cur];
+        const int nxt = 1 - cur;
+        float *Y = S(Bl.dX);
+        {
+            ActBwd Q{};
+            Q.G = dZt; Q.ldg = Hk;
+            Q.ptr = g->msg_gather_t.ptr; Q.idx = g->msg_gather_t.idx; Q.coef = g->msg_gather_t.coef;
+            Q.rows = D.R; Q.rows_p = D.Rp; Q.cols = Hk; Q.ld = Hk; Q.out = D.undirected ? S(Bl.dMs) : Y;
+            WD_TRY(act_bwd(Q));
+            if (D.undirected) {
+                ActBwd U{};
+                U.G = S(Bl.dMs); U.ldg = Hk; U.sym_rev = g->b2revb;
+                U.rows = D.R; U.rows_p = D.Rp; U.cols = Hk; U.ld = Hk; U.out = Y;
+                WD_TRY(act_bwd(U));
+            }
+        }
+        Seg m = seg_dense(F(L.Z[t - 1]), Hk, Hk);
+        m.kind = SEG_ACT; m.act = c->activation; m.slope = p->prelu; m.p_drop = t - 1 == 0 ? 0.f : c->dropout;
+        m.seed = c->seed; m.layer = t - 1;
+        WD_TRY(gemm_tn(make_src(D.R, {seg_dense(Y, Hk, Hk)}), make_src(D.R, {m, seg_ones()}), Hk, D.R, tph,
+                       S(Bl.slab), t != D.T - 1, st, dZt));
+        WD_TRY(gemm_nt(Y, Hk, Hk, nullptr, 0, 0, W(PL.WhT), Hk, D.Rp, Hk, epi_store(dZbuf[nxt], Hk), st, true));
+        ActBwd P = base_bwd(F(L.Z[t - 1]), t - 1, c->activation, D.R, D.Rp, Hk, dZbuf[nxt]);
+        P.G = dZbuf[nxt]; P.ldg = Hk;  // (elementwise, in place)
+        if (t - 1 == 0) P.add_in = S(Bl.dRes);
+        else { P.res_out = S(Bl.dRes); P.res_init = 0; }
+        WD_TRY(act_bwd(P));
+        cur = nxt;
+    }
+    for (int t = D.T - 1; t >= 1 && !D.blocked; --t) {
         float *dZt = dZbuf[cur];
         // dW_h, db_h (+)= dZ_t^T [X_t | 1]
         Src dZ = make_src(D.R, {seg_dense(dZt, Hk, Hk)});
         WD_TRY(gemm_tn(dZ, x_h(D, F(L.X[t - 1])), Hk, D.R, tph, S(Bl.slab), t != D.T - 1, st));
         // dX = dZ_t W_h[:, :H]
-        WD_TRY(gemm_nt(dZt, Hk, Hk, nullptr, 0, 0, W(PL.WhT), Hk, D.Rp, Hk, epi_store(S(Bl.dX), Hk), st));
+        WD_TRY(gemm_nt(dZt, Hk, Hk, nullptr, 0, 0, W(PL.WhT), Hk, D.Rp, Hk, epi_store(S(Bl.dX), Hk), st, true));
         // dM_{t-1} = gather^T(dX) (+ symmetrize), then through the activation of layer t-1
         const int nxt = 1 - cur;
         ActBwd P = base_bwd(F(L.Z[t - 1]), t - 1, c->activation, D.R, D.Rp, Hk, dZbuf[nxt]);
@@ -917,7 +991,7 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
     {
         Src dZ = make_src(D.R, {seg_dense(dZbuf[cur], Hk, Hk)});
         Src X = x_in(g, D);
-        TnPlan tp = tn_plan(Hk, X.cols_p, D.R);
+        TnPlan tp = tn_plan(Hk, X, D.R);
         WD_TRY(gemm_tn(dZ, X, Hk, D.R, tp, S(Bl.slab), 0, st));
         WD_TRY(slab_reduce(tp, S(Bl.slab), H, {{0, 0, D.Kin}}, grads->W_i, D.Kin, grads->b_i, X.s[1].kp0, st));
     }

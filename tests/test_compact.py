@@ -212,9 +212,10 @@ def test_generated_batches_forward_and_backward_vs_oracle(kind, b, hidden, depth
 
 @pytest.mark.gpu
 def test_compact_and_host_paths_agree():
-    """Training path (unblocked kernels on the device-built arrays): bitwise equal to the host-packed
-    graph.  Inference: the compact graph's input layer and W_o atom half are sums of weight columns
-    (embed_kernel) instead of GEMMs over the one-hot rows, so only rounding differs."""
+    """Compact (device-built) vs host-packed graph, inference and training (both run the fused
+    molecule-blocked kernels): the compact graph's input layer and W_o atom half are sums of weight
+    columns (embed_kernel) instead of GEMMs over the one-hot rows, so only rounding differs (outputs
+    and gradients within 1e-5 normwise, the parity bar)."""
     from chemprop_amd.mpn import MPNEncoder
     mols = synthetic.make_batch('polymer', 64, 13)
     args = TrainArgs(hidden_size=300, depth=3)
@@ -231,5 +232,7 @@ def test_compact_and_host_paths_agree():
         o2.square().sum().backward()
         outs.append([o1.cpu(), o2.detach().cpu()] + [q.grad.cpu().clone() for q in enc.parameters() if q.grad is not None])
     (a, *ra), (b, *rb) = outs
-    assert all(torch.equal(x, y) for x, y in zip(ra, rb))
+    assert len(ra) == len(rb)
+    for x, y in zip(ra, rb):
+        assert golden_io.normwise(x.numpy(), y.numpy()) <= 1e-5
     assert golden_io.normwise(a.numpy(), b.numpy()) <= 1e-6

@@ -64,7 +64,8 @@ def test_stream_other_kinds_fit_their_slots(kind):
 
 def test_training_on_streamed_batches_matches_host_packed():
     """train_step on streamed (device-built) batches = the same steps on BatchMolGraphs packed on the host
-    from the decoded tables (compact=False): identical losses and parameters."""
+    from the decoded tables (compact=False): the same losses and parameters up to the rounding of the
+    compact input layer (sums of weight columns instead of a GEMM over one-hot rows)."""
     from chemprop_amd.model import MoleculeModel
     from chemprop_amd.nn_utils import initialize_weights
     from chemprop_amd.train import build_optimizer, get_loss_func, train_step
@@ -82,8 +83,9 @@ def test_training_on_streamed_batches_matches_host_packed():
         opt = build_optimizer(m, 1e-3)
         losses = [float(train_step(m, [g], t, get_loss_func('regression'), opt)) for g, t in zip(batches, targets)]
         res.append((losses, [q.detach().cpu() for q in m.parameters()]))
-    assert res[0][0] == res[1][0]
-    assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+    np.testing.assert_allclose(res[0][0], res[1][0], rtol=1e-5)
+    for a, b in zip(res[0][1], res[1][1]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
 
 
 def _molgraphs(g):
