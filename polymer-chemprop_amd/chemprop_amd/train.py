@@ -88,6 +88,30 @@ def build_optimizer(model: nn.Module, args=1e-4, weight_decay: float = 0.0) -> O
     return Adam(groups, fused=fused or None)
 
 
+# pinned host tables of batch_loss, reused per (device, shape): allocating pinned memory every step costs
+# more than the rest of the loss; the event of a table's last copy is waited on before refilling it
+_PINNED_TABLES = {}
+
+
+def _host_table(rows: np.ndarray, dev: torch.device) -> torch.Tensor:
+    """rows (float32 [B][2T]) -> device tensor through a reused pinned buffer (asynchronous copy)."""
+    if dev.type != 'cuda':
+        return torch.from_numpy(rows).to(dev)
+    key = (dev, rows.shape)
+    ent = _PINNED_TABLES.get(key)
+    if ent is None:
+        buf = torch.empty(rows.shape, dtype=torch.float32, pin_memory=True)
+        ev = torch.cuda.Event()
+    else:
+        buf, ev = ent
+        ev.synchronize()  # (the previous step's copy: long finished)
+    buf.numpy()[...] = rows
+    table = buf.to(dev, non_blocking=True)
+    ev.record(torch.cuda.current_stream(dev))
+    _PINNED_TABLES[key] = (buf, ev)
+    return table
+
+
 def batch_loss(preds: torch.Tensor, target_batch: Sequence[Sequence[Optional[float]]], loss_func: Callable,
                dataset_type: str = 'regression', target_weights: Sequence[float] = None,
                data_weights: Sequence[float] = None) -> torch.Tensor:
@@ -96,20 +120,21 @@ def batch_loss(preds: torch.Tensor, target_batch: Sequence[Sequence[Optional[flo
     ``mask.sum()`` is a host count: two fewer device ops forward and backward, the same loss (W is
     rounded once to fp32 instead of twice)."""
     dev = preds.device
-    n_t = len(target_batch[0]) if len(target_batch) else 0
-    tw = [1.0] * n_t if target_weights is None else [float(x) for x in target_weights]
-    # targets and W travel as one host table: on a GPU one pinned, asynchronous copy (pageable copies
-    # would each stall the host until the forward has drained)
-    rows, n_mask = [], 0
-    for i, tb in enumerate(target_batch):
-        dw = 1.0 if data_weights is None else float(data_weights[i])
-        rows.append([0.0 if x is None else float(x) for x in tb]
-                    + [0.0 if x is None else tw[j] * dw for j, x in enumerate(tb)])
-        n_mask += sum(x is not None for x in tb)
-    host = torch.tensor(rows, dtype=torch.float32).reshape(len(target_batch), 2 * n_t)
-    if dev.type == 'cuda':
-        host = host.pin_memory()
-    table = host.to(dev, non_blocking=True)
+    n_b = len(target_batch)
+    n_t = len(target_batch[0]) if n_b else 0
+    # missing targets are None (train.py:47-48); numpy's float conversion would turn them into NaN, so the
+    # mask comes from an object array (a NaN target stays a NaN, as in the reference)
+    obj = np.array(target_batch, dtype=object).reshape(n_b, n_t)
+    present = obj != None  # noqa: E711 (elementwise)
+    tgt = np.where(present, obj, 0.0).astype(np.float64)
+    mask = present.astype(np.float64)
+    tw = np.ones(n_t) if target_weights is None else np.asarray(target_weights, dtype=np.float64)
+    dw = np.ones(n_b) if data_weights is None else np.asarray(data_weights, dtype=np.float64)
+    # targets and W travel as one host table (one pinned, asynchronous copy: pageable copies would each
+    # stall the host until the forward has drained); W = tw * dw * mask, rounded once
+    rows = np.concatenate([tgt, tw[None, :] * dw[:, None] * mask], axis=1).astype(np.float32)
+    n_mask = int(mask.sum())
+    table = _host_table(rows, dev)
     targets, w = table[:, :n_t], table[:, n_t:]
     if dataset_type == 'multiclass':
         targets = targets.long()
@@ -126,11 +151,12 @@ def train_step(model: nn.Module, mol_batch, target_batch, loss_func: Callable, o
                bucket: GradBucket = None) -> torch.Tensor:
     """One optimisation step (train.py:55-86).  With ``bucket`` the gradients are averaged over the
     data-parallel ranks (one all-reduce) before clipping and the optimizer step."""
-    model.train()
+    if not model.training:  # (module.train() walks every submodule: the reference sets it once per epoch)
+        model.train()
     if bucket is not None:
         bucket.zero()
     else:
-        model.zero_grad()
+        optimizer.zero_grad(set_to_none=True)  # (the optimizer holds every model parameter: build_optimizer)
     preds = model(mol_batch, features_batch)
     loss = batch_loss(preds, target_batch, loss_func, dataset_type, target_weights, data_weights)
     loss.backward()

@@ -167,13 +167,32 @@ __global__ __launch_bounds__(4 * BM) void gemm_x6_kernel(X6Params P) {
 //     slab[z][i][bias_col] (+)= sum_{m in split z} A[m][i]      (the bias: X's ones column)
 // Both operands are row-major in the reduction index m (thousands of bond / atom rows).  A 32-row
 // chunk is loaded as 4 rows x 4 columns per thread (16 consecutive lanes read one 256-byte row
-// piece), split into bf16x3 planes in registers and written K-major: column i (or j) becomes the LDS
-// row and the four m values one 8-byte piece of it, so the 16x16x32 fragments read 8 consecutive m
-// per lane exactly as in gemm_x6_kernel (same image, same products hh hm mh hl lh mm).  Threads 0-127
-// stage A, 128-255 B.  The bias column is not a GEMM tile: the j-tile-0 workgroups sum their staged
-// A registers per column and reduce the eight row groups in a fixed order.  Deterministic: fixed
-// split ranges, fixed in-tile order, slabs reduced in split order by slab_reduce_kernel.
+// piece), split into bf16x3 planes in registers and stored in the same orientation: LDS image
+// [32 m][64 columns] per plane, one conflict-free ds_write_b64 per row and plane.  The MFMA operands
+// need 8 consecutive m per lane; ds_read_b64_tr_b16 (MI355X transposed LDS read, cdna_hip_programming
+// T10) delivers them from the row-major image, two reads per fragment, conflict-free under the row
+// swizzle of tn_unit (brute-forced over both lane halves).  Same products as gemm_x6_kernel (hh hm mh hl
+// lh mm).  Threads 0-127 stage A, 128-255 B.  The bias column is not a GEMM tile: the j-tile-0
+// workgroups sum their staged rows per column and reduce the eight row groups in a fixed order.
+// Deterministic: fixed split ranges, fixed in-tile order, slabs reduced in split order by
+// slab_reduce_kernel.
 // ---------------------------------------------------------------------------------------------
+// byte offset of 8-byte unit u (columns 4u .. 4u+3) of row r in a [32][64] bf16 plane image (128-byte
+// rows); the xor spreads the 8 rows of one transposed read over all 64 banks
+__device__ __forceinline__ int tn_unit(int r, int u) { return r * 128 + 8 * (u ^ (4 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)))); }
+
+typedef short tn_v4s __attribute__((ext_vector_type(4)));
+// bf16x8 MFMA fragment of column c (lane-varying), rows 8g .. 8g+7 of a plane image: two transposed reads
+__device__ __forceinline__ bf16x8 tn_frag(const uint8_t *plane, int c0, int lane) {
+    const int i16 = lane & 15, g = lane >> 4;
+    const int u = (c0 >> 2) + (i16 & 3);
+    const tn_v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) tn_v4s *)(plane + tn_unit(8 * g + (i16 >> 2), u)));
+    const tn_v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) tn_v4s *)(plane + tn_unit(8 * g + 4 + (i16 >> 2), u)));
+    const short v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+}
 struct TnX6Params {
     Src A, B;              // A: rows m, cols i (dZ);  B: rows m, cols j (dense segments; the ones column is
                            // the bias and is never read)
@@ -193,15 +212,19 @@ struct TnX6Params {
 template <int SACT, bool BEXT>
 __global__ __launch_bounds__(256) void gemm_tn_x6_kernel(TnX6Params P) {
     constexpr int BM = 64, BN = 64, NT = 256, BKC = 32;
-    constexpr int PL = 64 * 64;            // one plane: 64 rows x 32 K x 2 B
+    constexpr int PL = 32 * 128;           // one plane image: 32 rows (m) x 64 columns x 2 B
     constexpr int STAGE = 6 * PL;          // A planes, then B planes (24 KB)
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wi = wave >> 1, wj = wave & 1, g = lane >> 4, i16 = lane & 15;
-    const int tile = blockIdx.x;
+    // 1-D grid of tiles x splits, XCD-aware (common.hpp xcd_tile): the tiles of one split (same rows of
+    // dZ and X) run on one XCD and read those rows through its L2 once
+    const int ntile = P.tiles_m * P.tiles_n;
+    const int lin = xcd_tile(blockIdx.x, gridDim.x);
+    const int split = lin / ntile, tile = lin % ntile;
     const int mt = tile / P.tiles_n, nt = tile % P.tiles_n;
     const int m0 = mt * BM, n0 = nt * BN;
-    const int kbeg = blockIdx.y * P.k_per_split;
+    const int kbeg = split * P.k_per_split;
     const int kend = min(P.K, kbeg + P.k_per_split);
     const int nchunks = kend > kbeg ? (kend - kbeg + BKC - 1) / BKC : 0;
     // staging role: operand (A for tid < 128), column quad q (4 columns), row quad h4 (4 rows of the chunk).
@@ -223,10 +246,10 @@ __global__ __launch_bounds__(256) void gemm_tn_x6_kernel(TnX6Params P) {
     const bool bias = isA && nt == 0 && P.bias_col >= 0;
     const bool bias_ext = BEXT && bias;
     float bsum[4] = {0.f, 0.f, 0.f, 0.f};
-    // LDS byte offset of this thread's 8-byte piece in row r (plane 0): unit h4 / 2, half h4 % 2
+    // LDS byte offsets of this thread's 8-byte pieces (rows 4 h4 + s, columns 4q .. 4q+3) in plane 0
     int dst[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) dst[c] = (isA ? 0 : 3 * PL) + x6_off<32>(4 * q + c, h4 >> 1) + 8 * (h4 & 1);
+    for (int r = 0; r < 4; ++r) dst[r] = (isA ? 0 : 3 * PL) + tn_unit(4 * h4 + r, q);
     // branch-free loads: every lane loads (rows past kend clamped to the last row, dead columns from a valid
     // dummy address) and the values are masked when staged, so the loads pipeline ahead of the MFMAs
     const float *abase = live ? sg.src + kk : P.A.s[0].src;
@@ -277,17 +300,15 @@ __global__ __launch_bounds__(256) void gemm_tn_x6_kernel(TnX6Params P) {
     auto store_chunk = [&](Regs &R, int kc, uint8_t *stg) {
         mask_rows(R, kc);
         act_rows(R, kc);
-        // column c of the 4x4 block: m values R.v[0..3].c -> three packed pairs per plane
-        const float a[4][4] = {{R.v[0].x, R.v[1].x, R.v[2].x, R.v[3].x}, {R.v[0].y, R.v[1].y, R.v[2].y, R.v[3].y},
-                               {R.v[0].z, R.v[1].z, R.v[2].z, R.v[3].z}, {R.v[0].w, R.v[1].w, R.v[2].w, R.v[3].w}};
+        // row s of the 4x4 block: columns 4q .. 4q+3 -> three packed pairs per plane
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
+        for (int r = 0; r < 4; ++r) {
             uint32_t h0, md0, l0, h1, md1, l1;
-            split_pair(a[c][0], a[c][1], h0, md0, l0);
-            split_pair(a[c][2], a[c][3], h1, md1, l1);
-            *reinterpret_cast<uint2 *>(stg + dst[c]) = make_uint2(h0, h1);
-            *reinterpret_cast<uint2 *>(stg + dst[c] + PL) = make_uint2(md0, md1);
-            *reinterpret_cast<uint2 *>(stg + dst[c] + 2 * PL) = make_uint2(l0, l1);
+            split_pair(R.v[r].x, R.v[r].y, h0, md0, l0);
+            split_pair(R.v[r].z, R.v[r].w, h1, md1, l1);
+            *reinterpret_cast<uint2 *>(stg + dst[r]) = make_uint2(h0, h1);
+            *reinterpret_cast<uint2 *>(stg + dst[r] + PL) = make_uint2(md0, md1);
+            *reinterpret_cast<uint2 *>(stg + dst[r] + 2 * PL) = make_uint2(l0, l1);
         }
         if (bias) {
 #pragma unroll
@@ -307,11 +328,9 @@ __global__ __launch_bounds__(256) void gemm_tn_x6_kernel(TnX6Params P) {
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
-                af[a][p] = *reinterpret_cast<const bf16x8 *>(stg + p * PL + x6_off<32>(wi * 32 + a * 16 + i16, g));
+            for (int a = 0; a < 2; ++a) af[a][p] = tn_frag(stg + p * PL, wi * 32 + a * 16, lane);
 #pragma unroll
-            for (int b = 0; b < 2; ++b)
-                bfr[b][p] = *reinterpret_cast<const bf16x8 *>(stg + 3 * PL + p * PL + x6_off<32>(wj * 32 + b * 16 + i16, g));
+            for (int b = 0; b < 2; ++b) bfr[b][p] = tn_frag(stg + 3 * PL + p * PL, wj * 32 + b * 16, lane);
         }
         constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};
 #pragma unroll
@@ -360,7 +379,7 @@ __global__ __launch_bounds__(256) void gemm_tn_x6_kernel(TnX6Params P) {
         for (int c = 0; c < 4; ++c) bl[h4 * 64 + 4 * q + c] = bsum[c];
     }
     __syncthreads();
-    float *Y = P.slab + (size_t)blockIdx.y * P.slab_stride;
+    float *Y = P.slab + (size_t)split * P.slab_stride;
     Epi E{};
     E.kind = EPI_STORE; E.Y = Y; E.ld = P.ld_slab; E.accumulate = P.accumulate;
     EpiPrefetch<BM, BN, NT> ep;

@@ -362,8 +362,9 @@ void tn_cols(const Src &X, int &n_dense, int &bias_col) {
     bias_col = ones ? X.s[X.nseg - 1].kp0 : -1;
 }
 
-// split-K plan of the weight-gradient GEMM: about TN_TARGET workgroups over the output tiles (64 x 64
-// of [n_out][n_dense]), 32-row chunks; the slabs keep X's padded column space [n_out][cols_p]
+// split-K plan of the weight-gradient GEMM: at most TN_TARGET workgroups (512 = two per CU, the kernel's
+// occupancy: a grid just past it runs a second, nearly empty round) over the output tiles (64 x 64 of
+// [n_out][n_dense]), 32-row chunks; the slabs keep X's padded column space [n_out][cols_p]
 TnPlan tn_plan(int n_out, const Src &X, int m_rows) {
     static const int target = [] {
         const char *e = getenv("WDMPNN_TN_TARGET");
@@ -373,7 +374,7 @@ TnPlan tn_plan(int n_out, const Src &X, int m_rows) {
     tn_cols(X, t.n_dense, t.bias_col);
     const int tiles = ((n_out + 63) / 64) * ((t.n_dense + 63) / 64);
     const int chunks = (m_rows + 31) / 32;
-    int ns = (target + tiles - 1) / tiles;
+    int ns = target / tiles;
     if (ns > chunks) ns = chunks;
     if (ns < 1) ns = 1;
     const int cps = (chunks + ns - 1) / ns;
@@ -398,7 +399,7 @@ int gemm_tn(const Src &dZ, const Src &X, int n_out, int m_rows, const TnPlan &tp
     P.bias_src = bias_src; P.bias_ld = dZ.s[0].ld;
     if (tp.ld_slab % 4 || tp.slab_stride % 4 || ((uintptr_t)slab & 15))
         return fail(WD_ERR_SHAPE, "gemm_tn: unaligned slab");
-    const dim3 grid(P.tiles_m * P.tiles_n, tp.nsplit);
+    const dim3 grid(P.tiles_m * P.tiles_n * tp.nsplit);
     int sact = -1;
     for (int q = 0; q < X.nseg; ++q)
         if (X.s[q].kind == SEG_ACT) sact = X.s[q].act;
