@@ -25,6 +25,11 @@
 
 namespace wd {
 
+// WD_EXP: experiment builds for kernel-time A/Bs (tools/exp_libs.sh); 0 = the product
+#ifndef WD_EXP
+#define WD_EXP 0
+#endif
+
 constexpr int BLK_BONDS = 128, BLK_ATOMS = 64;  // block capacity (rows of the blocked layouts)
 constexpr int BLK_MOLS = 64;                     // molecules per block (empty molecules have no rows)
 // gather entries per row in the block-local ELL form (WdGraph.*_ell_*, WDMPNN_ELL_WIDTH; 12 measured
@@ -382,7 +387,7 @@ __global__ __launch_bounds__(512) void embed_kernel(EmbedP P) {
         fma4(s, cd.last, ld4(wt + (P.Fa - 1) * BN + c));
         fma4(so, cd.last, ld4(wo + (P.Fa - 1) * BN + c));
         st4(ea + la * LDC + c, s);
-        st4(P.eo + ((size_t)blk * BLK_ATOMS + la) * P.Hk + n0 + c, so);
+        if (WD_EXP != 1) st4(P.eo + ((size_t)blk * BLK_ATOMS + la) * P.Hk + n0 + c, so);
     }
     __syncthreads();
     const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
@@ -404,13 +409,15 @@ __global__ __launch_bounds__(512) void embed_kernel(EmbedP P) {
         z0.x += b0.x; z0.y += b0.y; z0.z += b0.z; z0.w += b0.w;
         z1.x += b1.x; z1.y += b1.y; z1.z += b1.z; z1.w += b1.w;
         float *zr = P.inp + (size_t)b * P.Hk + n0 + c;
-        st4(zr, z0);
-        st4(zr + 4, z1);
+        if (WD_EXP != 2) {
+            st4(zr, z0);
+            st4(zr + 4, z1);
+        }
         const float4 y0 = make_float4(act_fwd(ACT, z0.x, slope), act_fwd(ACT, z0.y, slope),
                                       act_fwd(ACT, z0.z, slope), act_fwd(ACT, z0.w, slope));
         const float4 y1 = make_float4(act_fwd(ACT, z1.x, slope), act_fwd(ACT, z1.y, slope),
                                       act_fwd(ACT, z1.z, slope), act_fwd(ACT, z1.w, slope));
-        x6_store8_blk<BLK_BONDS>(mrs, lb, n0 + c, y0, y1);
+        if (WD_EXP != 3) x6_store8_blk<BLK_BONDS>(mrs, lb, n0 + c, y0, y1);
     }
     });
     if (blk == 0 && tid < C4) st4(P.inp + n0 + 4 * tid, f4zero());  // pad row 0 (Z_0 of the backward)

@@ -22,7 +22,9 @@ namespace wd {
 
 constexpr int BK = 32;
 
-enum EpiKind : int { EPI_ACT = 0, EPI_STORE = 1 };
+// EPI_ACTBWD: the activation backward of the layer below fused into a data-gradient GEMM (the elementwise
+// branch of act_bwd_kernel): Y = dZ = C * dropout * act'(Z) (+ add_in), res_out (+)= dZ, PReLU slope partials
+enum EpiKind : int { EPI_ACT = 0, EPI_STORE = 1, EPI_ACTBWD = 2 };
 
 struct Epi {
     int kind;
@@ -41,6 +43,12 @@ struct Epi {
     float p_drop;
     uint64_t seed;
     uint32_t layer;
+    // EPI_ACTBWD
+    const float *add_in;   // [M][ld] or null
+    float *res_out;        // [M][ld] or null: res_out = (res_init ? 0 : res_out) + dZ
+    int res_init;
+    int rows_valid;        // rows >= rows_valid get dZ = 0
+    float *prelu_part;     // per-workgroup PReLU slope partial (indexed by blockIdx.x) or null
 };
 
 template <int ACT, int TM, int TN>
@@ -171,6 +179,59 @@ __device__ __forceinline__ void epilogue_v4_act(const Epi &E, const float *C, in
 }
 
 
+template <int ACT, int BM, int BN, int NT>
+__device__ __forceinline__ void epilogue_v4_actbwd(const Epi &E, const float *C, int ldc, int m0, int n0, int M, int N) {
+    using EP = EpiPrefetch<BM, BN, NT>;
+    const int t = threadIdx.x, cl = (t % EP::C4) * 4, j = n0 + cl;
+    const float slope = ACT == ACT_PRELU ? E.slope[0] : 0.f;
+    float pp = 0.f;
+    if (j < N) {  // (N % 4 == 0: checked by the launcher)
+#pragma unroll
+        for (int p = 0; p < EP::NP; ++p) {
+            const int rl = t / EP::C4 + p * EP::RS, i = m0 + rl;
+            if (i >= M) continue;
+            const size_t o = (size_t)i * E.ld + j;
+            const float4 g = ld4(C + rl * ldc + cl);
+            float4 dz = f4zero();
+            if (i < E.rows_valid) {
+                const float4 z = ld4(E.Z + o);
+                const float gg[4] = {g.x, g.y, g.z, g.w}, zz[4] = {z.x, z.y, z.z, z.w};
+                float d[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float sd = E.p_drop > 0.f ? dropout_scale(E.seed, E.layer, i, j + q, E.p_drop) : 1.f;
+                    d[q] = gg[q] * sd * act_grad(ACT, zz[q], slope);
+                    if (ACT == ACT_PRELU && !(zz[q] > 0.f)) pp += zz[q] * gg[q] * sd;
+                }
+                dz = make_float4(d[0], d[1], d[2], d[3]);
+                if (E.add_in) {
+                    const float4 a = ld4(E.add_in + o);
+                    dz.x += a.x; dz.y += a.y; dz.z += a.z; dz.w += a.w;
+                }
+            }
+            if (E.res_out) {
+                float4 r = dz;
+                if (!E.res_init) {
+                    const float4 r0 = ld4(E.res_out + o);
+                    r.x += r0.x; r.y += r0.y; r.z += r0.z; r.w += r0.w;
+                }
+                st4(E.res_out + o, r);
+            }
+            st4(E.Y + o, dz);
+        }
+    }
+    if (ACT == ACT_PRELU && E.prelu_part) {  // fixed-order block sum (deterministic)
+        __shared__ float red[NT];
+        red[t] = pp;
+        __syncthreads();
+        for (int s2 = NT / 2; s2 > 0; s2 >>= 1) {
+            if (t < s2) red[t] += red[t + s2];
+            __syncthreads();
+        }
+        if (t == 0) E.prelu_part[blockIdx.x] = red[0];
+    }
+}
+
 // the epilogues with the activation dispatched once per call (common.hpp with_act)
 template <int TM, int TN>
 __device__ __forceinline__ void epilogue(const Epi &E, floatx16 (&acc)[TM][TN], int i0, int j0, int h, int l32,
@@ -185,6 +246,8 @@ __device__ __forceinline__ void epilogue_v4(const Epi &E, const float *C, int ld
                                             const EpiPrefetch<BM, BN, NT> &ep) {
     if (E.kind == EPI_ACT)
         with_act(E.act, [&](auto a) { epilogue_v4_act<decltype(a)::value>(E, C, ldc, m0, n0, M, N, ep); });
+    else if (E.kind == EPI_ACTBWD)
+        with_act(E.act, [&](auto a) { epilogue_v4_actbwd<decltype(a)::value, BM, BN, NT>(E, C, ldc, m0, n0, M, N); });
     else
         epilogue_v4_act<ACT_IDENTITY>(E, C, ldc, m0, n0, M, N, ep);
 }

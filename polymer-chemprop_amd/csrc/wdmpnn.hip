@@ -256,7 +256,8 @@ Epi epi_store(float *Y, int ld, long long slab_stride = 0, int accumulate = 0) {
 constexpr int NBM = 64, NBN = 64;
 
 bool epi_aligned(const Epi &epi) {
-    const uintptr_t al = (uintptr_t)epi.Y | (uintptr_t)epi.Z | (uintptr_t)epi.resid | (uintptr_t)epi.bias;
+    const uintptr_t al = (uintptr_t)epi.Y | (uintptr_t)epi.Z | (uintptr_t)epi.resid | (uintptr_t)epi.bias |
+                         (uintptr_t)epi.add_in | (uintptr_t)epi.res_out;
     return epi.ld % 4 == 0 && al % 16 == 0;
 }
 
@@ -534,7 +535,7 @@ BwdLayout bwd_layout(const WdGraph *g, const Dims &D) {
     upd(D.Hk, x_o(g, D, nullptr), D.Va);
     if (D.desc) upd(D.Hdk, x_d(g, D, nullptr), D.Va);
     L.slab = take(slab);
-    L.prelu_floats = (size_t)(D.T + 2) * 4096;
+    L.prelu_floats = (size_t)(D.T + 2) * std::max(4096, (D.Rp / 128) * (D.Hk / 64));
     L.prelu = take(L.prelu_floats);
     L.total = off;
     return L;
@@ -686,10 +687,12 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
             EmbedP E{};
             E.codes = g->atom_codes; E.src_blk = g->bond_src_blk; E.tail = g->bond_tail;
             E.wt = W(PL.WiT); E.woat = W(PL.WoaT); E.eo = F(L.Eo); E.bias = p->b_i ? W(PL.bi) : nullptr; E.blocks = g->blocks;
-            E.Fa = D.Fa; E.Fb = D.Fb; E.Hk = Hk; E.n_tiles = Hk / BNf;
+            const bool bn40 = WD_EXP == 4 && Hk % 40 == 0;
+            E.Fa = D.Fa; E.Fb = D.Fb; E.Hk = Hk; E.n_tiles = Hk / (bn40 ? 40 : BNf);
             E.act = c->activation; E.slope = p->prelu;
             E.inp = F(L.Z[0]); E.mplanes = (uint8_t *)(ws + L.Mb[0]);
-            if (bn80) hipLaunchKernelGGL(embed_kernel<80>, dim3(D.nblk * E.n_tiles), dim3(512), 0, st, E);
+            if (bn40) hipLaunchKernelGGL(embed_kernel<40>, dim3(D.nblk * E.n_tiles), dim3(512), 0, st, E);
+            else if (bn80) hipLaunchKernelGGL(embed_kernel<80>, dim3(D.nblk * E.n_tiles), dim3(512), 0, st, E);
             else hipLaunchKernelGGL(embed_kernel<64>, dim3(D.nblk * E.n_tiles), dim3(512), 0, st, E);
             WD_CHECK_LAUNCH("embed");
         } else {
@@ -947,12 +950,21 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
         m.seed = c->seed; m.layer = t - 1;
         WD_TRY(gemm_tn(make_src(D.R, {seg_dense(Y, Hk, Hk)}), make_src(D.R, {m, seg_ones()}), Hk, D.R, tph,
                        S(Bl.slab), t != D.T - 1, st, dZt));
-        WD_TRY(gemm_nt(Y, Hk, Hk, nullptr, 0, 0, W(PL.WhT), Hk, D.Rp, Hk, epi_store(dZbuf[nxt], Hk), st, true));
-        ActBwd P = base_bwd(F(L.Z[t - 1]), t - 1, c->activation, D.R, D.Rp, Hk, dZbuf[nxt]);
-        P.G = dZbuf[nxt]; P.ldg = Hk;  // (elementwise, in place)
-        if (t - 1 == 0) P.add_in = S(Bl.dRes);
-        else { P.res_out = S(Bl.dRes); P.res_init = 0; }
-        WD_TRY(act_bwd(P));
+        // dZ_{t-1} = (Y_t W_h) * dropout * act'(Z_{t-1}), the residual sum of mpn.py:123 accumulated, in
+        // the GEMM's epilogue (EPI_ACTBWD)
+        Epi e{};
+        e.kind = EPI_ACTBWD; e.Y = dZbuf[nxt]; e.ld = Hk; e.Z = F(L.Z[t - 1]); e.act = c->activation;
+        e.slope = p->prelu; e.p_drop = t - 1 == 0 ? 0.f : c->dropout; e.seed = c->seed; e.layer = t - 1;
+        e.rows_valid = D.R;
+        if (t - 1 == 0) e.add_in = S(Bl.dRes);
+        else { e.res_out = S(Bl.dRes); e.res_init = 0; }
+        if (prelu) {
+            const int tiles = (D.Rp / 128) * (Hk / 64);
+            if (prelu_used + tiles > (int)Bl.prelu_floats) return fail(WD_ERR_SHAPE, "PReLU partials overflow");
+            e.prelu_part = prelu_part + prelu_used;
+            prelu_used += tiles;
+        }
+        WD_TRY(gemm_nt(Y, Hk, Hk, nullptr, 0, 0, W(PL.WhT), Hk, D.Rp, Hk, e, st, true));
         cur = nxt;
     }
     for (int t = D.T - 1; t >= 1 && !D.blocked; --t) {

@@ -7,7 +7,7 @@ for v in prod ${EXPS-1 2 3}; do
   lib=polymer-chemprop_amd/chemprop_amd/libwdmpnn.so
   [ "$v" != prod ] && lib=$PWD/gpurun_exp_$v.so
   WDMPNN_LIB=$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/exp/$v${EXP_TAG:-} -o run -- \
-      python bench.py --steps 100 --warmup 10 --no-cpu --no-secondary --streams 1 ${EXP_BENCH_ARGS:-} > gpurun_out/exp/$v${EXP_TAG:-}.log 2>&1 || { echo "exp $v failed"; tail -5 gpurun_out/exp/$v${EXP_TAG:-}.log; exit 1; }
+      python bench.py --steps 100 --warmup 10 --no-cpu --no-secondary --streams 1 --stream-graphs 0 --stream-train-graphs 0 ${EXP_BENCH_ARGS:-} > gpurun_out/exp/$v${EXP_TAG:-}.log 2>&1 || { echo "exp $v failed"; tail -5 gpurun_out/exp/$v${EXP_TAG:-}.log; exit 1; }
   echo "== $v  $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/exp/$v${EXP_TAG:-}.log)"
   python3 -c "
 import csv, sys
