@@ -34,6 +34,7 @@ for s in "$@"; do
     profx6) step rocprof_x6 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof_x6 -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu --no-secondary --streams 1 --variant ${VARIANT:-10} ;;
     counters) step counters 120 rocprofv3 -L ;;
     pmc) step pmc 1500 bash tools/pmc.sh ;;
+    profqm9) step rocprof_qm9 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof_qm9 -o run --output-format csv -- python bench.py --kind qm9 --steps 100 --warmup 10 --no-cpu --no-secondary --streams 1 --stream-graphs 0 --stream-train-graphs 0 ;;
     sweep) step sweep 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/sweep -o run -- python tools/size_sweep.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
