@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define WDMPNN_ABI_VERSION 3
+#define WDMPNN_ABI_VERSION 4
 #define WDMPNN_ELL_WIDTH 8
 
 enum WdActivation {     /* nn_utils.py:70-99 get_activation_function */
@@ -303,6 +303,26 @@ int wdmpnn_index_select_rows(const float *src, int64_t n_src_rows, int64_t row_l
  * each source row in perm.  Every dsrc row is written (0 for rows never selected). */
 int wdmpnn_index_select_rows_backward(const float *grad, int64_t n_index, int64_t row_len, const int64_t *perm,
                                       const int64_t *ptr, int64_t n_src_rows, float *dsrc, void *stream);
+
+/* One Adam / AdamW optimizer step (torch.optim.Adam / AdamW semantics without amsgrad: the optimizer
+ * step of train/train.py:84, built by utils.py:295-310) over n tensors in one launch per 16 tensors.
+ * Replaces torch's multi-tensor / fused Adam kernels; per element: g += wd p (AdamW: p -= lr wd p),
+ * m = b1 m + (1 - b1) g, v = b2 v + (1 - b2) g^2, p -= lr / (1 - b1^step) * m / (sqrt(v) /
+ * sqrt(1 - b2^step) + eps).  step is the 1-based step count after this update.  Every pointer is a
+ * device pointer to contiguous fp32 data; tensors with numel 0 are skipped. */
+typedef struct WdAdamTensor {
+    float *param;
+    const float *grad;
+    float *exp_avg;
+    float *exp_avg_sq;
+    int64_t numel;
+} WdAdamTensor;
+typedef struct WdAdamHyper {
+    float lr, beta1, beta2, eps, weight_decay;
+    int32_t step;         /* >= 1 */
+    int32_t decoupled;    /* 1 = AdamW */
+} WdAdamHyper;
+int wdmpnn_adam_step(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *h, void *stream);
 
 #ifdef __cplusplus
 }

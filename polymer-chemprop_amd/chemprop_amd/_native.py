@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get('WDMPNN_LIB', os.path.join(HERE, 'libwdmpnn.so'))
 ACTIVATIONS = {'ReLU': 0, 'LeakyReLU': 1, 'PReLU': 2, 'tanh': 3, 'SELU': 4, 'ELU': 5}
 ACT_IDENTITY = 6
 AGGREGATIONS = {'mean': 0, 'sum': 1, 'norm': 2}
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace_bytes',
                     'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace
                     'wdmpnn_event_pool_elapsed_ms', 'wdmpnn_packed_params_bytes', 'wdmpnn_pack_params',
                     'wdmpnn_plane_bytes', 'wdmpnn_split_planes', 'wdmpnn_split_planes_rows',
                     'wdmpnn_build_bond_features', 'wdmpnn_index_select_rows_backward',
-                    'wdmpnn_saved_layout', 'wdmpnn_graph_bytes', 'wdmpnn_build_graph')
+                    'wdmpnn_saved_layout', 'wdmpnn_graph_bytes', 'wdmpnn_build_graph', 'wdmpnn_adam_step')
 
 
 class WdCsr(Structure):
@@ -80,6 +80,16 @@ class WdGrads(Structure):
     _fields_ = [(n, c_void_p) for n in ('W_i', 'b_i', 'W_h', 'b_h', 'W_o', 'b_o', 'W_d', 'b_d', 'prelu')]
 
 
+class WdAdamTensor(Structure):
+    _fields_ = [('param', c_void_p), ('grad', c_void_p), ('exp_avg', c_void_p), ('exp_avg_sq', c_void_p),
+                ('numel', c_int64)]
+
+
+class WdAdamHyper(Structure):
+    _fields_ = [('lr', c_float), ('beta1', c_float), ('beta2', c_float), ('eps', c_float), ('weight_decay', c_float),
+                ('step', c_int32), ('decoupled', c_int32)]
+
+
 class NativeError(RuntimeError):
     pass
 
@@ -121,13 +131,14 @@ def lib() -> ctypes.CDLL:
                                            c_void_p]
     L.wdmpnn_build_bond_features.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_int32, c_int32,
                                              c_int32, c_void_p, c_int32, c_void_p]
+    L.wdmpnn_adam_step.argtypes = [POINTER(WdAdamTensor), c_int32, POINTER(WdAdamHyper), c_void_p]
     L.wdmpnn_event_pool_create.argtypes = [c_int32, POINTER(c_void_p)]
     L.wdmpnn_event_pool_destroy.argtypes = [c_void_p]
     L.wdmpnn_event_pool_elapsed_ms.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_float)]
     for fn in ('wdmpnn_packed_params_bytes', 'wdmpnn_pack_params', 'wdmpnn_event_pool_create', 'wdmpnn_event_pool_destroy', 'wdmpnn_event_pool_elapsed_ms',
                'wdmpnn_workspace_bytes', 'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
                'wdmpnn_index_select_rows', 'wdmpnn_plane_bytes', 'wdmpnn_split_planes', 'wdmpnn_split_planes_rows',
-               'wdmpnn_build_bond_features'):
+               'wdmpnn_build_bond_features', 'wdmpnn_adam_step'):
         getattr(L, fn).restype = c_int
     v = L.wdmpnn_abi_version()
     if v != ABI_VERSION:

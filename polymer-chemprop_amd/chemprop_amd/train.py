@@ -10,6 +10,7 @@
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Callable, List, Optional, Sequence, Union
 
 import numpy as np
@@ -71,21 +72,93 @@ def get_loss_func(dataset_type: str) -> nn.Module:
     raise ValueError(f'Dataset type "{dataset_type}" not supported.')
 
 
+class HipAdam(Optimizer):
+    """torch.optim.Adam / AdamW (no amsgrad, no maximize) whose update is ONE HIP launch per 16
+    parameters (``wdmpnn_adam_step``): torch's fused Adam kernel took 40 us per training step for the
+    355 k parameters of the default model (profiles/round2_train_kernel_trace_v2.txt), this one a few.
+    Same per-element arithmetic as torch's fused Adam; lr / weight_decay / betas / eps are read from the
+    param groups at every step, so schedulers (NoamLR) work unchanged.  State per parameter:
+    ``step`` (int), ``exp_avg``, ``exp_avg_sq`` (as torch's Adam)."""
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 decoupled: bool = False):
+        if lr < 0.0 or eps < 0.0 or not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0) or weight_decay < 0.0:
+            raise ValueError('invalid Adam hyperparameter')
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
+        self.decoupled = bool(decoupled)
+        self._tables = {}  # group index -> (param pointers, ctypes tensor table, state list)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        from . import _native
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        L = _native.lib()
+        for gi, group in enumerate(self.param_groups):
+            ps = [p for p in group['params'] if p.grad is not None]
+            if not ps:
+                continue
+            key = tuple(p.data_ptr() for p in ps)
+            ent = self._tables.get(gi)
+            if ent is None or ent[0] != key:
+                sts = []
+                for p in ps:
+                    if p.device.type != 'cuda' or p.dtype != torch.float32 or not p.is_contiguous():
+                        raise TypeError('HipAdam expects contiguous float32 CUDA parameters')
+                    st = self.state[p]
+                    if 'exp_avg' not in st:
+                        st['step'] = 0
+                        st['exp_avg'] = torch.zeros_like(p)
+                        st['exp_avg_sq'] = torch.zeros_like(p)
+                    sts.append(st)
+                steps = {st['step'] for st in sts}
+                if len(steps) != 1:
+                    raise RuntimeError('HipAdam: parameters of one group at different step counts')
+                tab = (_native.WdAdamTensor * len(ps))()
+                for k, (p, st) in enumerate(zip(ps, sts)):
+                    tab[k].param, tab[k].exp_avg, tab[k].exp_avg_sq = p.data_ptr(), st['exp_avg'].data_ptr(), \
+                        st['exp_avg_sq'].data_ptr()
+                    tab[k].numel = p.numel()
+                ent = (key, tab, sts, ps)
+                self._tables[gi] = ent
+            tab, sts = ent[1], ent[2]
+            for k, p in enumerate(ps):
+                g = p.grad
+                if g.is_sparse or g.dtype != torch.float32 or not g.is_contiguous():
+                    raise TypeError('HipAdam expects dense contiguous float32 gradients')
+                tab[k].grad = g.data_ptr()
+            step = sts[0]['step'] + 1
+            for st in sts:
+                st['step'] = step
+            h = _native.WdAdamHyper(float(group['lr']), float(group['betas'][0]), float(group['betas'][1]),
+                                    float(group['eps']), float(group['weight_decay']), step, int(self.decoupled))
+            _native.check(L.wdmpnn_adam_step(tab, len(ps), ctypes.byref(h), _native.current_stream(ps[0].device)),
+                          'adam step')
+        return loss
+
+    def load_state_dict(self, state_dict) -> None:
+        super().load_state_dict(state_dict)
+        self._tables.clear()  # the moment buffers were replaced: rebuild the pointer tables
+
+
 def build_optimizer(model: nn.Module, args=1e-4, weight_decay: float = 0.0) -> Optimizer:
     """utils.py:295-310: Adam (or AdamW when ``args.optimizer == 'adamw'``) over all parameters.
     ``args`` is a TrainArgs-like object (``init_lr``, optional ``weight_decay`` / ``optimizer``) as in
-    the reference, or a plain learning rate.  On a GPU the update runs as torch's fused
-    single-kernel Adam (same update rule; the multi-tensor version issues ~7 launches per step)."""
+    the reference, or a plain learning rate.  On a GPU the update runs as :class:`HipAdam` (same update
+    rule, one HIP launch per step)."""
     if isinstance(args, (int, float)):
         lr, wd, kind = float(args), weight_decay, 'adam'
     else:
         lr, wd, kind = args.init_lr, getattr(args, 'weight_decay', 0.0), getattr(args, 'optimizer', 'adam')
     params = list(model.parameters())
-    fused = bool(params) and all(p.device.type == 'cuda' for p in params)
     groups = [{'params': params, 'lr': lr, 'weight_decay': wd}]
+    if bool(params) and all(p.device.type == 'cuda' and p.dtype == torch.float32 for p in params):
+        return HipAdam(groups, lr=lr, weight_decay=wd, decoupled=kind == 'adamw')
     if kind == 'adamw':
-        return torch.optim.AdamW(groups, fused=fused or None)
-    return Adam(groups, fused=fused or None)
+        return torch.optim.AdamW(groups)
+    return Adam(groups)
 
 
 # pinned host tables of batch_loss, reused per (device, shape): allocating pinned memory every step costs

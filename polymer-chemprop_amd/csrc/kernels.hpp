@@ -4,6 +4,7 @@
 #pragma once
 #include "common.hpp"
 #include "planes.hpp"
+#include "wdmpnn.h"
 
 namespace wd {
 
@@ -424,4 +425,45 @@ __global__ __launch_bounds__(256) void build_bond_features_kernel(const float *_
     }
 }
 
+}  // namespace wd
+
+// One Adam / AdamW step over up to ADAM_MAX tensors in one launch (the optimizer step of train.py:84,
+// torch.optim.Adam / AdamW as built by utils.py:295-310).  Each tensor owns a contiguous range of
+// workgroups (blk0), each workgroup 1024 elements (4 per thread, strided by 256: coalesced), so the
+// tensor lookup is a uniform scan of the launch table.  Same per-element arithmetic as torch's fused
+// Adam: L2 weight decay folded into the gradient (AdamW: decoupled, on the parameter), moments as
+// beta * m + (1 - beta) * g, denom = sqrt(v) / sqrt(bc2) + eps, p -= (lr / bc1) * m / denom.
+namespace wd {
+constexpr int ADAM_MAX = 16, ADAM_PER_BLOCK = 1024;
+struct AdamLaunch {
+    WdAdamTensor t[ADAM_MAX];
+    int blk0[ADAM_MAX + 1];
+    int n;
+    float beta1, beta2, eps, wd, lr, step_size, bc2_sqrt;
+    int decoupled;
+};
+
+__global__ __launch_bounds__(256) void adam_kernel(AdamLaunch A) {
+    const int b = blockIdx.x;
+    int k = 0;
+    while (k + 1 < A.n && b >= A.blk0[k + 1]) ++k;
+    const WdAdamTensor &T = A.t[k];
+    const int64_t i0 = (int64_t)(b - A.blk0[k]) * ADAM_PER_BLOCK + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < ADAM_PER_BLOCK / 256; ++j) {
+        const int64_t i = i0 + 256 * j;
+        if (i >= T.numel) break;
+        float p = T.param[i], g = T.grad[i];
+        if (A.wd != 0.f) {
+            if (A.decoupled) p -= A.lr * A.wd * p;
+            else g += p * A.wd;
+        }
+        const float m = A.beta1 * T.exp_avg[i] + (1.f - A.beta1) * g;
+        const float v = A.beta2 * T.exp_avg_sq[i] + (1.f - A.beta2) * g * g;
+        T.exp_avg[i] = m;
+        T.exp_avg_sq[i] = v;
+        const float denom = sqrtf(v) / A.bc2_sqrt + A.eps;
+        T.param[i] = p - A.step_size * m / denom;
+    }
+}
 }  // namespace wd

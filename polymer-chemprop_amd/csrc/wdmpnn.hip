@@ -22,6 +22,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -1199,6 +1200,36 @@ int wdmpnn_index_select_rows_backward(const float *grad, int64_t n_index, int64_
     hipLaunchKernelGGL(index_select_rows_bwd_kernel, dim3(ew_blocks(total)), dim3(256), 0, (hipStream_t)stream, grad,
                        row_len, perm, ptr, n_src_rows, dsrc);
     WD_CHECK_LAUNCH("index_select_rows_backward");
+    return 0;
+}
+
+int wdmpnn_adam_step(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *h, void *stream) {
+    if (n < 0 || !h || (n && !tensors)) return fail(WD_ERR_ARG, "null or negative argument");
+    if (h->step < 1) return fail(WD_ERR_ARG, "adam step must be >= 1");
+    const double bc1 = 1.0 - std::pow((double)h->beta1, (double)h->step);
+    const double bc2 = 1.0 - std::pow((double)h->beta2, (double)h->step);
+    for (int s = 0; s < n; s += ADAM_MAX) {
+        AdamLaunch A{};
+        A.beta1 = h->beta1; A.beta2 = h->beta2; A.eps = h->eps; A.wd = h->weight_decay; A.lr = h->lr;
+        A.step_size = (float)(h->lr / bc1); A.bc2_sqrt = (float)std::sqrt(bc2); A.decoupled = h->decoupled;
+        int blocks = 0;
+        for (int i = s; i < n && i < s + ADAM_MAX; ++i) {
+            const WdAdamTensor &T = tensors[i];
+            if (T.numel < 0) return fail(WD_ERR_ARG, "negative numel");
+            if (T.numel == 0) continue;
+            if (!T.param || !T.grad || !T.exp_avg || !T.exp_avg_sq) return fail(WD_ERR_ARG, "null tensor pointer");
+            const int64_t nb = (T.numel + ADAM_PER_BLOCK - 1) / ADAM_PER_BLOCK;
+            if (blocks + nb > INT32_MAX / 2) return fail(WD_ERR_SHAPE, "adam launch too large");
+            A.t[A.n] = T;
+            A.blk0[A.n] = blocks;
+            blocks += (int)nb;
+            ++A.n;
+        }
+        if (!A.n) continue;
+        A.blk0[A.n] = blocks;
+        hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, A);
+        WD_CHECK_LAUNCH("adam");
+    }
     return 0;
 }
 

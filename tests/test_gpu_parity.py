@@ -377,7 +377,7 @@ def test_dropout_masks_agree_across_paths(extra):
 
 
 def test_training_step_fused_adam_and_pinned_targets():
-    """train_step on the GPU (pinned target table, fused Adam from build_optimizer) agrees with the
+    """train_step on the GPU (pinned target table, the HIP Adam from build_optimizer) agrees with the
     same steps through torch's plain per-parameter Adam (the reference's optimizer)."""
     from chemprop_amd.nn_utils import initialize_weights
     from chemprop_amd.train import build_optimizer, get_loss_func, train_step
@@ -392,7 +392,7 @@ def test_training_step_fused_adam_and_pinned_targets():
         initialize_weights(m)
         m = m.to(DEV)
         opt = build_optimizer(m, 1e-3) if fused else torch.optim.Adam(m.parameters(), lr=1e-3, foreach=False)
-        assert opt.param_groups[0]['fused'] == (True if fused else None)
+        assert type(opt).__name__ == ('HipAdam' if fused else 'Adam')
         models.append(m)
         opts.append(opt)
     for _ in range(3):
@@ -401,6 +401,43 @@ def test_training_step_fused_adam_and_pinned_targets():
     for (n, a), b in zip(models[0].named_parameters(), models[1].parameters()):
         d = float((a - b).detach().abs().max())
         assert d <= 1e-6, (n, d)
+
+
+@pytest.mark.parametrize('kind', ['adam', 'adamw'])
+def test_hip_adam_matches_torch_adam(kind):
+    """HipAdam (one wdmpnn_adam_step launch) vs torch's single-tensor Adam / AdamW over 6 steps: weight
+    decay, an lr changed between steps (what NoamLR does), a parameter without gradient, more than 16
+    tensors (two launches) and a state_dict round trip; every parameter and moment within 1e-6."""
+    from chemprop_amd.train import HipAdam
+    gen = torch.Generator().manual_seed(5)
+    shapes = [(300, 147), (300,), (1,), (7, 3), (1025,)] + [(13 + k,) for k in range(14)]
+    base = [torch.randn(s, generator=gen) for s in shapes]
+    ref = [torch.nn.Parameter(t.clone()) for t in base]
+    hip = [torch.nn.Parameter(t.clone().to(DEV)) for t in base]
+    cls = torch.optim.AdamW if kind == 'adamw' else torch.optim.Adam
+    o_ref = cls(ref, lr=1e-2, weight_decay=0.05, foreach=False)
+    o_hip = HipAdam(hip, lr=1e-2, weight_decay=0.05, decoupled=kind == 'adamw')
+    for step in range(6):
+        grads = [torch.randn(s, generator=gen) for s in shapes]
+        for k, (a, b, g) in enumerate(zip(ref, hip, grads)):
+            a.grad = None if k == 3 else g.clone()
+            b.grad = None if k == 3 else g.clone().to(DEV)
+        for o in (o_ref, o_hip):
+            o.param_groups[0]['lr'] = 1e-2 / (1 + step)
+        o_ref.step()
+        o_hip.step()
+        if step == 2:
+            sd = o_hip.state_dict()
+            o_hip = HipAdam(hip, lr=1e-2, weight_decay=0.05, decoupled=kind == 'adamw')
+            o_hip.load_state_dict(sd)
+    for k, (a, b) in enumerate(zip(ref, hip)):
+        d = float((a.detach() - b.detach().cpu()).abs().max())
+        assert d <= 1e-6 * max(1.0, float(a.detach().abs().max())), (k, d)
+        if k != 3:
+            for name in ('exp_avg', 'exp_avg_sq'):
+                x, y = o_ref.state[a][name], o_hip.state[b][name].cpu()
+                assert float((x - y).abs().max()) <= 1e-6 * max(1.0, float(x.abs().max())), (k, name)
+    assert 3 not in [i for i, b in enumerate(hip) if b in o_hip.state]
 
 
 def test_inference_plan_cache_follows_config_and_weights():
