@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define WDMPNN_ABI_VERSION 4
+#define WDMPNN_ABI_VERSION 5
 #define WDMPNN_ELL_WIDTH 8
 
 enum WdActivation {     /* nn_utils.py:70-99 get_activation_function */
@@ -323,6 +323,27 @@ typedef struct WdAdamHyper {
     int32_t decoupled;    /* 1 = AdamW */
 } WdAdamHyper;
 int wdmpnn_adam_step(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *h, void *stream);
+
+/* The training step's FFN head + masked MSE loss and their gradients in two launches (model.py:57-121
+ * with ffn_num_layers = 2 and no dropout, train.py:55-74 with MSELoss): replaces the ~25 small torch ops
+ * (and their host time) of ffn(emb), loss_func(preds, targets) * weights, .sum() / mask.sum() and their
+ * autograd backward.  Row-major fp32 device arrays; w = target weight * data weight * mask per entry. */
+typedef struct WdHead {
+    const float *x; int32_t ld_x;          /* encoder output [B][ld_x], first F columns used        */
+    int32_t B, F, Hf, T;                   /* rows, input width, hidden width, outputs (tasks)      */
+    const float *W1, *b1, *W2, *b2;        /* nn.Linear(F, Hf), nn.Linear(Hf, T) (biases may be NULL) */
+    const float *table; int32_t ld_table;  /* [B][ld_table]: targets [T], then weights w [T]        */
+    float inv_n;                           /* 1 / mask.sum()                                        */
+    int32_t act;                           /* WdActivation of the FFN (not PReLU)                   */
+    float *a, *dh, *dout, *lossrow;        /* scratch [B][Hf], [B][Hf], [B][T], [B]                 */
+    float *dx;                             /* [B][ld_x]: d loss / d x                               */
+    float *dW1, *db1, *dW2, *db2;          /* parameter gradients (db1 / db2 NULL = skip)           */
+    float *loss;                           /* [1]                                                   */
+} WdHead;
+int wdmpnn_head_mse(const WdHead *h, void *stream);
+/* p_i[0 .. n_i) *= *s (device scalar) for k <= 8 buffers: the head's gradients times the loss's
+ * incoming gradient in one launch. */
+int wdmpnn_scale(float *const *p, const int64_t *n, int32_t k, const float *s, void *stream);
 
 #ifdef __cplusplus
 }

@@ -185,14 +185,9 @@ def _host_table(rows: np.ndarray, dev: torch.device) -> torch.Tensor:
     return table
 
 
-def batch_loss(preds: torch.Tensor, target_batch: Sequence[Sequence[Optional[float]]], loss_func: Callable,
-               dataset_type: str = 'regression', target_weights: Sequence[float] = None,
-               data_weights: Sequence[float] = None) -> torch.Tensor:
-    """train.py:46-74: ``(loss_func(preds, targets) * target_weights * data_weights * mask).sum() /
-    mask.sum()``.  The three weight factors are multiplied on the host into one weight table W, and
-    ``mask.sum()`` is a host count: two fewer device ops forward and backward, the same loss (W is
-    rounded once to fp32 instead of twice)."""
-    dev = preds.device
+def _loss_table(target_batch, target_weights, data_weights, dev):
+    """train.py:46-74's targets and weights as one device table [B][2T] (targets | w = target weight *
+    data weight * mask, rounded once to fp32) and the host count mask.sum()."""
     n_b = len(target_batch)
     n_t = len(target_batch[0]) if n_b else 0
     # missing targets are None (train.py:47-48); numpy's float conversion would turn them into NaN, so the
@@ -204,10 +199,19 @@ def batch_loss(preds: torch.Tensor, target_batch: Sequence[Sequence[Optional[flo
     tw = np.ones(n_t) if target_weights is None else np.asarray(target_weights, dtype=np.float64)
     dw = np.ones(n_b) if data_weights is None else np.asarray(data_weights, dtype=np.float64)
     # targets and W travel as one host table (one pinned, asynchronous copy: pageable copies would each
-    # stall the host until the forward has drained); W = tw * dw * mask, rounded once
+    # stall the host until the forward has drained)
     rows = np.concatenate([tgt, tw[None, :] * dw[:, None] * mask], axis=1).astype(np.float32)
-    n_mask = int(mask.sum())
-    table = _host_table(rows, dev)
+    return _host_table(rows, dev), n_t, int(mask.sum())
+
+
+def batch_loss(preds: torch.Tensor, target_batch: Sequence[Sequence[Optional[float]]], loss_func: Callable,
+               dataset_type: str = 'regression', target_weights: Sequence[float] = None,
+               data_weights: Sequence[float] = None) -> torch.Tensor:
+    """train.py:46-74: ``(loss_func(preds, targets) * target_weights * data_weights * mask).sum() /
+    mask.sum()``.  The three weight factors are multiplied on the host into one weight table W, and
+    ``mask.sum()`` is a host count: two fewer device ops forward and backward, the same loss (W is
+    rounded once to fp32 instead of twice)."""
+    table, n_t, n_mask = _loss_table(target_batch, target_weights, data_weights, preds.device)
     targets, w = table[:, :n_t], table[:, n_t:]
     if dataset_type == 'multiclass':
         targets = targets.long()
@@ -218,20 +222,125 @@ def batch_loss(preds: torch.Tensor, target_batch: Sequence[Sequence[Optional[flo
     return loss.sum() / float(n_mask)
 
 
+# ------------------------------------------------------------------------------------------------
+# Fused FFN head + masked MSE loss (wdmpnn_head_mse).  The reference's step evaluates ffn(emb) (model.py:
+# 57-121), loss_func(preds, targets) * weights and .sum() / mask.sum() (train.py:55-74) and autograd runs
+# their backward: ~25 small torch ops whose host time left the GPU idle for most of the step
+# (profiles/round2_train_kernel_trace_v3.txt).  For the default regression head (two Linear layers, an
+# activation, no active dropout, MSELoss) the loss and every gradient of the head come from two HIP
+# launches in the forward; the backward scales them by the loss's incoming gradient (one launch).
+# ------------------------------------------------------------------------------------------------
+def _head_act(m: nn.Module) -> Optional[int]:
+    """WdActivation of an FFN activation module the fused head supports (not PReLU), else None."""
+    if type(m) is nn.ReLU:
+        return 0
+    if type(m) is nn.LeakyReLU and m.negative_slope == 0.1:
+        return 1
+    if type(m) is nn.Tanh:
+        return 3
+    if type(m) is nn.SELU:
+        return 4
+    if type(m) is nn.ELU and m.alpha == 1.0:
+        return 5
+    return None
+
+
+def _fusable_head(model: nn.Module, loss_func: Callable, dataset_type: str):
+    """(Linear 1, Linear 2, activation code) when the step's head + loss can run fused, else None."""
+    from .model import MoleculeModel
+    if dataset_type != 'regression' or type(loss_func) is not nn.MSELoss or loss_func.reduction != 'none':
+        return None
+    if not isinstance(model, MoleculeModel) or type(model).forward is not MoleculeModel.forward:
+        return None
+    ffn = model.ffn
+    if len(ffn) != 5:
+        return None
+    d0, l1, act, d1, l2 = ffn
+    if type(d0) is not nn.Dropout or type(d1) is not nn.Dropout or type(l1) is not nn.Linear \
+            or type(l2) is not nn.Linear:
+        return None
+    if model.training and (d0.p > 0 or d1.p > 0):
+        return None
+    code = _head_act(act)
+    if code is None:
+        return None
+    for t in (l1.weight, l1.bias, l2.weight, l2.bias):
+        if t is not None and (t.device.type != 'cuda' or t.dtype != torch.float32 or not t.is_contiguous()):
+            return None
+    if l1.in_features > 4096 or l1.out_features > 4096 or l2.out_features > 64:
+        return None
+    return l1, l2, code
+
+
+class _HeadMSE(torch.autograd.Function):
+    """loss = sum(w (W2 act(W1 x + b1) + b2 - y)^2) / n, with every gradient computed in the forward."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2, table, inv_n, act):
+        from . import _native
+        x = x.contiguous()
+        dev = x.device
+        B, F = x.shape
+        Hf, T = W1.shape[0], W2.shape[0]
+        scratch = torch.empty(B * (2 * Hf + T + 1), dtype=torch.float32, device=dev)
+        dx = torch.empty_like(x)
+        dW1, dW2 = torch.empty_like(W1), torch.empty_like(W2)
+        db1 = torch.empty_like(b1) if b1 is not None else None
+        db2 = torch.empty_like(b2) if b2 is not None else None
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        ptr = _native.ptr
+        sp = scratch.data_ptr()
+        h = _native.WdHead(ptr(x), F, B, F, Hf, T, ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(table), table.shape[1],
+                           float(inv_n), act, sp, sp + 4 * B * Hf, sp + 8 * B * Hf, sp + 4 * B * (2 * Hf + T),
+                           ptr(dx), ptr(dW1), ptr(db1), ptr(dW2), ptr(db2), ptr(loss))
+        _native.check(_native.lib().wdmpnn_head_mse(ctypes.byref(h), _native.current_stream(dev)), 'FFN head + loss')
+        ctx.grads = (dx, dW1, db1, dW2, db2)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        from . import _native
+        grads, ctx.grads = ctx.grads, None  # (sole owner: autograd adopts the tensors instead of copying)
+        live = [g for g in grads if g is not None]
+        gl = gl.to(torch.float32).contiguous()
+        ptrs = (ctypes.c_void_p * len(live))(*[g.data_ptr() for g in live])
+        ns = (ctypes.c_int64 * len(live))(*[g.numel() for g in live])
+        _native.check(_native.lib().wdmpnn_scale(ptrs, ns, len(live), gl.data_ptr(),
+                                                 _native.current_stream(gl.device)), 'scale')
+        return grads + (None, None, None)
+
+
+def head_loss(emb: torch.Tensor, head, target_batch, target_weights=None, data_weights=None) -> torch.Tensor:
+    """``batch_loss(model.ffn(emb), ...)`` for a head accepted by ``_fusable_head`` (regression, MSE)."""
+    l1, l2, act = head
+    table, n_t, n_mask = _loss_table(target_batch, target_weights, data_weights, emb.device)
+    if n_t != l2.out_features:
+        raise ValueError(f'{n_t} targets per row for {l2.out_features} outputs')
+    inv_n = 1.0 / n_mask if n_mask else float('inf')
+    return _HeadMSE.apply(emb, l1.weight, l1.bias, l2.weight, l2.bias, table, inv_n, act)
+
+
 def train_step(model: nn.Module, mol_batch, target_batch, loss_func: Callable, optimizer: Optimizer,
                scheduler: _LRScheduler = None, dataset_type: str = 'regression', features_batch=None,
                target_weights=None, data_weights=None, grad_clip: float = None,
-               bucket: GradBucket = None) -> torch.Tensor:
+               bucket: GradBucket = None, fused_head: bool = True) -> torch.Tensor:
     """One optimisation step (train.py:55-86).  With ``bucket`` the gradients are averaged over the
-    data-parallel ranks (one all-reduce) before clipping and the optimizer step."""
+    data-parallel ranks (one all-reduce) before clipping and the optimizer step.  ``fused_head``: the
+    default regression head + loss run as ``wdmpnn_head_mse`` (same loss and gradients within fp32
+    summation order; ``False`` = the torch ops of the reference)."""
     if not model.training:  # (module.train() walks every submodule: the reference sets it once per epoch)
         model.train()
     if bucket is not None:
         bucket.zero()
     else:
         optimizer.zero_grad(set_to_none=True)  # (the optimizer holds every model parameter: build_optimizer)
-    preds = model(mol_batch, features_batch)
-    loss = batch_loss(preds, target_batch, loss_func, dataset_type, target_weights, data_weights)
+    head = _fusable_head(model, loss_func, dataset_type) if fused_head else None
+    if head is not None:  # the default regression head: ffn + loss + their gradients as two HIP launches
+        loss = head_loss(model.encoder(mol_batch, features_batch), head, target_batch, target_weights,
+                         data_weights)
+    else:
+        preds = model(mol_batch, features_batch)
+        loss = batch_loss(preds, target_batch, loss_func, dataset_type, target_weights, data_weights)
     loss.backward()
     if bucket is not None:
         bucket.allreduce_mean()

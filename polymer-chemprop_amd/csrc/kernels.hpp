@@ -467,3 +467,162 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamLaunch A) {
     }
 }
 }  // namespace wd
+
+// ------------------------------------------------------------------------------------------------
+// The training step's FFN head and masked loss (model.py:57-121 with ffn_num_layers = 2, no dropout;
+// train.py:55-74 with MSELoss): per molecule row x (the encoder output),
+//     h = W1 x + b1, a = act(h), out = W2 a + b2,
+//     loss = sum_rows sum_t w[t] (out[t] - y[t])^2 / n      (w = target weight * data weight * mask)
+// and, in the same pass, the gradients of that loss: dout = 2 w (out - y) / n, dh = act'(h) W2^T dout,
+// dx = W1^T dh, dW1 = sum_rows dh x^T, db1 = sum dh, dW2 = sum dout a^T, db2 = sum dout.  Three launches:
+// the H GEMM, one wave per row for the loss and dh, then the dX and dW1 GEMMs and the small sums (fixed
+// summation orders).  fp32 FMA throughout (the GEMMs are 128 x 300 x 300: latency, not FLOPs).
+// ------------------------------------------------------------------------------------------------
+namespace wd {
+constexpr int HEAD_MAX_F = 4096, HEAD_MAX_H = 4096, HEAD_MAX_T = 64;
+
+__device__ __forceinline__ float wave_sum(float s) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    return s;
+}
+
+// C[i][j] (+ bias[j]) = sum_k A(i, k) B(k, j) for one 32 x 32 tile of C (M x N), 256 threads (2 x 2
+// outputs each), K in 32-wide chunks through LDS.  Strided operands: A(i, k) = A[i sai + k sak],
+// B(k, j) = B[k sbk + j sbj] -- the head's three small GEMMs (X W1^T, dH W1, dH^T X) differ only in
+// their strides; every operand is L2-resident (<= 0.5 MB).
+struct SmallGemm {
+    const float *A; long long sai, sak;
+    const float *B; long long sbk, sbj;
+    const float *bias;
+    float *C; long long ldc;
+    int M, N, K;
+};
+__device__ __forceinline__ void small_gemm_tile(const SmallGemm &G, int tile, float (*as)[33], float (*bs)[33]) {
+    const int tn = (G.N + 31) / 32, i0 = (tile / tn) * 32, j0 = (tile % tn) * 32;
+    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+    float c[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+    for (int k0 = 0; k0 < G.K; k0 += 32) {
+        // stage A[i0 .. +32][k0 .. +32] and B[k0 .. +32][j0 .. +32] (4 elements per thread each), consecutive
+        // lanes along each operand's contiguous index (coalesced loads; the padded rows keep the
+        // transposed LDS writes conflict-free)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = tid + 256 * q, hi = e >> 5, lo = e & 31;
+            const int ra = G.sak == 1 ? hi : lo, ca = G.sak == 1 ? lo : hi;  // (i, k) of A
+            const int ia = i0 + ra, ka = k0 + ca;
+            as[ra][ca] = ia < G.M && ka < G.K ? G.A[ia * G.sai + ka * G.sak] : 0.f;
+            const int rb = G.sbj == 1 ? hi : lo, cb = G.sbj == 1 ? lo : hi;  // (k, j) of B
+            const int kb = k0 + rb, jb = j0 + cb;
+            bs[rb][cb] = kb < G.K && jb < G.N ? G.B[kb * G.sbk + jb * G.sbj] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int k = 0; k < 32; ++k) {
+            const float a0 = as[2 * ty][k], a1 = as[2 * ty + 1][k], b0 = bs[k][2 * tx], b1 = bs[k][2 * tx + 1];
+            c[0][0] = fmaf(a0, b0, c[0][0]); c[0][1] = fmaf(a0, b1, c[0][1]);
+            c[1][0] = fmaf(a1, b0, c[1][0]); c[1][1] = fmaf(a1, b1, c[1][1]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int i = i0 + 2 * ty + a, j = j0 + 2 * tx + b;
+            if (i < G.M && j < G.N) G.C[i * G.ldc + j] = c[a][b] + (G.bias ? G.bias[j] : 0.f);
+        }
+}
+__device__ __forceinline__ int small_gemm_tiles(const SmallGemm &G) { return ((G.M + 31) / 32) * ((G.N + 31) / 32); }
+
+// head step 1: H = X W1^T + b1 -> P.a (pre-activation, [B][Hf])
+__global__ __launch_bounds__(256) void head_h_kernel(WdHead P) {
+    __shared__ float as[32][33], bs[32][33];
+    SmallGemm G{P.x, P.ld_x, 1, P.W1, 1, P.F, P.b1, P.a, P.Hf, P.B, P.Hf, P.F};
+    small_gemm_tile(G, blockIdx.x, as, bs);
+}
+
+// head step 2, one wave per row: out = W2 act(h) + b2, the row's loss terms, dout = 2 w (out - y) / n,
+// dh = act'(h) * (W2^T dout); act(h) replaces h in P.a (for dW2)
+__global__ __launch_bounds__(256) void head_rows_kernel(WdHead P) {
+    __shared__ float dsh[4][HEAD_MAX_T];  // the row's dout (every lane writes the same value; LDS keeps a wave's order)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, row = blockIdx.x * 4 + wave;
+    if (row >= P.B) return;
+    const int Hf = P.Hf, T = P.T;
+    float *h = P.a + (size_t)row * Hf;
+    const float *tab = P.table + (size_t)row * P.ld_table;
+    with_act(P.act, [&](auto act_c) {
+        constexpr int ACT = decltype(act_c)::value;
+        float l = 0.f;
+        for (int t = 0; t < T; ++t) {
+            const float *w2 = P.W2 + (size_t)t * Hf;
+            float s = 0.f;
+            for (int j = lane; j < Hf; j += 64) s = fmaf(w2[j], act_fwd(ACT, h[j], 0.f), s);
+            s = wave_sum(s) + (P.b2 ? P.b2[t] : 0.f);
+            const float r = s - tab[t], w = tab[T + t];
+            l = fmaf(w * r, r, l);
+            const float d = 2.f * w * r * P.inv_n;
+            dsh[wave][t] = d;
+            if (lane == 0) P.dout[(size_t)row * T + t] = d;
+        }
+        if (lane == 0) P.lossrow[row] = l;
+        for (int j = lane; j < Hf; j += 64) {
+            float s = 0.f;
+            for (int t = 0; t < T; ++t) s = fmaf(dsh[wave][t], P.W2[(size_t)t * Hf + j], s);
+            const float z = h[j];
+            P.dh[(size_t)row * Hf + j] = s * act_grad(ACT, z, 0.f);
+            h[j] = act_fwd(ACT, z, 0.f);
+        }
+    });
+}
+
+// head step 3: dX = dH W1 (tiles 0 .. n1), dW1 = dH^T X (next n2 tiles), then db1, dW2, db2 and the loss
+// (one thread per element, rows summed in order)
+__global__ __launch_bounds__(256) void head_grads_kernel(WdHead P) {
+    __shared__ float as[32][33], bs[32][33];
+    const SmallGemm GX{P.dh, P.Hf, 1, P.W1, P.F, 1, nullptr, P.dx, P.ld_x, P.B, P.F, P.Hf};
+    const SmallGemm GW{P.dh, 1, P.Hf, P.x, P.ld_x, 1, nullptr, P.dW1, P.F, P.Hf, P.F, P.B};
+    const int n1 = small_gemm_tiles(GX), n2 = small_gemm_tiles(GW);
+    const int b = blockIdx.x;
+    if (b < n1) { small_gemm_tile(GX, b, as, bs); return; }
+    if (b < n1 + n2) { small_gemm_tile(GW, b - n1, as, bs); return; }
+    const int Hf = P.Hf, T = P.T, B = P.B;
+    const long long q = (long long)(b - n1 - n2) * 256 + threadIdx.x;
+    if (q < Hf) {
+        float s = 0.f;
+        for (int r = 0; r < B; ++r) s += P.dh[(size_t)r * Hf + q];
+        if (P.db1) P.db1[q] = s;
+    } else if (q < Hf + (long long)T * Hf) {
+        const int u = (int)(q - Hf), t = u / Hf, j = u % Hf;
+        float s = 0.f;
+        for (int r = 0; r < B; ++r) s = fmaf(P.dout[(size_t)r * T + t], P.a[(size_t)r * Hf + j], s);
+        P.dW2[u] = s;
+    } else if (q < Hf + (long long)T * Hf + T) {
+        const int t = (int)(q - Hf - (long long)T * Hf);
+        float s = 0.f;
+        for (int r = 0; r < B; ++r) s += P.dout[(size_t)r * T + t];
+        if (P.db2) P.db2[t] = s;
+    } else if (q == Hf + (long long)T * Hf + T) {
+        float s = 0.f;
+        for (int r = 0; r < B; ++r) s += P.lossrow[r];
+        P.loss[0] = s * P.inv_n;
+    }
+}
+
+// launch sizes of the head steps
+__host__ __device__ inline int head_tiles(int M, int N) { return ((M + 31) / 32) * ((N + 31) / 32); }
+
+// y_i *= s[0] for up to 8 buffers (the head's gradients times the incoming gradient of the loss)
+struct ScaleJobs {
+    float *p[8];
+    long long n[8];
+    int k;
+    const float *s;
+};
+__global__ __launch_bounds__(256) void scale_kernel(ScaleJobs J) {
+    const float s = J.s[0];
+    for (int i = 0; i < J.k; ++i)
+        for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < J.n[i]; e += (long long)gridDim.x * 256)
+            J.p[i][e] *= s;
+}
+}  // namespace wd

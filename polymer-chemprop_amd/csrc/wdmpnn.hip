@@ -1233,4 +1233,47 @@ int wdmpnn_adam_step(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *
     return 0;
 }
 
+int wdmpnn_head_mse(const WdHead *h, void *stream) {
+    if (!h) return fail(WD_ERR_ARG, "null head");
+    if (h->B < 0 || h->F <= 0 || h->Hf <= 0 || h->T <= 0 || h->ld_x < h->F || h->ld_table < 2 * h->T)
+        return fail(WD_ERR_SHAPE, "head: bad sizes");
+    if (h->F > HEAD_MAX_F || h->Hf > HEAD_MAX_H || h->T > HEAD_MAX_T)
+        return fail(WD_ERR_UNSUPPORTED, "head: F, Hf <= 4096 and T <= 64");
+    if (h->act < 0 || h->act > WD_ACT_ELU || h->act == WD_ACT_PRELU) return fail(WD_ERR_UNSUPPORTED, "head activation");
+    if (!h->W1 || !h->W2 || !h->a || !h->dh || !h->dout || !h->lossrow || !h->dW1 || !h->dW2 || !h->loss ||
+        (h->B && (!h->x || !h->table || !h->dx)))
+        return fail(WD_ERR_ARG, "head: null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    if (h->B > 0) {
+        hipLaunchKernelGGL(head_h_kernel, dim3(head_tiles(h->B, h->Hf)), dim3(256), 0, st, *h);
+        WD_CHECK_LAUNCH("head_h");
+        hipLaunchKernelGGL(head_rows_kernel, dim3((h->B + 3) / 4), dim3(256), 0, st, *h);
+        WD_CHECK_LAUNCH("head_rows");
+    }
+    const long long rest = h->Hf + (long long)h->T * h->Hf + h->T + 1;
+    const long long blocks = head_tiles(h->B, h->F) + head_tiles(h->Hf, h->F) + (rest + 255) / 256;
+    hipLaunchKernelGGL(head_grads_kernel, dim3((unsigned)blocks), dim3(256), 0, st, *h);
+    WD_CHECK_LAUNCH("head_grads");
+    return 0;
+}
+
+int wdmpnn_scale(float *const *p, const int64_t *n, int32_t k, const float *s, void *stream) {
+    if (k < 0 || k > 8 || !s || (k && (!p || !n))) return fail(WD_ERR_ARG, "scale: bad arguments");
+    ScaleJobs J{};
+    long long most = 0;
+    for (int i = 0; i < k; ++i) {
+        if (n[i] < 0 || (n[i] && !p[i])) return fail(WD_ERR_ARG, "scale: bad buffer");
+        J.p[i] = p[i];
+        J.n[i] = n[i];
+        most = std::max<long long>(most, n[i]);
+    }
+    J.k = k;
+    J.s = s;
+    if (!most) return 0;
+    hipLaunchKernelGGL(scale_kernel, dim3((unsigned)std::min<long long>((most + 255) / 256, 1024)), dim3(256), 0,
+                       (hipStream_t)stream, J);
+    WD_CHECK_LAUNCH("scale");
+    return 0;
+}
+
 }  // extern "C"

@@ -440,6 +440,47 @@ def test_hip_adam_matches_torch_adam(kind):
     assert 3 not in [i for i, b in enumerate(hip) if b in o_hip.state]
 
 
+@pytest.mark.parametrize('b,tasks,act,features', [(128, 1, 'ReLU', 0), (16, 2, 'tanh', 0), (33, 3, 'ELU', 5),
+                                                   (8, 1, 'LeakyReLU', 0), (20, 2, 'SELU', 0)])
+def test_fused_head_loss_matches_torch(b, tasks, act, features):
+    """The fused FFN head + masked MSE (wdmpnn_head_mse: the train step's default regression path) gives
+    the torch head's loss and every gradient (head, encoder) within 1e-5; missing targets, target and
+    data weights, several tasks, extra molecule features, and a scaled incoming gradient."""
+    from chemprop_amd.nn_utils import initialize_weights
+    from chemprop_amd.train import _fusable_head, batch_loss, get_loss_func, head_loss
+    args = TrainArgs(hidden_size=96, depth=3, activation=act, ffn_hidden_size=80, device=DEV)
+    args.num_tasks = tasks
+    if features:
+        args.use_input_features, args.features_size = True, features
+    g = BatchMolGraph(synthetic.make_batch('polymer', b, 31 + b), device_bond_features=True)
+    rng = np.random.default_rng(b)
+    targets = [[None if rng.random() < 0.2 else float(rng.normal()) for _ in range(tasks)] for _ in range(b)]
+    tw = list(rng.uniform(0.5, 1.5, tasks))
+    dw = list(rng.uniform(0.5, 1.5, b))
+    feats = [rng.normal(size=features).astype(np.float32) for _ in range(b)] if features else None
+    torch.manual_seed(0)
+    m = MoleculeModel(args)
+    initialize_weights(m)
+    m = m.to(DEV).train()
+    lf = get_loss_func('regression')
+    head = _fusable_head(m, lf, 'regression')
+    assert head is not None
+    res = []
+    for fused in (True, False):
+        m.zero_grad(set_to_none=True)
+        if fused:
+            loss = head_loss(m.encoder([g], feats), head, targets, tw, dw)
+        else:
+            loss = batch_loss(m([g], feats), targets, lf, 'regression', tw, dw)
+        (loss * 0.75).backward()
+        res.append((float(loss), {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}))
+    (l0, g0), (l1, g1) = res
+    assert abs(l0 - l1) <= 1e-6 * max(1.0, abs(l1))
+    assert g0.keys() == g1.keys()
+    for n in g1:
+        assert golden_io.normwise(g0[n].cpu().numpy(), g1[n].cpu().numpy()) <= TOL, n
+
+
 def test_inference_plan_cache_follows_config_and_weights():
     """The cached inference call (MPNEncoder._infer: per-graph plan + packed weights) picks up a changed
     aggregation and in-place weight updates, and agrees with the
