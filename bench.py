@@ -201,10 +201,19 @@ def training_workload(device, batch=128, steps=100, warmup=10):
     torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
     E = sum(batches[i % 4][0][0].n_bonds - 1 for i in range(steps))
+    # training roofline: the encoder's algorithmic forward FLOPs (SURVEY §8(d) formula, mpn.py:92-171) x 3
+    # (each GEMM's backward = two GEMMs of the same size: data and weight gradients), per step
+    import types
+    fwd = forward_roofline([batches[i][0][0] for i in range(4)], types.SimpleNamespace(hidden=300, depth=3), dt / steps)
+    flops = 3.0 * fwd['algorithmic_flops']
     return {'workload': f'training step: MoleculeModel on synthetic polymer batches of {batch}, depth 3, hidden 300, '
                         'MSE + Adam (forward, backward, optimizer step)',
             'value': E / dt, 'unit': 'edges/s', 'ms_per_step': dt / steps * 1e3, 'graphs_per_s': batch * steps / dt,
-            'steps': steps}
+            'steps': steps,
+            'roofline': {'flops_per_step': flops, 'achieved_tflops': flops / (dt / steps) / 1e12,
+                         'mfma_fp32_frac': flops / (dt / steps) / (FP32_MFMA_PEAK_TFLOPS * 1e12),
+                         'note': 'encoder forward FLOPs x 3 per step over the measured step time, against the '
+                                 'fp32 dense MFMA peak (the FFN head, loss and optimizer are not counted)'}}
 
 
 def streamed_workload(device, args, rank, world, graphs_per_rank, batch=64, producers=4, barrier=None):
