@@ -51,14 +51,18 @@ def _f32(t):
     return t
 
 
-def _forward_call(gstruct, cfg, pstruct, hidden_out, device):
-    """One wdmpnn_forward on the current stream into caller-owned (caching-allocator) buffers."""
+def _forward_call(gstruct, cfg, pstruct, hidden_out, device, pre_launch=None):
+    """One wdmpnn_forward on the current stream into caller-owned (caching-allocator) buffers.
+    ``pre_launch`` (the weight pack of a training forward) is enqueued after the host-side preparation,
+    right before the forward, so that the GPU does not idle between the two."""
     L = _native.lib()
     nbytes = ctypes.c_size_t()
     _native.check(L.wdmpnn_workspace_bytes(ctypes.byref(gstruct), ctypes.byref(pstruct), ctypes.byref(cfg),
                                            ctypes.byref(nbytes)), 'MPNEncoder workspace')
     ws = torch.empty(max(nbytes.value, 256), dtype=torch.uint8, device=device)
     out = torch.empty((gstruct.n_mols, hidden_out), dtype=torch.float32, device=device)
+    if pre_launch is not None:
+        pre_launch()
     _native.check(L.wdmpnn_forward(ctypes.byref(gstruct), ctypes.byref(pstruct), ctypes.byref(cfg), ws.data_ptr(),
                                    nbytes.value, out.data_ptr(), _native.current_stream(device)),
                   'MPNEncoder forward')
@@ -72,7 +76,7 @@ class _EncoderFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, enc, gstruct, cfg, pstruct, keep, hidden_out, device, W_i, b_i, W_h, b_h, W_o, b_o, W_d, b_d,
                 prelu):
-        out, ws, ws_bytes = _forward_call(gstruct, cfg, pstruct, hidden_out, device)
+        out, ws, ws_bytes = _forward_call(gstruct, cfg, pstruct, hidden_out, device, pre_launch=keep[3])
         if cfg.save_for_backward:
             ctx.save_for_backward(W_i, b_i, W_h, b_h, W_o, b_o, W_d, b_d, prelu)
             ctx.ws, ctx.ws_bytes, ctx.gstruct, ctx.cfg, ctx.p, ctx.keep = ws, ws_bytes, gstruct, cfg, pstruct, keep
@@ -299,20 +303,22 @@ class MPNEncoder(nn.Module):
         params = [_f32(t) for t in params]
         save = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in params)
         cfg = self._config(save)
-        pstruct, packed = self._packed_params(gs, cfg, params, device, cache=not save)
         if not save:  # inference: the same C-ABI call without the autograd.Function wrapper
+            pstruct, packed = self._packed_params(gs, cfg, params, device, cache=True)
             return _forward_call(gs, cfg, pstruct, hidden_out, device)[0]
+        # training: the weights are repacked every call; the pack is enqueued right before the forward
+        pstruct, packed, pack = self._packed_params(gs, cfg, params, device, cache=False, defer=True)
         # the autograd context keeps the device graph alive with the packed weights and descriptors: the
         # backward reads its buffers through raw pointers (gs), and the caller may drop the BatchMolGraph
         # before calling backward (``model([BatchMolGraph(mols)]).sum().backward()``)
-        return _EncoderFunction.apply(self, gs, cfg, pstruct, (packed, desc, dg), hidden_out, device, *params)
+        return _EncoderFunction.apply(self, gs, cfg, pstruct, (packed, desc, dg, pack), hidden_out, device, *params)
 
     def invalidate_packed_params(self) -> None:
         """Drop the cached padded weights.  Needed only after writing the parameters in a way that
         bypasses both their version counters and ``torch.optim`` (e.g. ``p.data.copy_(...)``)."""
         self._pack_cache = None
 
-    def _packed_params(self, gs, cfg, params, device, cache=True, stream=None):
+    def _packed_params(self, gs, cfg, params, device, cache=True, stream=None, defer=False):
         """WdParams + the padded weight copies (wdmpnn_pack_params).  Inference caches them per
         (parameter pointer, version counter, optimizer-step generation): fused optimizers update the
         weights without bumping version counters, so every ``Optimizer.step`` also bumps
@@ -339,9 +345,16 @@ class MPNEncoder(nn.Module):
         _native.check(L.wdmpnn_packed_params_bytes(ctypes.byref(gs), ctypes.byref(p), ctypes.byref(cfg),
                                                    ctypes.byref(nbytes)), 'pack size')
         buf = torch.empty(nbytes.value, dtype=torch.uint8, device=device)
-        _native.check(L.wdmpnn_pack_params(ctypes.byref(gs), ctypes.byref(p), ctypes.byref(cfg), buf.data_ptr(),
-                                           nbytes.value, stream.cuda_stream if stream is not None
-                                           else _native.current_stream(device)), 'pack params')
+
+        def launch():
+            _native.check(L.wdmpnn_pack_params(ctypes.byref(gs), ctypes.byref(p), ctypes.byref(cfg), buf.data_ptr(),
+                                               nbytes.value, stream.cuda_stream if stream is not None
+                                               else _native.current_stream(device)), 'pack params')
+        if defer:  # (training: the caller enqueues it on the current stream, before the forward)
+            p.packed, p.packed_bytes = buf.data_ptr(), buf.numel()
+            self._pack_cache = None
+            return p, buf, launch
+        launch()
         p.packed, p.packed_bytes = buf.data_ptr(), buf.numel()
         if cache:  # (a training forward uses its packed weights on this stream only: no event)
             if stream is None:
