@@ -502,21 +502,35 @@ __device__ __forceinline__ void small_gemm_tile(const SmallGemm &G, int tile, fl
     const int tn = (G.N + 31) / 32, i0 = (tile / tn) * 32, j0 = (tile % tn) * 32;
     const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
     float c[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
-    for (int k0 = 0; k0 < G.K; k0 += 32) {
-        // stage A[i0 .. +32][k0 .. +32] and B[k0 .. +32][j0 .. +32] (4 elements per thread each), consecutive
-        // lanes along each operand's contiguous index (coalesced loads; the padded rows keep the
-        // transposed LDS writes conflict-free)
+    // staging: consecutive lanes along each operand's contiguous index (coalesced loads; the padded rows
+    // keep the transposed LDS writes conflict-free); the next chunk is loaded into registers while this
+    // one is multiplied (these GEMMs are load-latency-bound: 128 x 300 x 300)
+    float ra[4], rb[4];
+    auto load = [&](int k0) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int e = tid + 256 * q, hi = e >> 5, lo = e & 31;
-            const int ra = G.sak == 1 ? hi : lo, ca = G.sak == 1 ? lo : hi;  // (i, k) of A
-            const int ia = i0 + ra, ka = k0 + ca;
-            as[ra][ca] = ia < G.M && ka < G.K ? G.A[ia * G.sai + ka * G.sak] : 0.f;
-            const int rb = G.sbj == 1 ? hi : lo, cb = G.sbj == 1 ? lo : hi;  // (k, j) of B
-            const int kb = k0 + rb, jb = j0 + cb;
-            bs[rb][cb] = kb < G.K && jb < G.N ? G.B[kb * G.sbk + jb * G.sbj] : 0.f;
+            const int ar = G.sak == 1 ? hi : lo, ac = G.sak == 1 ? lo : hi;  // (i, k) of A
+            const int ia = i0 + ar, ka = k0 + ac;
+            ra[q] = ia < G.M && ka < G.K ? G.A[ia * G.sai + ka * G.sak] : 0.f;
+            const int br = G.sbj == 1 ? hi : lo, bc = G.sbj == 1 ? lo : hi;  // (k, j) of B
+            const int kb = k0 + br, jb = j0 + bc;
+            rb[q] = kb < G.K && jb < G.N ? G.B[kb * G.sbk + jb * G.sbj] : 0.f;
         }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = tid + 256 * q, hi = e >> 5, lo = e & 31;
+            as[G.sak == 1 ? hi : lo][G.sak == 1 ? lo : hi] = ra[q];
+            bs[G.sbj == 1 ? hi : lo][G.sbj == 1 ? lo : hi] = rb[q];
+        }
+    };
+    load(0);
+    for (int k0 = 0; k0 < G.K; k0 += 32) {
+        store();
         __syncthreads();
+        if (k0 + 32 < G.K) load(k0 + 32);
 #pragma unroll 8
         for (int k = 0; k < 32; ++k) {
             const float a0 = as[2 * ty][k], a1 = as[2 * ty + 1][k], b0 = bs[k][2 * tx], b1 = bs[k][2 * tx + 1];
@@ -532,6 +546,23 @@ __device__ __forceinline__ void small_gemm_tile(const SmallGemm &G, int tile, fl
             const int i = i0 + 2 * ty + a, j = j0 + 2 * tx + b;
             if (i < G.M && j < G.N) G.C[i * G.ldc + j] = c[a][b] + (G.bias ? G.bias[j] : 0.f);
         }
+}
+// sum_{r < B} x[r * ld] (+ fma with y[r * ldy] when y): rows in order, eight loads in flight
+__device__ __forceinline__ float row_sum(const float *x, long long ld, const float *y, long long ldy, int B) {
+    float s = 0.f;
+    int r = 0;
+    for (; r + 8 <= B; r += 8) {
+        float v[8], w[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            v[q] = x[(r + q) * ld];
+            w[q] = y ? y[(r + q) * ldy] : 1.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s = y ? fmaf(v[q], w[q], s) : s + v[q];
+    }
+    for (; r < B; ++r) s = y ? fmaf(x[r * ld], y[r * ldy], s) : s + x[r * ld];
+    return s;
 }
 __device__ __forceinline__ int small_gemm_tiles(const SmallGemm &G) { return ((G.M + 31) / 32) * ((G.N + 31) / 32); }
 
@@ -589,23 +620,17 @@ __global__ __launch_bounds__(256) void head_grads_kernel(WdHead P) {
     const int Hf = P.Hf, T = P.T, B = P.B;
     const long long q = (long long)(b - n1 - n2) * 256 + threadIdx.x;
     if (q < Hf) {
-        float s = 0.f;
-        for (int r = 0; r < B; ++r) s += P.dh[(size_t)r * Hf + q];
+        const float s = row_sum(P.dh + q, Hf, nullptr, 0, B);
         if (P.db1) P.db1[q] = s;
     } else if (q < Hf + (long long)T * Hf) {
         const int u = (int)(q - Hf), t = u / Hf, j = u % Hf;
-        float s = 0.f;
-        for (int r = 0; r < B; ++r) s = fmaf(P.dout[(size_t)r * T + t], P.a[(size_t)r * Hf + j], s);
-        P.dW2[u] = s;
+        P.dW2[u] = row_sum(P.dout + t, T, P.a + j, Hf, B);
     } else if (q < Hf + (long long)T * Hf + T) {
         const int t = (int)(q - Hf - (long long)T * Hf);
-        float s = 0.f;
-        for (int r = 0; r < B; ++r) s += P.dout[(size_t)r * T + t];
+        const float s = row_sum(P.dout + t, T, nullptr, 0, B);
         if (P.db2) P.db2[t] = s;
     } else if (q == Hf + (long long)T * Hf + T) {
-        float s = 0.f;
-        for (int r = 0; r < B; ++r) s += P.lossrow[r];
-        P.loss[0] = s * P.inv_n;
+        P.loss[0] = row_sum(P.lossrow, 1, nullptr, 0, B) * P.inv_n;
     }
 }
 
