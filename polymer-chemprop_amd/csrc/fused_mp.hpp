@@ -359,35 +359,70 @@ __device__ __forceinline__ void stage_rows2(float *dst0, const float *src0, int 
 
 template <int BN>
 __global__ __launch_bounds__(512) void embed_kernel(EmbedP P) {
-    constexpr int NT = 512, LDC = BN + 4, C4 = BN / 4, U8 = BN / 8, MAXK = 160;
-    __shared__ __attribute__((aligned(16))) float wt[MAXK * BN];        // W_i^T rows of the tile
-    __shared__ __attribute__((aligned(16))) float wo[MAXK * BN];        // W_o[:, :Fa]^T rows of the tile
+    constexpr int NT = 512, LDC = BN + 4, C4 = BN / 4, U8 = BN / 8, MAXK = 160, PER = (MAXK * C4 + NT - 1) / NT;
+    // one weight tile in LDS at a time -- W_o[:, :Fa]^T for Eo, then W_i^T for Ea and the bonds -- so
+    // that the kernel takes < 80 KB of LDS and a layer kernel of a batch on another stream co-resides
+    // with it on a CU (both tiles at once took 133 KB: one workgroup per CU, nothing beside it)
+    __shared__ __attribute__((aligned(16))) float wt[MAXK * BN];        // the staged weight tile
     __shared__ __attribute__((aligned(16))) float ea[BLK_ATOMS * LDC];  // Ea of the block's atoms
     __shared__ __attribute__((aligned(16))) float bb[BN];
     __shared__ WdAtomCode code[BLK_ATOMS];
+    static_assert(sizeof(float) * (MAXK * BN + BLK_ATOMS * LDC + BN) + sizeof(WdAtomCode) * BLK_ATOMS <= 80 * 1024,
+                  "LDS of two co-resident workgroups");
     const int tile = xcd_tile(blockIdx.x, gridDim.x);
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
     const int tid = threadIdx.x;
     if (tid < B.an) code[tid] = P.codes[B.as + tid];
     if (tid >= NT - C4) st4(bb + 4 * (tid - (NT - C4)), P.bias ? ld4(P.bias + n0 + 4 * (tid - (NT - C4))) : f4zero());
-    stage_rows2<BN, NT, MAXK>(wt, P.wt, P.Fb, wo, P.woat, P.Fa, P.Hk, n0);
+    // both tiles' loads go out together; the W_i^T rows wait in registers while Eo is summed
+    float4 ro[PER], ri[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int v = tid + NT * q, k = v / C4, c = 4 * (v % C4);
+        ro[q] = k < P.Fa ? ld4(P.woat + (size_t)k * P.Hk + n0 + c) : f4zero();
+        ri[q] = k < P.Fb ? ld4(P.wt + (size_t)k * P.Hk + n0 + c) : f4zero();
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int v = tid + NT * q, k = v / C4, c = 4 * (v % C4);
+        if (k < P.Fa) st4(wt + k * BN + c, ro[q]);
+    }
     __syncthreads();
+    // Eo[a] = sum_{c in code(a)} W_o[:, c] + last(a) W_o[:, Fa-1] (the f_atoms half of W_o)
     for (int v = tid; v < B.an * C4; v += NT) {
         const int la = v / C4, c = 4 * (v % C4);
         const WdAtomCode &cd = code[la];
-        float4 s = f4zero(), so = f4zero();
+        float4 so = f4zero();
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             if (cd.col[q] == 0xFF) continue;
-            const float4 w = ld4(wt + cd.col[q] * BN + c), u = ld4(wo + cd.col[q] * BN + c);
-            s.x += w.x; s.y += w.y; s.z += w.z; s.w += w.w;
+            const float4 u = ld4(wt + cd.col[q] * BN + c);
             so.x += u.x; so.y += u.y; so.z += u.z; so.w += u.w;
         }
-        fma4(s, cd.last, ld4(wt + (P.Fa - 1) * BN + c));
-        fma4(so, cd.last, ld4(wo + (P.Fa - 1) * BN + c));
-        st4(ea + la * LDC + c, s);
+        fma4(so, cd.last, ld4(wt + (P.Fa - 1) * BN + c));
         if (WD_EXP != 1) st4(P.eo + ((size_t)blk * BLK_ATOMS + la) * P.Hk + n0 + c, so);
+    }
+    __syncthreads();  // every read of the W_o tile done
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int v = tid + NT * q, k = v / C4, c = 4 * (v % C4);
+        if (k < P.Fb) st4(wt + k * BN + c, ri[q]);
+    }
+    __syncthreads();
+    // Ea[a] = sum_{c in code(a)} W_i[:, c] + last(a) W_i[:, Fa-1]
+    for (int v = tid; v < B.an * C4; v += NT) {
+        const int la = v / C4, c = 4 * (v % C4);
+        const WdAtomCode &cd = code[la];
+        float4 s = f4zero();
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (cd.col[q] == 0xFF) continue;
+            const float4 w = ld4(wt + cd.col[q] * BN + c);
+            s.x += w.x; s.y += w.y; s.z += w.z; s.w += w.w;
+        }
+        fma4(s, cd.last, ld4(wt + (P.Fa - 1) * BN + c));
+        st4(ea + la * LDC + c, s);
     }
     __syncthreads();
     const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
