@@ -228,13 +228,15 @@ def streamed_workload(device, args, rank, world, graphs_per_rank, batch=64, prod
     n = -(-graphs_per_rank // batch)
     warm = 32
     with torch.no_grad():
-        for g in StreamedBatches('polymer', batch, warm, seed=99, device=device, rank=rank, producers=producers):
+        for g in StreamedBatches('polymer', batch, warm, seed=99, device=device, rank=rank, producers=producers,
+                                 lean=True):
             enc(g)
         barrier()
         t0 = time.perf_counter()
         edges = 0
         h2d = 0
-        for g in StreamedBatches('polymer', batch, n, seed=2024, device=device, rank=rank, producers=producers):
+        for g in StreamedBatches('polymer', batch, n, seed=2024, device=device, rank=rank, producers=producers,
+                                 lean=True):
             enc(g)
             edges += g.n_bonds - 1
             h2d += g.device_graph(device, False, get_bond_fdim()).h2d_bytes
@@ -324,6 +326,7 @@ def main():
     ap.add_argument('--variant', type=int, default=0, help='WdConfig.gemm_variant (0 = default path; 9 = f32 MFMA)')
     ap.add_argument('--stream-graphs', type=int, default=10_000_000 // 8,
                     help='configs[4]: polymer graphs streamed per rank (default 10 M / 8 GPUs); 0 = skip')
+    ap.add_argument('--producers', type=int, default=4, help='native generator threads of the streamed workloads')
     ap.add_argument('--stream-train-graphs', type=int, default=131_072,
                     help='configs[4] as DP training: streamed graphs per rank (batches of 128); 0 = skip')
     a = ap.parse_args()
@@ -419,9 +422,11 @@ def main():
     st_dt = st_edges = st_graphs = st_h2d = tr_dt = tr_edges = tr_steps = 0
     if a.stream_graphs > 0:
         st_dt, st_edges, st_graphs, st_h2d = streamed_workload(device, args, rank, world, a.stream_graphs,
+                                                               producers=a.producers,
                                                                barrier=barrier)
     if a.stream_train_graphs > 0:
-        tr_dt, tr_edges, tr_steps = streamed_training(device, rank, world, a.stream_train_graphs, barrier=barrier)
+        tr_dt, tr_edges, tr_steps = streamed_training(device, rank, world, a.stream_train_graphs,
+                                                      producers=a.producers, barrier=barrier)
 
     t = torch.tensor([elapsed, elapsed_prof, single or 0.0, st_dt, tr_dt], dtype=torch.float64, device=device)
     e = torch.tensor([my_edges, st_edges, st_graphs, st_h2d, tr_edges], dtype=torch.float64, device=device)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define WDMPNN_ABI_VERSION 5
+#define WDMPNN_ABI_VERSION 6
 #define WDMPNN_ELL_WIDTH 8
 
 enum WdActivation {     /* nn_utils.py:70-99 get_activation_function */
@@ -291,6 +291,11 @@ int wdmpnn_graph_bytes(const WdCompact *c, size_t *bytes);
  * on `stream`; *g receives the struct (bond-message mode, blocks set, no descriptors) whose pointers
  * point into `buffer`.  All arrays of c are device pointers. */
 int wdmpnn_build_graph(const WdCompact *c, void *buffer, size_t bytes, WdGraph *g, void *stream);
+/* The same with flags.  WDMPNN_GRAPH_LEAN: skip the dense feature rows, their plane tiles and the
+ * transposed gathers (about 2/3 of the bytes written for a polymer batch); the graph then serves only
+ * the fused inference forward (categorical codes) -- anything else returns WD_ERR_UNSUPPORTED. */
+#define WDMPNN_GRAPH_LEAN 1
+int wdmpnn_build_graph_ex(const WdCompact *c, void *buffer, size_t bytes, WdGraph *g, int32_t flags, void *stream);
 
 /* index_select_ND (nn_utils.py:50-67): out[i, :] = src[index[i], :], row_len floats per row.
  * Indices are int64 like the reference's LongTensor; out-of-range indices are an error checked by

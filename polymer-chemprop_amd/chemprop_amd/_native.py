@@ -21,7 +21,8 @@ LIB_PATH = os.environ.get('WDMPNN_LIB', os.path.join(HERE, 'libwdmpnn.so'))
 ACTIVATIONS = {'ReLU': 0, 'LeakyReLU': 1, 'PReLU': 2, 'tanh': 3, 'SELU': 4, 'ELU': 5}
 ACT_IDENTITY = 6
 AGGREGATIONS = {'mean': 0, 'sum': 1, 'norm': 2}
-ABI_VERSION = 5
+ABI_VERSION = 6
+GRAPH_LEAN = 1  # WDMPNN_GRAPH_LEAN
 
 EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace_bytes',
                     'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
@@ -29,7 +30,7 @@ EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace
                     'wdmpnn_event_pool_elapsed_ms', 'wdmpnn_packed_params_bytes', 'wdmpnn_pack_params',
                     'wdmpnn_plane_bytes', 'wdmpnn_split_planes', 'wdmpnn_split_planes_rows',
                     'wdmpnn_build_bond_features', 'wdmpnn_index_select_rows_backward',
-                    'wdmpnn_saved_layout', 'wdmpnn_graph_bytes', 'wdmpnn_build_graph', 'wdmpnn_adam_step', 'wdmpnn_head_mse', 'wdmpnn_scale')
+                    'wdmpnn_saved_layout', 'wdmpnn_graph_bytes', 'wdmpnn_build_graph', 'wdmpnn_adam_step', 'wdmpnn_head_mse', 'wdmpnn_scale', 'wdmpnn_build_graph_ex')
 
 
 class WdCsr(Structure):
@@ -139,6 +140,7 @@ def lib() -> ctypes.CDLL:
                                            c_void_p]
     L.wdmpnn_build_bond_features.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_int32, c_int32,
                                              c_int32, c_void_p, c_int32, c_void_p]
+    L.wdmpnn_build_graph_ex.argtypes = [POINTER(WdCompact), c_void_p, c_size_t, POINTER(WdGraph), c_int32, c_void_p]
     L.wdmpnn_head_mse.argtypes = [POINTER(WdHead), c_void_p]
     L.wdmpnn_scale.argtypes = [POINTER(c_void_p), POINTER(c_int64), c_int32, c_void_p, c_void_p]
     L.wdmpnn_adam_step.argtypes = [POINTER(WdAdamTensor), c_int32, POINTER(WdAdamHyper), c_void_p]
@@ -148,7 +150,7 @@ def lib() -> ctypes.CDLL:
     for fn in ('wdmpnn_packed_params_bytes', 'wdmpnn_pack_params', 'wdmpnn_event_pool_create', 'wdmpnn_event_pool_destroy', 'wdmpnn_event_pool_elapsed_ms',
                'wdmpnn_workspace_bytes', 'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
                'wdmpnn_index_select_rows', 'wdmpnn_plane_bytes', 'wdmpnn_split_planes', 'wdmpnn_split_planes_rows',
-               'wdmpnn_build_bond_features', 'wdmpnn_adam_step', 'wdmpnn_head_mse', 'wdmpnn_scale'):
+               'wdmpnn_build_bond_features', 'wdmpnn_adam_step', 'wdmpnn_head_mse', 'wdmpnn_scale', 'wdmpnn_build_graph_ex'):
         getattr(L, fn).restype = c_int
     v = L.wdmpnn_abi_version()
     if v != ABI_VERSION:

@@ -621,10 +621,13 @@ class BatchMolGraph:
         return dg
 
 
-def upload_compact(device, staged: torch.Tensor, info, atom_fdim: int, bond_fdim: int) -> DeviceGraph:
+def upload_compact(device, staged: torch.Tensor, info, atom_fdim: int, bond_fdim: int,
+                   lean: bool = False) -> DeviceGraph:
     """H2D of a staged compact image (pinned host tensor from ``compact_stage`` / ``generate_stage``)
     on the current stream, then ``wdmpnn_build_graph`` into one device buffer: the DeviceGraph of the
-    batch.  ``info`` = (copied, counts, offsets, total) as the native stage functions return it."""
+    batch.  ``info`` = (copied, counts, offsets, total) as the native stage functions return it.
+    ``lean``: an inference-only graph (WDMPNN_GRAPH_LEAN: no dense feature rows, planes or transposed
+    gathers); a training forward or an unblocked path on it raises NotImplementedError."""
     _, (n_mols, n_atoms, n_bonds, n_blocks, nnz_msg, nnz_agg), off, total = info
     buf = staged[:total].to(device, non_blocking=True)
     base = buf.data_ptr()
@@ -637,14 +640,16 @@ def upload_compact(device, staged: torch.Tensor, info, atom_fdim: int, bond_fdim
     _native.check(L.wdmpnn_graph_bytes(ctypes.byref(c), ctypes.byref(nbytes)), 'graph bytes')
     gbuf = torch.empty(nbytes.value, dtype=torch.uint8, device=device)
     s = _native.WdGraph()
-    _native.check(L.wdmpnn_build_graph(ctypes.byref(c), gbuf.data_ptr(), nbytes.value, ctypes.byref(s),
-                                       _native.current_stream(device)), 'device graph build')
+    _native.check(L.wdmpnn_build_graph_ex(ctypes.byref(c), gbuf.data_ptr(), nbytes.value, ctypes.byref(s),
+                                          _native.GRAPH_LEAN if lean else 0, _native.current_stream(device)),
+                  'device graph build')
     dg = DeviceGraph(gbuf, {'compact': buf}, s)
     dg.finish()
     dg.n_edges = n_bonds - 1
     dg.h2d_bytes = total
     dg.nnz_msg = nnz_msg
     dg.built_on_device = True
+    dg.lean = bool(lean)
     return dg
 
 

@@ -43,7 +43,7 @@ class StreamedBatches:
 
     def __init__(self, kind: str, batch_size: int, n_batches: int, seed: int, device, rank: int = 0,
                  producers: int = 4, slots: Optional[int] = None, keep_host: bool = False,
-                 target_blocks: int = BLK_TARGET):
+                 target_blocks: int = BLK_TARGET, lean: bool = False):
         if kind not in KINDS:
             raise ValueError(f'unknown kind {kind!r}')
         self.kind, self.B, self.n, self.device = kind, int(batch_size), int(n_batches), torch.device(device)
@@ -51,6 +51,7 @@ class StreamedBatches:
         self.P = max(1, int(producers))
         self.R = max(self.P + 2, int(slots or 0))
         self.keep = keep_host
+        self.lean = bool(lean)  # inference-only device graphs (upload_compact lean)
         self.target = target_blocks
         self.cap = stage_capacity(kind, self.B)
         self.host = [torch.empty(self.cap, dtype=torch.uint8, pin_memory=True) for _ in range(self.R)]
@@ -102,7 +103,7 @@ class StreamedBatches:
                 self.full[s].clear()
                 info, arrays = self.info[s]
                 with torch.cuda.stream(self.feed):
-                    dg = upload_compact(self.device, self.host[s], info, 133, 147)
+                    dg = upload_compact(self.device, self.host[s], info, 133, 147, lean=self.lean)
                     ev = torch.cuda.Event()
                     ev.record(self.feed)
                 self.copy_done[s] = ev

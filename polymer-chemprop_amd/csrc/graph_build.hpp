@@ -38,6 +38,7 @@ struct GraphBuildP {
     float *msg_ell_coef, *agg_ell_coef;
     int32_t *msg_ptr, *msg_idx, *agg_ptr, *agg_idx, *msgt_ptr, *msgt_idx, *aggt_ptr, *aggt_idx;
     float *msg_coef, *agg_coef, *msgt_coef, *aggt_coef;
+    int lean;  // 1: no dense feature rows / planes and no transposed gathers (inference-only graph)
 };
 
 // value of f_atoms column c for an atom code (c < Fa)
@@ -65,11 +66,11 @@ __global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
         const int V1 = C.n_atoms, E1 = C.n_bonds;
         const int na_pad = 1 + (P.Vap - V1), nb_pad = 1 + (P.Rbp - E1);
         const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int u = tid; u < na_pad * UA; u += 256) {
+        for (int u = tid; u < (P.lean ? 0 : na_pad * UA); u += 256) {
             const int i = u / UA, r = i == 0 ? 0 : V1 + i - 1, c0 = (u % UA) * 8;
             put_row8(P.f_atoms + (size_t)r * P.lda, P.fa_x6, P.lda, r, c0, z);
         }
-        for (int u = tid; u < nb_pad * UB; u += 256) {
+        for (int u = tid; u < (P.lean ? 0 : nb_pad * UB); u += 256) {
             const int i = u / UB, r = i == 0 ? 0 : E1 + i - 1, c0 = (u % UB) * 8;
             put_row8(P.f_bonds + (size_t)r * P.ldb, P.fb_x6, P.ldb, r, c0, z);
         }
@@ -243,24 +244,26 @@ __global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
             P.msg_ell_idx[(size_t)GB_ELLW * b + q] = eidx[q];
             P.msg_ell_coef[(size_t)GB_ELLW * b + q] = ecoef[q];
         }
-        // msg_gather_t row b: the rows lb in out(dst(b)), increasing lb
-        o = om + s_pt[tid];
-        const int d = s_dst[tid];
-        for (int e = s_start[d]; e < s_start[d + 1]; ++e) {
-            const int lb = s_out[e];
-            const float c = tid == (lb ^ 1) ? s_w[tid] - 1.0f : s_w[tid];
-            if (c == 0.f) continue;
-            P.msgt_idx[o] = bs + lb;
-            P.msgt_coef[o] = c;
-            ++o;
+        if (!P.lean) {  // (a lean graph has no transposed gathers: the backward never runs on it)
+            // msg_gather_t row b: the rows lb in out(dst(b)), increasing lb
+            o = om + s_pt[tid];
+            const int d = s_dst[tid];
+            for (int e = s_start[d]; e < s_start[d + 1]; ++e) {
+                const int lb = s_out[e];
+                const float c = tid == (lb ^ 1) ? s_w[tid] - 1.0f : s_w[tid];
+                if (c == 0.f) continue;
+                P.msgt_idx[o] = bs + lb;
+                P.msgt_coef[o] = c;
+                ++o;
+            }
+            P.msgt_ptr[b + 1] = om + s_pt[tid + 1];
+            // atom_gather_t row b: (dst(b), w_b)
+            if (s_w[tid] != 0.f) {
+                P.aggt_idx[oa + s_pg[tid]] = as + s_dst[tid];
+                P.aggt_coef[oa + s_pg[tid]] = s_w[tid];
+            }
+            P.aggt_ptr[b + 1] = oa + s_pg[tid + 1];
         }
-        P.msgt_ptr[b + 1] = om + s_pt[tid + 1];
-        // atom_gather_t row b: (dst(b), w_b)
-        if (s_w[tid] != 0.f) {
-            P.aggt_idx[oa + s_pg[tid]] = as + s_dst[tid];
-            P.aggt_coef[oa + s_pg[tid]] = s_w[tid];
-        }
-        P.aggt_ptr[b + 1] = oa + s_pg[tid + 1];
     }
     if (tid < an) {  // atom_gather row a + its ELL-8 row
         const int a = as + tid;
@@ -286,6 +289,7 @@ __global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
             P.agg_ell_coef[(size_t)GB_ELLW * a + q] = ecoef[q];
         }
     }
+    if (P.lean) return;
     // feature rows (8 columns per thread-step): atoms natural + blocked (zero rows past an), bonds natural
     for (int u = tid; u < GB_ATOMS * UA; u += 256) {
         const int la = u / UA, c0 = (u % UA) * 8;

@@ -111,13 +111,20 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     D.x6 = !D.f32 && !D.atom;
     // molecule-blocked fused forward, also for training (the fused kernels then save Z_t, A and Zo in
     // natural rows for the backward)
+    // (an embed-capable graph -- categorical codes -- needs no feature planes)
+    const bool codes = g->atom_codes && g->bond_src_blk && g->bond_tail && D.Fb <= WO_MAXK && D.Fa <= WO_MAXK;
     D.blocked = D.x6 && !D.desc && D.T >= 2 && g->n_blocks > 0 && g->blocks && g->bond_blk_row &&
-                g->f_atoms_blk_x6 && g->f_bonds_x6 && g->msg_ell_idx && g->msg_ell_coef && g->atom_ell_idx &&
-                g->atom_ell_coef;
+                (codes || (g->f_atoms_blk_x6 && g->f_bonds_x6)) && g->msg_ell_idx && g->msg_ell_coef &&
+                g->atom_ell_idx && g->atom_ell_coef;
     D.nblk = D.blocked ? g->n_blocks : 0;
     if (D.atom && D.undirected)
         return fail(WD_ERR_UNSUPPORTED, "undirected with atom_messages (the reference indexes atom messages "
                                         "with b2revb, mpn.py:101-102)");
+    // (a lean graph has neither table; two distinct arrays of a real graph cannot both sit at address 0 --
+    // host-only tests pass buffer offsets as pointers)
+    if (!g->f_atoms && !g->f_bonds && !(D.blocked && codes && !D.save))
+        return fail(WD_ERR_UNSUPPORTED, "graph built without feature rows (WDMPNN_GRAPH_LEAN): only the fused "
+                                        "inference forward runs on it");
     if (D.desc && (!p->W_d || !p->b_d)) return fail(WD_ERR_ARG, "atom descriptors need W_d and b_d");
     if (!p->W_i || !p->W_h || !p->W_o || !p->b_o || !p->zero_vec) return fail(WD_ERR_ARG, "missing weights");
     if (g->ld_atoms < D.Fak || g->ld_atoms % 4 || g->ld_bonds < D.Fbk || g->ld_bonds % 4 || g->bond_col0 != 0)
@@ -735,7 +742,10 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
         }
         if (D.B > 0) {
             WoReadoutP R{};
-            R.fa = (const uint8_t *)g->f_atoms_blk_x6; R.kpa = g->ld_atoms; R.kcw = D.Fak / 32;
+            // (codes: the f_atoms segment is not read; a lean graph has no planes -- the A planes stand in as
+        // the segment's non-null base)
+        R.fa = g->f_atoms_blk_x6 ? (const uint8_t *)g->f_atoms_blk_x6 : (const uint8_t *)(ws + L.Ab);
+        R.kpa = g->ld_atoms; R.kcw = D.Fak / 32;
             R.kca = codes ? 0 : R.kcw;
             R.eo = codes ? F(L.Eo) : nullptr; R.Hk = Hk;
             R.ag = (const uint8_t *)(ws + L.Ab); R.kp = Hk;
@@ -1140,6 +1150,12 @@ int wdmpnn_graph_bytes(const WdCompact *c, size_t *bytes) {
 }
 
 int wdmpnn_build_graph(const WdCompact *c, void *buffer, size_t bytes, WdGraph *g, void *stream) {
+    return wdmpnn_build_graph_ex(c, buffer, bytes, g, 0, stream);
+}
+
+int wdmpnn_build_graph_ex(const WdCompact *c, void *buffer, size_t bytes, WdGraph *g, int32_t flags, void *stream) {
+    if (flags & ~WDMPNN_GRAPH_LEAN) return fail(WD_ERR_ARG, "unknown graph build flags 0x%x", flags);
+    const bool lean = flags & WDMPNN_GRAPH_LEAN;
     GraphLayout L;
     WD_TRY(graph_layout(c, L));
     if (!buffer || !g) return fail(WD_ERR_ARG, "null buffer / graph");
@@ -1167,6 +1183,7 @@ int wdmpnn_build_graph(const WdCompact *c, void *buffer, size_t bytes, WdGraph *
     P.agg_ptr = I(L.csr[1][0]); P.agg_idx = I(L.csr[1][1]); P.agg_coef = F(L.csr[1][2]);
     P.msgt_ptr = I(L.csr[2][0]); P.msgt_idx = I(L.csr[2][1]); P.msgt_coef = F(L.csr[2][2]);
     P.aggt_ptr = I(L.csr[3][0]); P.aggt_idx = I(L.csr[3][1]); P.aggt_coef = F(L.csr[3][2]);
+    P.lean = lean;
     hipLaunchKernelGGL(graph_build_kernel, dim3(c->n_blocks + 1), dim3(256), 0, (hipStream_t)stream, P);
     WD_CHECK_LAUNCH("graph_build");
     WdGraph G{};
@@ -1187,6 +1204,12 @@ int wdmpnn_build_graph(const WdCompact *c, void *buffer, size_t bytes, WdGraph *
     G.msg_ell_idx = P.msg_ell_idx; G.msg_ell_coef = P.msg_ell_coef;
     G.atom_ell_idx = P.agg_ell_idx; G.atom_ell_coef = P.agg_ell_coef;
     G.atom_codes = c->atoms; G.bond_src_blk = P.bond_src_blk; G.bond_tail = P.bond_tail;
+    if (lean) {  // what was not built is not handed out: a path that needs it fails in get_dims
+        G.f_atoms = G.f_bonds = nullptr;
+        G.f_atoms_x6 = G.f_bonds_x6 = G.f_atoms_blk_x6 = nullptr;
+        G.msg_gather_t = WdCsr{nullptr, nullptr, nullptr};
+        G.atom_gather_t = WdCsr{nullptr, nullptr, nullptr};
+    }
     *g = G;
     return 0;
 }

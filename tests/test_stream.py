@@ -45,6 +45,25 @@ def test_stream_60_batches_vs_oracle_and_replay():
     assert not torch.equal(outs[0], outs[1])
 
 
+def test_lean_graphs_give_the_same_forward_and_refuse_training():
+    """Inference-only device graphs (upload_compact lean: no feature rows, planes or transposed gathers)
+    give bitwise the full graphs' fused forward; a training forward or an unblocked path on one raises
+    instead of reading the missing arrays."""
+    enc = _encoder()
+    with torch.no_grad():
+        full = [enc(g) for g in StreamedBatches('polymer', 64, 6, seed=21, device=DEV)]
+        lean = [enc(g) for g in StreamedBatches('polymer', 64, 6, seed=21, device=DEV, lean=True)]
+    assert all(torch.equal(a, b) for a, b in zip(full, lean))
+    g = next(iter(StreamedBatches('polymer', 16, 1, seed=4, device=DEV, lean=True)))
+    assert g.device_graph(DEV, False, get_bond_fdim()).lean
+    with pytest.raises(NotImplementedError):
+        enc.train()(g)  # grad enabled: the training forward needs the feature rows for its backward
+    enc.eval()
+    enc._gemm_variant = 9  # the unblocked f32 path
+    with torch.no_grad(), pytest.raises(NotImplementedError):
+        enc(g)
+
+
 def test_streams_of_two_ranks_are_disjoint():
     a = next(iter(StreamedBatches('polymer', 8, 1, seed=5, device=DEV, rank=0, keep_host=True)))
     b = next(iter(StreamedBatches('polymer', 8, 1, seed=5, device=DEV, rank=1, keep_host=True)))
