@@ -316,6 +316,9 @@ def head_loss(emb: torch.Tensor, head, target_batch, target_weights=None, data_w
     table, n_t, n_mask = _loss_table(target_batch, target_weights, data_weights, emb.device)
     if n_t != l2.out_features:
         raise ValueError(f'{n_t} targets per row for {l2.out_features} outputs')
+    if table.shape[0] != emb.shape[0] or emb.dim() != 2 or emb.shape[1] != l1.in_features:
+        raise ValueError(f'{table.shape[0]} target rows for encodings of shape {tuple(emb.shape)} '
+                         f'(FFN input {l1.in_features})')
     inv_n = 1.0 / n_mask if n_mask else float('inf')
     return _HeadMSE.apply(emb, l1.weight, l1.bias, l2.weight, l2.bias, table, inv_n, act)
 
