@@ -119,13 +119,15 @@ struct MpLayerP {
     float *zsave, *asave;
 };
 
-// Wave layout of the fused kernels per column-tile width: BN = 64 -> 4 x 2 waves, BN = 80 -> 2 x 5.
-// 80-column tiles give 4 tiles for Hk = 320 and so exactly one workgroup per CU at the benchmark size
-// (64 blocks x 4 = 256): a grid of 1.25 workgroups per CU left a quarter of the CUs with twice the
-// bytes to stream.
+// Wave layout of the fused layer kernels per column-tile width: BN = 64 -> 4 x 2 waves, BN = 80 -> 8 x 1
+// (each wave 16 rows x all 80 columns).  80-column tiles give 4 tiles for Hk = 320 and so exactly one
+// workgroup per CU at the benchmark size (64 blocks x 4 = 256): a grid of 1.25 workgroups per CU left a
+// quarter of the CUs with twice the bytes to stream.  8 x 1 (512 threads, two waves per SIMD) against the
+// earlier 2 x 5 (640 threads: 3 + 3 + 2 + 2 waves on the four SIMDs): +1.8 % with two batches in flight,
+// equal with one (profiles/round2_wave_layout_ab.txt); 1 x 5 (320 threads) -11 %.
 template <int BN> struct MpWaves;
 template <> struct MpWaves<64> { static constexpr int WM = 4, WN = 2; };
-template <> struct MpWaves<80> { static constexpr int WM = 2, WN = 5; };
+template <> struct MpWaves<80> { static constexpr int WM = 8, WN = 1; };
 
 // mp_layer epilogue, shared by both layer kernels: residual rows and gather lists prefetched during the
 // GEMM, then (P tile in LDS) the in-block gather, bias, residual, activation, dropout and the plane
