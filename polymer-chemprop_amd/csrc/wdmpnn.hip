@@ -695,7 +695,10 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
             EmbedP E{};
             E.codes = g->atom_codes; E.src_blk = g->bond_src_blk; E.tail = g->bond_tail;
             E.wt = W(PL.WiT); E.woat = W(PL.WoaT); E.eo = F(L.Eo); E.bias = p->b_i ? W(PL.bi) : nullptr; E.blocks = g->blocks;
-            const bool bn40 = WD_EXP == 4 && Hk % 40 == 0;
+            // 40-column tiles when they divide Hk: twice the workgroups of the layer tiling (two per CU at the
+            // benchmark size, 37 KB of LDS each), so one's staging overlaps the other's sums (+0.8 % with two
+            // batches in flight, same-box ABAB, profiles/round2_wave_layout_ab.txt)
+            const bool bn40 = Hk % 40 == 0;
             E.Fa = D.Fa; E.Fb = D.Fb; E.Hk = Hk; E.n_tiles = Hk / (bn40 ? 40 : BNf);
             E.act = c->activation; E.slope = p->prelu;
             E.inp = F(L.Z[0]); E.mplanes = (uint8_t *)(ws + L.Mb[0]);
