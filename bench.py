@@ -374,6 +374,8 @@ def main():
         if world > 1:
             dist.barrier()
 
+    if rank == 0:  # progress on stderr (stdout carries only the JSON line): long quiet phases look hung
+        log(f'[bench] resident batches ready; timing {a.steps} steps on {a.streams} streams')
     with torch.no_grad():
         step(0)  # packs the weights on the default stream; the other streams wait on its event
         barrier()
@@ -421,10 +423,14 @@ def main():
     # same stream as data-parallel training with one gradient all-reduce per step
     st_dt = st_edges = st_graphs = st_h2d = tr_dt = tr_edges = tr_steps = 0
     if a.stream_graphs > 0:
+        if rank == 0:
+            log(f'[bench] streamed workload: {a.stream_graphs} graphs per rank')
         st_dt, st_edges, st_graphs, st_h2d = streamed_workload(device, args, rank, world, a.stream_graphs,
                                                                producers=a.producers,
                                                                barrier=barrier)
     if a.stream_train_graphs > 0:
+        if rank == 0:
+            log(f'[bench] streamed training: {a.stream_train_graphs} graphs per rank')
         tr_dt, tr_edges, tr_steps = streamed_training(device, rank, world, a.stream_train_graphs,
                                                       producers=a.producers, barrier=barrier)
 
@@ -510,12 +516,15 @@ def main():
                 'steps_per_rank': tr_steps, 'n_gpus': world, 'value': tr_edges / tr_dt, 'unit': 'edges/s',
                 'ms_per_step': tr_dt / tr_steps * 1e3, 'graphs_per_s': tr_steps * 128 * world / tr_dt,
                 'scaling': 'weak'}
+        log('[bench] packing report')
         line['packing'] = packing_report(a, device, elapsed / a.steps)
         if world == 1 and a.kind == 'polymer' and not a.no_secondary:
+            log('[bench] secondary workloads (qm9, zinc, training step)')
             line['secondary'] = [secondary_workload(device, 'qm9', 64, 3, 300, 200, streams=a.streams),
                                  secondary_workload(device, 'zinc', 512, 5, 512, 30, streams=a.streams),
                                  training_workload(device)]
         if not a.no_cpu and world == 1:  # the CPU leg is timed at N=1 only
+            log(f'[bench] CPU baseline (~{a.cpu_seconds:.0f} s + a one-thread sample)')
             cpu = cpu_baseline(TrainArgs(hidden_size=H, depth=a.depth, device=torch.device('cpu')), graphs[0],
                                a.cpu_seconds)
             line['cpu_baseline'] = cpu
