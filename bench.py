@@ -331,20 +331,12 @@ def main():
                     help='configs[4] as DP training: streamed graphs per rank (batches of 128); 0 = skip')
     a = ap.parse_args()
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
     # one process per GPU over RCCL (backend "nccl"); BENCH_BACKEND=gloo rehearses the multi-rank path
-    # with several ranks on one GPU (device = local rank modulo the visible GPUs)
-    backend = os.environ.get('BENCH_BACKEND', 'nccl')
-    local = local % max(1, torch.cuda.device_count())
-    if world > 1:
-        torch.cuda.set_device(local)
-        if backend == 'nccl':
-            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-        else:
-            dist.init_process_group(backend)
-    device = torch.device('cuda', local)
+    # with several ranks on one GPU (device = local rank modulo the visible GPUs).  The process group comes
+    # from chemprop_amd.dp.init_distributed, the package's one initialisation path.
+    from chemprop_amd.dp import init_distributed
+    env = init_distributed(os.environ.get('BENCH_BACKEND', 'nccl'), device='cuda')
+    world, rank, device = env.world_size, env.rank, env.device
     args = TrainArgs(hidden_size=a.hidden, depth=a.depth, device=device)
 
     # inputs: packed + resident in HBM before timing (featurization.py:757-813 equivalent on host)

@@ -24,7 +24,11 @@ restated here:
   (run_training.py:440-491, cross_validate.py:149-172) and ``test_preds.csv``.
 
 The encoder runs on the HIP path (a GPU is required, like every ``chemprop_amd`` forward).  Checkpoints
-are plain state dicts (``torch.load(..., weights_only=True)``) with the reference's key names.
+(``model.pt``, ``best_model.pt``) have the layout of the reference's ``save_checkpoint`` (utils.py:47-73):
+``args`` (a plain dict), ``state_dict`` (the reference's parameter names), ``data_scaler`` /
+``features_scaler`` / ``atom_descriptor_scaler`` / ``bond_feature_scaler`` as ``{'means', 'stds'}`` lists
+or None -- only plain types, so ``torch.load(..., weights_only=True)`` reads them; ``load_checkpoint`` and
+``load_scalers`` read them back (utils.py:80-131, 263-293).
 """
 from __future__ import annotations
 
@@ -33,6 +37,7 @@ import csv
 import json
 import math
 import os
+import re
 import sys
 from random import Random
 from typing import Dict, List, Optional
@@ -73,6 +78,63 @@ class StandardScaler:
         X = np.array(X).astype(float)
         t = X * self.stds + self.means
         return np.where(np.isnan(t), self.replace_nan_token, t)
+
+
+def _scaler_to_dict(sc: Optional[StandardScaler]):
+    """utils.py:58-62: means / stds as plain lists (None without a scaler)."""
+    if sc is None:
+        return None
+    conv = (lambda v: np.asarray(v, dtype=float).tolist() if v is not None else None)
+    return {'means': conv(sc.means), 'stds': conv(sc.stds)}
+
+
+def _plain(v):
+    if isinstance(v, (bool, int, float, str)) or v is None:
+        return v
+    if isinstance(v, (list, tuple)):
+        return [_plain(x) for x in v]
+    return str(v)  # e.g. torch.device
+
+
+def save_checkpoint(path: str, model, scaler: Optional[StandardScaler] = None,
+                    features_scaler: Optional[StandardScaler] = None, args=None) -> None:
+    """utils.py:47-73: {'args', 'state_dict', 'data_scaler', 'features_scaler', 'atom_descriptor_scaler',
+    'bond_feature_scaler'}; every value a plain type (weights_only-loadable)."""
+    a = {} if args is None else {k: _plain(v) for k, v in (vars(args) if not isinstance(args, dict) else args).items()}
+    torch.save({'args': a, 'state_dict': model.state_dict(), 'data_scaler': _scaler_to_dict(scaler),
+                'features_scaler': _scaler_to_dict(features_scaler), 'atom_descriptor_scaler': None,
+                'bond_feature_scaler': None}, path)
+
+
+def load_checkpoint(path: str, device=None):
+    """utils.py:80-131 for this module's checkpoints: a MoleculeModel rebuilt from the stored args with the
+    stored weights (``encoder.encoder.W*`` names of older checkpoints remapped to ``encoder.encoder.0.W*``,
+    utils.py:114-115).  Loaded with weights_only=True: nothing in the file is executed."""
+    state = torch.load(path, map_location='cpu', weights_only=True)
+    if not isinstance(state, dict) or 'state_dict' not in state:
+        raise ValueError(f'{path} is not a checkpoint (no state_dict)')
+    sd = {re.sub(r'^encoder\.encoder\.([Wc])', r'encoder.encoder.0.\1', k): v for k, v in state['state_dict'].items()}
+    if 'args' not in state:
+        return sd
+    fields = set(TrainArgs.__dataclass_fields__)
+    kw = {k: v for k, v in state['args'].items() if k in fields and k != 'device'}
+    args = TrainArgs(**kw, device=torch.device(device) if device is not None else torch.device('cpu'))
+    model = MoleculeModel(args)
+    model.load_state_dict(sd)
+    return model.to(args.device)
+
+
+def load_scalers(path: str):
+    """utils.py:263-293: (data scaler, features scaler, atom descriptor scaler, bond feature scaler)."""
+    state = torch.load(path, map_location='cpu', weights_only=True)
+
+    def mk(d, nan_token=None):
+        if d is None:
+            return None
+        return StandardScaler(np.asarray(d['means'], dtype=float), np.asarray(d['stds'], dtype=float),
+                              replace_nan_token=nan_token)
+    return (mk(state.get('data_scaler')), mk(state.get('features_scaler'), 0),
+            mk(state.get('atom_descriptor_scaler'), 0), mk(state.get('bond_feature_scaler'), 0))
 
 
 def random_split(n: int, sizes, seed: int):
@@ -241,14 +303,13 @@ def run_training(a: argparse.Namespace) -> Dict[str, list]:
             w.writerow([epoch, float(np.mean(losses)) if losses else float('nan')] +
                        [float(np.nanmean(tr_scores[m])) if tr_scores[m] else float('nan') for m in metrics] +
                        [float(np.nanmean(val_scores[m])) if val_scores[m] else float('nan') for m in metrics])
-            torch.save({'model_state_dict': model.state_dict(), 'epoch': epoch}, os.path.join(a.save_dir, 'model.pt'))
+            save_checkpoint(os.path.join(a.save_dir, 'model.pt'), model, scaler, None, args)
             v = float(np.nanmean(val_scores[metric])) if val_scores[metric] else float('nan')
             if (minimize and v < best) or (not minimize and v > best) or (epoch == 0 and math.isnan(v)):
                 best, best_epoch = v, epoch
-                torch.save({'model_state_dict': model.state_dict(), 'epoch': epoch},
-                           os.path.join(a.save_dir, 'best_model.pt'))
+                save_checkpoint(os.path.join(a.save_dir, 'best_model.pt'), model, scaler, None, args)
     ckpt = torch.load(os.path.join(a.save_dir, 'best_model.pt'), map_location=device, weights_only=True)
-    model.load_state_dict(ckpt['model_state_dict'])
+    model.load_state_dict(ckpt['state_dict'])
     test_targets = [targets[i] for i in test_idx]
     test_preds = predict(model, graphs, test_idx, a.batch_size, scaler)
     scores = evaluate_predictions(test_preds, test_targets, num_tasks, metrics, a.dataset_type)

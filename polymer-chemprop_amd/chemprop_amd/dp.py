@@ -37,24 +37,33 @@ class DistEnv:
         return self.world_size > 1
 
 
-def init_distributed(backend: str = None) -> DistEnv:
+def init_distributed(backend: str = None, device: str = None) -> DistEnv:
     """Read RANK / WORLD_SIZE / LOCAL_RANK (torch.distributed.run) and initialise the process group.
-    Single process (no env): no process group, rank 0 of 1."""
+    Single process (no env): no process group, rank 0 of 1.
+
+    ``backend``: 'nccl' (RCCL over xGMI, the multi-GPU default) or 'gloo'.  ``device``: 'cuda' puts the
+    rank on GPU ``LOCAL_RANK % visible GPUs`` (several ranks may share one GPU: the gloo rehearsal of the
+    multi-GPU path), 'cpu' keeps it on the host; default: cuda with nccl, cpu with gloo.  This is the one
+    initialisation path of the package: bench.py and the DP training tests call it, so the 8-GPU run
+    differs from the rehearsal only in the backend string."""
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if backend is None:
         backend = 'nccl' if torch.cuda.is_available() else 'gloo'
-    if backend == 'nccl':
-        torch.cuda.set_device(local)
-        device = torch.device('cuda', local)
+    if device is None:
+        device = 'cuda' if backend == 'nccl' else 'cpu'
+    if device == 'cuda':
+        ordinal = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(ordinal)
+        dev = torch.device('cuda', ordinal)
     else:
-        device = torch.device('cpu')
+        dev = torch.device('cpu')
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        kwargs = {'device_id': device} if backend == 'nccl' else {}
+        kwargs = {'device_id': dev} if backend == 'nccl' else {}
         dist.init_process_group(backend, rank=rank, world_size=world, **kwargs)
-    return DistEnv(rank, world, local, device)
+    return DistEnv(rank, world, local, dev)
 
 
 def shard(items: Sequence[T], rank: int, world_size: int) -> List[T]:

@@ -539,6 +539,13 @@ class BatchMolGraph:
                                                                                      blk_of_atom)):
                 ell_idx, ell_coef = ell_rows(c, rows_p, bstart[rb[:len(c.ptr) - 1]])
                 arrays += [(name + '_idx', ell_idx), (name + '_coef', ell_coef)]
+            # per bond row: its source atom (b2a) as a block-local atom index (the fused layer's X[b] =
+            # A[src(b)] - P[rev(b)], mpn.py:119-120); rows outside the blocks 0
+            src_blk = np.zeros(fb_p.shape[0], np.uint8)
+            nb = len(self._np['b2a'])
+            inb = np.nonzero(blk_of_bond[:nb] >= 0)[0]
+            src_blk[inb] = (self._np['b2a'][inb] - blocks[blk_of_bond[inb], 2]).astype(np.uint8)
+            arrays.append(('bond_src_blk', src_blk))
         csrs = [('msg', msg), ('agg', agg), ('msg_t', msg_t), ('agg_t', agg_t)]
         if feat is not None:
             csrs.append(('feat', feat))
@@ -609,6 +616,7 @@ class BatchMolGraph:
                 s.n_blocks, s.blocks, s.bond_blk_row = len(blocks), P('blocks'), P('bond_blk_row')
                 s.msg_ell_idx, s.msg_ell_coef = P('msg_ell_idx'), P('msg_ell_coef')
                 s.atom_ell_idx, s.atom_ell_coef = P('agg_ell_idx'), P('agg_ell_coef')
+                s.bond_src_blk = P('bond_src_blk')
                 s.f_atoms_blk_x6 = planes.data_ptr()
         dg = DeviceGraph(buf, views, s)
         dg.finish()

@@ -8,8 +8,11 @@ form (include/wdmpnn.h "Compact graphs": ~14 bytes per directed edge) and expand
     generate + block plan + stage  --pinned-->  H2D + wdmpnn_build_graph  --event-->  forward / train step
 
 * ``producers`` threads run ``_wdpack.generate_stage`` (csrc/compact.hpp) for batches t, t + P, ...
-  into a ring of pinned host slots; a slot is rewritten only after the H2D that read it has completed
-  (its CUDA event), so nothing is copied twice and nothing is overwritten early.
+  into a ring of R pinned host slots.  Batch i goes to slot i % R, and only on that slot's turn: the slot
+  carries the index of the next batch allowed to write it (i, then i + R once the consumer has issued
+  the H2D of batch i), so batches arrive in order whatever the thread timing.  A slot is rewritten only
+  after the H2D that read it has completed (its CUDA event), so nothing is copied twice and nothing is
+  overwritten early.
 * The consumer (the caller's thread) takes the batches in order.  It enqueues the batch's H2D and graph
   build on a feed stream; the caller's forward waits on the graph's ready event on its own stream
   (``DeviceGraph.use_on``), so batch i + 1 is uploaded and built while batch i is encoded.
@@ -57,9 +60,8 @@ class StreamedBatches:
         self.host = [torch.empty(self.cap, dtype=torch.uint8, pin_memory=True) for _ in range(self.R)]
         self.info = [None] * self.R
         self.full = [threading.Event() for _ in range(self.R)]
-        self.free = [threading.Event() for _ in range(self.R)]
-        for e in self.free:
-            e.set()
+        self.turn = list(range(self.R))  # per slot: the batch index allowed to write it next
+        self.cv = threading.Condition()
         self.copy_done = [None] * self.R  # CUDA event after the H2D that read the slot
         self.feed = torch.cuda.Stream(self.device)
         self.error = None
@@ -73,10 +75,11 @@ class StreamedBatches:
         try:
             for i in range(t, self.n, self.P):
                 s = i % self.R
-                while not self.free[s].wait(0.1):
-                    if self.stop:
-                        return
-                self.free[s].clear()
+                with self.cv:
+                    while self.turn[s] != i:
+                        if self.stop:
+                            return
+                        self.cv.wait(0.1)
                 if self.copy_done[s] is not None:
                     self.copy_done[s].synchronize()  # the previous H2D out of this slot has run
                 res = P.generate_stage(KINDS[self.kind], self.B, (self.seed0 + i) & 0xFFFFFFFFFFFFFFFF, self.target,
@@ -86,7 +89,7 @@ class StreamedBatches:
                 info, arrays = res if self.keep else (res, None)
                 if not info[0]:
                     raise RuntimeError(f'staged batch larger than the slot ({info[3]} > {self.cap} bytes)')
-                self.info[s] = (info, arrays)
+                self.info[s] = (i, info, arrays)
                 self.full[s].set()
         except BaseException as e:  # surfaced by the consumer
             self.error = e
@@ -101,21 +104,25 @@ class StreamedBatches:
                 if self.error is not None:
                     raise RuntimeError('stream producer failed') from self.error
                 self.full[s].clear()
-                info, arrays = self.info[s]
+                idx, info, arrays = self.info[s]
+                if idx != i:
+                    raise RuntimeError(f'stream slot {s} holds batch {idx}, expected {i}')
                 with torch.cuda.stream(self.feed):
                     dg = upload_compact(self.device, self.host[s], info, 133, 147, lean=self.lean)
                     ev = torch.cuda.Event()
                     ev.record(self.feed)
                 self.copy_done[s] = ev
-                self.free[s].set()
+                with self.cv:
+                    self.turn[s] = i + self.R
+                    self.cv.notify_all()
                 yield _device_batch(dg, info, arrays)
         finally:
             self.close()
 
     def close(self) -> None:
-        self.stop = True
-        for e in self.free:
-            e.set()
+        with self.cv:
+            self.stop = True
+            self.cv.notify_all()
         for th in self.threads:
             th.join()
 

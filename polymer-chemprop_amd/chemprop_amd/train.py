@@ -86,7 +86,7 @@ class HipAdam(Optimizer):
             raise ValueError('invalid Adam hyperparameter')
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
         self.decoupled = bool(decoupled)
-        self._tables = {}  # group index -> (param pointers, ctypes tensor table, state list)
+        self._tables = {}  # parameter pointers of one launch -> its ctypes tensor table
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -96,46 +96,44 @@ class HipAdam(Optimizer):
             with torch.enable_grad():
                 loss = closure()
         L = _native.lib()
-        for gi, group in enumerate(self.param_groups):
+        for group in self.param_groups:
             ps = [p for p in group['params'] if p.grad is not None]
             if not ps:
                 continue
-            key = tuple(p.data_ptr() for p in ps)
-            ent = self._tables.get(gi)
-            if ent is None or ent[0] != key:
-                sts = []
-                for p in ps:
+            # torch's Adam keeps one step count per parameter: a parameter that had no gradient on some
+            # steps lags behind the others, so the launches are grouped by step count (usually one group)
+            by_step = {}
+            for p in ps:
+                st = self.state[p]
+                if 'exp_avg' not in st:
                     if p.device.type != 'cuda' or p.dtype != torch.float32 or not p.is_contiguous():
                         raise TypeError('HipAdam expects contiguous float32 CUDA parameters')
-                    st = self.state[p]
-                    if 'exp_avg' not in st:
-                        st['step'] = 0
-                        st['exp_avg'] = torch.zeros_like(p)
-                        st['exp_avg_sq'] = torch.zeros_like(p)
-                    sts.append(st)
-                steps = {st['step'] for st in sts}
-                if len(steps) != 1:
-                    raise RuntimeError('HipAdam: parameters of one group at different step counts')
-                tab = (_native.WdAdamTensor * len(ps))()
-                for k, (p, st) in enumerate(zip(ps, sts)):
-                    tab[k].param, tab[k].exp_avg, tab[k].exp_avg_sq = p.data_ptr(), st['exp_avg'].data_ptr(), \
-                        st['exp_avg_sq'].data_ptr()
-                    tab[k].numel = p.numel()
-                ent = (key, tab, sts, ps)
-                self._tables[gi] = ent
-            tab, sts = ent[1], ent[2]
-            for k, p in enumerate(ps):
-                g = p.grad
-                if g.is_sparse or g.dtype != torch.float32 or not g.is_contiguous():
-                    raise TypeError('HipAdam expects dense contiguous float32 gradients')
-                tab[k].grad = g.data_ptr()
-            step = sts[0]['step'] + 1
-            for st in sts:
-                st['step'] = step
-            h = _native.WdAdamHyper(float(group['lr']), float(group['betas'][0]), float(group['betas'][1]),
-                                    float(group['eps']), float(group['weight_decay']), step, int(self.decoupled))
-            _native.check(L.wdmpnn_adam_step(tab, len(ps), ctypes.byref(h), _native.current_stream(ps[0].device)),
-                          'adam step')
+                    st['step'] = 0
+                    st['exp_avg'] = torch.zeros_like(p)
+                    st['exp_avg_sq'] = torch.zeros_like(p)
+                by_step.setdefault(int(st['step']) + 1, []).append(p)
+            for step, sub in by_step.items():
+                key = tuple(p.data_ptr() for p in sub)
+                ent = self._tables.get(key)
+                if ent is None:
+                    tab = (_native.WdAdamTensor * len(sub))()
+                    for k, p in enumerate(sub):
+                        st = self.state[p]
+                        tab[k].param, tab[k].exp_avg, tab[k].exp_avg_sq = p.data_ptr(), st['exp_avg'].data_ptr(), \
+                            st['exp_avg_sq'].data_ptr()
+                        tab[k].numel = p.numel()
+                    ent = self._tables[key] = tab
+                tab = ent
+                for k, p in enumerate(sub):
+                    g = p.grad
+                    if g.is_sparse or g.dtype != torch.float32 or not g.is_contiguous():
+                        raise TypeError('HipAdam expects dense contiguous float32 gradients')
+                    tab[k].grad = g.data_ptr()
+                    self.state[p]['step'] = step
+                h = _native.WdAdamHyper(float(group['lr']), float(group['betas'][0]), float(group['betas'][1]),
+                                        float(group['eps']), float(group['weight_decay']), step, int(self.decoupled))
+                _native.check(L.wdmpnn_adam_step(tab, len(sub), ctypes.byref(h), _native.current_stream(sub[0].device)),
+                              'adam step')
         return loss
 
     def load_state_dict(self, state_dict) -> None:

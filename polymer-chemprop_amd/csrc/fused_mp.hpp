@@ -25,11 +25,6 @@
 
 namespace wd {
 
-// WD_EXP: experiment builds for kernel-time A/Bs (tools/exp_libs.sh); 0 = the product
-#ifndef WD_EXP
-#define WD_EXP 0
-#endif
-
 constexpr int BLK_BONDS = 128, BLK_ATOMS = 64;  // block capacity (rows of the blocked layouts)
 constexpr int BLK_MOLS = 64;                     // molecules per block (empty molecules have no rows)
 // gather entries per row in the block-local ELL form (WdGraph.*_ell_*, WDMPNN_ELL_WIDTH; 12 measured
@@ -79,24 +74,6 @@ __device__ __forceinline__ void lds_term(const float *T, int j, int c, float w, 
     fma4(s1, w, ld4(T + j * LDC + c + 4));
 }
 
-// one message term of row j (natural id jn): P[j] or (P[j] + P[rev j]) / 2 (mpn.py:101-102)
-template <int LDC>
-__device__ __forceinline__ void msg_term(const float *Pt, int jn, int bs, const int32_t *sym_rev, int c, float w,
-                                         float4 &s0, float4 &s1) {
-    const int j = jn - bs;
-    float4 p0 = ld4(Pt + j * LDC + c), p1 = ld4(Pt + j * LDC + c + 4);
-    if (sym_rev) {
-        const int jr = sym_rev[jn] - bs;
-        const float4 q0 = ld4(Pt + jr * LDC + c), q1 = ld4(Pt + jr * LDC + c + 4);
-        p0.x = (p0.x + q0.x) / 2.0f; p0.y = (p0.y + q0.y) / 2.0f;
-        p0.z = (p0.z + q0.z) / 2.0f; p0.w = (p0.w + q0.w) / 2.0f;
-        p1.x = (p1.x + q1.x) / 2.0f; p1.y = (p1.y + q1.y) / 2.0f;
-        p1.z = (p1.z + q1.z) / 2.0f; p1.w = (p1.w + q1.w) / 2.0f;
-    }
-    fma4(s0, w, p0);
-    fma4(s1, w, p1);
-}
-
 struct MpLayerP {
     const uint8_t *mprev;       // M_{t-1}: blocked bond plane tiles [nblk * 128][kp]
     uint8_t *mnext;             // M_t (not written by the last layer)
@@ -105,12 +82,12 @@ struct MpLayerP {
     const float *inp;           // fp32 [Rp][Hk] natural rows (mpn.py:95 input)
     const float *bias;          // b_h (padded) or null
     const int32_t *blocks;
-    const int32_t *ptr, *idx; const float *coef;   // msg gather, natural rows
-    const uint8_t *ell_idx; const float *ell_coef;  // its first ELLW entries per row, block-local (WdGraph)
-    const int32_t *sym_rev;     // undirected (mpn.py:101-102) or null
+    const int32_t *rev;         // b2revb (natural bond ids)
+    const uint8_t *src_blk;     // per natural bond row: block-local source atom (b2a)
+    int undirected;             // mpn.py:101-102
     int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;
     const int32_t *aptr, *aidx; const float *acoef;  // atom gather (natural atom rows -> natural bond rows)
-    const uint8_t *aell_idx; const float *aell_coef;
+    const uint8_t *aell_idx; const float *aell_coef; // its first ELLW entries per row, block-local (WdGraph)
     uint8_t *aplanes;           // A: blocked atom plane tiles [nblk * 64][kp]
     int n_tiles;                // Hk / BN
     // training forward (save_for_backward) or null: the pre-activation Z_t (mpn.py:123) as fp32 natural
@@ -129,47 +106,62 @@ template <int BN> struct MpWaves;
 template <> struct MpWaves<64> { static constexpr int WM = 4, WN = 2; };
 template <> struct MpWaves<80> { static constexpr int WM = 8, WN = 1; };
 
-// mp_layer epilogue, shared by both layer kernels: residual rows and gather lists prefetched during the
-// GEMM, then (P tile in LDS) the in-block gather, bias, residual, activation, dropout and the plane
-// stores of M_t -- or, in the last layer, the atom aggregate of M_t.
+// mp_layer epilogue: the gather G applied to the P = M_{t-1} W_h^T tile in LDS in the reference's two
+// steps (mpn.py:110-120), then bias, residual, activation, dropout and the plane stores of M_t -- or, in
+// the last layer, the atom aggregate of M_t (mpn.py:126-131):
+//     (undirected: P <- (P + P[rev]) / 2, mpn.py:101-102)
+//     A[a] = sum_{b into a} w_b P[b]      (the block's atoms, slot order, into LDS)
+//     X[b] = A[src(b)] - P[rev(b)]
+// Only the atom gather lists and the rows' source / reverse ids are prefetched during the GEMM (a few
+// registers: with <= 128 VGPRs two layer workgroups co-reside on a CU -- one's epilogue beside the
+// other's GEMM when batches are in flight on two streams); the residual rows are loaded when the
+// epilogue starts and land behind the atom sums.
 template <int BN, int NT, bool LAST>
 struct MpEpilogue {
     static constexpr int BM = BLK_BONDS, LDC = BN + 4;
     static constexpr int UPR = BN / 8, UNITS = BM * UPR, UPT = (UNITS + NT - 1) / NT;  // 8-column units
-    static constexpr int AUNITS = BLK_ATOMS * UPR, AUPT = LAST ? (AUNITS + NT - 1) / NT : 1;
-    float4 res[UPT][2];
-    EllRow ell[UPT];
+    static constexpr int AUNITS = BLK_ATOMS * UPR, AUPT = (AUNITS + NT - 1) / NT;
+    static constexpr int LDS_FLOATS = (BM + BLK_ATOMS) * LDC;  // P tile, then the atom sums
     EllRow aell[AUPT];
+    int32_t rv[UPT];
+    uint32_t sa[UPT];
 
-    // residual rows and the rows' gather lists (ELL) (unit v = tid + NT i: row v / UPR, columns 8 (v %
-    // UPR) ..); the last layer also prefetches the atom gather rows of its atom-aggregate units (unit v =
-    // tid + NT i: atom v / UPR)
-    __device__ __forceinline__ void prefetch(const MpLayerP &P, const BlockRow &B, int n0) {
+    // during the GEMM: the atom gather rows of this thread's atom units (unit v = tid + NT i: atom v / UPR)
+    // and the source / reverse ids of its bond units (unit v: row v / UPR) -- loads only, no arithmetic on
+    // what they return (that would wait for them inside the GEMM)
+    __device__ __forceinline__ void prefetch(const MpLayerP &P, const BlockRow &B) {
         const int tid = threadIdx.x;
 #pragma unroll
-        for (int i = 0; i < AUPT; ++i) aell[i] = ell_zero();
+        for (int i = 0; i < AUPT; ++i) {
+            const int v = tid + NT * i;
+            aell[i] = ell_zero();
+            if (v < AUNITS && v / UPR < B.an) aell[i] = ell_load(P.aell_idx, P.aell_coef, (size_t)B.as + v / UPR);
+        }
 #pragma unroll
         for (int i = 0; i < UPT; ++i) {
-            const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
-            res[i][0] = res[i][1] = f4zero();
-            ell[i] = ell_zero();
+            const int v = tid + NT * i, lr = v / UPR;
+            rv[i] = 0;
+            sa[i] = 0;
             if (v < UNITS && lr < B.bn) {
-                const size_t b = B.bs + lr;
-                const float *s = P.inp + b * P.kp + n0 + c;
-                res[i][0] = ld4(s);
-                res[i][1] = ld4(s + 4);
-                ell[i] = ell_load(P.ell_idx, P.ell_coef, b);
+                rv[i] = P.rev[B.bs + lr];
+                sa[i] = P.src_blk[B.bs + lr];
             }
         }
-        if constexpr (LAST)
-#pragma unroll
-            for (int i = 0; i < AUPT; ++i) {
-                const int v = tid + NT * i;
-                if (v / UPR < B.an) aell[i] = ell_load(P.aell_idx, P.aell_coef, (size_t)B.as + v / UPR);
-            }
     }
 
-    // Pt: the P = M_{t-1} W_hᵀ tile [BM][LDC] fp32 in LDS (every write of it done and synchronised)
+    // A[la][c..c+7] = sum over the atom's in-bonds (ELL slots, then the CSR rest) of w * T[bond]
+    __device__ __forceinline__ void atom_sum(const MpLayerP &P, const BlockRow &B, const EllRow &E, int la, int c,
+                                             const float *T, float4 &s0, float4 &s1) {
+        s0 = s1 = f4zero();
+#pragma unroll
+        for (int k = 0; k < ELLW; ++k)
+            if (E.w[k] != 0.f) lds_term<LDC>(T, ell_idx(E, k), c, E.w[k], s0, s1);
+        if (ell_more(E))
+            for (int q = P.aptr[B.as + la] + ELLW; q < P.aptr[B.as + la + 1]; ++q)
+                lds_term<LDC>(T, P.aidx[q] - B.bs, c, P.acoef ? P.acoef[q] : 1.0f, s0, s1);
+    }
+
+    // Pt: the P tile [BM][LDC] fp32 in LDS (every write of it done and synchronised); At = Pt + BM * LDC
     __device__ __forceinline__ void run(const MpLayerP &P, const BlockRow &B, int blk, int n0, float *Pt) {
         with_act(P.act, [&](auto act_c) { run_act<decltype(act_c)::value>(P, B, blk, n0, Pt); });
     }
@@ -177,8 +169,49 @@ struct MpEpilogue {
     template <int ACT>
     __device__ __forceinline__ void run_act(const MpLayerP &P, const BlockRow &B, int blk, int n0, float *Pt) {
         const int tid = threadIdx.x;
+        float *At = Pt + BM * LDC;
+        // residual rows (mpn.py:123 input): issued now, consumed after the atom sums
+        float4 res[UPT][2];
+#pragma unroll
+        for (int i = 0; i < UPT; ++i) {
+            const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
+            res[i][0] = res[i][1] = f4zero();
+            if (v < UNITS && lr < B.bn) {
+                const float *s = P.inp + (size_t)(B.bs + lr) * P.kp + n0 + c;
+                res[i][0] = ld4(s);
+                res[i][1] = ld4(s + 4);
+            }
+        }
+        if (P.undirected) {  // P <- (P + P[rev]) / 2, one thread per reverse pair (the lower row)
+#pragma unroll
+            for (int i = 0; i < UPT; ++i) {
+                const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
+                const int rl = rv[i] - B.bs;
+                if (v < UNITS && lr < B.bn && lr < rl) {
+                    float4 p0 = ld4(Pt + lr * LDC + c), p1 = ld4(Pt + lr * LDC + c + 4);
+                    const float4 q0 = ld4(Pt + rl * LDC + c), q1 = ld4(Pt + rl * LDC + c + 4);
+                    p0.x = (p0.x + q0.x) / 2.0f; p0.y = (p0.y + q0.y) / 2.0f;
+                    p0.z = (p0.z + q0.z) / 2.0f; p0.w = (p0.w + q0.w) / 2.0f;
+                    p1.x = (p1.x + q1.x) / 2.0f; p1.y = (p1.y + q1.y) / 2.0f;
+                    p1.z = (p1.z + q1.z) / 2.0f; p1.w = (p1.w + q1.w) / 2.0f;
+                    st4(Pt + lr * LDC + c, p0); st4(Pt + lr * LDC + c + 4, p1);
+                    st4(Pt + rl * LDC + c, p0); st4(Pt + rl * LDC + c + 4, p1);
+                }
+            }
+            __syncthreads();
+        }
+        // A[a] = sum_{b into a} w_b P[b] (mpn.py:112-118)
+#pragma unroll
+        for (int i = 0; i < AUPT; ++i) {
+            const int v = tid + NT * i, la = v / UPR, c = 8 * (v % UPR);
+            if (v >= AUNITS || la >= B.an) break;
+            float4 s0, s1;
+            atom_sum(P, B, aell[i], la, c, Pt, s0, s1);
+            st4(At + la * LDC + c, s0);
+            st4(At + la * LDC + c + 4, s1);
+        }
+        __syncthreads();
         const float slope = ACT == ACT_PRELU ? P.slope[0] : 0.f;
-        float4 b0 = f4zero(), b1 = f4zero();
         const __amdgpu_buffer_rsrc_t mrs = x6_block_rsrc<BM>(LAST ? P.aplanes : P.mnext, P.kp, blk);
         float4 ym[LAST ? UPT : 1][2];  // LAST: this thread's M_t units until P is dead
 #pragma unroll
@@ -187,30 +220,19 @@ struct MpEpilogue {
             if (v >= UNITS) break;
             float4 y0 = f4zero(), y1 = f4zero();
             if (lr < B.bn) {
-                const int b = B.bs + lr;
-                float4 s0 = f4zero(), s1 = f4zero();
-                // the first ELLW entries from the prefetched ELL row, in CSR order (the reference's slot
-                // order); unused slots have weight 0 and are skipped (the CSR lists hold no zero weights)
-                const EllRow &E = ell[i];
-                if (P.sym_rev) {
-#pragma unroll
-                    for (int k = 0; k < ELLW; ++k)
-                        if (E.w[k] != 0.f) msg_term<LDC>(Pt, B.bs + ell_idx(E, k), B.bs, P.sym_rev, c, E.w[k], s0, s1);
-                } else {
-#pragma unroll
-                    for (int k = 0; k < ELLW; ++k)
-                        if (E.w[k] != 0.f) lds_term<LDC>(Pt, ell_idx(E, k), c, E.w[k], s0, s1);
-                }
-                if (ell_more(E))  // more than ELLW entries: the rest from the CSR list
-                    for (int e = P.ptr[b] + ELLW; e < P.ptr[b + 1]; ++e)
-                        msg_term<LDC>(Pt, P.idx[e], B.bs, P.sym_rev, c, P.coef ? P.coef[e] : 1.0f, s0, s1);
+                const int b = B.bs + lr, rl = rv[i] - B.bs, a = (int)sa[i];
+                // X[b] = A[src(b)] - P[rev(b)] (mpn.py:119-120)
+                const float4 a0 = ld4(At + a * LDC + c), a1 = ld4(At + a * LDC + c + 4);
+                const float4 q0 = ld4(Pt + rl * LDC + c), q1 = ld4(Pt + rl * LDC + c + 4);
+                float z[8] = {a0.x - q0.x, a0.y - q0.y, a0.z - q0.z, a0.w - q0.w,
+                              a1.x - q1.x, a1.y - q1.y, a1.z - q1.z, a1.w - q1.w};
+                float4 b0 = f4zero(), b1 = f4zero();
                 if (P.bias) { b0 = ld4(P.bias + n0 + c); b1 = ld4(P.bias + n0 + c + 4); }
-                float z[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
                 const float r8[8] = {res[i][0].x, res[i][0].y, res[i][0].z, res[i][0].w,
                                      res[i][1].x, res[i][1].y, res[i][1].z, res[i][1].w};
                 const float b8[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-                for (int q = 0; q < 8; ++q) z[q] = r8[q] + (z[q] + b8[q]);  // mpn.py:123
+                for (int q = 0; q < 8; ++q) z[q] = r8[q] + (z[q] + b8[q]);  // mpn.py:122-123
                 if (P.zsave) {
                     float *zr = P.zsave + (size_t)b * P.kp + n0 + c;
                     st4(zr, make_float4(z[0], z[1], z[2], z[3]));
@@ -242,24 +264,17 @@ struct MpEpilogue {
                 st4(Mt + lr * LDC + c + 4, ym[i][1]);
             }
             __syncthreads();
-            // atom aggregate of this column tile: A[a] = Σ_{b into a} w_b M_t[b] (mpn.py:126-131)
+            // atom aggregate of this column tile: A[a] = sum_{b into a} w_b M_t[b] (mpn.py:126-131)
             const __amdgpu_buffer_rsrc_t ars = x6_block_rsrc<BLK_ATOMS>(P.aplanes, P.kp, blk);
 #pragma unroll
             for (int i = 0; i < AUPT; ++i) {
-                const int v = tid + NT * i;
-                if (v >= B.an * UPR) break;  // rows past the block's atoms are never loaded
-                const int la = v / UPR, c = 8 * (v % UPR), a = B.as + la;
-                const EllRow &E = aell[i];
-                float4 s0 = f4zero(), s1 = f4zero();
-#pragma unroll
-                for (int k = 0; k < ELLW; ++k)
-                    if (E.w[k] != 0.f) lds_term<LDC>(Mt, ell_idx(E, k), c, E.w[k], s0, s1);
-                if (ell_more(E))
-                    for (int q = P.aptr[a] + ELLW; q < P.aptr[a + 1]; ++q)
-                        lds_term<LDC>(Mt, P.aidx[q] - B.bs, c, P.acoef ? P.acoef[q] : 1.0f, s0, s1);
+                const int v = tid + NT * i, la = v / UPR, c = 8 * (v % UPR);
+                if (v >= AUNITS || la >= B.an) break;  // rows past the block's atoms are never loaded
+                float4 s0, s1;
+                atom_sum(P, B, aell[i], la, c, Mt, s0, s1);
                 x6_store8_blk<BLK_ATOMS>(ars, la, n0 + c, s0, s1);
                 if (P.asave) {
-                    float *ar = P.asave + (size_t)a * P.kp + n0 + c;
+                    float *ar = P.asave + (size_t)(B.as + la) * P.kp + n0 + c;
                     st4(ar, s0);
                     st4(ar + 4, s1);
                 }
@@ -272,23 +287,27 @@ struct MpEpilogue {
 // LDS: two GEMM stages, reused by the epilogue as P [128][BN + 4] fp32; the last layer then
 // overwrites P with M_t (held in registers across a barrier) for the atom aggregate.
 template <int BN, bool LAST>
-__global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_layer_kernel(MpLayerP P) {
-    constexpr int BM = BLK_BONDS, LDC = BN + 4, WM = MpWaves<BN>::WM, WN = MpWaves<BN>::WN, NT = 64 * WM * WN;
+// (__launch_bounds__ min 4 waves per SIMD: <= 128 VGPRs, so that two layer workgroups -- batches in flight
+// on two streams -- co-reside on a CU, 2 x 78 KB of LDS)
+__global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN, 4) void mp_layer_kernel(MpLayerP P) {
+    constexpr int BM = BLK_BONDS, WM = MpWaves<BN>::WM, WN = MpWaves<BN>::WN, NT = 64 * WM * WN;
     // two stages of one chunk (measured: 3 stages slower; two-chunk stages, one barrier per two
     // chunks, no faster: the chunk time is not bound by load latency or barriers)
     constexpr int S = 2, CPS = 1;
     // (<= 80 KB: two workgroups fit one CU's 160 KB, so layers of batches in flight on other
     // streams co-reside)
-    constexpr int LDS_BYTES = BM * LDC * 4 > S * CPS * x6_stage_bytes<BM, BN>()
-                                  ? BM * LDC * 4
-                                  : S * CPS * x6_stage_bytes<BM, BN>();
+    constexpr int EPI_BYTES = MpEpilogue<BN, NT, LAST>::LDS_FLOATS * 4;  // P tile + the atom sums
+    constexpr int LDS_BYTES = EPI_BYTES > S * CPS * x6_stage_bytes<BM, BN>() ? EPI_BYTES
+                                                                              : S * CPS * x6_stage_bytes<BM, BN>();
     static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU");
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
     const int tile = xcd_tile(blockIdx.x, gridDim.x);
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
     MpEpilogue<BN, NT, LAST> E;
-    auto prefetch = [&]() { E.prefetch(P, B, n0); };
+    auto prefetch = [&](int phase) {
+        if (phase == 0) E.prefetch(P, B);
+    };
     X6Operands O{};
     O.a0 = P.mprev; O.nkc0 = P.kp >> 5; O.kc0 = P.kp >> 5;
     O.a1 = P.mprev; O.nkc1 = P.kp >> 5; O.kc1 = 0;  // no second segment (a non-null alias: no null arithmetic)
@@ -296,7 +315,7 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN) void mp_lay
     O.a_rows = B.bn;
     O.b = P.wh + (size_t)nt * (P.kp >> 5) * (3 * BN * 64);
     floatx4 acc[BM / WM / 16][BN / WN / 16];
-    x6_mainloop<BM, BN, WM, WN, S, CPS>(O, lds, acc, prefetch);
+    x6_mainloop<BM, BN, WM, WN, S, CPS, true>(O, lds, acc, prefetch);
     __syncthreads();
     float *Pt = reinterpret_cast<float *>(lds);
     x6_acc_to_lds<BM, BN, WM, WN>(acc, Pt);
@@ -403,7 +422,7 @@ __global__ __launch_bounds__(512) void embed_kernel(EmbedP P) {
             so.x += u.x; so.y += u.y; so.z += u.z; so.w += u.w;
         }
         fma4(so, cd.last, ld4(wt + (P.Fa - 1) * BN + c));
-        if (WD_EXP != 1) st4(P.eo + ((size_t)blk * BLK_ATOMS + la) * P.Hk + n0 + c, so);
+        st4(P.eo + ((size_t)blk * BLK_ATOMS + la) * P.Hk + n0 + c, so);
     }
     __syncthreads();  // every read of the W_o tile done
 #pragma unroll
@@ -446,15 +465,13 @@ __global__ __launch_bounds__(512) void embed_kernel(EmbedP P) {
         z0.x += b0.x; z0.y += b0.y; z0.z += b0.z; z0.w += b0.w;
         z1.x += b1.x; z1.y += b1.y; z1.z += b1.z; z1.w += b1.w;
         float *zr = P.inp + (size_t)b * P.Hk + n0 + c;
-        if (WD_EXP != 2) {
-            st4(zr, z0);
-            st4(zr + 4, z1);
-        }
+        st4(zr, z0);
+        st4(zr + 4, z1);
         const float4 y0 = make_float4(act_fwd(ACT, z0.x, slope), act_fwd(ACT, z0.y, slope),
                                       act_fwd(ACT, z0.z, slope), act_fwd(ACT, z0.w, slope));
         const float4 y1 = make_float4(act_fwd(ACT, z1.x, slope), act_fwd(ACT, z1.y, slope),
                                       act_fwd(ACT, z1.z, slope), act_fwd(ACT, z1.w, slope));
-        if (WD_EXP != 3) x6_store8_blk<BLK_BONDS>(mrs, lb, n0 + c, y0, y1);
+        x6_store8_blk<BLK_BONDS>(mrs, lb, n0 + c, y0, y1);
     }
     });
     if (blk == 0 && tid < C4) st4(P.inp + n0 + 4 * tid, f4zero());  // pad row 0 (Z_0 of the backward)
@@ -524,7 +541,8 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     // codes path: this thread's rows of the precomputed f_atoms W_o[:, :Fa]^T (the epilogue units below)
     constexpr int EPU = (BM * C4 + NT - 1) / NT;
     float4 eo[EPU];
-    auto prefetch = [&]() {
+    auto prefetch = [&](int phase) {
+        if (phase != 0) return;
         bb = ld4(P.bias + n0 + 4 * (tid % C4));
         if (tid < B.an) watom = P.w_atoms[B.as + tid];
 #pragma unroll

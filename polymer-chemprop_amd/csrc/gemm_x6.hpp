@@ -449,7 +449,7 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // tile (BM / WM) x (BN / WN), S LDS stages (S - 1 chunks in flight behind the one multiplied) of CPS
 // chunks each.  Uses lds[0 .. S * CPS * x6_stage_bytes<BM, BN>()); on return every DMA has landed and
 // all waves are past their last LDS read (the caller may reuse the LDS after one __syncthreads()).
-struct NoHook { __device__ void operator()() const {} };
+struct NoHook { __device__ void operator()(int) const {} };
 
 // f(std::integral_constant<int, n>) for a wave-uniform runtime n in [0, N]
 template <int N, typename F>
@@ -462,9 +462,14 @@ __device__ __forceinline__ void dispatch_upto(int n, F &&f) {
     }
 }
 
-// hook(): called once, right after the DMA of the second chunk is issued (register prefetches placed
-// there land behind the first chunk's MFMAs instead of delaying the first chunk's wait)
-template <int BM, int BN, int WM, int WN, int S = 2, int CPS = 1, typename Hook = NoHook>
+// hook(0): called once, right after the DMA of the second chunk is issued (register prefetches placed
+// there land behind the first chunk's MFMAs instead of delaying the first chunk's wait); hook(1): once
+// more one chunk later (or right after hook(0) with a single chunk), when hook(0)'s loads have landed --
+// for loads whose addresses depend on them
+
+// BPIPE: B fragments one column tile at a time, the next one in flight (two sets of 3 registers x 4
+// instead of TN sets): fewer VGPRs for kernels that must co-reside two per CU
+template <int BM, int BN, int WM, int WN, int S = 2, int CPS = 1, bool BPIPE = false, typename Hook = NoHook>
 __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
                                             floatx4 (&acc)[BM / WM / 16][BN / WN / 16], const Hook &hook = Hook()) {
     constexpr int NW = WM * WN, TM = BM / WM / 16, TN = BN / WN / 16;
@@ -515,6 +520,29 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
     const int na = min(TM, max(0, (O.a_rows - wi * (BM / WM) + 15) >> 4));
     auto compute_n = [&](const uint8_t *st, auto na_c) {
         constexpr int NA = decltype(na_c)::value;
+        // plane products hh, hm, mh, hl, lh, mm
+        constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};
+        if constexpr (BPIPE) {
+            bf16x8 af[TM][3], bq[2][3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+#pragma unroll
+                for (int a = 0; a < NA; ++a) af[a][p] = *reinterpret_cast<const bf16x8 *>(st + p * APL + ao[a]);
+                bq[0][p] = *reinterpret_cast<const bf16x8 *>(st + p * BPL + bo[0]);
+            }
+#pragma unroll
+            for (int b = 0; b < TN; ++b) {
+                if (b + 1 < TN)
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) bq[(b + 1) & 1][p] = *reinterpret_cast<const bf16x8 *>(st + p * BPL + bo[b + 1]);
+#pragma unroll
+                for (int t = 0; t < 6; ++t)
+#pragma unroll
+                    for (int a = 0; a < NA; ++a)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][PA[t]], bq[b & 1][PB[t]], acc[a][b], 0, 0, 0);
+            }
+            return;
+        }
         bf16x8 af[TM][3], bfr[TN][3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
@@ -523,8 +551,6 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
 #pragma unroll
             for (int b = 0; b < TN; ++b) bfr[b][p] = *reinterpret_cast<const bf16x8 *>(st + p * BPL + bo[b]);
         }
-        // plane products hh, hm, mh, hl, lh, mm
-        constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};
 #pragma unroll
         for (int t = 0; t < 6; ++t)
 #pragma unroll
@@ -563,7 +589,8 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             if (sc + 1 < nsc) issue_sc(sc + 1, (sc + 1) & 1);
-            if (sc == 0) hook();
+            if (sc == 0) hook(0);
+            if (sc == 1 || (sc == 0 && nsc == 1)) hook(1);
 #pragma unroll
             for (int q = 0; q < CPS; ++q)
                 if (sc * CPS + q < nchunks) compute(lds + ((sc & 1) * CPS + q) * STAGE);
@@ -581,11 +608,15 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
             __builtin_amdgcn_s_barrier();
             // S > 2: the hook's loads go out before the DMA of chunk S - 1, so that the partial
             // vmcnt waits above (which count only DMA instructions) find them among the older ones
-            if constexpr (S > 2)
-                if (kc == 0) hook();
+            if constexpr (S > 2) {
+                if (kc == 0) hook(0);
+                if (kc == 1 || (kc == 0 && nchunks == 1)) hook(1);
+            }
             if (kc + S - 1 < nchunks) issue(kc + S - 1, (kc + S - 1) % S);
-            if constexpr (S == 2)
-                if (kc == 0) hook();
+            if constexpr (S == 2) {
+                if (kc == 0) hook(0);
+                if (kc == 1 || (kc == 0 && nchunks == 1)) hook(1);
+            }
             compute(lds + (kc % S) * STAGE);
         }
     }

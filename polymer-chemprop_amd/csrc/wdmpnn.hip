@@ -114,7 +114,7 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     // (an embed-capable graph -- categorical codes -- needs no feature planes)
     const bool codes = g->atom_codes && g->bond_src_blk && g->bond_tail && D.Fb <= WO_MAXK && D.Fa <= WO_MAXK;
     D.blocked = D.x6 && !D.desc && D.T >= 2 && g->n_blocks > 0 && g->blocks && g->bond_blk_row &&
-                (codes || (g->f_atoms_blk_x6 && g->f_bonds_x6)) && g->msg_ell_idx && g->msg_ell_coef &&
+                (codes || (g->f_atoms_blk_x6 && g->f_bonds_x6)) && g->bond_src_blk && g->b2revb &&
                 g->atom_ell_idx && g->atom_ell_coef;
     D.nblk = D.blocked ? g->n_blocks : 0;
     if (D.atom && D.undirected)
@@ -718,9 +718,7 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
             M.wh = (const uint8_t *)(pkb + (bn80 ? PL.WhX80 : PL.WhX)); M.inp = F(L.Z[0]);
             M.bias = p->b_h ? W(PL.bh) : nullptr;
             M.blocks = g->blocks;
-            M.ptr = g->msg_gather.ptr; M.idx = g->msg_gather.idx; M.coef = g->msg_gather.coef;
-            M.ell_idx = g->msg_ell_idx; M.ell_coef = g->msg_ell_coef;
-            M.sym_rev = D.undirected ? g->b2revb : nullptr;
+            M.rev = g->b2revb; M.src_blk = g->bond_src_blk; M.undirected = D.undirected;
             M.act = c->activation; M.slope = p->prelu; M.p_drop = c->dropout; M.seed = c->seed; M.layer = t;
             M.aptr = g->atom_gather.ptr; M.aidx = g->atom_gather.idx; M.acoef = g->atom_gather.coef;
             M.aell_idx = g->atom_ell_idx; M.aell_coef = g->atom_ell_coef;

@@ -440,6 +440,34 @@ def test_hip_adam_matches_torch_adam(kind):
     assert 3 not in [i for i, b in enumerate(hip) if b in o_hip.state]
 
 
+def test_hip_adam_parameter_without_gradient_on_some_steps():
+    """torch's Adam keeps a step count per parameter: a parameter whose gradient is None on some steps
+    (a layer used only under some conditions) lags behind; HipAdam groups its launches by step count and
+    matches torch on every parameter and moment."""
+    from chemprop_amd.train import HipAdam
+    gen = torch.Generator().manual_seed(9)
+    shapes = [(64, 33), (17,), (5, 5)]
+    base = [torch.randn(s, generator=gen) for s in shapes]
+    ref = [torch.nn.Parameter(t.clone()) for t in base]
+    hip = [torch.nn.Parameter(t.clone().to(DEV)) for t in base]
+    o_ref = torch.optim.Adam(ref, lr=1e-2, foreach=False)
+    o_hip = HipAdam(hip, lr=1e-2)
+    for step in range(7):
+        for k, (a, b, s) in enumerate(zip(ref, hip, shapes)):
+            g = torch.randn(s, generator=gen)
+            skip = (k == 1 and step in (1, 2, 5)) or (k == 2 and step == 0)
+            a.grad = None if skip else g.clone()
+            b.grad = None if skip else g.clone().to(DEV)
+        o_ref.step()
+        o_hip.step()
+    for a, b in zip(ref, hip):
+        assert float((a.detach() - b.detach().cpu()).abs().max()) <= 1e-6 * max(1.0, float(a.detach().abs().max()))
+        assert int(o_ref.state[a]['step']) == int(o_hip.state[b]['step'])
+        for name in ('exp_avg', 'exp_avg_sq'):
+            x, y = o_ref.state[a][name], o_hip.state[b][name].cpu()
+            assert float((x - y).abs().max()) <= 1e-6 * max(1.0, float(x.abs().max()))
+
+
 @pytest.mark.parametrize('b,tasks,act,features', [(128, 1, 'ReLU', 0), (16, 2, 'tanh', 0), (33, 3, 'ELU', 5),
                                                    (8, 1, 'LeakyReLU', 0), (20, 2, 'SELU', 0)])
 def test_fused_head_loss_matches_torch(b, tasks, act, features):

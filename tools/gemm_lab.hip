@@ -131,8 +131,8 @@ float time_it(int reps, F &&launch) {
 // 4 column tiles of 80), wave layouts WM x WN per K-group, KG K-groups (group g multiplies the
 // chunks c with c % KG == g; one barrier per KG chunks), DMA / MFMA switchable to find the bound.
 // ---------------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int KG, bool DMA, bool MFMA, int S = 2>
-__global__ __launch_bounds__(64 * WM * WN * KG) void ml_kernel(const uint8_t *A, const uint8_t *Bw, int nkc, int n_tiles,
+template <int BM, int BN, int WM, int WN, int KG, bool DMA, bool MFMA, int S = 2, bool BPIPE = false, int OCC = 1>
+__global__ __launch_bounds__(64 * WM * WN * KG, OCC) void ml_kernel(const uint8_t *A, const uint8_t *Bw, int nkc, int n_tiles,
                                                              float *sink) {
     constexpr int NW = WM * WN * KG, TM = BM / WM / 16, TN = BN / WN / 16;
     constexpr int APL = BM * 64, BPL = BN * 64, STAGE = 3 * APL + 3 * BPL;
@@ -181,6 +181,29 @@ __global__ __launch_bounds__(64 * WM * WN * KG) void ml_kernel(const uint8_t *A,
 #pragma unroll
         for (int b = 0; b < TN; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
     auto compute = [&](const uint8_t *st) {
+        constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};
+        if constexpr (BPIPE && MFMA) {
+            // B fragments one column tile at a time (two in flight): 24 instead of 12 TN registers
+            bf16x8 af[TM][3], bq[2][3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+#pragma unroll
+                for (int a = 0; a < TM; ++a) af[a][p] = *reinterpret_cast<const bf16x8 *>(st + p * APL + ao[a]);
+                bq[0][p] = *reinterpret_cast<const bf16x8 *>(st + p * BPL + bo[0]);
+            }
+#pragma unroll
+            for (int b = 0; b < TN; ++b) {
+                if (b + 1 < TN)
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) bq[(b + 1) & 1][p] = *reinterpret_cast<const bf16x8 *>(st + p * BPL + bo[b + 1]);
+#pragma unroll
+                for (int t = 0; t < 6; ++t)
+#pragma unroll
+                    for (int a = 0; a < TM; ++a)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][PA[t]], bq[b & 1][PB[t]], acc[a][b], 0, 0, 0);
+            }
+            return;
+        }
         bf16x8 af[TM][3], bfr[TN][3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
@@ -190,7 +213,6 @@ __global__ __launch_bounds__(64 * WM * WN * KG) void ml_kernel(const uint8_t *A,
             for (int b = 0; b < TN; ++b) bfr[b][p] = *reinterpret_cast<const bf16x8 *>(st + p * BPL + bo[b]);
         }
         if constexpr (MFMA) {
-            constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};
 #pragma unroll
             for (int t = 0; t < 6; ++t)
 #pragma unroll
@@ -253,33 +275,63 @@ static void mainloop_lab(int reps) {
     CK(hipMalloc(&B, bbytes));
     CK(hipMemset(B, 0x3c, bbytes));
     CK(hipMalloc(&sink, 4096 * 4));
+    hipStream_t s2[2];
+    CK(hipStreamCreateWithFlags(&s2[0], hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&s2[1], hipStreamNonBlocking));
+    // single: one launch at a time (L2 / MALL state of a rotating A set); pair: two launches in flight on
+    // two streams (does a second workgroup per CU co-reside and overlap?), time per launch
     auto run = [&](const char *name, auto kern, int nthreads) {
+        hipFuncAttributes fa{};
+        CK(hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kern)));
         float us = time_it(reps, [&](int i) {
             hipLaunchKernelGGL(kern, dim3(nblk * NTILES), dim3(nthreads), 0, 0, A[i % NA], B, nkc, NTILES, sink);
         });
-        printf("mainloop %-40s %8.2f us\n", name, us);
+        float usp = 0;
+        {
+            hipEvent_t a, b;
+            CK(hipEventCreate(&a));
+            CK(hipEventCreate(&b));
+            for (int w = 0; w < 2; ++w) {
+                CK(hipDeviceSynchronize());
+                CK(hipEventRecord(a, 0));
+                CK(hipStreamWaitEvent(s2[0], a, 0));
+                CK(hipStreamWaitEvent(s2[1], a, 0));
+                for (int i = 0; i < reps; ++i)
+                    hipLaunchKernelGGL(kern, dim3(nblk * NTILES), dim3(nthreads), 0, s2[i & 1], A[i % NA], B, nkc, NTILES, sink);
+                hipEvent_t e0, e1;
+                CK(hipEventCreate(&e0));
+                CK(hipEventCreate(&e1));
+                CK(hipEventRecord(e0, s2[0]));
+                CK(hipEventRecord(e1, s2[1]));
+                CK(hipStreamWaitEvent(0, e0, 0));
+                CK(hipStreamWaitEvent(0, e1, 0));
+                CK(hipEventRecord(b, 0));
+                CK(hipEventSynchronize(b));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, a, b));
+                usp = ms * 1000.f / reps;
+                CK(hipEventDestroy(e0));
+                CK(hipEventDestroy(e1));
+            }
+            CK(hipEventDestroy(a));
+            CK(hipEventDestroy(b));
+        }
+        printf("mainloop %-40s %8.2f us  two streams %8.2f us/launch  vgpr %d lds %zu\n", name, us, usp, fa.numRegs,
+               fa.sharedSizeBytes);
     };
-    run("2x5 KG1 (current)", ml_kernel<128, 80, 2, 5, 1, true, true>, 640);
-    run("2x5 KG1 no-DMA", ml_kernel<128, 80, 2, 5, 1, false, true>, 640);
-    run("2x5 KG1 no-MFMA", ml_kernel<128, 80, 2, 5, 1, true, false>, 640);
-    run("2x5 KG1 LDS-only", ml_kernel<128, 80, 2, 5, 1, false, false>, 640);
-    run("4x1 KG1", ml_kernel<128, 80, 4, 1, 1, true, true>, 256);
-    run("4x1 KG1 no-DMA", ml_kernel<128, 80, 4, 1, 1, false, true>, 256);
-    run("4x1 KG1 no-MFMA", ml_kernel<128, 80, 4, 1, 1, true, false>, 256);
-    run("4x1 KG2", ml_kernel<128, 80, 4, 1, 2, true, true>, 512);
-    run("4x1 KG2 no-DMA", ml_kernel<128, 80, 4, 1, 2, false, true>, 512);
-    run("8x1 KG1", ml_kernel<128, 80, 8, 1, 1, true, true>, 512);
+    run("8x1 KG1 (current)", ml_kernel<128, 80, 8, 1, 1, true, true>, 512);
     run("8x1 KG1 no-DMA", ml_kernel<128, 80, 8, 1, 1, false, true>, 512);
-    run("2x1 KG2", ml_kernel<128, 80, 2, 1, 2, true, true>, 256);
-    run("4x1 KG1 DMA-only", ml_kernel<128, 80, 4, 1, 1, true, false>, 256);
     run("8x1 KG1 DMA-only", ml_kernel<128, 80, 8, 1, 1, true, false>, 512);
+    run("8x1 KG1 BP", ml_kernel<128, 80, 8, 1, 1, true, true, 2, true>, 512);
+    run("8x1 KG1 BP no-DMA", ml_kernel<128, 80, 8, 1, 1, false, true, 2, true>, 512);
+    run("8x1 KG1 BP occ4", ml_kernel<128, 80, 8, 1, 1, true, true, 2, true, 4>, 512);
+    run("8x1 KG2 (16 waves)", ml_kernel<128, 80, 8, 1, 2, true, true>, 1024);
+    run("8x1 KG2 DMA-only", ml_kernel<128, 80, 8, 1, 2, true, false>, 1024);
+    run("4x1 KG2", ml_kernel<128, 80, 4, 1, 2, true, true>, 512);
+    run("4x1 KG1 BP", ml_kernel<128, 80, 4, 1, 1, true, true, 2, true>, 256);
     run("8x1 S3", ml_kernel<128, 80, 8, 1, 1, true, true, 3>, 512);
-    run("8x1 S3 DMA-only", ml_kernel<128, 80, 8, 1, 1, true, false, 3>, 512);
-    run("8x1 S4 DMA-only", ml_kernel<128, 80, 8, 1, 1, true, false, 4>, 512);
-    run("4x1 S3", ml_kernel<128, 80, 4, 1, 1, true, true, 3>, 256);
-    run("4x1 S3 DMA-only", ml_kernel<128, 80, 4, 1, 1, true, false, 3>, 256);
-    run("2x5 S3", ml_kernel<128, 80, 2, 5, 1, true, true, 3>, 640);
-    run("2x5 S3 DMA-only", ml_kernel<128, 80, 2, 5, 1, true, false, 3>, 640);
+    CK(hipStreamDestroy(s2[0]));
+    CK(hipStreamDestroy(s2[1]));
     for (int i = 0; i < NA; ++i) CK(hipFree(A[i]));
     CK(hipFree(B));
     CK(hipFree(sink));
