@@ -134,11 +134,12 @@ def forward_roofline(graphs, a, t_fwd):
             'note': 'SURVEY 8(d) formulas; combined = max(bytes/8 TB/s, flops/157.3 TF/s) / measured time'}
 
 
-def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_batches=4, streams=1):
+def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_batches=8, streams=1, many=8):
     """Other BASELINE.json configs' shapes (configs[1]: QM9-like molecules, batch 64, depth 3, hidden
     300; configs[3]: ZINC-like molecules, batch 512, depth 5, hidden 512), timed like the headline:
     resident graphs, eval forward, synchronised wall time over ``steps`` forwards, with ``streams``
-    independent batches in flight (as the headline) and with one."""
+    independent batches in flight (as the headline) and with one; and ``many`` batches per call on one
+    stream (MPNEncoder.forward_many: one set of launches for all of them)."""
     enc = make_encoder(TrainArgs(hidden_size=hidden, depth=depth, device=device), device)
     graphs = [BatchMolGraph(synthetic.make_batch(kind, batch, 5000 + i), device_bond_features=True)
               for i in range(n_batches)]
@@ -161,16 +162,33 @@ def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_b
         torch.cuda.synchronize(device)
         return time.perf_counter() - t0
 
+    def timed_many(k):
+        # k batches per call on one stream (wdmpnn_forward_many: one set of launches for the k batches)
+        sets = [[graphs[(i * k + j) % len(graphs)] for j in range(k)] for i in range(len(graphs))]
+        for i in range(warmup):
+            enc.forward_many(sets[i % len(sets)])
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for i in range(steps // k):
+            enc.forward_many(sets[i % len(sets)])
+        torch.cuda.synchronize(device)
+        return time.perf_counter() - t0, sum(g.n_bonds - 1 for i in range(steps // k) for g in sets[i % len(sets)])
+
     with torch.no_grad():
         enc(graphs[0])  # weights packed once, on the default stream
         torch.cuda.synchronize(device)
         dt = timed(len(ss))
         dt1 = timed(1) if len(ss) > 1 else dt
+        dtm, Em = timed_many(many)
     E = sum(graphs[i % len(graphs)].n_bonds - 1 for i in range(steps))
     return {'workload': f'{kind}-like synthetic batches of {batch} molecules, depth {depth}, hidden {hidden}',
             'value': E / dt, 'unit': 'edges/s', 'ms_per_step': dt / steps * 1e3, 'steps': steps,
             'avg_edges': E / steps, 'streams': len(ss),
-            'single_stream': {'value': E / dt1, 'ms_per_step': dt1 / steps * 1e3}}
+            'single_stream': {'value': E / dt1, 'ms_per_step': dt1 / steps * 1e3},
+            'forward_many': {'value': Em / dtm, 'ms_per_step': dtm / (steps // many * many) * 1e3,
+                             'batches_per_call': many,
+                             'note': 'one stream; MPNEncoder.forward_many: embed, layers and W_o + readout '
+                                     'launched once per call for all its batches'}}
 
 
 def training_workload(device, batch=128, steps=100, warmup=10):
@@ -216,30 +234,29 @@ def training_workload(device, batch=128, steps=100, warmup=10):
                                  'fp32 dense MFMA peak (the FFN head, loss and optimizer are not counted)'}}
 
 
-def streamed_workload(device, args, rank, world, graphs_per_rank, batch=64, producers=4, barrier=None):
+def streamed_workload(device, args, rank, world, graphs_per_rank, batch=64, producers=4, barrier=None, k=8):
     """BASELINE.json configs[4]: synthetic polymer graphs streamed per rank (10 M over 8 GPUs = 1.25 M per
     rank by default: weak scaling), generated on the fly by native producer threads, staged in compact
-    form (~14 B per edge), uploaded and expanded on the GPU (wdmpnn_build_graph) while the previous batch
-    is encoded (chemprop_amd.stream).  Everything is inside the timed region: generation, block plan,
-    H2D, device graph build and the B=64 forward.  Disjoint seeds per rank, no collective on the data
-    path; value = edges of all ranks / max-over-ranks time."""
-    from chemprop_amd.stream import StreamedBatches
+    form (~14 B per edge), uploaded and expanded on the GPU by the native feed thread (wdmpnn_feed_*,
+    chemprop_amd.stream.NativeFeed) while earlier batches are encoded, k batches per launch set
+    (wdmpnn_feed_forward).  Everything is inside the timed region: generation, block plan, H2D, device
+    graph build and the B=64 forwards.  Disjoint seeds per rank, no collective on the data path; value =
+    edges of all ranks / max-over-ranks time."""
+    from chemprop_amd.stream import NativeFeed
     enc = make_encoder(args, device)
     n = -(-graphs_per_rank // batch)
-    warm = 32
     with torch.no_grad():
-        for g in StreamedBatches('polymer', batch, warm, seed=99, device=device, rank=rank, producers=producers,
-                                 lean=True):
-            enc(g)
+        for _ in NativeFeed('polymer', batch, 4 * k, seed=99, device=device, rank=rank, producers=producers,
+                            lean=True).encode(enc, k):
+            pass
         barrier()
         t0 = time.perf_counter()
-        edges = 0
-        h2d = 0
-        for g in StreamedBatches('polymer', batch, n, seed=2024, device=device, rank=rank, producers=producers,
-                                 lean=True):
-            enc(g)
-            edges += g.n_bonds - 1
-            h2d += g.device_graph(device, False, get_bond_fdim()).h2d_bytes
+        edges = h2d = 0
+        feed = NativeFeed('polymer', batch, n, seed=2024, device=device, rank=rank, producers=producers, lean=True,
+                          slots=4 * k)
+        for out, got, e, up in feed.encode(enc, k):
+            edges += e
+            h2d += up
         barrier()
         dt = time.perf_counter() - t0
     return dt, edges, n * batch, h2d
@@ -247,11 +264,12 @@ def streamed_workload(device, args, rank, world, graphs_per_rank, batch=64, prod
 
 def streamed_training(device, rank, world, graphs_per_rank, batch=128, producers=4, barrier=None):
     """configs[4] as data-parallel training: each rank trains MoleculeModel (depth 3, hidden 300, one
-    regression task, Adam) on its own streamed batches of ``batch`` graphs; one flat fp32 gradient
-    all-reduce per step (chemprop_amd.dp.GradBucket: RCCL over xGMI when world > 1)."""
+    regression task, Adam) on its own streamed batches of ``batch`` graphs (native feed: generation,
+    upload and device graph build off the training thread); one flat fp32 gradient all-reduce per step
+    (chemprop_amd.dp.GradBucket: RCCL over xGMI when world > 1)."""
     from chemprop_amd.dp import GradBucket, broadcast_parameters
     from chemprop_amd.model import MoleculeModel
-    from chemprop_amd.stream import StreamedBatches
+    from chemprop_amd.stream import NativeFeed
     from chemprop_amd.train import build_optimizer, get_loss_func, train_step
     args = TrainArgs(hidden_size=300, depth=3, device=device)
     torch.manual_seed(0)
@@ -265,13 +283,13 @@ def streamed_training(device, rank, world, graphs_per_rank, batch=128, producers
     gen = torch.Generator().manual_seed(rank)
     targets = [torch.randn(batch, 1, generator=gen).tolist() for _ in range(8)]
     steps = -(-graphs_per_rank // batch)
-    for i, g in enumerate(StreamedBatches('polymer', batch, 10, seed=77, device=device, rank=rank, producers=producers)):
+    for i, g in enumerate(NativeFeed('polymer', batch, 10, seed=77, device=device, rank=rank, producers=producers)):
         train_step(model, [g], targets[i % 8], loss_func, opt, bucket=bucket)
     barrier()
     t0 = time.perf_counter()
     edges = 0
-    for i, g in enumerate(StreamedBatches('polymer', batch, steps, seed=4048, device=device, rank=rank,
-                                          producers=producers)):
+    for i, g in enumerate(NativeFeed('polymer', batch, steps, seed=4048, device=device, rank=rank,
+                                     producers=producers)):
         train_step(model, [g], targets[i % 8], loss_func, opt, bucket=bucket)
         edges += g.n_bonds - 1
     barrier()
@@ -323,6 +341,7 @@ def main():
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--no-secondary', action='store_true', help='skip the QM9 / ZINC-shaped secondary workloads')
     ap.add_argument('--streams', type=int, default=2, help='batches in flight per GPU (one HIP stream each)')
+    ap.add_argument('--many', type=int, default=4, help='batches per MPNEncoder.forward_many call (0 = skip)')
     ap.add_argument('--variant', type=int, default=0, help='WdConfig.gemm_variant (0 = default path; 9 = f32 MFMA)')
     ap.add_argument('--stream-graphs', type=int, default=10_000_000 // 8,
                     help='configs[4]: polymer graphs streamed per rank (default 10 M / 8 GPUs); 0 = skip')
@@ -392,6 +411,21 @@ def main():
             barrier()
             single = time.perf_counter() - t2
 
+        # the same K steps as MPNEncoder.forward_many calls of a.many batches on one stream (one set of
+        # launches per call; the batches' tiles share one grid)
+        many_dt = None
+        if a.many > 1 and a.steps >= a.many:
+            sets = [[graphs[(i * a.many + j) % len(graphs)] for j in range(a.many)] for i in range(len(graphs))]
+            for i in range(2):
+                enc.forward_many(sets[i % len(sets)])
+            barrier()
+            t3 = time.perf_counter()
+            for i in range(a.steps // a.many):
+                enc.forward_many(sets[i % len(sets)])
+            barrier()
+            many_dt = time.perf_counter() - t3
+            many_edges = sum(g.n_bonds - 1 for i in range(a.steps // a.many) for g in sets[i % len(sets)])
+
         # second pass: HIP events around the dominant launches (the message-passing layers) on the
         # stream they run on
         L = _native.lib()
@@ -426,8 +460,10 @@ def main():
         tr_dt, tr_edges, tr_steps = streamed_training(device, rank, world, a.stream_train_graphs,
                                                       producers=a.producers, barrier=barrier)
 
-    t = torch.tensor([elapsed, elapsed_prof, single or 0.0, st_dt, tr_dt], dtype=torch.float64, device=device)
-    e = torch.tensor([my_edges, st_edges, st_graphs, st_h2d, tr_edges], dtype=torch.float64, device=device)
+    t = torch.tensor([elapsed, elapsed_prof, single or 0.0, st_dt, tr_dt, many_dt or 0.0], dtype=torch.float64,
+                     device=device)
+    e = torch.tensor([my_edges, st_edges, st_graphs, st_h2d, tr_edges, many_edges if many_dt else 0.0],
+                     dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(e, op=dist.ReduceOp.SUM)
@@ -436,6 +472,7 @@ def main():
     total_edges = float(e[0])
     st_dt, tr_dt = float(t[3]), float(t[4])
     st_edges, st_graphs, st_h2d, tr_edges = float(e[1]), float(e[2]), float(e[3]), float(e[4])
+    many_dt, many_edges = (float(t[5]), float(e[5])) if many_dt else (None, 0.0)
 
     if rank == 0:
         H = a.hidden
@@ -478,6 +515,11 @@ def main():
             'single_stream': ({'value': total_edges / single, 'ms_per_step': single / a.steps * 1e3,
                                'note': 'same steps, one batch in flight (each forward waits for the previous)'}
                               if single else None),
+            'forward_many': ({'value': many_edges / many_dt, 'ms_per_step': many_dt / (a.steps // a.many * a.many) * 1e3,
+                              'batches_per_call': a.many,
+                              'note': 'one stream, MPNEncoder.forward_many (wdmpnn_forward_many): the batches of a '
+                                      'call share one grid per kernel; every batch a full B=64 forward'}
+                             if many_dt else None),
             'roofline': {'bound': 'mfma',
                          'kernel': 'mp_layer_kernel: one message-passing layer, W_h split-plane GEMM + in-block CSR '
                                    'gather + residual/activation (mpn.py:110-124)',

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define WDMPNN_ABI_VERSION 6
+#define WDMPNN_ABI_VERSION 7
 #define WDMPNN_ELL_WIDTH 8
 
 enum WdActivation {     /* nn_utils.py:70-99 get_activation_function */
@@ -205,6 +205,18 @@ int wdmpnn_backward_workspace_bytes(const WdGraph *g, const WdParams *p, const W
 int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c,
                    void *workspace, size_t workspace_bytes, float *out, void *stream);
 
+/* Several independent batches through the fused inference forward in one set of launches: the embed,
+ * the depth - 1 message-passing layers and W_o + readout each run ONCE for up to 8 batches (their tiles
+ * concatenated in one grid), instead of once per batch.  Replaces a loop of MPNEncoder.forward calls
+ * over batches (the caller of chemprop/train/predict.py:30-40 issues one forward per batch) for batches
+ * that are ready together; batch j's output equals wdmpnn_forward(graphs[j], ...) bitwise.
+ * graphs[j]: each a molecule-blocked graph (WdGraph.blocks; compact-code or host-built), same feature
+ * sizes; p->packed must hold the packed parameters (wdmpnn_pack_params); c->save_for_backward = 0;
+ * workspaces[j] of wdmpnn_workspace_bytes(graphs[j], ...) bytes; outs[j] [n_mols_j, H].  Any n >= 0
+ * (chunks of 8 per launch set). */
+int wdmpnn_forward_many(int32_t n, const WdGraph *graphs, const WdParams *p, const WdConfig *c,
+                        void *const *workspaces, const size_t *workspace_bytes, float *const *outs, void *stream);
+
 /* Gradient of MPNEncoder.forward w.r.t. its parameters, given dout [n_mols, H (+desc_dim)] and the
  * workspace of a forward run with save_for_backward = 1 and identical g/p/c. */
 int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c,
@@ -349,6 +361,53 @@ int wdmpnn_head_mse(const WdHead *h, void *stream);
 /* p_i[0 .. n_i) *= *s (device scalar) for k <= 8 buffers: the head's gradients times the loss's
  * incoming gradient in one launch. */
 int wdmpnn_scale(float *const *p, const int64_t *n, int32_t k, const float *s, void *stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Native streamed batches (BASELINE.json configs[4]: millions of synthetic polymer graphs per rank,
+ * never materialised).  Replaces chemprop's DataLoader + construct_molecule_batch + BatchMolGraph
+ * (data.py:594-607, featurization.py:757-813) for the synthetic stream, and the per-batch
+ * MPNEncoder.forward host work (mpn.py:77-90): generator threads stage compact batches into pinned
+ * slots, a feed thread uploads them and builds each device graph (wdmpnn_build_graph_ex) on its own
+ * stream, the caller's stream only waits on each graph's ready event.  Batch i is generated from
+ * seed + i (mix the rank into the seed for disjoint shards) and handed out in order.
+ * ------------------------------------------------------------------------------------------------ */
+typedef struct WdFeedSpec {
+    int32_t kind;           /* synthetic generator: 0 polymer, 1 QM9-like, 2 ZINC-like */
+    int32_t batch;          /* graphs per batch */
+    int64_t n_batches;
+    uint64_t seed;          /* batch i: seed + i */
+    int32_t producers;      /* generator threads (>= 1) */
+    int32_t slots;          /* batches in flight: host and device slots (>= 2) */
+    int32_t target_blocks;  /* molecule-block plan target (>= 1) */
+    int32_t flags;          /* WDMPNN_GRAPH_LEAN: inference-only device graphs */
+    int32_t atom_fdim, bond_fdim;
+    void *pinned;           /* caller-owned pinned host memory: slots x host slot bytes */
+    void *device;           /* caller-owned device memory: slots x device slot bytes, 256-byte aligned */
+} WdFeedSpec;
+typedef struct WdFeedBatch {
+    int64_t index;
+    int32_t n_mols, n_atoms, n_bonds, n_blocks, nnz_msg, reserved;
+    size_t h2d_bytes;       /* the staged image uploaded for this batch */
+} WdFeedBatch;
+int wdmpnn_feed_slot_bytes(int32_t kind, int32_t batch, int32_t atom_fdim, int32_t bond_fdim, size_t *host_bytes,
+                           size_t *device_bytes);
+int wdmpnn_feed_create(const WdFeedSpec *spec, void **feed);
+/* The next batch: blocks until its graph has been enqueued, makes `stream` wait for it on the GPU and
+ * returns its WdGraph (device pointers into the feed's slot, valid until released).  Returns 1 when the
+ * stream is exhausted, 0 on success, < 0 on error (a producer's error included). */
+int wdmpnn_feed_next(void *feed, void *stream, WdGraph *g, WdFeedBatch *info);
+/* Every batch handed out so far is finished when `stream` reaches this point: their slots are reused
+ * after it (the feed stream waits on the GPU; the host does not block). */
+int wdmpnn_feed_release(void *feed, void *stream);
+/* Workspace of wdmpnn_feed_forward for up to k batches of this feed. */
+int wdmpnn_feed_forward_workspace_bytes(void *feed, const WdParams *p, const WdConfig *c, int32_t k, size_t *bytes);
+/* Up to k next batches through the fused inference forward in one launch set (wdmpnn_forward_many),
+ * then released: outputs [sum n_mols, H] into out (out_rows available), *got batches (0 = exhausted),
+ * *rows output rows, *edges directed real edges, *h2d_bytes bytes uploaded for them. */
+int wdmpnn_feed_forward(void *feed, int32_t k, const WdParams *p, const WdConfig *c, void *workspace,
+                        size_t workspace_bytes, float *out, int64_t out_rows, void *stream, int32_t *got,
+                        int64_t *rows, int64_t *edges, int64_t *h2d_bytes);
+int wdmpnn_feed_destroy(void *feed);
 
 #ifdef __cplusplus
 }

@@ -21,8 +21,9 @@ LIB_PATH = os.environ.get('WDMPNN_LIB', os.path.join(HERE, 'libwdmpnn.so'))
 ACTIVATIONS = {'ReLU': 0, 'LeakyReLU': 1, 'PReLU': 2, 'tanh': 3, 'SELU': 4, 'ELU': 5}
 ACT_IDENTITY = 6
 AGGREGATIONS = {'mean': 0, 'sum': 1, 'norm': 2}
-ABI_VERSION = 6
+ABI_VERSION = 7
 GRAPH_LEAN = 1  # WDMPNN_GRAPH_LEAN
+ERR_UNSUPPORTED = -1003  # WD_ERR_UNSUPPORTED
 
 EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace_bytes',
                     'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
@@ -30,7 +31,10 @@ EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace
                     'wdmpnn_event_pool_elapsed_ms', 'wdmpnn_packed_params_bytes', 'wdmpnn_pack_params',
                     'wdmpnn_plane_bytes', 'wdmpnn_split_planes', 'wdmpnn_split_planes_rows',
                     'wdmpnn_build_bond_features', 'wdmpnn_index_select_rows_backward',
-                    'wdmpnn_saved_layout', 'wdmpnn_graph_bytes', 'wdmpnn_build_graph', 'wdmpnn_adam_step', 'wdmpnn_head_mse', 'wdmpnn_scale', 'wdmpnn_build_graph_ex')
+                    'wdmpnn_saved_layout', 'wdmpnn_graph_bytes', 'wdmpnn_build_graph', 'wdmpnn_adam_step', 'wdmpnn_head_mse', 'wdmpnn_scale', 'wdmpnn_build_graph_ex',
+                    'wdmpnn_forward_many', 'wdmpnn_feed_slot_bytes', 'wdmpnn_feed_create', 'wdmpnn_feed_next',
+                    'wdmpnn_feed_release', 'wdmpnn_feed_forward_workspace_bytes', 'wdmpnn_feed_forward',
+                    'wdmpnn_feed_destroy')
 
 
 class WdCsr(Structure):
@@ -70,6 +74,17 @@ class WdCompact(Structure):
                 ('atom_fdim', c_int32), ('bond_fdim', c_int32), ('nnz_msg', c_int32), ('nnz_agg', c_int32),
                 ('mols', c_void_p), ('xn', c_void_p), ('atoms', c_void_p), ('pairs', c_void_p), ('blocks', c_void_p),
                 ('block_nnz', c_void_p)]
+
+
+class WdFeedSpec(Structure):
+    _fields_ = [('kind', c_int32), ('batch', c_int32), ('n_batches', c_int64), ('seed', c_uint64),
+                ('producers', c_int32), ('slots', c_int32), ('target_blocks', c_int32), ('flags', c_int32),
+                ('atom_fdim', c_int32), ('bond_fdim', c_int32), ('pinned', c_void_p), ('device', c_void_p)]
+
+
+class WdFeedBatch(Structure):
+    _fields_ = [('index', c_int64), ('n_mols', c_int32), ('n_atoms', c_int32), ('n_bonds', c_int32),
+                ('n_blocks', c_int32), ('nnz_msg', c_int32), ('reserved', c_int32), ('h2d_bytes', c_size_t)]
 
 
 class WdSaved(Structure):
@@ -142,6 +157,23 @@ def lib() -> ctypes.CDLL:
                                              c_int32, c_void_p, c_int32, c_void_p]
     L.wdmpnn_build_graph_ex.argtypes = [POINTER(WdCompact), c_void_p, c_size_t, POINTER(WdGraph), c_int32, c_void_p]
     L.wdmpnn_head_mse.argtypes = [POINTER(WdHead), c_void_p]
+    # (an experiment library of an older ABI, WDMPNN_LIB, may lack the newest entry points)
+    newest = hasattr(L, 'wdmpnn_forward_many')
+    if newest:
+        L.wdmpnn_forward_many.argtypes = [c_int32, POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig),
+                                          POINTER(c_void_p), POINTER(c_size_t), POINTER(c_void_p), c_void_p]
+    feed = hasattr(L, 'wdmpnn_feed_create')
+    if feed:
+        L.wdmpnn_feed_slot_bytes.argtypes = [c_int32, c_int32, c_int32, c_int32, POINTER(c_size_t), POINTER(c_size_t)]
+        L.wdmpnn_feed_create.argtypes = [POINTER(WdFeedSpec), POINTER(c_void_p)]
+        L.wdmpnn_feed_next.argtypes = [c_void_p, c_void_p, POINTER(WdGraph), POINTER(WdFeedBatch)]
+        L.wdmpnn_feed_release.argtypes = [c_void_p, c_void_p]
+        L.wdmpnn_feed_forward_workspace_bytes.argtypes = [c_void_p, POINTER(WdParams), POINTER(WdConfig), c_int32,
+                                                          POINTER(c_size_t)]
+        L.wdmpnn_feed_forward.argtypes = [c_void_p, c_int32, POINTER(WdParams), POINTER(WdConfig), c_void_p, c_size_t,
+                                          c_void_p, c_int64, c_void_p, POINTER(c_int32), POINTER(c_int64),
+                                          POINTER(c_int64), POINTER(c_int64)]
+        L.wdmpnn_feed_destroy.argtypes = [c_void_p]
     L.wdmpnn_scale.argtypes = [POINTER(c_void_p), POINTER(c_int64), c_int32, c_void_p, c_void_p]
     L.wdmpnn_adam_step.argtypes = [POINTER(WdAdamTensor), c_int32, POINTER(WdAdamHyper), c_void_p]
     L.wdmpnn_event_pool_create.argtypes = [c_int32, POINTER(c_void_p)]
@@ -150,10 +182,13 @@ def lib() -> ctypes.CDLL:
     for fn in ('wdmpnn_packed_params_bytes', 'wdmpnn_pack_params', 'wdmpnn_event_pool_create', 'wdmpnn_event_pool_destroy', 'wdmpnn_event_pool_elapsed_ms',
                'wdmpnn_workspace_bytes', 'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
                'wdmpnn_index_select_rows', 'wdmpnn_plane_bytes', 'wdmpnn_split_planes', 'wdmpnn_split_planes_rows',
-               'wdmpnn_build_bond_features', 'wdmpnn_adam_step', 'wdmpnn_head_mse', 'wdmpnn_scale', 'wdmpnn_build_graph_ex'):
+               'wdmpnn_build_bond_features', 'wdmpnn_adam_step', 'wdmpnn_head_mse', 'wdmpnn_scale', 'wdmpnn_build_graph_ex') + \
+            (('wdmpnn_forward_many',) if newest else ()) + \
+            (('wdmpnn_feed_slot_bytes', 'wdmpnn_feed_create', 'wdmpnn_feed_next', 'wdmpnn_feed_release',
+              'wdmpnn_feed_forward_workspace_bytes', 'wdmpnn_feed_forward', 'wdmpnn_feed_destroy') if feed else ()):
         getattr(L, fn).restype = c_int
     v = L.wdmpnn_abi_version()
-    if v != ABI_VERSION:
+    if v != ABI_VERSION and not ('WDMPNN_LIB' in os.environ and v == 6):
         raise NativeError(f'libwdmpnn ABI {v} != expected {ABI_VERSION}; rebuild the library')
     _LIB = L
     return L

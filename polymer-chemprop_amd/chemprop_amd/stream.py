@@ -21,6 +21,7 @@ form (include/wdmpnn.h "Compact graphs": ~14 bytes per directed edge) and expand
 """
 from __future__ import annotations
 
+import ctypes
 import threading
 from typing import Iterator, Optional
 
@@ -145,3 +146,135 @@ def _device_batch(dg, info, arrays) -> BatchMolGraph:
     g._device_cache[(dev, False, None)] = dg
     g._device_cache[(dev, False, 147)] = dg
     return g
+
+
+class _FeedGraph:
+    """DeviceGraph of a batch handed out by a NativeFeed: device memory owned by the feed's slot (valid
+    until the feed reuses the slot, after the consumer's release), already waited for on ``home``."""
+
+    def __init__(self, struct, info, device, home):
+        self.struct = struct
+        self.device = device
+        self.buffer = None
+        self.views = {}
+        self.encoder_structs = {}
+        self.encoder_plans = {}
+        self.home_stream = home
+        self._streams = {home}
+        self._ready = None
+        self.n_edges = info.n_bonds - 1
+        self.h2d_bytes = int(info.h2d_bytes)
+        self.nnz_msg = info.nnz_msg
+        self.built_on_device = True
+        self.lean = False
+        self.index = info.index
+
+    def use_on(self, stream) -> None:
+        sid = stream.cuda_stream
+        if sid in self._streams:
+            return
+        if self._ready is None:  # order the other stream after the home stream's wait on the build
+            self._ready = torch.cuda.Event()
+            self._ready.record(torch.cuda.ExternalStream(self.home_stream, device=self.device))
+        stream.wait_event(self._ready)
+        self._streams.add(sid)
+
+
+class NativeFeed:
+    """Streamed synthetic batches produced natively (``wdmpnn_feed_*``, csrc/feed.hpp): ``producers``
+    generator threads stage compact batches into pinned slots, a feed thread uploads each one and builds
+    its device graph on its own HIP stream; this object only hands out finished graphs (no Python in the
+    data path, no GIL held by the pipeline).  Batch i of rank r is generated from
+    ``seed + (r << 32) + i``, like :class:`StreamedBatches`, whose order and content it reproduces.
+
+    * iteration yields device-resident ``BatchMolGraph`` objects in order; the batch handed out last is
+      released (its slot may be reused) when the next one is requested, after the work enqueued for it on
+      the current stream;
+    * :meth:`encode` runs the whole stream through an encoder's fused inference forward, ``k`` batches
+      per launch set (``wdmpnn_feed_forward``)."""
+
+    def __init__(self, kind: str, batch_size: int, n_batches: int, seed: int, device, rank: int = 0,
+                 producers: int = 4, slots: Optional[int] = None, lean: bool = False,
+                 target_blocks: int = BLK_TARGET, atom_fdim: int = 133, bond_fdim: int = 147):
+        from . import _native
+        if kind not in KINDS:
+            raise ValueError(f'unknown kind {kind!r}')
+        self.L = L = _native.lib()
+        self.device = torch.device(device)
+        self.kind, self.B, self.n = kind, int(batch_size), int(n_batches)
+        self.R = max(int(slots or 0), max(1, int(producers)) + 2, 4)
+        hb, db = ctypes.c_size_t(), ctypes.c_size_t()
+        _native.check(L.wdmpnn_feed_slot_bytes(KINDS[kind], self.B, atom_fdim, bond_fdim, ctypes.byref(hb),
+                                               ctypes.byref(db)), 'feed slot bytes')
+        self.pinned = torch.empty(self.R * hb.value, dtype=torch.uint8, pin_memory=True)
+        self.arena = torch.empty(self.R * db.value + 256, dtype=torch.uint8, device=self.device)
+        base = (self.arena.data_ptr() + 255) & ~255
+        spec = _native.WdFeedSpec()
+        spec.kind, spec.batch, spec.n_batches = KINDS[kind], self.B, self.n
+        spec.seed = (int(seed) + (int(rank) << 32)) & 0xFFFFFFFFFFFFFFFF
+        spec.producers, spec.slots, spec.target_blocks = max(1, int(producers)), self.R, int(target_blocks)
+        spec.flags = _native.GRAPH_LEAN if lean else 0
+        spec.atom_fdim, spec.bond_fdim = atom_fdim, bond_fdim
+        spec.pinned, spec.device = self.pinned.data_ptr(), base
+        self.lean = bool(lean)
+        self.fdims = (atom_fdim, bond_fdim)
+        self.handle = ctypes.c_void_p()
+        _native.check(L.wdmpnn_feed_create(ctypes.byref(spec), ctypes.byref(self.handle)), 'feed create')
+        self._native = _native
+
+    def __iter__(self) -> Iterator[BatchMolGraph]:
+        L, check = self.L, self._native.check
+        try:
+            while True:
+                stream = torch.cuda.current_stream(self.device)
+                check(L.wdmpnn_feed_release(self.handle, stream.cuda_stream), 'feed release')
+                g = self._native.WdGraph()
+                info = self._native.WdFeedBatch()
+                rc = L.wdmpnn_feed_next(self.handle, stream.cuda_stream, ctypes.byref(g), ctypes.byref(info))
+                if rc == 1:
+                    return
+                check(rc, 'feed next')
+                dg = _FeedGraph(g, info, self.device, stream.cuda_stream)
+                dg.lean = self.lean
+                yield _device_batch(dg, ((True,), (info.n_mols, info.n_atoms, info.n_bonds)), None)
+        finally:
+            self.close()
+
+    def encode(self, enc, k: int = 8):
+        """Run every remaining batch through ``enc``'s fused inference forward, k batches per launch set.
+        Yields (out [rows, H] tensor, batches, directed edges, H2D bytes) per call."""
+        nat = self._native
+        L = self.L
+        params = enc._param_tuple()
+        stream = torch.cuda.current_stream(self.device)
+        cfg = enc._config(False)
+        dummy = nat.WdGraph()  # sizes only: the packed-parameter layout depends on the feature widths
+        dummy.n_atoms = dummy.n_bonds = 1
+        dummy.atom_fdim, dummy.bond_fdim = self.fdims
+        dummy.ld_atoms = dummy.ld_bonds = -(-max(self.fdims) // 32) * 32
+        dummy.f_atoms = dummy.f_bonds = self.arena.data_ptr() & ~255
+        pstruct, _ = enc._packed_params(dummy, cfg, tuple(t for t in params), self.device, stream=stream)
+        wsb = ctypes.c_size_t()
+        nat.check(L.wdmpnn_feed_forward_workspace_bytes(self.handle, ctypes.byref(pstruct), ctypes.byref(cfg), k,
+                                                        ctypes.byref(wsb)), 'feed workspace')
+        H = enc.hidden_size
+        got, rows, edges, h2d = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        try:
+            while True:
+                ws = torch.empty(wsb.value, dtype=torch.uint8, device=self.device)
+                out = torch.empty((k * self.B, H), dtype=torch.float32, device=self.device)
+                nat.check(L.wdmpnn_feed_forward(self.handle, k, ctypes.byref(pstruct), ctypes.byref(cfg), ws.data_ptr(),
+                                                wsb.value, out.data_ptr(), k * self.B, stream.cuda_stream,
+                                                ctypes.byref(got), ctypes.byref(rows), ctypes.byref(edges),
+                                                ctypes.byref(h2d)), 'feed forward')
+                if got.value == 0:
+                    return
+                yield out[:rows.value], got.value, edges.value, h2d.value
+        finally:
+            self.close()
+
+    def close(self) -> None:
+        if self.handle:
+            torch.cuda.current_stream(self.device).synchronize()  # the slots' last readers
+            self.L.wdmpnn_feed_destroy(self.handle)
+            self.handle = ctypes.c_void_p()

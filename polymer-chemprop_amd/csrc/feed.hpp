@@ -1,0 +1,176 @@
+// feed.hpp — native streamed batches (BASELINE.json configs[4]: millions of synthetic polymer graphs per
+// rank, never materialised).  Host-side engine behind wdmpnn_feed_* (include/wdmpnn.h):
+//
+//   producer threads            feed thread (its own HIP stream)             consumer (caller's stream)
+//   generate + plan + stage  -> H2D of the staged image + graph build  ->  wait on the graph's ready
+//   into pinned slot i % R      into device slot i % R, ready event          event, encode, release
+//
+// Batch i is generated from seed + i (the caller mixes the rank into the seed: disjoint shards), goes
+// through host slot i % R and device slot i % R, and is handed out in order.  A host slot is rewritten
+// only after the H2D that read it has completed (its copy event, waited on by the producer); a device
+// slot only after the consumer's work on its previous batch (the release event, waited on by the feed
+// stream on the GPU: the host never blocks on the consumer's kernels).  No Python, no GIL: the caller's
+// thread only takes finished graphs.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "compact.hpp"
+#include "wdmpnn.h"
+
+namespace wd {
+
+// upper bounds of one batch of `batch` generated graphs of `kind` (compact::generate)
+struct FeedBounds { int atoms_per_mol, pairs_per_mol; };
+inline FeedBounds feed_bounds(int kind) {
+    // skeleton: n - 1 chain bonds + n / 5 ring closures; polymer: two monomers of <= 24 atoms + 10 rules
+    if (kind == 0) return {48, 47 + 9 + 10};
+    if (kind == 1) return {9, 8 + 1};
+    return {37, 36 + 7};
+}
+inline size_t feed_host_bytes(int kind, int batch) {
+    const FeedBounds f = feed_bounds(kind);
+    const size_t V = (size_t)batch * f.atoms_per_mol + 1, P = (size_t)batch * f.pairs_per_mol;
+    // mols [B][4] int32 + xn [B] + atoms + pairs + blocks [<= B][8] + block_nnz [<= B][2], 256-aligned each
+    return 16 * (size_t)batch + 4 * (size_t)batch + sizeof(WdAtomCode) * V + sizeof(WdBondPair) * P +
+           32 * (size_t)batch + 8 * (size_t)batch + 7 * 256;
+}
+constexpr int FEED_MAX_DEG = 24;  // bound of the mean in-degree used to size a slot's gather lists
+
+struct Feed {
+    WdFeedSpec spec{};
+    hipStream_t fs = nullptr;
+    int R = 0;
+    size_t host_bytes = 0, dev_bytes = 0, graph_off = 0;
+    struct Slot {
+        int64_t turn = 0;       // producer: the batch allowed to write this host slot next
+        int64_t staged = -1;    // batch staged in the host slot
+        int counts[6] = {};     // n_mols, n_atoms, n_bonds, n_blocks, nnz_msg, nnz_agg
+        size_t off[6] = {}, total = 0;
+        bool copy_pending = false;
+        int64_t built = -1;     // batch whose device graph is enqueued (ready event recorded)
+        WdGraph g{};
+        hipEvent_t copy_done = nullptr, ready = nullptr, released = nullptr;
+    };
+    std::vector<Slot> slot;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<std::thread> threads;
+    int64_t handed = 0;         // consumer: batches handed out
+    int64_t released_upto = 0;  // batches [0, released_upto) released (their release events recorded)
+    bool stop = false;
+    std::string error;
+
+    uint8_t *host(int s) const { return (uint8_t *)spec.pinned + (size_t)s * host_bytes; }
+    uint8_t *dev(int s) const { return (uint8_t *)spec.device + (size_t)s * dev_bytes; }
+
+    void fail_locked(const std::string &e) {
+        if (error.empty()) error = e;
+        stop = true;
+        cv.notify_all();
+    }
+
+    void producer(int t) {
+        try {
+            for (int64_t i = t; i < spec.n_batches; i += spec.producers) {
+                const int s = (int)(i % R);
+                Slot &S = slot[(size_t)s];
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return stop || S.turn == i; });
+                    if (stop) return;
+                }
+                if (S.copy_pending && hipEventSynchronize(S.copy_done) != hipSuccess) throw std::runtime_error("copy event");
+                compact::Batch c;
+                compact::Plan p;
+                compact::generate(spec.kind, spec.batch, spec.seed + (uint64_t)i, c);
+                c.fa = spec.atom_fdim;
+                c.fb = spec.bond_fdim;
+                if (!compact::plan(c, spec.target_blocks, p)) throw std::runtime_error("generated molecule exceeds a block");
+                const compact::Staged st = compact::stage_layout(c, p);
+                if (st.total > host_bytes) throw std::runtime_error("staged batch larger than its slot");
+                compact::stage_copy(c, p, st, host(s));
+                std::lock_guard<std::mutex> lk(mu);
+                const int cnt[6] = {c.n_mols(), c.n_atoms(), c.n_bonds(), p.n_blocks(), (int)p.nnz_msg, (int)p.nnz_agg};
+                std::copy(cnt, cnt + 6, S.counts);
+                std::copy(st.off, st.off + 6, S.off);
+                S.total = st.total;
+                S.staged = i;
+                cv.notify_all();
+            }
+        } catch (const std::exception &e) {
+            std::lock_guard<std::mutex> lk(mu);
+            fail_locked(std::string("feed producer: ") + e.what());
+        }
+    }
+
+    // (build: wdmpnn_build_graph_ex on the feed stream)
+    void feeder() {
+        try {
+            for (int64_t i = 0; i < spec.n_batches; ++i) {
+                const int s = (int)(i % R);
+                Slot &S = slot[(size_t)s];
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    // staged, and the device slot's previous batch released by the consumer
+                    cv.wait(lk, [&] { return stop || (S.staged == i && released_upto >= i - R + 1); });
+                    if (stop) return;
+                }
+                if (i >= R && hipStreamWaitEvent(fs, S.released, 0) != hipSuccess) throw std::runtime_error("release wait");
+                if (hipMemcpyAsync(dev(s), host(s), S.total, hipMemcpyHostToDevice, fs) != hipSuccess ||
+                    hipEventRecord(S.copy_done, fs) != hipSuccess)
+                    throw std::runtime_error("H2D");
+                WdCompact c{};
+                c.n_mols = S.counts[0]; c.n_atoms = S.counts[1]; c.n_bonds = S.counts[2]; c.n_blocks = S.counts[3];
+                c.atom_fdim = spec.atom_fdim; c.bond_fdim = spec.bond_fdim;
+                c.nnz_msg = S.counts[4]; c.nnz_agg = S.counts[5];
+                uint8_t *d = dev(s);
+                c.mols = (const int32_t *)(d + S.off[0]); c.xn = (const float *)(d + S.off[1]);
+                c.atoms = (const WdAtomCode *)(d + S.off[2]); c.pairs = (const WdBondPair *)(d + S.off[3]);
+                c.blocks = (const int32_t *)(d + S.off[4]); c.block_nnz = (const int32_t *)(d + S.off[5]);
+                WdGraph g{};
+                if (wdmpnn_build_graph_ex(&c, d + graph_off, dev_bytes - graph_off, &g, spec.flags, fs) != 0)
+                    throw std::runtime_error(std::string("graph build: ") + wdmpnn_last_error());
+                if (hipEventRecord(S.ready, fs) != hipSuccess) throw std::runtime_error("ready event");
+                std::lock_guard<std::mutex> lk(mu);
+                S.copy_pending = true;
+                S.turn = i + R;  // the producer of batch i + R waits for copy_done itself
+                S.g = g;
+                S.built = i;
+                cv.notify_all();
+            }
+        } catch (const std::exception &e) {
+            std::lock_guard<std::mutex> lk(mu);
+            fail_locked(std::string("feed: ") + e.what());
+        }
+    }
+
+    void shutdown() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+            cv.notify_all();
+        }
+        for (auto &t : threads)
+            if (t.joinable()) t.join();
+        threads.clear();
+        if (fs) (void)hipStreamSynchronize(fs);
+    }
+
+    ~Feed() {
+        shutdown();
+        for (auto &S : slot) {
+            if (S.copy_done) (void)hipEventDestroy(S.copy_done);
+            if (S.ready) (void)hipEventDestroy(S.ready);
+            if (S.released) (void)hipEventDestroy(S.released);
+        }
+        if (fs) (void)hipStreamDestroy(fs);
+    }
+};
+
+}  // namespace wd

@@ -67,6 +67,23 @@ __device__ __forceinline__ BlockRow load_block(const int32_t *blocks, int i) {
     return BlockRow{a.x, a.y, a.z, a.w, b.x, b.y};
 }
 
+// Several independent batches in one launch (wdmpnn_forward_many): per batch its parameter struct and
+// its first tile in the grid; a workgroup finds its batch by a short uniform scan (the structs stay in
+// the kernel-argument segment: scalar loads).  One batch: n = 1.
+constexpr int WD_MULTI = 8;
+template <typename T> struct Multi {
+    T p[WD_MULTI];
+    int t0[WD_MULTI + 1];  // tile ranges: batch j owns grid tiles [t0[j], t0[j + 1])
+    int n;
+};
+template <typename T>
+__device__ __forceinline__ const T &multi_pick(const Multi<T> &M, int g, int &tile) {
+    int j = 0;
+    while (j + 1 < M.n && g >= M.t0[j + 1]) ++j;
+    tile = g - M.t0[j];
+    return M.p[j];
+}
+
 // s += w * T[j][c .. c+7] (LDS tile, row stride LDC)
 template <int LDC>
 __device__ __forceinline__ void lds_term(const float *T, int j, int c, float w, float4 &s0, float4 &s1) {
@@ -289,7 +306,7 @@ struct MpEpilogue {
 template <int BN, bool LAST>
 // (__launch_bounds__ min 4 waves per SIMD: <= 128 VGPRs, so that two layer workgroups -- batches in flight
 // on two streams -- co-reside on a CU, 2 x 78 KB of LDS)
-__global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN, 4) void mp_layer_kernel(MpLayerP P) {
+__global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN, 4) void mp_layer_kernel(const Multi<MpLayerP> MP) {
     constexpr int BM = BLK_BONDS, WM = MpWaves<BN>::WM, WN = MpWaves<BN>::WN, NT = 64 * WM * WN;
     // two stages of one chunk (measured: 3 stages slower; two-chunk stages, one barrier per two
     // chunks, no faster: the chunk time is not bound by load latency or barriers)
@@ -301,7 +318,8 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN, 4) void mp_
                                                                               : S * CPS * x6_stage_bytes<BM, BN>();
     static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU");
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
-    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    int tile;
+    const MpLayerP &P = multi_pick(MP, xcd_tile(blockIdx.x, gridDim.x), tile);
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
     MpEpilogue<BN, NT, LAST> E;
@@ -336,18 +354,17 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN, 4) void mp_
 //     Ea[a]  = sum_{c in code(a)} W_i[:, c] + last(a) W_i[:, Fa-1]          (per atom of the block)
 //     inp[b] = Ea[src(b)] + sum_{k in tail(b)} W_i[:, Fa + k] (+ b_i)       (per bond)
 //     M0[b]  = act(inp[b])
-//     Eo[a]  = sum_{c in code(a)} W_o[:, c] + last(a) W_o[:, Fa-1]          (the f_atoms half of W_o)
-// One workgroup per (block, BN-column tile), the tile's W_i^T and W_o[:, :Fa]^T rows staged in LDS.
-// Writes inp (fp32, natural rows: the residual of every layer), M0 (plane tiles, blocked rows) like
-// gemm_x6g's epilogue, and Eo (fp32, blocked atom rows) for wo_readout_kernel's epilogue.
+// One workgroup per (block, BN-column tile), the tile's W_i^T rows staged in LDS.  Writes inp (fp32,
+// natural rows: the residual of every layer) and M0 (plane tiles, blocked rows).  Every global load of
+// the workgroup (atom codes, the weight tile, the bonds' source atoms and tail bits) is issued up front,
+// so the kernel waits for memory once.  (The f_atoms half of W_o is summed the same way in
+// wo_readout_kernel's epilogue.)
 // ------------------------------------------------------------------------------------------------
 struct EmbedP {
     const WdAtomCode *codes;     // natural atom rows
     const uint8_t *src_blk;      // per natural bond row: block-local source atom
     const uint16_t *tail;        // per natural bond row: bond columns as bits
     const float *wt;             // W_i^T [>= Fb][Hk] (fp32, packed)
-    const float *woat;           // W_o[:, :Fa]^T [>= Fa][Hk] (fp32, packed)
-    float *eo;                   // [nblk * 64][Hk]
     const float *bias;           // b_i (padded) or null
     const int32_t *blocks;
     int Fa, Fb, Hk, n_tiles;
@@ -356,75 +373,61 @@ struct EmbedP {
     uint8_t *mplanes;            // M0 plane tiles, blocked bond rows (BR 128)
 };
 
-// Stage rows [0, rows0) of src0 and [0, rows1) of src1 (BN columns from n0, row stride ld, fp32) into
-// LDS dst0 / dst1 [rows][BN]: every load of the thread issued before the first LDS store (one latency,
-// not one per row group); rows <= MAXK.
-template <int BN, int NT, int MAXK>
-__device__ __forceinline__ void stage_rows2(float *dst0, const float *src0, int rows0, float *dst1,
-                                            const float *src1, int rows1, int ld, int n0) {
-    constexpr int C4 = BN / 4, PER = (MAXK * C4 + NT - 1) / NT;
-    float4 r0[PER], r1[PER];
+// s = sum_{c in code} T[c][c4 .. c4+3] + last * T[Fa - 1][c4 ..] (ascending columns, then the mass column:
+// the order of the f_atoms row's dot product terms that are not zero)
+template <int LDT>
+__device__ __forceinline__ float4 code_sum(const WdAtomCode &cd, const float *T, int Fa, int c) {
+    float4 s = f4zero();
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int v = threadIdx.x + NT * j, k = v / C4, c = 4 * (v % C4);
-        r0[j] = k < rows0 ? ld4(src0 + (size_t)k * ld + n0 + c) : f4zero();
-        r1[j] = k < rows1 ? ld4(src1 + (size_t)k * ld + n0 + c) : f4zero();
+    for (int q = 0; q < 8; ++q) {
+        if (cd.col[q] == 0xFF) continue;
+        const float4 w = ld4(T + cd.col[q] * LDT + c);
+        s.x += w.x; s.y += w.y; s.z += w.z; s.w += w.w;
     }
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const int v = threadIdx.x + NT * j, k = v / C4, c = 4 * (v % C4);
-        if (k < rows0) st4(dst0 + k * BN + c, r0[j]);
-        if (k < rows1) st4(dst1 + k * BN + c, r1[j]);
-    }
+    fma4(s, cd.last, ld4(T + (Fa - 1) * LDT + c));
+    return s;
 }
 
 template <int BN>
-__global__ __launch_bounds__(512) void embed_kernel(EmbedP P) {
+__global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP> MP) {
     constexpr int NT = 512, LDC = BN + 4, C4 = BN / 4, U8 = BN / 8, MAXK = 160, PER = (MAXK * C4 + NT - 1) / NT;
-    // one weight tile in LDS at a time -- W_o[:, :Fa]^T for Eo, then W_i^T for Ea and the bonds -- so
-    // that the kernel takes < 80 KB of LDS and a layer kernel of a batch on another stream co-resides
-    // with it on a CU (both tiles at once took 133 KB: one workgroup per CU, nothing beside it)
-    __shared__ __attribute__((aligned(16))) float wt[MAXK * BN];        // the staged weight tile
+    constexpr int BU = (BLK_BONDS * U8 + NT - 1) / NT;  // bond units (8 columns of a row) per thread
+    __shared__ __attribute__((aligned(16))) float wt[MAXK * BN];        // the staged W_i^T tile
     __shared__ __attribute__((aligned(16))) float ea[BLK_ATOMS * LDC];  // Ea of the block's atoms
     __shared__ __attribute__((aligned(16))) float bb[BN];
     __shared__ WdAtomCode code[BLK_ATOMS];
     static_assert(sizeof(float) * (MAXK * BN + BLK_ATOMS * LDC + BN) + sizeof(WdAtomCode) * BLK_ATOMS <= 80 * 1024,
                   "LDS of two co-resident workgroups");
-    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    int tile;
+    const EmbedP &P = multi_pick(MP, xcd_tile(blockIdx.x, gridDim.x), tile);
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
     const int tid = threadIdx.x;
-    if (tid < B.an) code[tid] = P.codes[B.as + tid];
-    if (tid >= NT - C4) st4(bb + 4 * (tid - (NT - C4)), P.bias ? ld4(P.bias + n0 + 4 * (tid - (NT - C4))) : f4zero());
-    // both tiles' loads go out together; the W_i^T rows wait in registers while Eo is summed
-    float4 ro[PER], ri[PER];
+    // every load up front, in the order their values are needed (codes and bias, the weight tile, the
+    // bonds' source atoms and tails): each wait then covers only what it needs
+    static_assert(sizeof(WdAtomCode) == 16, "codes move as one 16-byte word");
+    u32x4 cd = {0u, 0u, 0u, 0u};  // (raw words: a struct with a byte array went to scratch)
+    if (tid < B.an) cd = reinterpret_cast<const u32x4 *>(P.codes)[B.as + tid];
+    float4 bq = f4zero();
+    if (tid >= NT - C4 && P.bias) bq = ld4(P.bias + n0 + 4 * (tid - (NT - C4)));
+    float4 ri[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const int v = tid + NT * q, k = v / C4, c = 4 * (v % C4);
-        ro[q] = k < P.Fa ? ld4(P.woat + (size_t)k * P.Hk + n0 + c) : f4zero();
         ri[q] = k < P.Fb ? ld4(P.wt + (size_t)k * P.Hk + n0 + c) : f4zero();
     }
+    uint32_t sa[BU], tl[BU];
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        const int v = tid + NT * q, k = v / C4, c = 4 * (v % C4);
-        if (k < P.Fa) st4(wt + k * BN + c, ro[q]);
-    }
-    __syncthreads();
-    // Eo[a] = sum_{c in code(a)} W_o[:, c] + last(a) W_o[:, Fa-1] (the f_atoms half of W_o)
-    for (int v = tid; v < B.an * C4; v += NT) {
-        const int la = v / C4, c = 4 * (v % C4);
-        const WdAtomCode &cd = code[la];
-        float4 so = f4zero();
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            if (cd.col[q] == 0xFF) continue;
-            const float4 u = ld4(wt + cd.col[q] * BN + c);
-            so.x += u.x; so.y += u.y; so.z += u.z; so.w += u.w;
+    for (int u = 0; u < BU; ++u) {
+        const int v = tid + NT * u, lb = v / U8;
+        sa[u] = tl[u] = 0;
+        if (lb < B.bn) {
+            sa[u] = P.src_blk[B.bs + lb];
+            tl[u] = P.tail[B.bs + lb];
         }
-        fma4(so, cd.last, ld4(wt + (P.Fa - 1) * BN + c));
-        st4(P.eo + ((size_t)blk * BLK_ATOMS + la) * P.Hk + n0 + c, so);
     }
-    __syncthreads();  // every read of the W_o tile done
+    if (tid < B.an) reinterpret_cast<u32x4 *>(code)[tid] = cd;
+    if (tid >= NT - C4) st4(bb + 4 * (tid - (NT - C4)), bq);
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const int v = tid + NT * q, k = v / C4, c = 4 * (v % C4);
@@ -434,28 +437,20 @@ __global__ __launch_bounds__(512) void embed_kernel(EmbedP P) {
     // Ea[a] = sum_{c in code(a)} W_i[:, c] + last(a) W_i[:, Fa-1]
     for (int v = tid; v < B.an * C4; v += NT) {
         const int la = v / C4, c = 4 * (v % C4);
-        const WdAtomCode &cd = code[la];
-        float4 s = f4zero();
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            if (cd.col[q] == 0xFF) continue;
-            const float4 w = ld4(wt + cd.col[q] * BN + c);
-            s.x += w.x; s.y += w.y; s.z += w.z; s.w += w.w;
-        }
-        fma4(s, cd.last, ld4(wt + (P.Fa - 1) * BN + c));
-        st4(ea + la * LDC + c, s);
+        st4(ea + la * LDC + c, code_sum<BN>(code[la], wt, P.Fa, c));
     }
     __syncthreads();
     const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
     const __amdgpu_buffer_rsrc_t mrs = x6_block_rsrc<BLK_BONDS>(P.mplanes, P.Hk, blk);
     with_act(P.act, [&](auto act_c) {
     constexpr int ACT = decltype(act_c)::value;
-    for (int v = tid; v < B.bn * U8; v += NT) {
-        const int lb = v / U8, c = 8 * (v % U8), b = B.bs + lb;
-        const int sa = P.src_blk[b];
-        const uint32_t tl = P.tail[b];
-        float4 z0 = ld4(ea + sa * LDC + c), z1 = ld4(ea + sa * LDC + c + 4);
-        for (uint32_t m = tl; m; m &= m - 1) {
+#pragma unroll
+    for (int u = 0; u < BU; ++u) {
+        const int v = tid + NT * u, lb = v / U8, c = 8 * (v % U8), b = B.bs + lb;
+        if (lb >= B.bn) break;
+        const int s_ = (int)sa[u];
+        float4 z0 = ld4(ea + s_ * LDC + c), z1 = ld4(ea + s_ * LDC + c + 4);
+        for (uint32_t m = tl[u]; m; m &= m - 1) {
             const float *w = wt + (P.Fa + __builtin_ctz(m)) * BN + c;
             const float4 w0 = ld4(w), w1 = ld4(w + 4);
             z0.x += w0.x; z0.y += w0.y; z0.z += w0.z; z0.w += w0.w;
@@ -491,9 +486,11 @@ struct WoReadoutP {
     int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;
     float *out; int ncols;                   // out [B][ncols] (ncols = H)
     int n_tiles;
-    // categorical codes (kca = 0): the f_atoms half of [f_atoms | A] W_o^T, precomputed per atom by
-    // embed_kernel as sums of W_o columns: fp32 [nblk * 64][Hk], blocked atom rows (null: GEMM segment)
-    const float *eo;
+    // categorical codes (kca = 0): the f_atoms half of [f_atoms | A] W_o^T summed per atom from the
+    // W_o[:, :Fa]^T rows of its code (code_sum); codes null: the GEMM's f_atoms segment
+    const WdAtomCode *codes;     // natural atom rows
+    const float *woat;           // W_o[:, :Fa]^T [>= Fa][Hk] (fp32, packed)
+    int Fa;
     int Hk;
     float *zosave;  // training forward or null: the W_o pre-activation (mpn.py:133) as fp32 natural atom rows [Vap][Hk]
 };
@@ -504,7 +501,7 @@ template <> struct WoWaves<80> { static constexpr int WM = 2, WN = 5; };
 
 // grid = nblk * n_tiles: 64 atom rows x BN columns per workgroup.
 template <int BN>
-__global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_readout_kernel(WoReadoutP P) {
+__global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_readout_kernel(const Multi<WoReadoutP> MP) {
     constexpr int BM = BLK_ATOMS, LDC = BN + 4, WM = WoWaves<BN>::WM, WN = WoWaves<BN>::WN, NT = 64 * WM * WN;
     // 80-column tiles (one workgroup per CU at the benchmark size): two chunks per barrier, since W_o's
     // 64-row chunks are short and one barrier per chunk cost 0.6 us (12.5 vs 13.1 us; three
@@ -513,11 +510,18 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     // (deeper single-chunk pipelines, with the mainloop hook's loads ordered ahead of the partial vmcnt
     // waits, measured slower: three / four stages 15.1 / 14.8 us here, 12.8 / 11.8 against 9.7 us on
     // QM9-shaped batches)
-    constexpr int CPS = BN == 80 ? 2 : 1;
+#ifndef WD_WO_CPS80
+#define WD_WO_CPS80 2
+#endif
+    constexpr int CPS = BN == 80 ? WD_WO_CPS80 : 1;
     constexpr int WS = 2;  // LDS stages
-    constexpr int LDS_BYTES = WS * CPS * x6_stage_bytes<BM, BN>();
+    // epilogue: h tile, atom weights, molecule table, then (codes) the W_o[:, :Fa]^T tile and the codes
+    constexpr int EPI_W = BM * LDC + BM + 3 * BLK_MOLS, EPI_BYTES = (EPI_W + WO_MAXK * BN) * 4 + BM * 16;
+    constexpr int LDS_BYTES = WS * CPS * x6_stage_bytes<BM, BN>() > EPI_BYTES ? WS * CPS * x6_stage_bytes<BM, BN>()
+                                                                             : EPI_BYTES;
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
-    const int tile = xcd_tile(blockIdx.x, gridDim.x);
+    int tile;
+    const WoReadoutP &P = multi_pick(MP, xcd_tile(blockIdx.x, gridDim.x), tile);
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
     const int tid = threadIdx.x;
@@ -538,17 +542,21 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     float4 bb = f4zero();
     float watom = 0.f, mxn = 0.f;
     int mstart = 0, msize = 0;
-    // codes path: this thread's rows of the precomputed f_atoms W_o[:, :Fa]^T (the epilogue units below)
-    constexpr int EPU = (BM * C4 + NT - 1) / NT;
-    float4 eo[EPU];
+    // codes path: the block's atom codes (thread a < an) and this thread's share of the W_o[:, :Fa]^T tile
+    constexpr int EPU = (BM * C4 + NT - 1) / NT, WP = (WO_MAXK * C4 + NT - 1) / NT;
+    u32x4 cd = {0u, 0u, 0u, 0u};  // (raw words: a struct with a byte array was promoted to LDS)
+    float4 wq[WP];
     auto prefetch = [&](int phase) {
         if (phase != 0) return;
         bb = ld4(P.bias + n0 + 4 * (tid % C4));
         if (tid < B.an) watom = P.w_atoms[B.as + tid];
+        if (P.codes) {
+            if (tid < B.an) cd = reinterpret_cast<const u32x4 *>(P.codes)[B.as + tid];
 #pragma unroll
-        for (int j = 0; j < EPU; ++j) {
-            const int v = tid + NT * j, la = v / C4, c = 4 * (v % C4);
-            eo[j] = P.eo && v < BM * C4 && la < B.an ? ld4(P.eo + ((size_t)blk * BM + la) * P.Hk + n0 + c) : f4zero();
+            for (int j = 0; j < WP; ++j) {
+                const int v = tid + NT * j, k = v / C4, c = 4 * (v % C4);
+                wq[j] = k < P.Fa ? ld4(P.woat + (size_t)k * P.Hk + n0 + c) : f4zero();
+            }
         }
         if (tid < nm) {
             mstart = P.mol_start[B.ml + tid];
@@ -562,9 +570,18 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     float *H = reinterpret_cast<float *>(lds);
     float *Wl = H + BM * LDC;           // [BM] atom weights of the block
     float *Ml = Wl + BM;                // [3][BLK_MOLS] per molecule: start (as float bits), size, Xn
-    static_assert((BM * LDC + BM + 3 * BLK_MOLS) * 4 <= LDS_BYTES, "readout staging fits");
+    float *Wt = H + EPI_W;              // codes: W_o[:, :Fa]^T tile [Fa][BN]
+    WdAtomCode *Cl = reinterpret_cast<WdAtomCode *>(Wt + WO_MAXK * BN);  // codes: [BM]
     static_assert(BLK_MOLS <= NT, "one molecule per thread in the prefetch");
     x6_acc_to_lds<BM, BN, WM, WN>(acc, H);
+    if (P.codes) {
+        if (tid < B.an) reinterpret_cast<u32x4 *>(Cl)[tid] = cd;
+#pragma unroll
+        for (int j = 0; j < WP; ++j) {
+            const int v = tid + NT * j, k = v / C4, c = 4 * (v % C4);
+            if (k < P.Fa) st4(Wt + k * BN + c, wq[j]);
+        }
+    }
     if (tid < BM) Wl[tid] = watom;
     if (tid < nm) {
         Ml[tid] = __int_as_float(mstart);
@@ -582,7 +599,10 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
             if (v >= BM * C4) break;
             const int la = v / C4, c = 4 * (v % C4);
             float4 hv = ld4(H + la * LDC + c);
-            hv.x += eo[j].x; hv.y += eo[j].y; hv.z += eo[j].z; hv.w += eo[j].w;  // (0 without codes)
+            if (P.codes && la < B.an) {  // + f_atoms W_o[:, :Fa]^T (mpn.py:132-133), as code_sum
+                const float4 eo = code_sum<BN>(Cl[la], Wt, P.Fa, c);
+                hv.x += eo.x; hv.y += eo.y; hv.z += eo.z; hv.w += eo.w;
+            }
             float z[4] = {hv.x + bb.x, hv.y + bb.y, hv.z + bb.z, hv.w + bb.w};
             if (P.zosave && la < B.an) st4(P.zosave + (size_t)(B.as + la) * P.Hk + n0 + c, make_float4(z[0], z[1], z[2], z[3]));
 #pragma unroll

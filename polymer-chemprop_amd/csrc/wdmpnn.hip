@@ -27,6 +27,7 @@
 #include <string>
 #include <vector>
 
+#include "feed.hpp"
 #include "fused_mp.hpp"
 #include "gemm.hpp"
 #include "gemm_x6.hpp"
@@ -465,7 +466,6 @@ struct FwdLayout {
     size_t packed = 0, A = 0, Zo = 0, h = 0, Zd = 0, hd = 0, total = 0;
     size_t Xp = 0, Ap = 0;  // plane tiles of X_t and A (D.x6)
     size_t Mb[2] = {0, 0}, Ab = 0;  // molecule-blocked plane tiles of M_t (ping-pong) and A (D.blocked)
-    size_t Eo = 0;                  // D.blocked: f_atoms W_o[:, :Fa]^T per blocked atom row (compact codes)
     bool own_pack = false;
 };
 
@@ -486,7 +486,6 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
     if (D.blocked) {
         for (int i = 0; i < 2; ++i) L.Mb[i] = take((size_t)D.nblk * BLK_BONDS * D.Hk * 6);
         L.Ab = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 6);
-        L.Eo = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 4);
     } else if (D.x6) {
         if (D.T > 1) L.Xp = take((size_t)D.Rp * D.Hk * 6);
         L.Ap = take((size_t)D.Vap * D.Hk * 6);
@@ -617,6 +616,149 @@ int graph_layout(const WdCompact *c, GraphLayout &L) {
     return 0;
 }
 
+// ------------------------------------------------------------------------------------------------
+// molecule-blocked fused forward (fused_mp.hpp): embed (or the W_i GEMM) -> (T-1) x mp_layer ->
+// wo_readout, for up to WD_MULTI independent batches per launch (wdmpnn_forward_many; one batch for
+// wdmpnn_forward).  Every job shares the parameters, the configuration and the packed weights.
+// ------------------------------------------------------------------------------------------------
+struct FusedJob {
+    const WdGraph *g;
+    Dims D;
+    FwdLayout L;
+    char *ws;
+    float *out;
+};
+
+bool fused_codes(const WdGraph *g, const Dims &D) {
+    return g->atom_codes && g->bond_src_blk && g->bond_tail && D.Fb <= WO_MAXK && D.Fa <= WO_MAXK;
+}
+
+template <typename T, typename Fill>
+int launch_multi(const FusedJob *jobs, int n, int tiles_per_blk, Fill &&fill, Multi<T> &M, int &grid) {
+    M = Multi<T>{};
+    M.n = n;
+    int t = 0;
+    for (int j = 0; j < n; ++j) {
+        M.t0[j] = t;
+        fill(M.p[j], jobs[j]);
+        t += jobs[j].D.nblk * tiles_per_blk;
+    }
+    for (int j = n; j <= WD_MULTI; ++j) M.t0[j] = t;
+    grid = t;
+    return 0;
+}
+
+int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig *c, const PackLayout &PL,
+                  const char *pk, hipStream_t st) {
+    if (n < 1 || n > WD_MULTI) return fail(WD_ERR_ARG, "fused forward: %d jobs per launch (1..%d)", n, WD_MULTI);
+    const Dims &D0 = jobs[0].D;
+    auto W = [&](size_t off) { return (const float *)(pk + off); };
+    auto F = [](const FusedJob &J, size_t off) { return (float *)(J.ws + off); };
+    const int Hk = D0.Hk;
+    // 80-column tiles when they divide Hk (Hk = 320: 4 tiles, one workgroup per CU at the benchmark
+    // size), else 64
+    const bool bn80 = Hk % 80 == 0;
+    const int BNf = bn80 ? 80 : 64;
+    // categorical codes (compact graphs): the input layer and the f_atoms half of W_o as sums of weight
+    // columns instead of GEMMs over the one-hot rows (fused_mp.hpp embed_kernel)
+    const bool codes = fused_codes(jobs[0].g, D0);
+    for (int j = 1; j < n; ++j)
+        if (fused_codes(jobs[j].g, jobs[j].D) != codes || jobs[j].D.Hk != Hk || jobs[j].D.T != D0.T ||
+            jobs[j].D.Fa != D0.Fa || jobs[j].D.Fb != D0.Fb || jobs[j].D.save != D0.save)
+            return fail(WD_ERR_UNSUPPORTED, "fused forward: batches of one launch differ in layout");
+    if (codes) {
+        // 40-column tiles when they divide Hk: twice the workgroups of the layer tiling (two per CU at the
+        // benchmark size, 37 KB of LDS each), so one's staging overlaps the other's sums
+        const bool bn40 = Hk % 40 == 0;
+        const int nt = Hk / (bn40 ? 40 : BNf);
+        Multi<EmbedP> M;
+        int grid;
+        launch_multi(jobs, n, nt, [&](EmbedP &E, const FusedJob &J) {
+            const WdGraph *g = J.g;
+            E.codes = g->atom_codes; E.src_blk = g->bond_src_blk; E.tail = g->bond_tail;
+            E.wt = W(PL.WiT); E.bias = p->b_i ? W(PL.bi) : nullptr;
+            E.blocks = g->blocks;
+            E.Fa = J.D.Fa; E.Fb = J.D.Fb; E.Hk = Hk; E.n_tiles = nt;
+            E.act = c->activation; E.slope = p->prelu;
+            E.inp = F(J, J.L.Z[0]); E.mplanes = (uint8_t *)(J.ws + J.L.Mb[0]);
+        }, M, grid);
+        if (bn40) hipLaunchKernelGGL(embed_kernel<40>, dim3(grid), dim3(512), 0, st, M);
+        else if (bn80) hipLaunchKernelGGL(embed_kernel<80>, dim3(grid), dim3(512), 0, st, M);
+        else hipLaunchKernelGGL(embed_kernel<64>, dim3(grid), dim3(512), 0, st, M);
+        WD_CHECK_LAUNCH("embed");
+    } else {
+        for (int j = 0; j < n; ++j) {
+            const FusedJob &J = jobs[j];
+            Epi e = epi_act(c->activation, p->prelu, W(PL.bi), nullptr, F(J, J.L.Z[0]), nullptr, Hk, c, 0);
+            e.planes = (uint8_t *)(J.ws + J.L.Mb[0]); e.plane_row = J.g->bond_blk_row; e.planes_kp = Hk;
+            if (!x6g_eligible(e)) return fail(WD_ERR_SHAPE, "fused forward: unaligned buffers");
+            WD_TRY(gemm_x6g(J.g->f_bonds_x6, J.g->ld_bonds, J.D.Kink, nullptr, 0, 0, pk + PL.WiX, J.D.Rp, Hk, e, st));
+        }
+    }
+    const int T = D0.T;
+    for (int t = 1; t < T; ++t) {
+        const bool last = t == T - 1;
+        Multi<MpLayerP> M;
+        int grid;
+        launch_multi(jobs, n, Hk / BNf, [&](MpLayerP &Q, const FusedJob &J) {
+            const WdGraph *g = J.g;
+            Q.mprev = (const uint8_t *)(J.ws + J.L.Mb[(t - 1) & 1]); Q.mnext = (uint8_t *)(J.ws + J.L.Mb[t & 1]);
+            Q.kp = Hk;
+            Q.wh = (const uint8_t *)(pk + (bn80 ? PL.WhX80 : PL.WhX)); Q.inp = F(J, J.L.Z[0]);
+            Q.bias = p->b_h ? W(PL.bh) : nullptr;
+            Q.blocks = g->blocks;
+            Q.rev = g->b2revb; Q.src_blk = g->bond_src_blk; Q.undirected = J.D.undirected;
+            Q.act = c->activation; Q.slope = p->prelu; Q.p_drop = c->dropout; Q.seed = c->seed; Q.layer = t;
+            Q.aptr = g->atom_gather.ptr; Q.aidx = g->atom_gather.idx; Q.acoef = g->atom_gather.coef;
+            Q.aell_idx = g->atom_ell_idx; Q.aell_coef = g->atom_ell_coef;
+            Q.aplanes = (uint8_t *)(J.ws + J.L.Ab);
+            Q.n_tiles = Hk / BNf;
+            Q.zsave = J.D.save ? F(J, J.L.Z[t]) : nullptr;
+            Q.asave = J.D.save && last ? F(J, J.L.A) : nullptr;
+        }, M, grid);
+        if (t == 1) WD_TRY(record_prof(c, 0, 0, st));  // one pair around all the layers
+        if (bn80) {
+            const dim3 blk(64 * MpWaves<80>::WM * MpWaves<80>::WN);
+            if (last) hipLaunchKernelGGL((mp_layer_kernel<80, true>), dim3(grid), blk, 0, st, M);
+            else hipLaunchKernelGGL((mp_layer_kernel<80, false>), dim3(grid), blk, 0, st, M);
+        } else {
+            const dim3 blk(64 * MpWaves<64>::WM * MpWaves<64>::WN);
+            if (last) hipLaunchKernelGGL((mp_layer_kernel<64, true>), dim3(grid), blk, 0, st, M);
+            else hipLaunchKernelGGL((mp_layer_kernel<64, false>), dim3(grid), blk, 0, st, M);
+        }
+        WD_CHECK_LAUNCH("mp_layer");
+        if (last) WD_TRY(record_prof(c, 0, 1, st));
+    }
+    // W_o + readout (empty batches -- no molecules -- have no blocks and write nothing)
+    Multi<WoReadoutP> M;
+    int grid;
+    launch_multi(jobs, n, Hk / BNf, [&](WoReadoutP &R, const FusedJob &J) {
+        const WdGraph *g = J.g;
+        // (codes: the f_atoms segment is not read; a lean graph has no planes -- the A planes stand in as the
+        // segment's non-null base)
+        R.fa = g->f_atoms_blk_x6 ? (const uint8_t *)g->f_atoms_blk_x6 : (const uint8_t *)(J.ws + J.L.Ab);
+        R.kpa = g->ld_atoms; R.kcw = J.D.Fak / 32;
+        R.kca = codes ? 0 : R.kcw;
+        R.codes = codes ? g->atom_codes : nullptr; R.woat = W(PL.WoaT); R.Fa = J.D.Fa; R.Hk = Hk;
+        R.ag = (const uint8_t *)(J.ws + J.L.Ab); R.kp = Hk;
+        R.wo = (const uint8_t *)(pk + (bn80 ? PL.WoX80 : PL.WoX)); R.bias = W(PL.bo);
+        R.blocks = g->blocks;
+        R.w_atoms = g->w_atoms; R.mol_start = g->mol_start; R.mol_size = g->mol_size; R.xn = g->degree_of_polym;
+        R.agg = c->aggregation; R.norm = c->aggregation_norm; R.zero_vec = p->zero_vec;
+        R.act = c->activation; R.slope = p->prelu; R.p_drop = c->dropout; R.seed = c->seed; R.layer = J.D.T;
+        R.out = J.out; R.ncols = J.D.H; R.n_tiles = Hk / BNf;
+        R.zosave = J.D.save ? F(J, J.L.Zo) : nullptr;
+    }, M, grid);
+    if (grid > 0) {
+        if (bn80)
+            hipLaunchKernelGGL(wo_readout_kernel<80>, dim3(grid), dim3(64 * WoWaves<80>::WM * WoWaves<80>::WN), 0, st, M);
+        else
+            hipLaunchKernelGGL(wo_readout_kernel<64>, dim3(grid), dim3(64 * WoWaves<64>::WM * WoWaves<64>::WN), 0, st, M);
+        WD_CHECK_LAUNCH("wo_readout");
+    }
+    return 0;
+}
+
 }  // namespace
 
 // ================================================================================================
@@ -683,88 +825,8 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
     const char *pkb = pk;
 
     if (D.blocked) {
-        // molecule-blocked fused forward (fused_mp.hpp): W_i -> (T-1) x mp_layer -> wo_readout
-        // 80-column tiles when they divide Hk (Hk = 320: 4 tiles, one workgroup per CU at the benchmark
-        // size), else 64
-        const bool bn80 = Hk % 80 == 0;
-        const int BNf = bn80 ? 80 : 64;
-        // categorical codes (compact graphs): the input layer and the f_atoms half of W_o as sums of
-        // weight columns instead of GEMMs over the one-hot rows (fused_mp.hpp embed_kernel)
-        const bool codes = g->atom_codes && g->bond_src_blk && g->bond_tail && D.Fb <= WO_MAXK && D.Fa <= WO_MAXK;
-        if (codes) {
-            EmbedP E{};
-            E.codes = g->atom_codes; E.src_blk = g->bond_src_blk; E.tail = g->bond_tail;
-            E.wt = W(PL.WiT); E.woat = W(PL.WoaT); E.eo = F(L.Eo); E.bias = p->b_i ? W(PL.bi) : nullptr; E.blocks = g->blocks;
-            // 40-column tiles when they divide Hk: twice the workgroups of the layer tiling (two per CU at the
-            // benchmark size, 37 KB of LDS each), so one's staging overlaps the other's sums (+0.8 % with two
-            // batches in flight, same-box ABAB, profiles/round2_wave_layout_ab.txt)
-            const bool bn40 = Hk % 40 == 0;
-            E.Fa = D.Fa; E.Fb = D.Fb; E.Hk = Hk; E.n_tiles = Hk / (bn40 ? 40 : BNf);
-            E.act = c->activation; E.slope = p->prelu;
-            E.inp = F(L.Z[0]); E.mplanes = (uint8_t *)(ws + L.Mb[0]);
-            if (bn40) hipLaunchKernelGGL(embed_kernel<40>, dim3(D.nblk * E.n_tiles), dim3(512), 0, st, E);
-            else if (bn80) hipLaunchKernelGGL(embed_kernel<80>, dim3(D.nblk * E.n_tiles), dim3(512), 0, st, E);
-            else hipLaunchKernelGGL(embed_kernel<64>, dim3(D.nblk * E.n_tiles), dim3(512), 0, st, E);
-            WD_CHECK_LAUNCH("embed");
-        } else {
-            Epi e = epi_act(c->activation, p->prelu, W(PL.bi), nullptr, F(L.Z[0]), nullptr, Hk, c, 0);
-            e.planes = (uint8_t *)(ws + L.Mb[0]); e.plane_row = g->bond_blk_row; e.planes_kp = Hk;
-            if (!x6g_eligible(e)) return fail(WD_ERR_SHAPE, "fused forward: unaligned buffers");
-            WD_TRY(gemm_x6g(g->f_bonds_x6, g->ld_bonds, D.Kink, nullptr, 0, 0, pkb + PL.WiX, D.Rp, Hk, e, st));
-        }
-        for (int t = 1; t < D.T; ++t) {
-            MpLayerP M{};
-            M.mprev = (const uint8_t *)(ws + L.Mb[(t - 1) & 1]); M.mnext = (uint8_t *)(ws + L.Mb[t & 1]); M.kp = Hk;
-            M.wh = (const uint8_t *)(pkb + (bn80 ? PL.WhX80 : PL.WhX)); M.inp = F(L.Z[0]);
-            M.bias = p->b_h ? W(PL.bh) : nullptr;
-            M.blocks = g->blocks;
-            M.rev = g->b2revb; M.src_blk = g->bond_src_blk; M.undirected = D.undirected;
-            M.act = c->activation; M.slope = p->prelu; M.p_drop = c->dropout; M.seed = c->seed; M.layer = t;
-            M.aptr = g->atom_gather.ptr; M.aidx = g->atom_gather.idx; M.acoef = g->atom_gather.coef;
-            M.aell_idx = g->atom_ell_idx; M.aell_coef = g->atom_ell_coef;
-            M.aplanes = (uint8_t *)(ws + L.Ab);
-            M.n_tiles = Hk / BNf;
-            M.zsave = D.save ? F(L.Z[t]) : nullptr;
-            M.asave = D.save && t == D.T - 1 ? F(L.A) : nullptr;
-            const dim3 grid(D.nblk * M.n_tiles);
-            const bool last = t == D.T - 1;
-            if (t == 1) WD_TRY(record_prof(c, 0, 0, st));  // one pair around all the layers
-            if (bn80) {
-                const dim3 blk(64 * MpWaves<80>::WM * MpWaves<80>::WN);
-                if (last) hipLaunchKernelGGL((mp_layer_kernel<80, true>), grid, blk, 0, st, M);
-                else hipLaunchKernelGGL((mp_layer_kernel<80, false>), grid, blk, 0, st, M);
-            } else {
-                const dim3 blk(64 * MpWaves<64>::WM * MpWaves<64>::WN);
-                if (last) hipLaunchKernelGGL((mp_layer_kernel<64, true>), grid, blk, 0, st, M);
-                else hipLaunchKernelGGL((mp_layer_kernel<64, false>), grid, blk, 0, st, M);
-            }
-            WD_CHECK_LAUNCH("mp_layer");
-            if (t == D.T - 1) WD_TRY(record_prof(c, 0, 1, st));
-        }
-        if (D.B > 0) {
-            WoReadoutP R{};
-            // (codes: the f_atoms segment is not read; a lean graph has no planes -- the A planes stand in as
-        // the segment's non-null base)
-        R.fa = g->f_atoms_blk_x6 ? (const uint8_t *)g->f_atoms_blk_x6 : (const uint8_t *)(ws + L.Ab);
-        R.kpa = g->ld_atoms; R.kcw = D.Fak / 32;
-            R.kca = codes ? 0 : R.kcw;
-            R.eo = codes ? F(L.Eo) : nullptr; R.Hk = Hk;
-            R.ag = (const uint8_t *)(ws + L.Ab); R.kp = Hk;
-            R.wo = (const uint8_t *)(pkb + (bn80 ? PL.WoX80 : PL.WoX)); R.bias = W(PL.bo);
-            R.blocks = g->blocks;
-            R.w_atoms = g->w_atoms; R.mol_start = g->mol_start; R.mol_size = g->mol_size; R.xn = g->degree_of_polym;
-            R.agg = c->aggregation; R.norm = c->aggregation_norm; R.zero_vec = p->zero_vec;
-            R.act = c->activation; R.slope = p->prelu; R.p_drop = c->dropout; R.seed = c->seed; R.layer = D.T;
-            R.out = out; R.ncols = D.H; R.n_tiles = Hk / BNf;
-            R.zosave = D.save ? F(L.Zo) : nullptr;
-            const dim3 grid(D.nblk * R.n_tiles);
-            if (bn80)
-                hipLaunchKernelGGL(wo_readout_kernel<80>, grid, dim3(64 * WoWaves<80>::WM * WoWaves<80>::WN), 0, st, R);
-            else
-                hipLaunchKernelGGL(wo_readout_kernel<64>, grid, dim3(64 * WoWaves<64>::WM * WoWaves<64>::WN), 0, st, R);
-            WD_CHECK_LAUNCH("wo_readout");
-        }
-        return 0;
+        FusedJob J{g, D, L, ws, out};
+        return fused_forward(&J, 1, p, c, PL, pk, st);
     }
 
     // L0: input layer (mpn.py:92-97)
@@ -835,6 +897,37 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
                            readout_params(g, p, c, hfin, ldfin, D.Hd, out));
         WD_CHECK_LAUNCH("readout");
     }
+    return 0;
+}
+
+int wdmpnn_forward_many(int32_t n, const WdGraph *graphs, const WdParams *p, const WdConfig *c,
+                        void *const *workspaces, const size_t *workspace_bytes, float *const *outs, void *stream) {
+    if (n < 0 || (n && (!graphs || !workspaces || !workspace_bytes || !outs))) return fail(WD_ERR_ARG, "forward_many: bad arrays");
+    if (n == 0) return 0;
+    if (!p || !c) return fail(WD_ERR_ARG, "null params/config");
+    if (!p->packed) return fail(WD_ERR_ARG, "forward_many needs packed parameters (wdmpnn_pack_params)");
+    if (c->save_for_backward) return fail(WD_ERR_UNSUPPORTED, "forward_many is inference only (save_for_backward = 0)");
+    std::vector<FusedJob> jobs((size_t)n);
+    for (int j = 0; j < n; ++j) {
+        FusedJob &J = jobs[j];
+        J.g = graphs + j;
+        WD_TRY(get_dims(J.g, p, c, J.D));
+        if (!J.D.blocked)
+            return fail(WD_ERR_UNSUPPORTED, "forward_many: graph %d does not take the fused forward (molecule blocks, "
+                                            "bond messages, no descriptors, depth >= 2)", j);
+        J.L = fwd_layout(J.D, false);
+        if (!workspaces[j] || workspace_bytes[j] < J.L.total)
+            return fail(WD_ERR_WORKSPACE, "forward_many: workspace %d too small: need %zu bytes, got %zu", j, J.L.total,
+                        workspace_bytes[j]);
+        if (!outs[j]) return fail(WD_ERR_ARG, "forward_many: null out %d", j);
+        J.ws = (char *)workspaces[j];
+        J.out = outs[j];
+    }
+    const PackLayout PL = pack_layout(jobs[0].D);
+    if (p->packed_bytes < PL.total) return fail(WD_ERR_WORKSPACE, "packed params too small");
+    for (int j = 0; j < n; j += WD_MULTI)
+        WD_TRY(fused_forward(jobs.data() + j, std::min(WD_MULTI, n - j), p, c, PL, (const char *)p->packed,
+                             (hipStream_t)stream));
     return 0;
 }
 
@@ -1212,6 +1305,180 @@ int wdmpnn_build_graph_ex(const WdCompact *c, void *buffer, size_t bytes, WdGrap
         G.atom_gather_t = WdCsr{nullptr, nullptr, nullptr};
     }
     *g = G;
+    return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// native streamed batches (feed.hpp)
+// ------------------------------------------------------------------------------------------------
+static int feed_graph_bound(int32_t kind, int32_t batch, int32_t fa, int32_t fb, size_t *bytes) {
+    const FeedBounds f = feed_bounds(kind);
+    WdCompact c{};
+    c.n_mols = batch;
+    c.n_atoms = batch * f.atoms_per_mol + 1;
+    c.n_bonds = 2 * batch * f.pairs_per_mol + 1;
+    c.n_blocks = batch;
+    c.atom_fdim = fa; c.bond_fdim = fb;
+    c.nnz_msg = (c.n_bonds - 1) * FEED_MAX_DEG;
+    c.nnz_agg = c.n_bonds - 1;
+    GraphLayout L;
+    WD_TRY(graph_layout(&c, L));
+    *bytes = L.total;
+    return 0;
+}
+
+int wdmpnn_feed_slot_bytes(int32_t kind, int32_t batch, int32_t atom_fdim, int32_t bond_fdim, size_t *host_bytes,
+                           size_t *device_bytes) {
+    if (kind < 0 || kind > 2 || batch < 1 || !host_bytes || !device_bytes) return fail(WD_ERR_ARG, "feed: bad slot request");
+    size_t g = 0;
+    WD_TRY(feed_graph_bound(kind, batch, atom_fdim, bond_fdim, &g));
+    *host_bytes = align256(feed_host_bytes(kind, batch));
+    *device_bytes = *host_bytes + g;
+    return 0;
+}
+
+int wdmpnn_feed_create(const WdFeedSpec *spec, void **feed) {
+    if (!spec || !feed) return fail(WD_ERR_ARG, "feed: null argument");
+    const WdFeedSpec &S = *spec;
+    if (S.kind < 0 || S.kind > 2 || S.batch < 1 || S.n_batches < 0 || S.producers < 1 || S.slots < 2 ||
+        S.target_blocks < 1 || (S.flags & ~WDMPNN_GRAPH_LEAN) || !S.pinned || !S.device || ((uintptr_t)S.device & 255))
+        return fail(WD_ERR_ARG, "feed: bad spec");
+    Feed *F = new Feed();
+    F->spec = S;
+    F->R = S.slots;
+    size_t hb = 0, db = 0;
+    if (int rc = wdmpnn_feed_slot_bytes(S.kind, S.batch, S.atom_fdim, S.bond_fdim, &hb, &db)) {
+        delete F;
+        return rc;
+    }
+    F->host_bytes = hb; F->dev_bytes = db; F->graph_off = hb;
+    F->slot.resize((size_t)F->R);
+    bool ok = hipStreamCreateWithFlags(&F->fs, hipStreamNonBlocking) == hipSuccess;
+    for (int s = 0; s < F->R && ok; ++s) {
+        Feed::Slot &Q = F->slot[(size_t)s];
+        Q.turn = s;
+        ok = hipEventCreateWithFlags(&Q.copy_done, hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&Q.ready, hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&Q.released, hipEventDisableTiming) == hipSuccess;
+    }
+    if (!ok) {
+        delete F;
+        return fail(WD_ERR_ARG, "feed: stream / event creation failed");
+    }
+    for (int t = 0; t < S.producers; ++t) F->threads.emplace_back(&Feed::producer, F, t);
+    F->threads.emplace_back(&Feed::feeder, F);
+    *feed = F;
+    return 0;
+}
+
+int wdmpnn_feed_next(void *feed, void *stream, WdGraph *g, WdFeedBatch *info) {
+    Feed *F = (Feed *)feed;
+    if (!F || !g) return fail(WD_ERR_ARG, "feed_next: null argument");
+    std::unique_lock<std::mutex> lk(F->mu);
+    const int64_t i = F->handed;
+    if (i >= F->spec.n_batches) return 1;
+    Feed::Slot &S = F->slot[(size_t)(i % F->R)];
+    F->cv.wait(lk, [&] { return !F->error.empty() || S.built == i; });
+    if (!F->error.empty()) return fail(WD_ERR_ARG, "%s", F->error.c_str());
+    if (hipStreamWaitEvent((hipStream_t)stream, S.ready, 0) != hipSuccess) return fail(WD_ERR_ARG, "feed_next: wait");
+    *g = S.g;
+    if (info) {
+        *info = WdFeedBatch{};
+        info->index = i;
+        info->n_mols = S.counts[0]; info->n_atoms = S.counts[1]; info->n_bonds = S.counts[2];
+        info->n_blocks = S.counts[3]; info->nnz_msg = S.counts[4];
+        info->h2d_bytes = S.total;
+    }
+    F->handed = i + 1;
+    return 0;
+}
+
+int wdmpnn_feed_release(void *feed, void *stream) {
+    Feed *F = (Feed *)feed;
+    if (!F) return fail(WD_ERR_ARG, "feed_release: null feed");
+    std::lock_guard<std::mutex> lk(F->mu);
+    for (int64_t b = F->released_upto; b < F->handed; ++b)
+        if (hipEventRecord(F->slot[(size_t)(b % F->R)].released, (hipStream_t)stream) != hipSuccess)
+            return fail(WD_ERR_ARG, "feed_release: event");
+    F->released_upto = F->handed;
+    F->cv.notify_all();
+    return 0;
+}
+
+// the workspace bound of one batch of the feed (the largest batch its generator makes)
+static int feed_batch_workspace(const Feed *F, const WdParams *p, const WdConfig *c, size_t *bytes) {
+    if (!p || !c || p->hidden <= 0 || c->depth < 2) return fail(WD_ERR_ARG, "feed forward: bad params / depth");
+    const FeedBounds f = feed_bounds(F->spec.kind);
+    Dims D{};
+    D.H = p->hidden; D.Hk = rup(D.H, 64); D.T = c->depth;
+    D.R = 2 * F->spec.batch * f.pairs_per_mol + 1; D.Rp = rup(D.R, 128);
+    D.Va = F->spec.batch * f.atoms_per_mol + 1; D.Vap = rup(D.Va, 128);
+    D.Fa = F->spec.atom_fdim; D.Fak = rup(D.Fa, 32); D.Fb = F->spec.bond_fdim; D.Fbk = rup(D.Fb, 32);
+    D.Hd = D.H; D.Hdk = rup(D.Hd, 64); D.Kin = D.Fb; D.Kink = D.Fbk; D.ldx = D.Hk; D.Ko = D.Fak + D.Hk; D.Kd = D.Hk;
+    D.x6 = true; D.blocked = true; D.nblk = F->spec.batch;
+    *bytes = align256(fwd_layout(D, false).total);
+    return 0;
+}
+
+int wdmpnn_feed_forward_workspace_bytes(void *feed, const WdParams *p, const WdConfig *c, int32_t k, size_t *bytes) {
+    Feed *F = (Feed *)feed;
+    if (!F || !bytes || k < 1) return fail(WD_ERR_ARG, "feed_forward_workspace_bytes: bad argument");
+    size_t one = 0;
+    WD_TRY(feed_batch_workspace(F, p, c, &one));
+    *bytes = one * (size_t)k;
+    return 0;
+}
+
+int wdmpnn_feed_forward(void *feed, int32_t k, const WdParams *p, const WdConfig *c, void *workspace,
+                        size_t workspace_bytes, float *out, int64_t out_rows, void *stream, int32_t *got,
+                        int64_t *rows, int64_t *edges, int64_t *h2d_bytes) {
+    Feed *F = (Feed *)feed;
+    if (!F || k < 1 || !p || !c || !workspace || !out || !got || !rows || !edges || !h2d_bytes)
+        return fail(WD_ERR_ARG, "feed_forward: bad argument");
+    if (!p->packed) return fail(WD_ERR_ARG, "feed_forward needs packed parameters (wdmpnn_pack_params)");
+    if (c->save_for_backward) return fail(WD_ERR_UNSUPPORTED, "feed_forward is inference only");
+    *got = 0; *rows = 0; *edges = 0; *h2d_bytes = 0;
+    // at most R batches held unreleased (the feed builds batch i only after batch i - R is released)
+    if (k > F->R) k = F->R;
+    std::vector<WdGraph> gs;
+    std::vector<void *> wsp;
+    std::vector<size_t> wsb;
+    std::vector<float *> outs;
+    size_t used = 0;
+    int64_t r = 0, e = 0;
+    const int H = p->hidden;
+    for (int j = 0; j < k; ++j) {
+        WdGraph g{};
+        WdFeedBatch info{};
+        const int rc = wdmpnn_feed_next(feed, stream, &g, &info);
+        if (rc == 1) break;
+        if (rc) return rc;
+        Dims D;
+        WD_TRY(get_dims(&g, p, c, D));
+        const size_t need = align256(fwd_layout(D, false).total);
+        if (used + need > workspace_bytes) return fail(WD_ERR_WORKSPACE, "feed_forward: workspace too small");
+        if (r + info.n_mols > out_rows) return fail(WD_ERR_WORKSPACE, "feed_forward: output too small");
+        gs.push_back(g);
+        wsp.push_back((char *)workspace + used);
+        wsb.push_back(need);
+        outs.push_back(out + (size_t)r * H);
+        used += need;
+        r += info.n_mols;
+        e += info.n_bonds - 1;
+        *h2d_bytes += (int64_t)info.h2d_bytes;
+    }
+    if (!gs.empty()) {
+        WD_TRY(wdmpnn_forward_many((int32_t)gs.size(), gs.data(), p, c, wsp.data(), wsb.data(), outs.data(), stream));
+        WD_TRY(wdmpnn_feed_release(feed, stream));
+    }
+    *got = (int32_t)gs.size();
+    *rows = r;
+    *edges = e;
+    return 0;
+}
+
+int wdmpnn_feed_destroy(void *feed) {
+    delete (Feed *)feed;
     return 0;
 }
 

@@ -110,3 +110,67 @@ def test_training_on_streamed_batches_matches_host_packed():
 def _molgraphs(g):
     from test_compact import _as_molgraphs
     return _as_molgraphs(g)
+
+
+# ---------------------------------------------------------------- native feed (wdmpnn_feed_*)
+def test_native_feed_reproduces_the_python_stream():
+    """Same seeds -> the same batches in the same order as StreamedBatches (generation, staging, upload
+    and device build now on native threads): bitwise equal encoder outputs, any producer / slot count."""
+    from chemprop_amd.stream import NativeFeed
+    enc = _encoder()
+    with torch.no_grad():
+        ref = [enc(g) for g in StreamedBatches('polymer', 64, 20, seed=17, device=DEV, rank=1, lean=True)]
+        for producers, slots in ((4, None), (1, 3), (7, 16)):
+            got = []
+            for g in NativeFeed('polymer', 64, 20, seed=17, device=DEV, rank=1, producers=producers, slots=slots,
+                                lean=True):
+                got.append(enc(g))
+            torch.cuda.synchronize()
+            assert len(got) == len(ref)
+            assert all(torch.equal(a, b) for a, b in zip(ref, got)), (producers, slots)
+
+
+def test_native_feed_encode_equals_per_batch_forward():
+    """NativeFeed.encode (wdmpnn_feed_forward: k batches per launch set, slots reused across calls) gives
+    the per-batch forwards' outputs bitwise, for a k that does not divide the batch count."""
+    from chemprop_amd.stream import NativeFeed
+    enc = _encoder(hidden=96, depth=3, bias=True)
+    with torch.no_grad():
+        ref = torch.cat([enc(g) for g in StreamedBatches('qm9', 32, 23, seed=3, device=DEV)])
+        outs, n, edges = [], 0, 0
+        for out, got, e, _ in NativeFeed('qm9', 32, 23, seed=3, device=DEV, producers=3, slots=6, lean=True).encode(enc, k=5):
+            outs.append(out.clone())
+            n += got
+            edges += e
+    assert n == 23 and edges > 0
+    assert torch.equal(torch.cat(outs), ref)
+
+
+def test_native_feed_training_matches_python_stream():
+    from chemprop_amd.model import MoleculeModel
+    from chemprop_amd.nn_utils import initialize_weights
+    from chemprop_amd.stream import NativeFeed
+    from chemprop_amd.train import build_optimizer, get_loss_func, train_step
+    args = TrainArgs(hidden_size=64, depth=3, device=DEV)
+    rng = np.random.default_rng(1)
+    targets = [[[float(x)] for x in rng.standard_normal(16)] for _ in range(6)]
+    res = []
+    for make in (lambda: StreamedBatches('polymer', 16, 6, seed=5, device=DEV),
+                 lambda: NativeFeed('polymer', 16, 6, seed=5, device=DEV, slots=4)):
+        torch.manual_seed(0)
+        m = MoleculeModel(args)
+        initialize_weights(m)
+        m = m.to(DEV)
+        opt = build_optimizer(m, 1e-3)
+        losses = [float(train_step(m, [g], t, get_loss_func('regression'), opt)) for g, t in zip(make(), targets)]
+        res.append((losses, [q.detach().cpu() for q in m.parameters()]))
+    assert res[0][0] == res[1][0]
+    assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+
+
+def test_native_feed_bad_spec_raises():
+    from chemprop_amd.stream import NativeFeed
+    with pytest.raises(ValueError):
+        NativeFeed('protein', 8, 1, seed=0, device=DEV)
+    f = NativeFeed('qm9', 8, 0, seed=0, device=DEV)
+    assert list(f) == []

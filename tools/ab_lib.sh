@@ -1,7 +1,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
-B="python bench.py --steps 300 --warmup 20 --no-cpu --stream-graphs 0 --stream-train-graphs 0 --no-secondary"
+B="python bench.py --steps 300 --warmup 20 --no-cpu --stream-graphs 0 --stream-train-graphs 0 --no-secondary --many 0"
 for v in new base new base; do
   if [ $v = base ]; then export WDMPNN_LIB=$PWD/exp/libwdmpnn_base.so; else unset WDMPNN_LIB; fi
   timeout -k 10 200 $B > gpurun_out/ab_$v.log 2>&1 || exit $?

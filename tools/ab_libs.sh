@@ -4,7 +4,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-B="python bench.py --steps 300 --warmup 20 --no-cpu --stream-graphs 0 --stream-train-graphs 0 --no-secondary"
+B="python bench.py --steps 300 --warmup 20 --no-cpu --stream-graphs 0 --stream-train-graphs 0 --no-secondary --many 0"
 for round in 1 2; do
   for v in "$@"; do
     export WDMPNN_LIB=$PWD/exp/libwdmpnn_$v.so

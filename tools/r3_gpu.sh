@@ -23,7 +23,7 @@ for s in "$@"; do
     ab) step ab 600 bash tools/ab_lib.sh ;;
     bench) step bench 600 python bench.py ;;
     benchq) step benchq 300 python bench.py --steps 200 --warmup 20 --no-cpu --no-secondary --stream-graphs 0 --stream-train-graphs 0 ;;
-    prof) step rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu --no-secondary --streams 1 --stream-graphs 0 --stream-train-graphs 0 && python tools/kstats.py gpurun_out/rocprof/run_kernel_stats.csv 8 ;;
+    prof) step rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu --no-secondary --streams 1 --many 0 --stream-graphs 0 --stream-train-graphs 0 && python tools/kstats.py gpurun_out/rocprof/run_kernel_stats.csv 8 ;;
     pmc) step pmc 900 bash tools/pmc.sh ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
