@@ -246,8 +246,10 @@ def streamed_workload(device, args, rank, world, graphs_per_rank, batch=64, prod
     enc = make_encoder(args, device)
     n = -(-graphs_per_rank // batch)
     with torch.no_grad():
-        for _ in NativeFeed('polymer', batch, 4 * k, seed=99, device=device, rank=rank, producers=producers,
-                            lean=True).encode(enc, k):
+        # warm-up: the first ~1000 streamed batches of a process run at half speed (HIP runtime / driver
+        # warm-up of the feed's copy, event and launch paths: tools/stream_encode.py, profiles/round3_*)
+        for _ in NativeFeed('polymer', batch, min(n, 1024), seed=99, device=device, rank=rank, producers=producers,
+                            lean=True, slots=4 * k).encode(enc, k):
             pass
         barrier()
         t0 = time.perf_counter()
@@ -345,7 +347,7 @@ def main():
     ap.add_argument('--variant', type=int, default=0, help='WdConfig.gemm_variant (0 = default path; 9 = f32 MFMA)')
     ap.add_argument('--stream-graphs', type=int, default=10_000_000 // 8,
                     help='configs[4]: polymer graphs streamed per rank (default 10 M / 8 GPUs); 0 = skip')
-    ap.add_argument('--producers', type=int, default=4, help='native generator threads of the streamed workloads')
+    ap.add_argument('--producers', type=int, default=12, help='native generator threads of the streamed workloads')
     ap.add_argument('--stream-train-graphs', type=int, default=131_072,
                     help='configs[4] as DP training: streamed graphs per rank (batches of 128); 0 = skip')
     a = ap.parse_args()

@@ -303,9 +303,10 @@ int wdmpnn_graph_bytes(const WdCompact *c, size_t *bytes);
  * on `stream`; *g receives the struct (bond-message mode, blocks set, no descriptors) whose pointers
  * point into `buffer`.  All arrays of c are device pointers. */
 int wdmpnn_build_graph(const WdCompact *c, void *buffer, size_t bytes, WdGraph *g, void *stream);
-/* The same with flags.  WDMPNN_GRAPH_LEAN: skip the dense feature rows, their plane tiles and the
- * transposed gathers (about 2/3 of the bytes written for a polymer batch); the graph then serves only
- * the fused inference forward (categorical codes) -- anything else returns WD_ERR_UNSUPPORTED. */
+/* The same with flags.  WDMPNN_GRAPH_LEAN: skip the dense feature rows, their plane tiles, the bond
+ * message gathers and the transposed gathers (most of the bytes written for a polymer batch); the graph
+ * then serves only the fused inference forward (categorical codes) -- anything else returns
+ * WD_ERR_UNSUPPORTED. */
 #define WDMPNN_GRAPH_LEAN 1
 int wdmpnn_build_graph_ex(const WdCompact *c, void *buffer, size_t bytes, WdGraph *g, int32_t flags, void *stream);
 

@@ -94,4 +94,21 @@ __device__ __forceinline__ int xcd_tile(int b, int ntiles) {
     return x * base + (x < rem ? x : rem) + local;
 }
 
+// Several independent batches in one launch (wdmpnn_forward_many, the stream feed's graph builds): per batch its parameter struct and
+// its first tile in the grid; a workgroup finds its batch by a short uniform scan (the structs stay in
+// the kernel-argument segment: scalar loads).  One batch: n = 1.
+constexpr int WD_MULTI = 8;
+template <typename T> struct Multi {
+    T p[WD_MULTI];
+    int t0[WD_MULTI + 1];  // tile ranges: batch j owns grid tiles [t0[j], t0[j + 1])
+    int n;
+};
+template <typename T>
+__device__ __forceinline__ const T &multi_pick(const Multi<T> &M, int g, int &tile) {
+    int j = 0;
+    while (j + 1 < M.n && g >= M.t0[j + 1]) ++j;
+    tile = g - M.t0[j];
+    return M.p[j];
+}
+
 }  // namespace wd

@@ -198,11 +198,13 @@ struct Plan {
     std::vector<int32_t> blocks;     // [nblk][8]
     std::vector<int32_t> block_nnz;  // [nblk][2]
     int64_t nnz_msg = 0, nnz_agg = 0;
+    std::vector<int32_t> nz;         // scratch: nonzero in-weights per atom
     int n_blocks() const { return (int)(blocks.size() / 8); }
 };
 
 inline bool plan(const Batch &c, int target_blocks, Plan &p) {
-    p = Plan{};
+    p.blocks.clear(); p.block_nnz.clear();  // (capacity kept: see generate)
+    p.nnz_msg = p.nnz_agg = 0;
     const int64_t B = c.n_mols();
     int64_t big = 0, tot = 0;
     for (int64_t i = 0; i < B; ++i) {
@@ -230,7 +232,8 @@ inline bool plan(const Batch &c, int target_blocks, Plan &p) {
     // entries: nz(a) = bonds into a with a nonzero weight; msg row a1 -> a2 (reverse weight w21):
     // nz(a1) - [w21 != 0] + [w21 != 1]; agg row a: nz(a)
     const int64_t V1 = c.n_atoms();
-    std::vector<int32_t> nz((size_t)V1, 0);
+    p.nz.assign((size_t)V1, 0);
+    std::vector<int32_t> &nz = p.nz;
     for (int64_t i = 0; i < B; ++i) {
         const int64_t ao = c.mols[4 * i], bo = c.mols[4 * i + 2];
         for (int64_t lb = 0; lb < c.mols[4 * i + 3]; lb += 2) {
@@ -309,23 +312,34 @@ inline uint16_t gen_bond_tail(Rng &r) {
     return t;
 }
 
-inline void skeleton(Rng &r, int n, int offset, std::set<std::pair<int, int>> &edges) {
-    for (int i = 0; i + 1 < n; ++i) edges.insert({offset + i, offset + i + 1});
+// Edges of a molecule: a sorted, duplicate-free list of (a1 < a2) pairs (the iteration order of the
+// std::set this replaced, so the generated batches are unchanged: no node allocations per edge).
+using EdgeList = std::vector<std::pair<int, int>>;
+
+inline void skeleton(Rng &r, int n, int offset, EdgeList &edges) {
+    for (int i = 0; i + 1 < n; ++i) edges.push_back({offset + i, offset + i + 1});
     for (int k = 0; k < n / 5; ++k) {
         if (n < 4) break;
         const int i = r.integers(0, n - 4), j = r.integers(i + 3, n - 1);
-        edges.insert({offset + i, offset + j});
+        edges.push_back({offset + i, offset + j});
     }
 }
 
-// one molecule appended to c (bonds: skeleton pairs in (a1 < a2) order, then rules in order)
-inline void add_molecule(Batch &c, Rng &r, int n_atoms, const std::set<std::pair<int, int>> &edges,
-                         const std::vector<std::pair<std::pair<int, int>, std::pair<float, float>>> &rules,
-                         const std::vector<float> &w_atoms, float xn) {
+inline void finish_edges(EdgeList &edges) {
+    std::sort(edges.begin(), edges.end());
+    edges.erase(std::unique(edges.begin(), edges.end()), edges.end());
+}
+
+struct Rule { int a, b; float w12, w21; };
+
+// one molecule appended to c (bonds: skeleton pairs in (a1 < a2) order, then rules in order); atom a
+// gets weight w_first for a < n_first, else w_rest
+inline void add_molecule(Batch &c, Rng &r, int n_atoms, const EdgeList &edges, const Rule *rules, int n_rules,
+                         int n_first, float w_first, float w_rest, float xn) {
     const int32_t ao = (int32_t)c.atoms.size(), bo = c.n_bonds();
-    std::vector<int> degree((size_t)n_atoms, 0);
-    for (const auto &e : edges) { ++degree[(size_t)e.first]; ++degree[(size_t)e.second]; }
-    for (int a = 0; a < n_atoms; ++a) c.atoms.push_back(gen_atom(r, degree[(size_t)a], w_atoms[(size_t)a]));
+    int degree[64] = {};
+    for (const auto &e : edges) { ++degree[e.first]; ++degree[e.second]; }
+    for (int a = 0; a < n_atoms; ++a) c.atoms.push_back(gen_atom(r, degree[a], a < n_first ? w_first : w_rest));
     for (const auto &e : edges) {
         WdBondPair q{};
         q.a1 = (uint16_t)e.first; q.a2 = (uint16_t)e.second;
@@ -333,14 +347,14 @@ inline void add_molecule(Batch &c, Rng &r, int n_atoms, const std::set<std::pair
         q.w12 = 1.f; q.w21 = 1.f;
         c.pairs.push_back(q);
     }
-    for (const auto &ru : rules) {
+    for (int k = 0; k < n_rules; ++k) {
         WdBondPair q{};
-        q.a1 = (uint16_t)ru.first.first; q.a2 = (uint16_t)ru.first.second;
+        q.a1 = (uint16_t)rules[k].a; q.a2 = (uint16_t)rules[k].b;
         q.tail = gen_bond_tail(r);
-        q.w12 = ru.second.first; q.w21 = ru.second.second;
+        q.w12 = rules[k].w12; q.w21 = rules[k].w21;
         c.pairs.push_back(q);
     }
-    const int32_t nb = 2 * (int32_t)(edges.size() + rules.size());
+    const int32_t nb = 2 * (int32_t)(edges.size() + n_rules);
     const int32_t row[4] = {ao, n_atoms, bo, nb};
     c.mols.insert(c.mols.end(), row, row + 4);
     c.xn.push_back(xn);
@@ -350,33 +364,47 @@ inline void add_molecule(Batch &c, Rng &r, int n_atoms, const std::set<std::pair
 // Dirichlet(1, 1) fractions, degree_of_polym = 1 + log10(U[1, 1000])), 1 = QM9-like U{5..9} atoms,
 // 2 = ZINC-like U{15..37} atoms (w = 1, Xn = 1)
 inline void generate(int kind, int B, uint64_t seed, Batch &c) {
-    c = Batch{};
+    // (c's vectors keep their capacity: a producer thread reuses one Batch, no allocation per batch)
+    c.fa = 133; c.fb = 147;
+    c.mols.clear(); c.xn.clear(); c.atoms.clear(); c.pairs.clear();
+    const int amax = kind == 0 ? 48 : kind == 1 ? 9 : 37;
+    c.atoms.reserve((size_t)B * amax + 1);
+    c.pairs.reserve((size_t)B * (amax + amax / 5 + 10));
+    c.mols.reserve((size_t)B * 4);
+    c.xn.reserve((size_t)B);
     c.atoms.push_back(pad_atom());
     Rng r(seed);
+    EdgeList edges;
+    edges.reserve(64);
     for (int i = 0; i < B; ++i) {
-        std::set<std::pair<int, int>> edges;
-        std::vector<std::pair<std::pair<int, int>, std::pair<float, float>>> rules;
+        edges.clear();
         if (kind == 0) {
             const int na = r.integers(10, 24), nb = r.integers(10, 24);
             skeleton(r, na, 0, edges);
             skeleton(r, nb, na, edges);
+            finish_edges(edges);
             int att[4];
             att[0] = r.integers(0, na - 1);
             do att[1] = r.integers(0, na - 1); while (att[1] == att[0]);
             att[2] = na + r.integers(0, nb - 1);
             do att[3] = na + r.integers(0, nb - 1); while (att[3] == att[2]);
+            Rule rules[10];
+            int nr = 0;
             for (int a = 0; a < 4; ++a)
-                for (int b = a; b < 4; ++b)
-                    rules.push_back({{att[a], att[b]}, {(float)r.uniform(0.1, 0.5), (float)r.uniform(0.1, 0.5)}});
+                for (int b = a; b < 4; ++b) {
+                    const float w12 = (float)r.uniform(0.1, 0.5);
+                    const float w21 = (float)r.uniform(0.1, 0.5);
+                    rules[nr++] = Rule{att[a], att[b], w12, w21};
+                }
             const double f0 = r.uniform();
-            std::vector<float> w((size_t)(na + nb));
-            for (int a = 0; a < na + nb; ++a) w[(size_t)a] = (float)(a < na ? f0 : 1.0 - f0);
             const double xn = r.uniform(1.0, 1000.0);
-            add_molecule(c, r, na + nb, edges, rules, w, (float)(1.0 + std::log10(xn)));
+            add_molecule(c, r, na + nb, edges, rules, nr, na, (float)f0, (float)(1.0 - f0),
+                         (float)(1.0 + std::log10(xn)));
         } else {
             const int n = kind == 1 ? r.integers(5, 9) : r.integers(15, 37);
             skeleton(r, n, 0, edges);
-            add_molecule(c, r, n, edges, rules, std::vector<float>((size_t)n, 1.f), 1.f);
+            finish_edges(edges);
+            add_molecule(c, r, n, edges, nullptr, 0, n, 1.f, 1.f, 1.f);
         }
     }
 }

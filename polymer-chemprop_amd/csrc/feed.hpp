@@ -21,7 +21,12 @@
 #include <vector>
 
 #include "compact.hpp"
+#include "graph_build.hpp"
 #include "wdmpnn.h"
+
+// (wdmpnn.hip) the build parameters / WdGraph of a compact batch, and one launch for several builds
+int graph_build_prepare(const WdCompact *c, void *buffer, size_t bytes, int32_t flags, wd::GraphBuildP &P, WdGraph &Gout);
+int graph_build_launch(const wd::GraphBuildP *P, int n, hipStream_t st);
 
 namespace wd {
 
@@ -77,6 +82,8 @@ struct Feed {
 
     void producer(int t) {
         try {
+            compact::Batch c;  // reused: no allocation per batch once the vectors have grown
+            compact::Plan p;
             for (int64_t i = t; i < spec.n_batches; i += spec.producers) {
                 const int s = (int)(i % R);
                 Slot &S = slot[(size_t)s];
@@ -86,8 +93,6 @@ struct Feed {
                     if (stop) return;
                 }
                 if (S.copy_pending && hipEventSynchronize(S.copy_done) != hipSuccess) throw std::runtime_error("copy event");
-                compact::Batch c;
-                compact::Plan p;
                 compact::generate(spec.kind, spec.batch, spec.seed + (uint64_t)i, c);
                 c.fa = spec.atom_fdim;
                 c.fb = spec.bond_fdim;
@@ -109,40 +114,62 @@ struct Feed {
         }
     }
 
-    // (build: wdmpnn_build_graph_ex on the feed stream)
+    // batch i is ready for the feed thread: staged, and its device slot's previous batch released
+    bool feedable(int64_t i) const {
+        const Slot &S = slot[(size_t)(i % R)];
+        return S.staged == i && released_upto >= i - R + 1;
+    }
+
+    // Batches go through in groups: every batch already staged (up to WD_MULTI) is uploaded, and their
+    // graphs are built by ONE launch (graph_build_launch): a build is a short launch of one workgroup per
+    // molecule block, so several batches per launch keep more CUs busy for the same latency.
     void feeder() {
         try {
-            for (int64_t i = 0; i < spec.n_batches; ++i) {
-                const int s = (int)(i % R);
-                Slot &S = slot[(size_t)s];
+            std::vector<GraphBuildP> P;
+            std::vector<WdGraph> G;
+            for (int64_t i = 0; i < spec.n_batches;) {
+                int64_t n = 0;
                 {
                     std::unique_lock<std::mutex> lk(mu);
-                    // staged, and the device slot's previous batch released by the consumer
-                    cv.wait(lk, [&] { return stop || (S.staged == i && released_upto >= i - R + 1); });
+                    cv.wait(lk, [&] { return stop || feedable(i); });
                     if (stop) return;
+                    while (n < WD_MULTI && i + n < spec.n_batches && feedable(i + n)) ++n;
                 }
-                if (i >= R && hipStreamWaitEvent(fs, S.released, 0) != hipSuccess) throw std::runtime_error("release wait");
-                if (hipMemcpyAsync(dev(s), host(s), S.total, hipMemcpyHostToDevice, fs) != hipSuccess ||
-                    hipEventRecord(S.copy_done, fs) != hipSuccess)
-                    throw std::runtime_error("H2D");
-                WdCompact c{};
-                c.n_mols = S.counts[0]; c.n_atoms = S.counts[1]; c.n_bonds = S.counts[2]; c.n_blocks = S.counts[3];
-                c.atom_fdim = spec.atom_fdim; c.bond_fdim = spec.bond_fdim;
-                c.nnz_msg = S.counts[4]; c.nnz_agg = S.counts[5];
-                uint8_t *d = dev(s);
-                c.mols = (const int32_t *)(d + S.off[0]); c.xn = (const float *)(d + S.off[1]);
-                c.atoms = (const WdAtomCode *)(d + S.off[2]); c.pairs = (const WdBondPair *)(d + S.off[3]);
-                c.blocks = (const int32_t *)(d + S.off[4]); c.block_nnz = (const int32_t *)(d + S.off[5]);
-                WdGraph g{};
-                if (wdmpnn_build_graph_ex(&c, d + graph_off, dev_bytes - graph_off, &g, spec.flags, fs) != 0)
+                P.assign((size_t)n, GraphBuildP{});
+                G.assign((size_t)n, WdGraph{});
+                for (int64_t j = 0; j < n; ++j) {
+                    const int s = (int)((i + j) % R);
+                    Slot &S = slot[(size_t)s];
+                    if (i + j >= R && hipStreamWaitEvent(fs, S.released, 0) != hipSuccess)
+                        throw std::runtime_error("release wait");
+                    if (hipMemcpyAsync(dev(s), host(s), S.total, hipMemcpyHostToDevice, fs) != hipSuccess ||
+                        hipEventRecord(S.copy_done, fs) != hipSuccess)
+                        throw std::runtime_error("H2D");
+                    WdCompact c{};
+                    c.n_mols = S.counts[0]; c.n_atoms = S.counts[1]; c.n_bonds = S.counts[2]; c.n_blocks = S.counts[3];
+                    c.atom_fdim = spec.atom_fdim; c.bond_fdim = spec.bond_fdim;
+                    c.nnz_msg = S.counts[4]; c.nnz_agg = S.counts[5];
+                    uint8_t *d = dev(s);
+                    c.mols = (const int32_t *)(d + S.off[0]); c.xn = (const float *)(d + S.off[1]);
+                    c.atoms = (const WdAtomCode *)(d + S.off[2]); c.pairs = (const WdBondPair *)(d + S.off[3]);
+                    c.blocks = (const int32_t *)(d + S.off[4]); c.block_nnz = (const int32_t *)(d + S.off[5]);
+                    if (graph_build_prepare(&c, d + graph_off, dev_bytes - graph_off, spec.flags, P[(size_t)j], G[(size_t)j]))
+                        throw std::runtime_error(std::string("graph build: ") + wdmpnn_last_error());
+                }
+                if (graph_build_launch(P.data(), (int)n, fs))
                     throw std::runtime_error(std::string("graph build: ") + wdmpnn_last_error());
-                if (hipEventRecord(S.ready, fs) != hipSuccess) throw std::runtime_error("ready event");
+                for (int64_t j = 0; j < n; ++j)
+                    if (hipEventRecord(slot[(size_t)((i + j) % R)].ready, fs) != hipSuccess) throw std::runtime_error("ready event");
                 std::lock_guard<std::mutex> lk(mu);
-                S.copy_pending = true;
-                S.turn = i + R;  // the producer of batch i + R waits for copy_done itself
-                S.g = g;
-                S.built = i;
+                for (int64_t j = 0; j < n; ++j) {
+                    Slot &S = slot[(size_t)((i + j) % R)];
+                    S.copy_pending = true;
+                    S.turn = i + j + R;  // the producer of batch i + j + R waits for copy_done itself
+                    S.g = G[(size_t)j];
+                    S.built = i + j;
+                }
                 cv.notify_all();
+                i += n;
             }
         } catch (const std::exception &e) {
             std::lock_guard<std::mutex> lk(mu);

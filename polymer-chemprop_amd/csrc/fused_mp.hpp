@@ -67,23 +67,6 @@ __device__ __forceinline__ BlockRow load_block(const int32_t *blocks, int i) {
     return BlockRow{a.x, a.y, a.z, a.w, b.x, b.y};
 }
 
-// Several independent batches in one launch (wdmpnn_forward_many): per batch its parameter struct and
-// its first tile in the grid; a workgroup finds its batch by a short uniform scan (the structs stay in
-// the kernel-argument segment: scalar loads).  One batch: n = 1.
-constexpr int WD_MULTI = 8;
-template <typename T> struct Multi {
-    T p[WD_MULTI];
-    int t0[WD_MULTI + 1];  // tile ranges: batch j owns grid tiles [t0[j], t0[j + 1])
-    int n;
-};
-template <typename T>
-__device__ __forceinline__ const T &multi_pick(const Multi<T> &M, int g, int &tile) {
-    int j = 0;
-    while (j + 1 < M.n && g >= M.t0[j + 1]) ++j;
-    tile = g - M.t0[j];
-    return M.p[j];
-}
-
 // s += w * T[j][c .. c+7] (LDS tile, row stride LDC)
 template <int LDC>
 __device__ __forceinline__ void lds_term(const float *T, int j, int c, float w, float4 &s0, float4 &s1) {

@@ -15,6 +15,8 @@
 //     their transposes (the backward's gathers): msg_gather_t row j = the rows b with src(b) = dst(j) in
 //     increasing b, atom_gather_t row j = (dst(j), w_j);
 //   * the ELL-8 rows, the block maps, b2revb, w_atoms and the molecule scope arrays.
+// A lean graph (WDMPNN_GRAPH_LEAN) gets only what the fused inference forward reads: the atom gather
+// (CSR + ELL), the block maps, b2revb, the bonds' source atoms and tails, the scope arrays.
 // Pair structure: bond ids 1 + 2p and 2 + 2p are pair p's b1 = a1 -> a2 and b2 = a2 -> a1 (pad bond 0),
 // so every molecule's first bond id is odd and a block-local bond index lb has rev(lb) = lb ^ 1.
 #pragma once
@@ -58,8 +60,11 @@ __device__ __forceinline__ void put_row8(float *row_f32, uint8_t *planes, int ld
     x6_store8<64>(planes, ld, r, c0, lo, hi);
 }
 
-__global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
-    const int tid = threadIdx.x, k = blockIdx.x;
+// grid: per batch its n_blocks + 1 workgroups (Multi: up to WD_MULTI batches per launch)
+__global__ __launch_bounds__(256) void graph_build_kernel(const Multi<GraphBuildP> MP) {
+    int k;
+    const GraphBuildP &P = multi_pick(MP, (int)blockIdx.x, k);
+    const int tid = threadIdx.x;
     const WdCompact &C = P.c;
     const int Fa = P.Fa, Fb = P.Fb, UA = P.lda / 8, UB = P.ldb / 8;
     if (k == C.n_blocks) {  // pad rows: atom / bond row 0, the rows up to the padded extents, CSR heads and tails
@@ -84,17 +89,21 @@ __global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
             P.bond_blk_row[r] = -1;
             P.bond_src_blk[r] = 0;
             P.bond_tail[r] = 0;
-            for (int s = 0; s < GB_ELLW; ++s) { P.msg_ell_idx[GB_ELLW * r + s] = 0; P.msg_ell_coef[GB_ELLW * r + s] = 0.f; }
+            if (!P.lean)
+                for (int s = 0; s < GB_ELLW; ++s) { P.msg_ell_idx[GB_ELLW * r + s] = 0; P.msg_ell_coef[GB_ELLW * r + s] = 0.f; }
         }
         if (tid < 2) {  // row 0 (pad atom / bond) has no entries
-            P.msg_ptr[tid] = 0; P.msgt_ptr[tid] = 0; P.aggt_ptr[tid] = 0; P.agg_ptr[tid] = 0;
+            P.agg_ptr[tid] = 0;
+            if (!P.lean) { P.msg_ptr[tid] = 0; P.msgt_ptr[tid] = 0; P.aggt_ptr[tid] = 0; }
         }
         if (tid == 0) { P.w_atoms[0] = 0.f; P.b2revb[0] = 0; }
         if (tid < GB_CSR_PAD) {  // readable dummy entries past the end (WdCsr)
-            P.msg_idx[C.nnz_msg + tid] = 0; P.msg_coef[C.nnz_msg + tid] = 0.f;
-            P.msgt_idx[C.nnz_msg + tid] = 0; P.msgt_coef[C.nnz_msg + tid] = 0.f;
             P.agg_idx[C.nnz_agg + tid] = 0; P.agg_coef[C.nnz_agg + tid] = 0.f;
-            P.aggt_idx[C.nnz_agg + tid] = 0; P.aggt_coef[C.nnz_agg + tid] = 0.f;
+            if (!P.lean) {
+                P.msg_idx[C.nnz_msg + tid] = 0; P.msg_coef[C.nnz_msg + tid] = 0.f;
+                P.msgt_idx[C.nnz_msg + tid] = 0; P.msgt_coef[C.nnz_msg + tid] = 0.f;
+                P.aggt_idx[C.nnz_agg + tid] = 0; P.aggt_coef[C.nnz_agg + tid] = 0.f;
+            }
         }
         return;
     }
@@ -219,7 +228,7 @@ __global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
     }
     __syncthreads();
     const int om = s_off[0], oa = s_off[1];
-    if (tid < bn) {
+    if (tid < bn && !P.lean) {  // (a lean graph serves only the fused forward, which gathers by src / rev)
         const int b = bs + tid, s = s_src[tid], rev = tid ^ 1;
         // msg_gather row b + its ELL-8 row
         int o = om + s_pm[tid], n = 0;
@@ -244,7 +253,7 @@ __global__ __launch_bounds__(256) void graph_build_kernel(GraphBuildP P) {
             P.msg_ell_idx[(size_t)GB_ELLW * b + q] = eidx[q];
             P.msg_ell_coef[(size_t)GB_ELLW * b + q] = ecoef[q];
         }
-        if (!P.lean) {  // (a lean graph has no transposed gathers: the backward never runs on it)
+        {
             // msg_gather_t row b: the rows lb in out(dst(b)), increasing lb
             o = om + s_pt[tid];
             const int d = s_dst[tid];

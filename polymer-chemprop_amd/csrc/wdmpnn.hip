@@ -764,6 +764,9 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
 // ================================================================================================
 // C-ABI
 // ================================================================================================
+int graph_build_prepare(const WdCompact *c, void *buffer, size_t bytes, int32_t flags, GraphBuildP &P, WdGraph &Gout);
+int graph_build_launch(const GraphBuildP *P, int n, hipStream_t st);
+
 extern "C" {
 
 int wdmpnn_abi_version(void) { return WDMPNN_ABI_VERSION; }
@@ -1248,11 +1251,26 @@ int wdmpnn_build_graph(const WdCompact *c, void *buffer, size_t bytes, WdGraph *
 }
 
 int wdmpnn_build_graph_ex(const WdCompact *c, void *buffer, size_t bytes, WdGraph *g, int32_t flags, void *stream) {
+    Multi<GraphBuildP> M{};
+    if (!g) return fail(WD_ERR_ARG, "null graph");
+    WD_TRY(graph_build_prepare(c, buffer, bytes, flags, M.p[0], *g));
+    M.n = 1;
+    M.t0[0] = 0;
+    for (int j = 1; j <= WD_MULTI; ++j) M.t0[j] = c->n_blocks + 1;
+    hipLaunchKernelGGL(graph_build_kernel, dim3(c->n_blocks + 1), dim3(256), 0, (hipStream_t)stream, M);
+    WD_CHECK_LAUNCH("graph_build");
+    return 0;
+}
+
+}  // extern "C"
+
+// the build parameters and the WdGraph of a compact batch in `buffer` (no launch)
+int graph_build_prepare(const WdCompact *c, void *buffer, size_t bytes, int32_t flags, GraphBuildP &P, WdGraph &Gout) {
     if (flags & ~WDMPNN_GRAPH_LEAN) return fail(WD_ERR_ARG, "unknown graph build flags 0x%x", flags);
     const bool lean = flags & WDMPNN_GRAPH_LEAN;
     GraphLayout L;
     WD_TRY(graph_layout(c, L));
-    if (!buffer || !g) return fail(WD_ERR_ARG, "null buffer / graph");
+    if (!buffer) return fail(WD_ERR_ARG, "null buffer");
     if (bytes < L.total) return fail(WD_ERR_WORKSPACE, "graph buffer too small: need %zu bytes, got %zu", L.total, bytes);
     if ((uintptr_t)buffer % 256) return fail(WD_ERR_ARG, "graph buffer must be 256-byte aligned");
     if (c->n_mols && (!c->mols || !c->xn)) return fail(WD_ERR_ARG, "null molecule arrays");
@@ -1262,7 +1280,7 @@ int wdmpnn_build_graph_ex(const WdCompact *c, void *buffer, size_t bytes, WdGrap
     auto F = [&](size_t o) { return (float *)(base + o); };
     auto I = [&](size_t o) { return (int32_t *)(base + o); };
     auto U = [&](size_t o) { return (uint8_t *)(base + o); };
-    GraphBuildP P{};
+    P = GraphBuildP{};
     P.c = *c;
     P.Fa = c->atom_fdim; P.Fb = c->bond_fdim; P.lda = L.lda; P.ldb = L.ldb; P.Vap = L.Vap; P.Rbp = L.Rbp;
     P.f_atoms = F(L.f_atoms); P.f_bonds = F(L.f_bonds);
@@ -1278,8 +1296,6 @@ int wdmpnn_build_graph_ex(const WdCompact *c, void *buffer, size_t bytes, WdGrap
     P.msgt_ptr = I(L.csr[2][0]); P.msgt_idx = I(L.csr[2][1]); P.msgt_coef = F(L.csr[2][2]);
     P.aggt_ptr = I(L.csr[3][0]); P.aggt_idx = I(L.csr[3][1]); P.aggt_coef = F(L.csr[3][2]);
     P.lean = lean;
-    hipLaunchKernelGGL(graph_build_kernel, dim3(c->n_blocks + 1), dim3(256), 0, (hipStream_t)stream, P);
-    WD_CHECK_LAUNCH("graph_build");
     WdGraph G{};
     G.n_atoms = c->n_atoms; G.n_bonds = c->n_bonds; G.n_mols = c->n_mols;
     G.atom_fdim = c->atom_fdim; G.bond_fdim = c->bond_fdim; G.ld_atoms = L.lda; G.ld_bonds = L.ldb; G.bond_col0 = 0;
@@ -1301,12 +1317,33 @@ int wdmpnn_build_graph_ex(const WdCompact *c, void *buffer, size_t bytes, WdGrap
     if (lean) {  // what was not built is not handed out: a path that needs it fails in get_dims
         G.f_atoms = G.f_bonds = nullptr;
         G.f_atoms_x6 = G.f_bonds_x6 = G.f_atoms_blk_x6 = nullptr;
-        G.msg_gather_t = WdCsr{nullptr, nullptr, nullptr};
+        G.msg_gather = G.msg_gather_t = WdCsr{nullptr, nullptr, nullptr};
         G.atom_gather_t = WdCsr{nullptr, nullptr, nullptr};
+        G.msg_ell_idx = nullptr; G.msg_ell_coef = nullptr;
     }
-    *g = G;
+    Gout = G;
     return 0;
 }
+
+// several prepared builds in one launch (the stream feed), chunks of WD_MULTI
+int graph_build_launch(const GraphBuildP *P, int n, hipStream_t st) {
+    for (int j0 = 0; j0 < n; j0 += WD_MULTI) {
+        Multi<GraphBuildP> M{};
+        M.n = std::min(WD_MULTI, n - j0);
+        int t = 0;
+        for (int j = 0; j < M.n; ++j) {
+            M.p[j] = P[j0 + j];
+            M.t0[j] = t;
+            t += P[j0 + j].c.n_blocks + 1;
+        }
+        for (int j = M.n; j <= WD_MULTI; ++j) M.t0[j] = t;
+        hipLaunchKernelGGL(graph_build_kernel, dim3(t), dim3(256), 0, st, M);
+        WD_CHECK_LAUNCH("graph_build");
+    }
+    return 0;
+}
+
+extern "C" {
 
 // ------------------------------------------------------------------------------------------------
 // native streamed batches (feed.hpp)
@@ -1353,7 +1390,12 @@ int wdmpnn_feed_create(const WdFeedSpec *spec, void **feed) {
     }
     F->host_bytes = hb; F->dev_bytes = db; F->graph_off = hb;
     F->slot.resize((size_t)F->R);
-    bool ok = hipStreamCreateWithFlags(&F->fs, hipStreamNonBlocking) == hipSuccess;
+    // the feed stream at the highest priority: a graph build is a short, latency-bound launch (one
+    // workgroup per molecule block); dispatched ahead of the queued forward workgroups it finishes while
+    // the forward keeps the CUs busy, instead of waiting behind them
+    int lo_pri = 0, hi_pri = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri);
+    bool ok = hipStreamCreateWithPriority(&F->fs, hipStreamNonBlocking, hi_pri) == hipSuccess;
     for (int s = 0; s < F->R && ok; ++s) {
         Feed::Slot &Q = F->slot[(size_t)s];
         Q.turn = s;
