@@ -104,6 +104,13 @@ class GradBucket:
             if p.grad is None or p.grad.data_ptr() != v.data_ptr():
                 p.grad = v  # a grad replaced by an optimizer / user: re-attach the view
 
+    def attach(self) -> None:
+        """Re-attach the views as the parameters' gradients without zeroing (a step that overwrites every
+        gradient: train.py's direct path)."""
+        for p, v in zip(self.params, self._views()):
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                p.grad = v
+
     def _views(self) -> Iterable[torch.Tensor]:
         off = 0
         for p in self.params:

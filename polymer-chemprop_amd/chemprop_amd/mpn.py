@@ -85,33 +85,38 @@ class _EncoderFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         W_i, b_i, W_h, b_h, W_o, b_o, W_d, b_d, prelu = ctx.saved_tensors
-        L = _native.lib()
-        dev = dout.device
-        dout = dout.contiguous()
-        nbytes = ctypes.c_size_t()
-        _native.check(L.wdmpnn_backward_workspace_bytes(ctypes.byref(ctx.gstruct), ctypes.byref(ctx.p),
-                                                        ctypes.byref(ctx.cfg), ctypes.byref(nbytes)),
-                      'MPNEncoder backward workspace')
-        scratch = torch.empty(max(nbytes.value, 256), dtype=torch.uint8, device=dev)
         want = ctx.needs_input_grad
-        grads = {}
-        g = _native.WdGrads()
         first = 7  # position of W_i in forward's arguments
+        out = {}
         for k, (name, t) in enumerate((('W_i', W_i), ('b_i', b_i), ('W_h', W_h), ('b_h', b_h), ('W_o', W_o),
                                        ('b_o', b_o), ('W_d', W_d), ('b_d', b_d), ('prelu', prelu))):
             if name in ('W_h', 'b_h') and ctx.cfg.depth == 1:
                 continue  # unused when depth == 1 (mpn.py:100 loop body never runs): no gradient, like autograd
             if t is not None and want[first + k]:
-                grads[name] = torch.empty_like(t)
-                setattr(g, name, grads[name].data_ptr())
-        _native.check(L.wdmpnn_backward(ctypes.byref(ctx.gstruct), ctypes.byref(ctx.p), ctypes.byref(ctx.cfg),
-                                        ctx.ws.data_ptr(), ctx.ws_bytes, dout.data_ptr(), scratch.data_ptr(),
-                                        nbytes.value, ctypes.byref(g), _native.current_stream(dev)),
-                      'MPNEncoder backward')
+                out[name] = torch.empty_like(t)
+        _backward_call(ctx.gstruct, ctx.p, ctx.cfg, ctx.ws, ctx.ws_bytes, dout, out)
         # ctx.ws stays alive until autograd frees ctx: a second backward through the same graph
         # (retain_graph=True) reads the same saved forward state
-        return (None,) * 7 + tuple(grads.get(n) for n in ('W_i', 'b_i', 'W_h', 'b_h', 'W_o', 'b_o', 'W_d', 'b_d',
-                                                           'prelu'))
+        return (None,) * 7 + tuple(out.get(n) for n in ('W_i', 'b_i', 'W_h', 'b_h', 'W_o', 'b_o', 'W_d', 'b_d',
+                                                         'prelu'))
+
+
+def _backward_call(gstruct, pstruct, cfg, ws, ws_bytes, dout, grads):
+    """One wdmpnn_backward into the tensors of ``grads`` (name -> tensor, names of WdGrads; absent names
+    are not computed)."""
+    L = _native.lib()
+    dev = dout.device
+    dout = dout.contiguous()
+    nbytes = ctypes.c_size_t()
+    _native.check(L.wdmpnn_backward_workspace_bytes(ctypes.byref(gstruct), ctypes.byref(pstruct), ctypes.byref(cfg),
+                                                    ctypes.byref(nbytes)), 'MPNEncoder backward workspace')
+    scratch = torch.empty(max(nbytes.value, 256), dtype=torch.uint8, device=dev)
+    g = _native.WdGrads()
+    for name, t in grads.items():
+        setattr(g, name, t.data_ptr())
+    _native.check(L.wdmpnn_backward(ctypes.byref(gstruct), ctypes.byref(pstruct), ctypes.byref(cfg), ws.data_ptr(),
+                                    ws_bytes, dout.data_ptr(), scratch.data_ptr(), nbytes.value, ctypes.byref(g),
+                                    _native.current_stream(dev)), 'MPNEncoder backward')
 
 
 def saved_preactivations(out: torch.Tensor):
@@ -240,6 +245,33 @@ class MPNEncoder(nn.Module):
         _native.check(_native.lib().wdmpnn_forward(plan[0], ctypes.byref(pstruct), plan[1], ws.data_ptr(), plan[2],
                                                    out.data_ptr(), stream.cuda_stream), 'MPNEncoder forward')
         return out
+
+    # ---------------------------------------------------------------- direct training step (train.py)
+    def _direct_names(self):
+        """(name, parameter) pairs the native backward fills, in WdGrads order (no descriptors)."""
+        base = self._param_tuple()
+        names = ('W_i', 'b_i', 'W_h', 'b_h', 'W_o', 'b_o', 'W_d', 'b_d', 'prelu')
+        return [(n, t) for n, t in zip(names, base) if t is not None]
+
+    def _train_forward(self, mol_graph):
+        """The training forward of ``forward`` (save_for_backward) without autograd: (out, state) for
+        :meth:`_train_backward`.  Used by ``train.train_step``'s direct path, whose fused head computes the
+        encoder's output gradient itself."""
+        base = self._param_tuple()
+        device = base[0].device
+        dg = mol_graph.device_graph(device, self.atom_messages, self.bond_fdim)
+        dg.use_on(torch.cuda.current_stream(device))
+        gs = self._graph_struct(dg)
+        params = [_f32(t) for t in base[:6]] + [None, None, _f32(base[8])]
+        cfg = self._config(True)
+        pstruct, packed, pack = self._packed_params(gs, cfg, params, device, cache=False, defer=True)
+        out, ws, ws_bytes = _forward_call(gs, cfg, pstruct, self.hidden_size, device, pre_launch=pack)
+        return out, (gs, cfg, pstruct, ws, ws_bytes, packed, dg)
+
+    def _train_backward(self, state, dout, grads) -> None:
+        """wdmpnn_backward of a :meth:`_train_forward` into ``grads`` (name -> tensor, WdGrads names)."""
+        gs, cfg, pstruct, ws, ws_bytes, packed, dg = state
+        _backward_call(gs, pstruct, cfg, ws, ws_bytes, dout, grads)
 
     def forward_many(self, mol_graphs: List[BatchMolGraph]) -> List[torch.Tensor]:
         """Inference forward of several independent batches in one set of launches

@@ -321,28 +321,105 @@ def head_loss(emb: torch.Tensor, head, target_batch, target_weights=None, data_w
     return _HeadMSE.apply(emb, l1.weight, l1.bias, l2.weight, l2.bias, table, inv_n, act)
 
 
+def _grad_buffer(p: torch.Tensor) -> torch.Tensor:
+    """The tensor a direct step writes p's gradient into: p.grad when it can be overwritten in place (a
+    GradBucket view, or the last step's gradient), else a fresh one (installed as p.grad)."""
+    g = p.grad
+    if g is None or g.shape != p.shape or g.dtype != torch.float32 or not g.is_contiguous() or g.device != p.device:
+        g = torch.empty_like(p)
+        p.grad = g
+    return g
+
+
+def _direct_encoder(model: nn.Module, mol_batch, features_batch):
+    """The MPNEncoder when the step can skip autograd: one molecule per input, no extra features or
+    descriptors, depth >= 2, every parameter trainable; else None."""
+    from .model import MoleculeModel
+    from .mpn import MPNEncoder
+    if not isinstance(model, MoleculeModel) or type(model).forward is not MoleculeModel.forward:
+        return None
+    mpn = model.encoder
+    if features_batch is not None or mpn.features_only or mpn.use_input_features or mpn.atom_descriptors or \
+            len(mpn.encoder) != 1 or not isinstance(mol_batch, (list, tuple)) or len(mol_batch) != 1:
+        return None
+    enc = mpn.encoder[0]
+    if type(enc) is not MPNEncoder or enc.depth < 2 or enc.atom_messages or hasattr(enc, 'atom_descriptors_layer'):
+        return None
+    if type(mol_batch[0]).__name__ != 'BatchMolGraph':
+        return None
+    if any(not p.requires_grad for n, p in model.named_parameters() if not n.endswith('cached_zero_vector')):
+        return None
+    return enc
+
+
+def _direct_step(model, enc, graph, head, target_batch, target_weights, data_weights) -> torch.Tensor:
+    """Forward, loss and every gradient of a fused-head step without the autograd engine: the encoder's
+    training forward, wdmpnn_head_mse (loss, d loss / d encoding, the head's gradients) and the encoder's
+    backward on that gradient (the incoming gradient of the loss is 1), each written straight into the
+    parameters' .grad buffers.  The same launches as the autograd path minus its host gaps (the engine
+    hand-off, the gradient-seed fill and the scale by 1; profiles/round3_*)."""
+    from . import _native
+    l1, l2, act = head
+    out, state = enc._train_forward(graph)
+    table, n_t, n_mask = _loss_table(target_batch, target_weights, data_weights, out.device)
+    if n_t != l2.out_features:
+        raise ValueError(f'{n_t} targets per row for {l2.out_features} outputs')
+    if table.shape[0] != out.shape[0] or out.shape[1] != l1.in_features:
+        raise ValueError(f'{table.shape[0]} target rows for encodings of shape {tuple(out.shape)} '
+                         f'(FFN input {l1.in_features})')
+    inv_n = 1.0 / n_mask if n_mask else float('inf')
+    dev = out.device
+    B, F = out.shape
+    Hf, T = l1.weight.shape[0], l2.weight.shape[0]
+    scratch = torch.empty(B * (2 * Hf + T + 1), dtype=torch.float32, device=dev)
+    dx = torch.empty_like(out)
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    dW1, dW2 = _grad_buffer(l1.weight), _grad_buffer(l2.weight)
+    db1 = _grad_buffer(l1.bias) if l1.bias is not None else None
+    db2 = _grad_buffer(l2.bias) if l2.bias is not None else None
+    ptr = _native.ptr
+    sp = scratch.data_ptr()
+    h = _native.WdHead(ptr(out), F, B, F, Hf, T, ptr(l1.weight), ptr(l1.bias), ptr(l2.weight), ptr(l2.bias), ptr(table),
+                       table.shape[1], float(inv_n), act, sp, sp + 4 * B * Hf, sp + 8 * B * Hf, sp + 4 * B * (2 * Hf + T),
+                       ptr(dx), ptr(dW1), ptr(db1), ptr(dW2), ptr(db2), ptr(loss))
+    _native.check(_native.lib().wdmpnn_head_mse(ctypes.byref(h), _native.current_stream(dev)), 'FFN head + loss')
+    enc._train_backward(state, dx, {n: _grad_buffer(p) for n, p in enc._direct_names()})
+    return loss
+
+
 def train_step(model: nn.Module, mol_batch, target_batch, loss_func: Callable, optimizer: Optimizer,
                scheduler: _LRScheduler = None, dataset_type: str = 'regression', features_batch=None,
                target_weights=None, data_weights=None, grad_clip: float = None,
-               bucket: GradBucket = None, fused_head: bool = True) -> torch.Tensor:
+               bucket: GradBucket = None, fused_head: bool = True, direct: bool = True) -> torch.Tensor:
     """One optimisation step (train.py:55-86).  With ``bucket`` the gradients are averaged over the
     data-parallel ranks (one all-reduce) before clipping and the optimizer step.  ``fused_head``: the
     default regression head + loss run as ``wdmpnn_head_mse`` (same loss and gradients within fp32
-    summation order; ``False`` = the torch ops of the reference)."""
+    summation order; ``False`` = the torch ops of the reference).  ``direct``: with the fused head and a
+    plain one-molecule encoder, skip the autograd engine (``_direct_step``: the same launches and results,
+    bitwise, without the engine's host gaps)."""
     if not model.training:  # (module.train() walks every submodule: the reference sets it once per epoch)
         model.train()
-    if bucket is not None:
+    head = _fusable_head(model, loss_func, dataset_type) if fused_head else None
+    enc = _direct_encoder(model, mol_batch, features_batch) if head is not None and direct else None
+    if enc is not None:
+        # every trainable parameter's gradient is overwritten: no zeroing, no autograd
+        if bucket is not None:
+            bucket.attach()
+        loss = _direct_step(model, enc, mol_batch[0], head, target_batch, target_weights, data_weights)
+    elif bucket is not None:
         bucket.zero()
     else:
         optimizer.zero_grad(set_to_none=True)  # (the optimizer holds every model parameter: build_optimizer)
-    head = _fusable_head(model, loss_func, dataset_type) if fused_head else None
-    if head is not None:  # the default regression head: ffn + loss + their gradients as two HIP launches
+    if enc is not None:
+        pass
+    elif head is not None:  # the default regression head: ffn + loss + their gradients as two HIP launches
         loss = head_loss(model.encoder(mol_batch, features_batch), head, target_batch, target_weights,
                          data_weights)
     else:
         preds = model(mol_batch, features_batch)
         loss = batch_loss(preds, target_batch, loss_func, dataset_type, target_weights, data_weights)
-    loss.backward()
+    if enc is None:
+        loss.backward()
     if bucket is not None:
         bucket.allreduce_mean()
     if grad_clip:

@@ -337,17 +337,20 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN, 4) void mp_
 //     Ea[a]  = sum_{c in code(a)} W_i[:, c] + last(a) W_i[:, Fa-1]          (per atom of the block)
 //     inp[b] = Ea[src(b)] + sum_{k in tail(b)} W_i[:, Fa + k] (+ b_i)       (per bond)
 //     M0[b]  = act(inp[b])
-// One workgroup per (block, BN-column tile), the tile's W_i^T rows staged in LDS.  Writes inp (fp32,
-// natural rows: the residual of every layer) and M0 (plane tiles, blocked rows).  Every global load of
-// the workgroup (atom codes, the weight tile, the bonds' source atoms and tail bits) is issued up front,
-// so the kernel waits for memory once.  (The f_atoms half of W_o is summed the same way in
-// wo_readout_kernel's epilogue.)
+//     Eo[a]  = sum_{c in code(a)} W_o[:, c] + last(a) W_o[:, Fa-1]          (the f_atoms half of W_o)
+// One workgroup per (block, BN-column tile), the tile's W_o[:, :Fa]^T and then W_i^T rows staged in LDS.
+// Writes inp (fp32, natural rows: the residual of every layer), M0 (plane tiles, blocked rows) and Eo
+// (fp32, blocked atom rows) for wo_readout_kernel's epilogue.  Every global load of the workgroup (atom
+// codes, both weight tiles, the bonds' source atoms and tail bits) is issued up front, so the kernel
+// waits for memory once.
 // ------------------------------------------------------------------------------------------------
 struct EmbedP {
     const WdAtomCode *codes;     // natural atom rows
     const uint8_t *src_blk;      // per natural bond row: block-local source atom
     const uint16_t *tail;        // per natural bond row: bond columns as bits
     const float *wt;             // W_i^T [>= Fb][Hk] (fp32, packed)
+    const float *woat;           // W_o[:, :Fa]^T [>= Fa][Hk] (fp32, packed)
+    float *eo;                   // [nblk * 64][Hk]
     const float *bias;           // b_i (padded) or null
     const int32_t *blocks;
     int Fa, Fb, Hk, n_tiles;
@@ -393,10 +396,11 @@ __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP> MP) {
     if (tid < B.an) cd = reinterpret_cast<const u32x4 *>(P.codes)[B.as + tid];
     float4 bq = f4zero();
     if (tid >= NT - C4 && P.bias) bq = ld4(P.bias + n0 + 4 * (tid - (NT - C4)));
-    float4 ri[PER];
+    float4 ro[PER], ri[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const int v = tid + NT * q, k = v / C4, c = 4 * (v % C4);
+        ro[q] = k < P.Fa ? ld4(P.woat + (size_t)k * P.Hk + n0 + c) : f4zero();
         ri[q] = k < P.Fb ? ld4(P.wt + (size_t)k * P.Hk + n0 + c) : f4zero();
     }
     uint32_t sa[BU], tl[BU];
@@ -411,6 +415,18 @@ __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP> MP) {
     }
     if (tid < B.an) reinterpret_cast<u32x4 *>(code)[tid] = cd;
     if (tid >= NT - C4) st4(bb + 4 * (tid - (NT - C4)), bq);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int v = tid + NT * q, k = v / C4, c = 4 * (v % C4);
+        if (k < P.Fa) st4(wt + k * BN + c, ro[q]);
+    }
+    __syncthreads();
+    // Eo[a] = sum_{c in code(a)} W_o[:, c] + last(a) W_o[:, Fa-1] (the f_atoms half of W_o)
+    for (int v = tid; v < B.an * C4; v += NT) {
+        const int la = v / C4, c = 4 * (v % C4);
+        st4(P.eo + ((size_t)blk * BLK_ATOMS + la) * P.Hk + n0 + c, code_sum<BN>(code[la], wt, P.Fa, c));
+    }
+    __syncthreads();  // every read of the W_o tile done
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const int v = tid + NT * q, k = v / C4, c = 4 * (v % C4);
@@ -469,11 +485,9 @@ struct WoReadoutP {
     int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;
     float *out; int ncols;                   // out [B][ncols] (ncols = H)
     int n_tiles;
-    // categorical codes (kca = 0): the f_atoms half of [f_atoms | A] W_o^T summed per atom from the
-    // W_o[:, :Fa]^T rows of its code (code_sum); codes null: the GEMM's f_atoms segment
-    const WdAtomCode *codes;     // natural atom rows
-    const float *woat;           // W_o[:, :Fa]^T [>= Fa][Hk] (fp32, packed)
-    int Fa;
+    // categorical codes (kca = 0): the f_atoms half of [f_atoms | A] W_o^T, precomputed per atom by
+    // embed_kernel as sums of W_o columns: fp32 [nblk * 64][Hk], blocked atom rows (null: GEMM segment)
+    const float *eo;
     int Hk;
     float *zosave;  // training forward or null: the W_o pre-activation (mpn.py:133) as fp32 natural atom rows [Vap][Hk]
 };
@@ -482,26 +496,20 @@ template <int BN> struct WoWaves;
 template <> struct WoWaves<64> { static constexpr int WM = 4, WN = 2; };
 template <> struct WoWaves<80> { static constexpr int WM = 2, WN = 5; };
 
-// grid = nblk * n_tiles: 64 atom rows x BN columns per workgroup.
-template <int BN>
+// grid = nblk * n_tiles: 64 atom rows x BN columns per workgroup.  CPS: K chunks per LDS stage (one
+// barrier per CPS chunks; two stages).  80-column tiles: CPS 2 (W_o's 64-row chunks are short: one barrier
+// per chunk cost 0.6 us alone on the chip, 12.5 vs 13.1 us) for launches of several batches, where
+// workgroups queue per CU; CPS 1 (55 KB of LDS) for one batch, whose 256 workgroups then co-reside
+// with the layer kernels of batches in flight on other streams (+5 % with two streams, same-box A/B,
+// profiles/round3_*).  64-column tiles: CPS 1.
+template <int BN, int CPS>
 __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_readout_kernel(const Multi<WoReadoutP> MP) {
     constexpr int BM = BLK_ATOMS, LDC = BN + 4, WM = WoWaves<BN>::WM, WN = WoWaves<BN>::WN, NT = 64 * WM * WN;
-    // 80-column tiles (one workgroup per CU at the benchmark size): two chunks per barrier, since W_o's
-    // 64-row chunks are short and one barrier per chunk cost 0.6 us (12.5 vs 13.1 us; three
-    // single-chunk stages measured 15.1 us).  64-column tiles (large batches, several workgroups per
-    // CU) keep one chunk per barrier and half the LDS
     // (deeper single-chunk pipelines, with the mainloop hook's loads ordered ahead of the partial vmcnt
     // waits, measured slower: three / four stages 15.1 / 14.8 us here, 12.8 / 11.8 against 9.7 us on
     // QM9-shaped batches)
-#ifndef WD_WO_CPS80
-#define WD_WO_CPS80 2
-#endif
-    constexpr int CPS = BN == 80 ? WD_WO_CPS80 : 1;
     constexpr int WS = 2;  // LDS stages
-    // epilogue: h tile, atom weights, molecule table, then (codes) the W_o[:, :Fa]^T tile and the codes
-    constexpr int EPI_W = BM * LDC + BM + 3 * BLK_MOLS, EPI_BYTES = (EPI_W + WO_MAXK * BN) * 4 + BM * 16;
-    constexpr int LDS_BYTES = WS * CPS * x6_stage_bytes<BM, BN>() > EPI_BYTES ? WS * CPS * x6_stage_bytes<BM, BN>()
-                                                                             : EPI_BYTES;
+    constexpr int LDS_BYTES = WS * CPS * x6_stage_bytes<BM, BN>();
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
     int tile;
     const WoReadoutP &P = multi_pick(MP, xcd_tile(blockIdx.x, gridDim.x), tile);
@@ -525,21 +533,17 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     float4 bb = f4zero();
     float watom = 0.f, mxn = 0.f;
     int mstart = 0, msize = 0;
-    // codes path: the block's atom codes (thread a < an) and this thread's share of the W_o[:, :Fa]^T tile
-    constexpr int EPU = (BM * C4 + NT - 1) / NT, WP = (WO_MAXK * C4 + NT - 1) / NT;
-    u32x4 cd = {0u, 0u, 0u, 0u};  // (raw words: a struct with a byte array was promoted to LDS)
-    float4 wq[WP];
+    // codes path: this thread's rows of the precomputed f_atoms W_o[:, :Fa]^T (the epilogue units below)
+    constexpr int EPU = (BM * C4 + NT - 1) / NT;
+    float4 eo[EPU];
     auto prefetch = [&](int phase) {
         if (phase != 0) return;
         bb = ld4(P.bias + n0 + 4 * (tid % C4));
         if (tid < B.an) watom = P.w_atoms[B.as + tid];
-        if (P.codes) {
-            if (tid < B.an) cd = reinterpret_cast<const u32x4 *>(P.codes)[B.as + tid];
 #pragma unroll
-            for (int j = 0; j < WP; ++j) {
-                const int v = tid + NT * j, k = v / C4, c = 4 * (v % C4);
-                wq[j] = k < P.Fa ? ld4(P.woat + (size_t)k * P.Hk + n0 + c) : f4zero();
-            }
+        for (int j = 0; j < EPU; ++j) {
+            const int v = tid + NT * j, la = v / C4, c = 4 * (v % C4);
+            eo[j] = P.eo && v < BM * C4 && la < B.an ? ld4(P.eo + ((size_t)blk * BM + la) * P.Hk + n0 + c) : f4zero();
         }
         if (tid < nm) {
             mstart = P.mol_start[B.ml + tid];
@@ -553,18 +557,9 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     float *H = reinterpret_cast<float *>(lds);
     float *Wl = H + BM * LDC;           // [BM] atom weights of the block
     float *Ml = Wl + BM;                // [3][BLK_MOLS] per molecule: start (as float bits), size, Xn
-    float *Wt = H + EPI_W;              // codes: W_o[:, :Fa]^T tile [Fa][BN]
-    WdAtomCode *Cl = reinterpret_cast<WdAtomCode *>(Wt + WO_MAXK * BN);  // codes: [BM]
+    static_assert((BM * LDC + BM + 3 * BLK_MOLS) * 4 <= LDS_BYTES, "readout staging fits");
     static_assert(BLK_MOLS <= NT, "one molecule per thread in the prefetch");
     x6_acc_to_lds<BM, BN, WM, WN>(acc, H);
-    if (P.codes) {
-        if (tid < B.an) reinterpret_cast<u32x4 *>(Cl)[tid] = cd;
-#pragma unroll
-        for (int j = 0; j < WP; ++j) {
-            const int v = tid + NT * j, k = v / C4, c = 4 * (v % C4);
-            if (k < P.Fa) st4(Wt + k * BN + c, wq[j]);
-        }
-    }
     if (tid < BM) Wl[tid] = watom;
     if (tid < nm) {
         Ml[tid] = __int_as_float(mstart);
@@ -582,10 +577,7 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
             if (v >= BM * C4) break;
             const int la = v / C4, c = 4 * (v % C4);
             float4 hv = ld4(H + la * LDC + c);
-            if (P.codes && la < B.an) {  // + f_atoms W_o[:, :Fa]^T (mpn.py:132-133), as code_sum
-                const float4 eo = code_sum<BN>(Cl[la], Wt, P.Fa, c);
-                hv.x += eo.x; hv.y += eo.y; hv.z += eo.z; hv.w += eo.w;
-            }
+            hv.x += eo[j].x; hv.y += eo[j].y; hv.z += eo[j].z; hv.w += eo[j].w;  // (0 without codes)
             float z[4] = {hv.x + bb.x, hv.y + bb.y, hv.z + bb.z, hv.w + bb.w};
             if (P.zosave && la < B.an) st4(P.zosave + (size_t)(B.as + la) * P.Hk + n0 + c, make_float4(z[0], z[1], z[2], z[3]));
 #pragma unroll

@@ -466,6 +466,7 @@ struct FwdLayout {
     size_t packed = 0, A = 0, Zo = 0, h = 0, Zd = 0, hd = 0, total = 0;
     size_t Xp = 0, Ap = 0;  // plane tiles of X_t and A (D.x6)
     size_t Mb[2] = {0, 0}, Ab = 0;  // molecule-blocked plane tiles of M_t (ping-pong) and A (D.blocked)
+    size_t Eo = 0;                  // D.blocked: f_atoms W_o[:, :Fa]^T per blocked atom row (compact codes)
     bool own_pack = false;
 };
 
@@ -486,6 +487,7 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
     if (D.blocked) {
         for (int i = 0; i < 2; ++i) L.Mb[i] = take((size_t)D.nblk * BLK_BONDS * D.Hk * 6);
         L.Ab = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 6);
+        L.Eo = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 4);
     } else if (D.x6) {
         if (D.T > 1) L.Xp = take((size_t)D.Rp * D.Hk * 6);
         L.Ap = take((size_t)D.Vap * D.Hk * 6);
@@ -669,14 +671,17 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
     if (codes) {
         // 40-column tiles when they divide Hk: twice the workgroups of the layer tiling (two per CU at the
         // benchmark size, 37 KB of LDS each), so one's staging overlaps the other's sums
-        const bool bn40 = Hk % 40 == 0;
+#ifndef WD_EMBED_BN40
+#define WD_EMBED_BN40 1
+#endif
+        const bool bn40 = WD_EMBED_BN40 && Hk % 40 == 0;
         const int nt = Hk / (bn40 ? 40 : BNf);
         Multi<EmbedP> M;
         int grid;
         launch_multi(jobs, n, nt, [&](EmbedP &E, const FusedJob &J) {
             const WdGraph *g = J.g;
             E.codes = g->atom_codes; E.src_blk = g->bond_src_blk; E.tail = g->bond_tail;
-            E.wt = W(PL.WiT); E.bias = p->b_i ? W(PL.bi) : nullptr;
+            E.wt = W(PL.WiT); E.woat = W(PL.WoaT); E.eo = F(J, J.L.Eo); E.bias = p->b_i ? W(PL.bi) : nullptr;
             E.blocks = g->blocks;
             E.Fa = J.D.Fa; E.Fb = J.D.Fb; E.Hk = Hk; E.n_tiles = nt;
             E.act = c->activation; E.slope = p->prelu;
@@ -739,7 +744,7 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
         R.fa = g->f_atoms_blk_x6 ? (const uint8_t *)g->f_atoms_blk_x6 : (const uint8_t *)(J.ws + J.L.Ab);
         R.kpa = g->ld_atoms; R.kcw = J.D.Fak / 32;
         R.kca = codes ? 0 : R.kcw;
-        R.codes = codes ? g->atom_codes : nullptr; R.woat = W(PL.WoaT); R.Fa = J.D.Fa; R.Hk = Hk;
+        R.eo = codes ? F(J, J.L.Eo) : nullptr; R.Hk = Hk;
         R.ag = (const uint8_t *)(J.ws + J.L.Ab); R.kp = Hk;
         R.wo = (const uint8_t *)(pk + (bn80 ? PL.WoX80 : PL.WoX)); R.bias = W(PL.bo);
         R.blocks = g->blocks;
@@ -750,10 +755,13 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
         R.zosave = J.D.save ? F(J, J.L.Zo) : nullptr;
     }, M, grid);
     if (grid > 0) {
-        if (bn80)
-            hipLaunchKernelGGL(wo_readout_kernel<80>, dim3(grid), dim3(64 * WoWaves<80>::WM * WoWaves<80>::WN), 0, st, M);
+        // one batch: single-chunk stages (55 KB, co-resident with other streams' layers); several: two
+        if (bn80 && n > 1)
+            hipLaunchKernelGGL((wo_readout_kernel<80, 2>), dim3(grid), dim3(64 * WoWaves<80>::WM * WoWaves<80>::WN), 0, st, M);
+        else if (bn80)
+            hipLaunchKernelGGL((wo_readout_kernel<80, 1>), dim3(grid), dim3(64 * WoWaves<80>::WM * WoWaves<80>::WN), 0, st, M);
         else
-            hipLaunchKernelGGL(wo_readout_kernel<64>, dim3(grid), dim3(64 * WoWaves<64>::WM * WoWaves<64>::WN), 0, st, M);
+            hipLaunchKernelGGL((wo_readout_kernel<64, 1>), dim3(grid), dim3(64 * WoWaves<64>::WM * WoWaves<64>::WN), 0, st, M);
         WD_CHECK_LAUNCH("wo_readout");
     }
     return 0;

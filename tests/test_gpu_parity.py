@@ -403,6 +403,36 @@ def test_training_step_fused_adam_and_pinned_targets():
         assert d <= 1e-6, (n, d)
 
 
+@pytest.mark.parametrize('act,bias', [('ReLU', False), ('PReLU', True), ('tanh', True)])
+def test_direct_training_step_equals_autograd_step(act, bias):
+    """train_step's direct path (no autograd engine: the encoder's training forward, the fused head's
+    gradients and the native backward written straight into .grad) gives the autograd path's losses,
+    gradients and parameters bitwise, over several steps (gradients overwritten, never accumulated), with
+    and without a GradBucket."""
+    from chemprop_amd.dp import GradBucket
+    from chemprop_amd.nn_utils import initialize_weights
+    from chemprop_amd.train import build_optimizer, get_loss_func, train_step
+    args = TrainArgs(hidden_size=48, depth=3, device=DEV, activation=act, bias=bias)
+    graphs = [BatchMolGraph(synthetic.make_batch('polymer', 12, 30 + i), device_bond_features=True) for i in range(3)]
+    targets = [[[0.3 * j - 1.0 + i] for j in range(12)] for i in range(3)]
+    for use_bucket in (False, True):
+        res = []
+        for direct in (True, False):
+            torch.manual_seed(0)
+            m = MoleculeModel(args)
+            initialize_weights(m)
+            m = m.to(DEV)
+            bucket = GradBucket(m) if use_bucket else None
+            opt = build_optimizer(m, 1e-3)
+            losses = [float(train_step(m, [g], t, get_loss_func('regression'), opt, bucket=bucket, direct=direct))
+                      for _ in range(2) for g, t in zip(graphs, targets)]
+            res.append((losses, [q.detach().clone() for q in m.parameters()],
+                        [q.grad.clone() for q in m.parameters() if q.requires_grad]))
+        assert res[0][0] == res[1][0]
+        assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+        assert all(torch.equal(a, b) for a, b in zip(res[0][2], res[1][2]))
+
+
 @pytest.mark.parametrize('kind', ['adam', 'adamw'])
 def test_hip_adam_matches_torch_adam(kind):
     """HipAdam (one wdmpnn_adam_step launch) vs torch's single-tensor Adam / AdamW over 6 steps: weight

@@ -8,7 +8,7 @@ run() {
   local name=$1; shift
   echo "== pmc $name: $*"
   timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/pmc/$name -o run -- \
-      python bench.py --steps 20 --warmup 3 --no-cpu --no-secondary --streams 1 --stream-graphs 0 --stream-train-graphs 0 ${PMC_BENCH_ARGS:-} > gpurun_out/pmc/$name.log 2>&1
+      python bench.py --steps 20 --warmup 3 --no-cpu --no-secondary --streams 1 --many 0 --stream-graphs 0 --stream-train-graphs 0 ${PMC_BENCH_ARGS:-} > gpurun_out/pmc/$name.log 2>&1
   local rc=$?
   echo "== pmc $name rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 gpurun_out/pmc/$name.log; exit $rc; fi
