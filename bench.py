@@ -62,10 +62,30 @@ def _cpu_model():
     return 'unknown'
 
 
+def _usable_cores(fallback):
+    """CPUs this process may run on: its affinity set, capped by the cgroup v2 CPU quota (a GPU box
+    shares its host: the affinity set can list every CPU of the machine while the quota is its share)."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or fallback
+    quota = None
+    try:
+        q, period = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if q != 'max':
+            quota = max(1, int(-(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return (min(affinity, quota) if quota else affinity), affinity, quota
+
+
 def cpu_baseline(args, graph, seconds):
-    """The oracle (op-for-op restatement of the reference forward, oracle/mpn_ref.py; within +-10 % of
-    the real reference at 8 threads, profiles/round2_cpu_port_check.txt) on the GPU box's host cores:
-    median over ~``seconds`` of forwards with torch's thread count, then a shorter 1-thread sample."""
+    """The oracle (op-for-op restatement of the reference forward, oracle/mpn_ref.py) on the GPU box's
+    host cores: median over ~``seconds`` of forwards with torch's thread count set to the cores this
+    process may run on (its affinity set), then a shorter 1-thread sample.  Fidelity to the real
+    reference (profiles/round2_cpu_port_check.txt, 8-CPU build container): at 1 thread the port takes
+    1.09-1.14x the reference's time; at 8 threads 0.86-0.96x, i.e. the port can be up to ~14 % faster
+    than the reference there, which understates the GPU's speed-up over the real reference."""
     from oracle import mpn_ref
     enc = make_encoder(args, torch.device('cpu'))
     p = {n: t.detach() for n, t in enc.named_parameters()}
@@ -81,17 +101,22 @@ def cpu_baseline(args, graph, seconds):
                 times.append(time.perf_counter() - t0)
         return statistics.median(times), len(times)
 
-    threads = torch.get_num_threads()
+    prev = torch.get_num_threads()
+    cores, affinity, quota = _usable_cores(prev)
+    torch.set_num_threads(cores)
     med, n = sample(seconds, 5)
     torch.set_num_threads(1)
     med1, n1 = sample(seconds / 3, 3)
-    torch.set_num_threads(threads)
+    torch.set_num_threads(prev)
     E = graph.n_bonds - 1
-    return {'value': E / med, 'unit': 'edges/s', 'cores': threads, 'kind': 'port',
+    return {'value': E / med, 'unit': 'edges/s', 'cores': cores, 'kind': 'port',
             'sample': f'{n} forwards of one polymer B={len(graph.a_scope)} batch (E={E} directed edges), median '
-                      f'{med * 1e3:.2f} ms at {threads} threads, eval/no_grad',
+                      f'{med * 1e3:.2f} ms at {cores} threads (the CPUs this process may use: affinity set, capped by '
+                      f'the cgroup CPU quota), eval/no_grad',
             'single_thread': {'value': E / med1, 'ms': med1 * 1e3, 'forwards': n1},
-            'host': {'cpu_model': _cpu_model(), 'logical_cpus': os.cpu_count(), 'torch': torch.__version__,
+            'host': {'cpu_model': _cpu_model(), 'logical_cpus': os.cpu_count(), 'affinity_cpus': affinity,
+                     'cgroup_cpu_quota': quota,
+                     'torch_default_threads': prev, 'torch': torch.__version__,
                      'mkl': bool(torch.backends.mkl.is_available()),
                      'mkldnn': bool(torch.backends.mkldnn.is_available())}}
 
@@ -134,7 +159,15 @@ def forward_roofline(graphs, a, t_fwd):
             'note': 'SURVEY 8(d) formulas; combined = max(bytes/8 TB/s, flops/157.3 TF/s) / measured time'}
 
 
-def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_batches=8, streams=1, many=8):
+def default_streams(edges_per_batch):
+    """Batches in flight per GPU for a batch size: two (one per HIP stream) while a batch's layer grid
+    leaves CUs idle in its ramp and epilogue (polymer / QM9-sized batches), one for large batches whose
+    grids fill the chip on their own (ZINC-sized B = 512: two streams measured 50.5 vs 52.6 M edges/s,
+    BENCH_r02.json)."""
+    return 2 if edges_per_batch < 16384 else 1
+
+
+def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_batches=8, streams=None, many=8):
     """Other BASELINE.json configs' shapes (configs[1]: QM9-like molecules, batch 64, depth 3, hidden
     300; configs[3]: ZINC-like molecules, batch 512, depth 5, hidden 512), timed like the headline:
     resident graphs, eval forward, synchronised wall time over ``steps`` forwards, with ``streams``
@@ -145,6 +178,8 @@ def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_b
               for i in range(n_batches)]
     for g in graphs:
         g.device_graph(device, False, get_bond_fdim())
+    if streams is None:
+        streams = default_streams(sum(g.n_bonds - 1 for g in graphs) / len(graphs))
     ss = [torch.cuda.current_stream(device)] + [torch.cuda.Stream(device) for _ in range(streams - 1)]
 
     def timed(n_streams):
@@ -342,7 +377,8 @@ def main():
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--no-secondary', action='store_true', help='skip the QM9 / ZINC-shaped secondary workloads')
-    ap.add_argument('--streams', type=int, default=2, help='batches in flight per GPU (one HIP stream each)')
+    ap.add_argument('--streams', type=int, default=0,
+                    help='batches in flight per GPU (one HIP stream each); 0 = by batch size (default_streams)')
     ap.add_argument('--many', type=int, default=4, help='batches per MPNEncoder.forward_many call (0 = skip)')
     ap.add_argument('--variant', type=int, default=0, help='WdConfig.gemm_variant (0 = default path; 9 = f32 MFMA)')
     ap.add_argument('--stream-graphs', type=int, default=10_000_000 // 8,
@@ -370,6 +406,8 @@ def main():
     enc = make_encoder(args, device)
     enc._gemm_variant = a.variant
     edges = [g.n_bonds - 1 for g in graphs]
+    if a.streams <= 0:
+        a.streams = default_streams(sum(edges) / len(edges))
 
     # independent batches in flight on a.streams HIP streams (round-robin): the kernels of one batch's
     # forward overlap another's ramp / drain / epilogue on the same GPU (graphs are independent units)
@@ -556,8 +594,8 @@ def main():
         line['packing'] = packing_report(a, device, elapsed / a.steps)
         if world == 1 and a.kind == 'polymer' and not a.no_secondary:
             log('[bench] secondary workloads (qm9, zinc, training step)')
-            line['secondary'] = [secondary_workload(device, 'qm9', 64, 3, 300, 200, streams=a.streams),
-                                 secondary_workload(device, 'zinc', 512, 5, 512, 30, streams=a.streams),
+            line['secondary'] = [secondary_workload(device, 'qm9', 64, 3, 300, 200),
+                                 secondary_workload(device, 'zinc', 512, 5, 512, 30),
                                  training_workload(device)]
         if not a.no_cpu and world == 1:  # the CPU leg is timed at N=1 only
             log(f'[bench] CPU baseline (~{a.cpu_seconds:.0f} s + a one-thread sample)')

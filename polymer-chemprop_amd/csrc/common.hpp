@@ -45,6 +45,19 @@ __device__ __forceinline__ void with_act(int act, F &&f) {
     default: f(std::integral_constant<int, ACT_IDENTITY>{}); break;
     }
 }
+// the same on the host (kernels instantiated per activation)
+template <typename F>
+inline void host_with_act(int act, F &&f) {
+    switch (act) {
+    case ACT_RELU: f(std::integral_constant<int, ACT_RELU>{}); break;
+    case ACT_LEAKY: f(std::integral_constant<int, ACT_LEAKY>{}); break;
+    case ACT_PRELU: f(std::integral_constant<int, ACT_PRELU>{}); break;
+    case ACT_TANH: f(std::integral_constant<int, ACT_TANH>{}); break;
+    case ACT_SELU: f(std::integral_constant<int, ACT_SELU>{}); break;
+    case ACT_ELU: f(std::integral_constant<int, ACT_ELU>{}); break;
+    default: f(std::integral_constant<int, ACT_IDENTITY>{}); break;
+    }
+}
 
 // d act / d z from the pre-activation z (torch's conventions at z == 0: ReLU 0, LeakyReLU/PReLU slope).
 __device__ __forceinline__ float act_grad(int act, float z, float slope) {

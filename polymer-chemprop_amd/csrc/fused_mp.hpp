@@ -3,20 +3,21 @@
 // Molecules are independent (block-diagonal batches, featurization.py:782-800), so a workgroup that
 // owns whole molecules needs no other workgroup's rows.  The host packer groups consecutive molecules
 // into blocks of <= 128 bond rows and <= 64 atom rows (WdGraph.blocks).  Intermediates live in
-// molecule-blocked plane tiles (planes.hpp, BR = 128 for bond rows, BR = 64 for atom rows), and
-// every stage after W_i is ONE launch per (block, 64- or 80-column tile):
+// fp32 natural rows (messages: split into bf16x3 planes while a layer stages them) and molecule-blocked
+// plane tiles (planes.hpp, BR = 64 for the atom aggregate), and every stage after W_i is ONE launch per
+// (block, 64- or 80-column tile):
 //
-//   mp_layer_kernel   P = M_{t-1} W_hᵀ (bf16x6 split-plane GEMM on the block's 128 rows), then the
-//                       CSR gather of P inside the block (GEMM first, gather second: X_t W_hᵀ =
-//                       (G M_{t-1}) W_hᵀ = G (M_{t-1} W_hᵀ), column-separable, mpn.py:110-124), bias,
-//                       residual inp and activation: M_t = act(inp + G P (+ b_h)) -> plane tiles of
-//                       the next layer.  The last layer also forms the atom aggregate
+//   mp_layer_kernel   P = M_{t-1} W_hᵀ (bf16x6 split-plane GEMM on the block's 128 rows; the first layer
+//                       stages M_0 = act(inp)), then the CSR gather of P inside the block (GEMM first,
+//                       gather second: X_t W_hᵀ = (G M_{t-1}) W_hᵀ = G (M_{t-1} W_hᵀ), column-separable,
+//                       mpn.py:110-124), bias, residual inp and activation: M_t = act(inp + G P (+ b_h))
+//                       -> fp32 rows for the next layer.  The last layer also forms the atom aggregate
 //                       A = Σ_{b into a} w_b M_t[b] (mpn.py:126-131) for its columns -> atom plane tiles.
 //   wo_readout_kernel   h = act([f_atoms | A] W_oᵀ + b_o) (mpn.py:132-134) on the block's atoms, then the
 //                       molecule readout (mpn.py:145-171) of those columns straight to out[mol].
 //
-// So the forward is W_i + (T - 1) layer launches + 1, with no gather kernels, no fp32 message
-// round trips through HBM and no separate readout.  Arithmetic per output element: the P and h GEMMs
+// So the forward is W_i + (T - 1) layer launches + 1, with no gather kernels, one 4-byte message
+// write + read per layer and no separate readout.  Arithmetic per output element: the P and h GEMMs
 // are fp32-accurate (gemm_x6.hpp), the gathers add in CSR order (the reference's slot order).
 #pragma once
 #include "gemm_x6.hpp"
@@ -24,6 +25,7 @@
 #include "wdmpnn.h"
 
 namespace wd {
+
 
 constexpr int BLK_BONDS = 128, BLK_ATOMS = 64;  // block capacity (rows of the blocked layouts)
 constexpr int BLK_MOLS = 64;                     // molecules per block (empty molecules have no rows)
@@ -75,8 +77,8 @@ __device__ __forceinline__ void lds_term(const float *T, int j, int c, float w, 
 }
 
 struct MpLayerP {
-    const uint8_t *mprev;       // M_{t-1}: blocked bond plane tiles [nblk * 128][kp]
-    uint8_t *mnext;             // M_t (not written by the last layer)
+    const float *mprev;         // M_{t-1}: fp32 natural bond rows [Rp][kp]; the first layer: inp (A = act(inp))
+    float *mnext;               // M_t, the same layout (not written by the last layer)
     int kp;                     // Hk
     const uint8_t *wh;          // W_h plane tiles [Hk][Hk] with BN-row blocks
     const float *inp;           // fp32 [Rp][Hk] natural rows (mpn.py:95 input)
@@ -96,15 +98,76 @@ struct MpLayerP {
     float *zsave, *asave;
 };
 
-// Wave layout of the fused layer kernels per column-tile width: BN = 64 -> 4 x 2 waves, BN = 80 -> 8 x 1
-// (each wave 16 rows x all 80 columns).  80-column tiles give 4 tiles for Hk = 320 and so exactly one
-// workgroup per CU at the benchmark size (64 blocks x 4 = 256): a grid of 1.25 workgroups per CU left a
-// quarter of the CUs with twice the bytes to stream.  8 x 1 (512 threads, two waves per SIMD) against the
-// earlier 2 x 5 (640 threads: 3 + 3 + 2 + 2 waves on the four SIMDs): +1.8 % with two batches in flight,
-// equal with one (profiles/round2_wave_layout_ab.txt); 1 x 5 (320 threads) -11 %.
-template <int BN> struct MpWaves;
-template <> struct MpWaves<64> { static constexpr int WM = 4, WN = 2; };
-template <> struct MpWaves<80> { static constexpr int WM = 8, WN = 1; };
+// The layer's A operand from fp32 message rows, split into bf16x3 planes while staging (the producer
+// waves of x6_mainloop_ws): producer thread t (0..255) stages rows t / 4 and t / 4 + 64 of the block,
+// columns 8 (t % 4) .. +7 of each 32-column chunk.  The first layer reads inp and applies the
+// activation here (M_0 = act(inp), mpn.py:97), so M_0 never goes through HBM; later layers read M_{t-1}
+// as the previous layer stored it (4 bytes per element where plane tiles took 6).  Rows past the block's
+// bonds read row 0 of the matrix instead: their accumulator rows are never read (row i of P depends on
+// row i of M only).
+template <int BM, int AACT>
+struct MsgAProd {
+    static constexpr int U = BM / 64;       // rows per producer thread
+    static constexpr int LOADS = 2 * U;     // global loads per register set
+    const float *row[U];
+    int r0, u;
+    float slope;
+    u32x4 v[2][U][2];                       // two register sets (raw fp32 bits)
+    __device__ __forceinline__ MsgAProd(const MpLayerP &P, const BlockRow &B) {
+        const int t = threadIdx.x & 255;
+        r0 = t >> 2; u = t & 3;
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            const int r = r0 + 64 * i;
+            row[i] = P.mprev + (r < B.bn ? (size_t)(B.bs + r) * P.kp : 0) + 8 * u;
+        }
+        slope = AACT == ACT_PRELU ? P.slope[0] : 0.f;
+    }
+    // The loads are inline asm, so that the compiler does not track them: across the mainloop's
+    // back-edge its waitcnt analysis lost their order and waited for the newest set as well.  wait<N>()
+    // is the matching s_waitcnt vmcnt(N), tied to the set's registers so that no use moves above it.
+    template <typename S>
+    __device__ __forceinline__ void load(S, int kc) {
+#pragma unroll
+        for (int i = 0; i < U; ++i)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v[S::value][i][h]) : "v"(row[i] + 32 * kc + 4 * h)
+                             : "memory");
+    }
+    template <int N, typename S>
+    __device__ __forceinline__ void wait(S) {
+        static_assert(U == 2, "four registers tied");
+        asm volatile("s_waitcnt vmcnt(%4)" : "+v"(v[S::value][0][0]), "+v"(v[S::value][0][1]), "+v"(v[S::value][1][0]),
+                     "+v"(v[S::value][1][1]) : "n"(N) : "memory");
+    }
+    template <typename S>
+    __device__ __forceinline__ void store(S, uint8_t *st) {
+#pragma unroll
+        for (int i = 0; i < U; ++i) {
+            const u32x4 a = v[S::value][i][0], b = v[S::value][i][1];
+            float x[8] = {__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w),
+                          __uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), __uint_as_float(b.w)};
+            if constexpr (AACT >= 0)
+#pragma unroll
+                for (int q = 0; q < 8; ++q) x[q] = act_fwd(AACT, x[q], slope);
+            uint32_t h[4], m[4], l[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) split_pair(x[2 * q], x[2 * q + 1], h[q], m[q], l[q]);
+            uint8_t *d = st + x6_slot(r0 + 64 * i, u);
+            *reinterpret_cast<u32x4 *>(d) = u32x4{h[0], h[1], h[2], h[3]};
+            *reinterpret_cast<u32x4 *>(d + BM * 64) = u32x4{m[0], m[1], m[2], m[3]};
+            *reinterpret_cast<u32x4 *>(d + 2 * BM * 64) = u32x4{l[0], l[1], l[2], l[3]};
+        }
+    }
+};
+
+// The fused layer kernel runs 512 threads for either column-tile width (64 or 80): 4 consumer waves of
+// 32 rows x all BN columns and their 4 producer partners (gemm_x6.hpp x6_mainloop_ws), then all 512
+// threads in the epilogue.  80-column tiles give 4 tiles for Hk = 320 and so exactly one workgroup per
+// CU at the benchmark size (64 blocks x 4 = 256): a grid of 1.25 workgroups per CU left a quarter of
+// the CUs with twice the bytes to stream.
+constexpr int MP_THREADS = 512;
 
 // mp_layer epilogue: the gather G applied to the P = M_{t-1} W_h^T tile in LDS in the reference's two
 // steps (mpn.py:110-120), then bias, residual, activation, dropout and the plane stores of M_t -- or, in
@@ -162,12 +225,8 @@ struct MpEpilogue {
     }
 
     // Pt: the P tile [BM][LDC] fp32 in LDS (every write of it done and synchronised); At = Pt + BM * LDC
-    __device__ __forceinline__ void run(const MpLayerP &P, const BlockRow &B, int blk, int n0, float *Pt) {
-        with_act(P.act, [&](auto act_c) { run_act<decltype(act_c)::value>(P, B, blk, n0, Pt); });
-    }
-
     template <int ACT>
-    __device__ __forceinline__ void run_act(const MpLayerP &P, const BlockRow &B, int blk, int n0, float *Pt) {
+    __device__ __forceinline__ void run(const MpLayerP &P, const BlockRow &B, int blk, int n0, float *Pt) {
         const int tid = threadIdx.x;
         float *At = Pt + BM * LDC;
         // residual rows (mpn.py:123 input): issued now, consumed after the atom sums
@@ -212,7 +271,9 @@ struct MpEpilogue {
         }
         __syncthreads();
         const float slope = ACT == ACT_PRELU ? P.slope[0] : 0.f;
-        const __amdgpu_buffer_rsrc_t mrs = x6_block_rsrc<BM>(LAST ? P.aplanes : P.mnext, P.kp, blk);
+        // M_t: the block's rows of the fp32 message matrix (natural rows), write-through buffer stores
+        const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
+            LAST ? (void *)P.aplanes : (void *)(P.mnext + (size_t)B.bs * P.kp), 0, B.bn * P.kp * 4, 0x00020000);
         float4 ym[LAST ? UPT : 1][2];  // LAST: this thread's M_t units until P is dead
 #pragma unroll
         for (int i = 0; i < UPT; ++i) {
@@ -250,7 +311,9 @@ struct MpEpilogue {
                 ym[i][0] = y0;
                 ym[i][1] = y1;
             } else if (lr < B.bn) {  // rows past the block's bonds are never loaded by the next layer
-                x6_store8_blk<BM>(mrs, lr, n0 + c, y0, y1);
+                const int o = (lr * P.kp + n0 + c) * 4;
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y0), mrs, o, 0, WD_WT_POL);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y1), mrs, o + 16, 0, WD_WT_POL);
             }
         }
         if constexpr (LAST) {
@@ -283,17 +346,17 @@ struct MpEpilogue {
     }
 };
 
-// grid = nblk * n_tiles (XCD-grouped: the column tiles of a block share an XCD), 64 WM WN threads.
+// grid = nblk * n_tiles (XCD-grouped: the column tiles of a block share an XCD), MP_THREADS threads.
 // LDS: two GEMM stages, reused by the epilogue as P [128][BN + 4] fp32; the last layer then
 // overwrites P with M_t (held in registers across a barrier) for the atom aggregate.
-template <int BN, bool LAST>
+// ACT: the activation (one instantiation each: the epilogue and, in the first layer (FIRST), the A
+// staging of M_0 = act(inp) fold it to straight-line code).
+template <int BN, bool LAST, int ACT, bool FIRST>
 // (__launch_bounds__ min 4 waves per SIMD: <= 128 VGPRs, so that two layer workgroups -- batches in flight
 // on two streams -- co-reside on a CU, 2 x 78 KB of LDS)
-__global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN, 4) void mp_layer_kernel(const Multi<MpLayerP> MP) {
-    constexpr int BM = BLK_BONDS, WM = MpWaves<BN>::WM, WN = MpWaves<BN>::WN, NT = 64 * WM * WN;
-    // two stages of one chunk (measured: 3 stages slower; two-chunk stages, one barrier per two
-    // chunks, no faster: the chunk time is not bound by load latency or barriers)
-    constexpr int S = 2, CPS = 1;
+__global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpLayerP> MP) {
+    constexpr int BM = BLK_BONDS, NT = MP_THREADS;
+    constexpr int S = 2, CPS = 1;  // two stages of one chunk
     // (<= 80 KB: two workgroups fit one CU's 160 KB, so layers of batches in flight on other
     // streams co-reside)
     constexpr int EPI_BYTES = MpEpilogue<BN, NT, LAST>::LDS_FLOATS * 4;  // P tile + the atom sums
@@ -306,22 +369,17 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN, 4) void mp_
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
     MpEpilogue<BN, NT, LAST> E;
-    auto prefetch = [&](int phase) {
-        if (phase == 0) E.prefetch(P, B);
-    };
-    X6Operands O{};
-    O.a0 = P.mprev; O.nkc0 = P.kp >> 5; O.kc0 = P.kp >> 5;
-    O.a1 = P.mprev; O.nkc1 = P.kp >> 5; O.kc1 = 0;  // no second segment (a non-null alias: no null arithmetic)
-    O.rb = blk;
-    O.a_rows = B.bn;
-    O.b = P.wh + (size_t)nt * (P.kp >> 5) * (3 * BN * 64);
-    floatx4 acc[BM / WM / 16][BN / WN / 16];
-    x6_mainloop<BM, BN, WM, WN, S, CPS, true>(O, lds, acc, prefetch);
+    MsgAProd<BM, FIRST ? ACT : -1> ap(P, B);
+    floatx4 acc[BM / 64][BN / 16];
+    x6_mainloop_ws<BM, BN>(P.wh + (size_t)nt * (P.kp >> 5) * (3 * BN * 64), P.kp >> 5, B.bn, lds, acc, ap);
+    // the epilogue's gather lists and ids: loaded now, not during the GEMM (live across the GEMM loop they
+    // pushed the consumers' accumulators and fragments past 128 VGPRs)
+    E.prefetch(P, B);
     __syncthreads();
     float *Pt = reinterpret_cast<float *>(lds);
-    x6_acc_to_lds<BM, BN, WM, WN>(acc, Pt);
+    if (threadIdx.x < 256) x6_acc_to_lds<BM, BN, 4, 1>(acc, Pt);  // (the consumer waves hold the tile)
     __syncthreads();
-    E.run(P, B, blk, n0, Pt);
+    E.template run<ACT>(P, B, blk, n0, Pt);
     // the pad row 0 (bond and atom) belongs to no block: its saved rows are written as zeros, which the
     // backward multiplies by its zero gradients (an uninitialised NaN would poison them)
     if (blk == 0 && threadIdx.x < BN / 4) {
@@ -336,11 +394,11 @@ __global__ __launch_bounds__(64 * MpWaves<BN>::WM * MpWaves<BN>::WN, 4) void mp_
 // featurization.py:190-250, 467-468), so f_bonds[b] W_i^T is a sum of W_i columns:
 //     Ea[a]  = sum_{c in code(a)} W_i[:, c] + last(a) W_i[:, Fa-1]          (per atom of the block)
 //     inp[b] = Ea[src(b)] + sum_{k in tail(b)} W_i[:, Fa + k] (+ b_i)       (per bond)
-//     M0[b]  = act(inp[b])
 //     Eo[a]  = sum_{c in code(a)} W_o[:, c] + last(a) W_o[:, Fa-1]          (the f_atoms half of W_o)
 // One workgroup per (block, BN-column tile), the tile's W_o[:, :Fa]^T and then W_i^T rows staged in LDS.
-// Writes inp (fp32, natural rows: the residual of every layer), M0 (plane tiles, blocked rows) and Eo
-// (fp32, blocked atom rows) for wo_readout_kernel's epilogue.  Every global load of the workgroup (atom
+// Writes inp (fp32, natural rows: the residual of every layer, and the first layer's A operand, which
+// applies the activation M_0 = act(inp) while staging) and Eo (fp32, blocked atom rows) for
+// wo_readout_kernel's epilogue.  Every global load of the workgroup (atom
 // codes, both weight tiles, the bonds' source atoms and tail bits) is issued up front, so the kernel
 // waits for memory once.
 // ------------------------------------------------------------------------------------------------
@@ -354,9 +412,7 @@ struct EmbedP {
     const float *bias;           // b_i (padded) or null
     const int32_t *blocks;
     int Fa, Fb, Hk, n_tiles;
-    int act; const float *slope;
     float *inp;                  // [Rp][Hk]
-    uint8_t *mplanes;            // M0 plane tiles, blocked bond rows (BR 128)
 };
 
 // s = sum_{c in code} T[c][c4 .. c4+3] + last * T[Fa - 1][c4 ..] (ascending columns, then the mass column:
@@ -439,10 +495,6 @@ __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP> MP) {
         st4(ea + la * LDC + c, code_sum<BN>(code[la], wt, P.Fa, c));
     }
     __syncthreads();
-    const float slope = P.act == ACT_PRELU ? P.slope[0] : 0.f;
-    const __amdgpu_buffer_rsrc_t mrs = x6_block_rsrc<BLK_BONDS>(P.mplanes, P.Hk, blk);
-    with_act(P.act, [&](auto act_c) {
-    constexpr int ACT = decltype(act_c)::value;
 #pragma unroll
     for (int u = 0; u < BU; ++u) {
         const int v = tid + NT * u, lb = v / U8, c = 8 * (v % U8), b = B.bs + lb;
@@ -461,13 +513,7 @@ __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP> MP) {
         float *zr = P.inp + (size_t)b * P.Hk + n0 + c;
         st4(zr, z0);
         st4(zr + 4, z1);
-        const float4 y0 = make_float4(act_fwd(ACT, z0.x, slope), act_fwd(ACT, z0.y, slope),
-                                      act_fwd(ACT, z0.z, slope), act_fwd(ACT, z0.w, slope));
-        const float4 y1 = make_float4(act_fwd(ACT, z1.x, slope), act_fwd(ACT, z1.y, slope),
-                                      act_fwd(ACT, z1.z, slope), act_fwd(ACT, z1.w, slope));
-        x6_store8_blk<BLK_BONDS>(mrs, lb, n0 + c, y0, y1);
     }
-    });
     if (blk == 0 && tid < C4) st4(P.inp + n0 + 4 * tid, f4zero());  // pad row 0 (Z_0 of the backward)
 }
 

@@ -623,6 +623,147 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+// ---------------------------------------------------------------------------------------------
+// Warp-specialised split-plane GEMM core (the message-passing layer): acc (+)= A · Bᵀ for a BM x BN
+// tile on 512 threads, two LDS stages of one 32-column chunk, one s_barrier per chunk:
+//   waves 0-3 (consumers, one per SIMD) multiply: wave w owns rows 32 w .. 32 w + 31 and all BN
+//             columns (2 x BN/16 accumulators), so every B fragment read from LDS feeds two row tiles
+//             (84 KB of fragment reads per chunk where 16-row wave tiles read 144 KB); before chunk kc's
+//             MFMAs they issue the LDS-DMA of chunk kc + 1's B (plane tiles, no registers);
+//   waves 4-7 (producers, the consumers' SIMD partners) stage A through registers (AProd: fp32 rows,
+//             loads, activation, bf16x3 split, ds_write), two chunks ahead: chunk c lives in register
+//             set c & 1 from its loads (issued while chunk c - 2 is multiplied) to its LDS write (while
+//             chunk c - 1 is multiplied).
+// The two roles run separate loops with the same barrier count, so the register allocator can give the
+// producer's staging sets the registers that hold the consumer's accumulators (a shared loop keeps both
+// live at once; aliasing them by hand made the compiler wait for the producer's loads inside the
+// consumer's MFMAs).
+// AProd interface (producer thread t = threadIdx.x & 255): LOADS (global loads per set); load(set, kc)
+// issues chunk kc's loads into register set `set`; store(set, stage) writes the stage's A image
+// (3 x BM x 64 B, x6_slot layout) from it.
+// On return every wave is past its last LDS access of the stages; the consumers' acc holds the tile
+// (the producers' acc is left undefined: the caller reads it in threads 0..255 only).
+// ---------------------------------------------------------------------------------------------
+template <int BM, int BN, typename AProd>
+__device__ __forceinline__ void x6_mainloop_ws(const uint8_t *bsrc_base, int nchunks, int a_rows, uint8_t *lds,
+                                               floatx4 (&acc)[BM / 64][BN / 16], AProd &ap) {
+    static_assert(BM == 128, "four consumer waves of 32 rows");
+    constexpr int TM = BM / 64, TN = BN / 16;
+    constexpr int APL = BM * 64, BPL = BN * 64, STAGE = x6_stage_bytes<BM, BN>();
+    constexpr int BP = 3 * BN / 16, BPW = (BP + 3) / 4;  // B: 1 KB DMA pieces per chunk, per consumer wave
+    constexpr int VM = AProd::LOADS;
+    static_assert(VM <= 15, "vmcnt immediate");
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int w4 = wave & 3, g = lane >> 4, i16 = lane & 15;
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+
+    if (wave >= 4) {  // ---- producers
+        ap.load(S0{}, 0);
+        if (nchunks > 1) {
+            ap.load(S1{}, 1);
+            ap.template wait<VM>(S0{});  // chunk 0 landed
+        } else {
+            ap.template wait<0>(S0{});
+        }
+        ap.store(S0{}, lds);
+        if (nchunks > 2) ap.load(S0{}, 2);
+        auto produce = [&](int kc, auto set) {  // set = (kc + 1) & 1 holds chunk kc + 1
+            if (kc + 1 >= nchunks) return;
+            if (kc + 2 < nchunks) ap.template wait<VM>(set);  // all but the newest set landed
+            else ap.template wait<0>(set);
+            ap.store(set, lds + ((kc + 1) & 1) * STAGE);
+            if (kc + 3 < nchunks) ap.load(set, kc + 3);
+        };
+        int kc = 0;
+        for (; kc + 1 < nchunks; kc += 2) {
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's stage writes done
+            __builtin_amdgcn_s_barrier();
+            produce(kc, S1{});
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_s_barrier();
+            produce(kc + 1, S0{});
+        }
+        if (kc < nchunks) {
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_s_barrier();
+            produce(kc, S1{});
+        }
+        // every load landed before the registers go to other values (the asm loads' late writes)
+        ap.template wait<0>(S0{});
+        ap.template wait<0>(S1{});
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        return;
+    }
+    // ---- consumers: B piece c = 4 j + w4 of the chunk block; lane l -> image unit q = 64 c + l, whose
+    // source carries the bank swizzle (the DMA writes LDS lane-linearly)
+    int bsrc[BPW];
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) {
+        const int q = 64 * (4 * j + w4) + lane, p = (q / (BN * 4)) % 3, r = (q >> 2) % BN, sl = q & 3;
+        bsrc[j] = p * BPL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
+    }
+    auto issue_b = [&](int kc) {
+        const uint8_t *bblk = bsrc_base + (size_t)kc * (3 * BPL);
+        uint8_t *st = lds + (kc & 1) * STAGE + 3 * APL;
+#pragma unroll
+        for (int j = 0; j < BPW; ++j)
+            if (BP % 4 == 0 || 4 * j + w4 < BP) glds16(bblk + bsrc[j], st + 1024 * (4 * j + w4));
+    };
+    int ao[TM], bo[TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) ao[a] = x6_slot(32 * w4 + 16 * a + i16, g);
+#pragma unroll
+    for (int b = 0; b < TN; ++b) bo[b] = 3 * APL + x6_slot(16 * b + i16, g);
+    const int na = min(TM, max(0, (a_rows - 32 * w4 + 15) >> 4));
+    auto compute_n = [&](const uint8_t *st, auto na_c) {
+        constexpr int NA = decltype(na_c)::value;
+        constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};  // hh hm mh hl lh mm
+        bf16x8 af[TM][3], bq[2][3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+#pragma unroll
+            for (int a = 0; a < NA; ++a) af[a][p] = *reinterpret_cast<const bf16x8 *>(st + p * APL + ao[a]);
+            bq[0][p] = *reinterpret_cast<const bf16x8 *>(st + p * BPL + bo[0]);
+        }
+        // column tile b: three products, the next tile's fragment reads, the other three products -- pinned
+        // in that order (left to itself the scheduler issued each tile's reads just before their use, and
+        // its LDS wait then also covered the reads issued after them)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+#pragma unroll
+                for (int a = 0; a < NA; ++a)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][PA[t]], bq[b & 1][PB[t]], acc[a][b], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (b + 1 < TN)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) bq[(b + 1) & 1][p] = *reinterpret_cast<const bf16x8 *>(st + p * BPL + bo[b + 1]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int t = 3; t < 6; ++t)
+#pragma unroll
+                for (int a = 0; a < NA; ++a)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][PA[t]], bq[b & 1][PB[t]], acc[a][b], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    issue_b(0);
+    for (int kc = 0; kc < nchunks; ++kc) {
+        __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): this wave's B DMA landed, its reads done
+        __builtin_amdgcn_s_barrier();
+        if (kc + 1 < nchunks) issue_b(kc + 1);
+        const uint8_t *st = lds + (kc & 1) * STAGE;
+        dispatch_upto<TM>(na, [&](auto c) { compute_n(st, c); });
+    }
+    __builtin_amdgcn_s_waitcnt(0x0070);
+}
+
 // acc tile -> LDS fp32 [BM][BN + 4] (C/D map of 16x16: col = lane & 15, row = 4 (lane >> 4) + reg)
 template <int BM, int BN, int WM, int WN>
 __device__ __forceinline__ void x6_acc_to_lds(const floatx4 (&acc)[BM / WM / 16][BN / WN / 16], float *cl) {

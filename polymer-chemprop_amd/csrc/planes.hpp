@@ -63,6 +63,7 @@ __device__ __forceinline__ size_t x6_tile_off(int r, int k, int kp) {
 #ifndef WD_WT
 #define WD_WT 1
 #endif
+constexpr int WD_WT_POL = WD_WT == 1 ? 16 : WD_WT == 3 ? 2 : 0;  // buffer-store aux bits: sc1 = 16, nt = 2
 __device__ __forceinline__ void gst8(void *p, const uint2 &v) {
     if constexpr (WD_WT == 1) {
         const unsigned long long w = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
@@ -115,10 +116,9 @@ __device__ __forceinline__ void x6_store8_blk(__amdgpu_buffer_rsrc_t rs, int r, 
     split_pair(hi.x, hi.y, h[2], m[2], l[2]);
     split_pair(hi.z, hi.w, h[3], m[3], l[3]);
     const int o = (k >> 5) * (3 * BR * 64) + r * 64 + 2 * (k & 31);
-    constexpr int POL = WD_WT == 1 ? 16 : WD_WT == 3 ? 2 : 0;  // aux: sc1 = 16, nt = 2
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{h[0], h[1], h[2], h[3]}, rs, o, 0, POL);
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{m[0], m[1], m[2], m[3]}, rs, o + BR * 64, 0, POL);
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{l[0], l[1], l[2], l[3]}, rs, o + 2 * BR * 64, 0, POL);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{h[0], h[1], h[2], h[3]}, rs, o, 0, WD_WT_POL);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{m[0], m[1], m[2], m[3]}, rs, o + BR * 64, 0, WD_WT_POL);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{l[0], l[1], l[2], l[3]}, rs, o + 2 * BR * 64, 0, WD_WT_POL);
 }
 
 // columns k..k+3 (k % 4 == 0): three 8-byte pieces

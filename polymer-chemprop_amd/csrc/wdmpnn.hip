@@ -465,7 +465,7 @@ struct FwdLayout {
     std::vector<size_t> Z, M, X;
     size_t packed = 0, A = 0, Zo = 0, h = 0, Zd = 0, hd = 0, total = 0;
     size_t Xp = 0, Ap = 0;  // plane tiles of X_t and A (D.x6)
-    size_t Mb[2] = {0, 0}, Ab = 0;  // molecule-blocked plane tiles of M_t (ping-pong) and A (D.blocked)
+    size_t Mb[2] = {0, 0}, Ab = 0;  // fp32 rows of M_t (ping-pong) and molecule-blocked plane tiles of A (D.blocked)
     size_t Eo = 0;                  // D.blocked: f_atoms W_o[:, :Fa]^T per blocked atom row (compact codes)
     bool own_pack = false;
 };
@@ -485,7 +485,8 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
     }
     L.A = take(atm);
     if (D.blocked) {
-        for (int i = 0; i < 2; ++i) L.Mb[i] = take((size_t)D.nblk * BLK_BONDS * D.Hk * 6);
+        // fp32 message rows M_t, ping-pong (layer t writes Mb[t & 1]; the first reads inp, the last writes none)
+        for (int i = 0; i < 2 && i < D.T - 2; ++i) L.Mb[1 - i] = take(msg);
         L.Ab = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 6);
         L.Eo = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 4);
     } else if (D.x6) {
@@ -684,8 +685,7 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
             E.wt = W(PL.WiT); E.woat = W(PL.WoaT); E.eo = F(J, J.L.Eo); E.bias = p->b_i ? W(PL.bi) : nullptr;
             E.blocks = g->blocks;
             E.Fa = J.D.Fa; E.Fb = J.D.Fb; E.Hk = Hk; E.n_tiles = nt;
-            E.act = c->activation; E.slope = p->prelu;
-            E.inp = F(J, J.L.Z[0]); E.mplanes = (uint8_t *)(J.ws + J.L.Mb[0]);
+            E.inp = F(J, J.L.Z[0]);
         }, M, grid);
         if (bn40) hipLaunchKernelGGL(embed_kernel<40>, dim3(grid), dim3(512), 0, st, M);
         else if (bn80) hipLaunchKernelGGL(embed_kernel<80>, dim3(grid), dim3(512), 0, st, M);
@@ -694,8 +694,8 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
     } else {
         for (int j = 0; j < n; ++j) {
             const FusedJob &J = jobs[j];
-            Epi e = epi_act(c->activation, p->prelu, W(PL.bi), nullptr, F(J, J.L.Z[0]), nullptr, Hk, c, 0);
-            e.planes = (uint8_t *)(J.ws + J.L.Mb[0]); e.plane_row = J.g->bond_blk_row; e.planes_kp = Hk;
+            // inp only: the first layer stages M_0 = act(inp) itself
+            Epi e = epi_act(ACT_IDENTITY, nullptr, W(PL.bi), nullptr, F(J, J.L.Z[0]), nullptr, Hk, c, 0);
             if (!x6g_eligible(e)) return fail(WD_ERR_SHAPE, "fused forward: unaligned buffers");
             WD_TRY(gemm_x6g(J.g->f_bonds_x6, J.g->ld_bonds, J.D.Kink, nullptr, 0, 0, pk + PL.WiX, J.D.Rp, Hk, e, st));
         }
@@ -707,7 +707,9 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
         int grid;
         launch_multi(jobs, n, Hk / BNf, [&](MpLayerP &Q, const FusedJob &J) {
             const WdGraph *g = J.g;
-            Q.mprev = (const uint8_t *)(J.ws + J.L.Mb[(t - 1) & 1]); Q.mnext = (uint8_t *)(J.ws + J.L.Mb[t & 1]);
+            // M_{t-1}: the first layer stages act(inp) itself; then fp32 rows ping-pong
+            Q.mprev = t == 1 ? F(J, J.L.Z[0]) : F(J, J.L.Mb[(t - 1) & 1]);
+            Q.mnext = last ? nullptr : F(J, J.L.Mb[t & 1]);
             Q.kp = Hk;
             Q.wh = (const uint8_t *)(pk + (bn80 ? PL.WhX80 : PL.WhX)); Q.inp = F(J, J.L.Z[0]);
             Q.bias = p->b_h ? W(PL.bh) : nullptr;
@@ -722,14 +724,25 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
             Q.asave = J.D.save && last ? F(J, J.L.A) : nullptr;
         }, M, grid);
         if (t == 1) WD_TRY(record_prof(c, 0, 0, st));  // one pair around all the layers
+        // one instantiation per (tile width, last layer, activation, first layer)
+        auto go = [&](auto bn_c, auto last_c, auto first_c) {
+            constexpr int BN = decltype(bn_c)::value;
+            constexpr bool LAST = decltype(last_c)::value, FIRST = decltype(first_c)::value;
+            const dim3 blk(MP_THREADS);
+            host_with_act(c->activation, [&](auto act_c) {
+                hipLaunchKernelGGL((mp_layer_kernel<BN, LAST, decltype(act_c)::value, FIRST>), dim3(grid), blk, 0, st, M);
+            });
+        };
+        using I80 = std::integral_constant<int, 80>;
+        using I64 = std::integral_constant<int, 64>;
+        using BT = std::true_type;
+        using BF = std::false_type;
         if (bn80) {
-            const dim3 blk(64 * MpWaves<80>::WM * MpWaves<80>::WN);
-            if (last) hipLaunchKernelGGL((mp_layer_kernel<80, true>), dim3(grid), blk, 0, st, M);
-            else hipLaunchKernelGGL((mp_layer_kernel<80, false>), dim3(grid), blk, 0, st, M);
+            if (t == 1) { if (last) go(I80{}, BT{}, BT{}); else go(I80{}, BF{}, BT{}); }
+            else { if (last) go(I80{}, BT{}, BF{}); else go(I80{}, BF{}, BF{}); }
         } else {
-            const dim3 blk(64 * MpWaves<64>::WM * MpWaves<64>::WN);
-            if (last) hipLaunchKernelGGL((mp_layer_kernel<64, true>), dim3(grid), blk, 0, st, M);
-            else hipLaunchKernelGGL((mp_layer_kernel<64, false>), dim3(grid), blk, 0, st, M);
+            if (t == 1) { if (last) go(I64{}, BT{}, BT{}); else go(I64{}, BF{}, BT{}); }
+            else { if (last) go(I64{}, BT{}, BF{}); else go(I64{}, BF{}, BF{}); }
         }
         WD_CHECK_LAUNCH("mp_layer");
         if (last) WD_TRY(record_prof(c, 0, 1, st));
@@ -778,6 +791,8 @@ int graph_build_launch(const GraphBuildP *P, int n, hipStream_t st);
 extern "C" {
 
 int wdmpnn_abi_version(void) { return WDMPNN_ABI_VERSION; }
+
+
 
 const char *wdmpnn_last_error(void) { return g_err.c_str(); }
 
