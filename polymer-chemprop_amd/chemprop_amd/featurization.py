@@ -163,7 +163,7 @@ class BatchMolGraph:
     """featurization.py:742-875; the tables are concatenated by the native packer (csrc/packer.cpp)."""
 
     def __init__(self, mol_graphs: Sequence, device_bond_features: bool = False, check_bond_features: bool = False,
-                 compact: bool = True):
+                 compact: bool = True, block_target: int = BLK_TARGET):
         """``device_bond_features``: keep only the bond-feature tail of every f_bonds
         row on the host (the reference builds each row as ``f_atoms[b2a] ‖ bond features``,
         featurization.py:467-468, 545-546, 616-617); ``check_bond_features`` verifies that layout while
@@ -175,7 +175,14 @@ class BatchMolGraph:
         the batch also gets its compact codes (include/wdmpnn.h "Compact graphs", ~14 bytes per edge) and
         ``device_graph`` builds every device array from them on the GPU (``wdmpnn_build_graph``).
         Other batches (extra / overwritten features, atom messages, molecules larger than a block) take
-        the host-built path: gather lists packed here, fp32 rows uploaded."""
+        the host-built path: gather lists packed here, fp32 rows uploaded.
+
+        ``block_target``: the molecule blocks a small batch is spread over at least (``molecule_blocks``).
+        The default (BLK_TARGET) cuts a small batch into many part-filled blocks, so that ONE forward spreads
+        over the CUs; batches that are encoded several per launch (``MPNEncoder.forward_many``) are better
+        packed into full blocks (``block_target=1``): the launch then has enough workgroups anyway and each
+        one streams W_h once for a full block instead of a sliver.  Results do not depend on the plan."""
+        self.block_target = int(block_target)
         self.overwrite_default_atom_features = mol_graphs[0].overwrite_default_atom_features
         self.overwrite_default_bond_features = mol_graphs[0].overwrite_default_bond_features
         self.atom_fdim = get_atom_fdim(overwrite_default_atom=self.overwrite_default_atom_features)
@@ -413,13 +420,15 @@ class BatchMolGraph:
         keep = coef != 0.0
         return Csr.from_rows(rows[keep], src[keep], coef[keep], V1)
 
-    def molecule_blocks(self, target_blocks: int = BLK_TARGET):
+    def molecule_blocks(self, target_blocks: int = None):
         """Consecutive molecules grouped greedily into blocks of <= BLK_BONDS bond rows, <= BLK_ATOMS atom
         rows and <= BLK_MOLS molecules (WdGraph.blocks, int32 [n_blocks, 8]); None when a molecule alone
         exceeds a limit.  A batch too small to give ``target_blocks`` full blocks is cut into smaller
         ones (fill limit: the 16-row-rounded share of the bond rows, never below the largest molecule):
         every block is one workgroup per column tile, and the kernels skip the empty 16-row groups, so
         small batches spread over more CUs instead of a few full blocks."""
+        if target_blocks is None:
+            target_blocks = getattr(self, 'block_target', BLK_TARGET)
         nb = np.array([n for _, n in self.b_scope], np.int64)
         big = int(nb.max()) if len(nb) else 0
         share = -(-int(nb.sum()) // max(1, target_blocks))
@@ -446,7 +455,8 @@ class BatchMolGraph:
         """The compact path of ``device_graph``: plan + image (native, one pinned buffer), one H2D,
         one build launch; None when a molecule exceeds a block."""
         host = torch.empty(_stage_bound(self._compact), dtype=torch.uint8, pin_memory=True)
-        info = _packer().compact_stage(*self._compact, *self._compact_dims, BLK_TARGET, host.data_ptr(),
+        info = _packer().compact_stage(*self._compact, *self._compact_dims,
+                                       getattr(self, 'block_target', BLK_TARGET), host.data_ptr(),
                                        host.numel())
         if info is None:
             return None

@@ -3,21 +3,20 @@
 // Molecules are independent (block-diagonal batches, featurization.py:782-800), so a workgroup that
 // owns whole molecules needs no other workgroup's rows.  The host packer groups consecutive molecules
 // into blocks of <= 128 bond rows and <= 64 atom rows (WdGraph.blocks).  Intermediates live in
-// fp32 natural rows (messages: split into bf16x3 planes while a layer stages them) and molecule-blocked
-// plane tiles (planes.hpp, BR = 64 for the atom aggregate), and every stage after W_i is ONE launch per
-// (block, 64- or 80-column tile):
+// molecule-blocked plane tiles (planes.hpp, BR = 128 for bond rows, BR = 64 for atom rows), and
+// every stage after W_i is ONE launch per (block, 64- or 80-column tile):
 //
 //   mp_layer_kernel   P = M_{t-1} W_hᵀ (bf16x6 split-plane GEMM on the block's 128 rows; the first layer
-//                       stages M_0 = act(inp)), then the CSR gather of P inside the block (GEMM first,
-//                       gather second: X_t W_hᵀ = (G M_{t-1}) W_hᵀ = G (M_{t-1} W_hᵀ), column-separable,
-//                       mpn.py:110-124), bias, residual inp and activation: M_t = act(inp + G P (+ b_h))
-//                       -> fp32 rows for the next layer.  The last layer also forms the atom aggregate
+//                       stages M_0 = act(inp) from the fp32 inp rows itself), then the CSR gather of P
+//                       inside the block (GEMM first, gather second: X_t W_hᵀ = (G M_{t-1}) W_hᵀ =
+//                       G (M_{t-1} W_hᵀ), column-separable, mpn.py:110-124), bias, residual inp and
+//                       activation: M_t = act(inp + G P (+ b_h)) -> plane tiles of the next layer.  The last layer also forms the atom aggregate
 //                       A = Σ_{b into a} w_b M_t[b] (mpn.py:126-131) for its columns -> atom plane tiles.
 //   wo_readout_kernel   h = act([f_atoms | A] W_oᵀ + b_o) (mpn.py:132-134) on the block's atoms, then the
 //                       molecule readout (mpn.py:145-171) of those columns straight to out[mol].
 //
-// So the forward is W_i + (T - 1) layer launches + 1, with no gather kernels, one 4-byte message
-// write + read per layer and no separate readout.  Arithmetic per output element: the P and h GEMMs
+// So the forward is W_i + (T - 1) layer launches + 1, with no gather kernels, no M_0 round trip through
+// HBM and no separate readout.  Arithmetic per output element: the P and h GEMMs
 // are fp32-accurate (gemm_x6.hpp), the gathers add in CSR order (the reference's slot order).
 #pragma once
 #include "gemm_x6.hpp"
@@ -77,8 +76,9 @@ __device__ __forceinline__ void lds_term(const float *T, int j, int c, float w, 
 }
 
 struct MpLayerP {
-    const float *mprev;         // M_{t-1}: fp32 natural bond rows [Rp][kp]; the first layer: inp (A = act(inp))
-    float *mnext;               // M_t, the same layout (not written by the last layer)
+    const float *mprev;         // the first layer: inp, fp32 natural bond rows [Rp][kp] (A = act(inp))
+    const uint8_t *mprev_pl;    // later layers: M_{t-1} as blocked bond plane tiles [nblk * 128][kp]
+    uint8_t *mnext_pl;          // M_t, the same layout (not written by the last layer)
     int kp;                     // Hk
     const uint8_t *wh;          // W_h plane tiles [Hk][Hk] with BN-row blocks
     const float *inp;           // fp32 [Rp][Hk] natural rows (mpn.py:95 input)
@@ -98,13 +98,11 @@ struct MpLayerP {
     float *zsave, *asave;
 };
 
-// The layer's A operand from fp32 message rows, split into bf16x3 planes while staging (the producer
-// waves of x6_mainloop_ws): producer thread t (0..255) stages rows t / 4 and t / 4 + 64 of the block,
-// columns 8 (t % 4) .. +7 of each 32-column chunk.  The first layer reads inp and applies the
-// activation here (M_0 = act(inp), mpn.py:97), so M_0 never goes through HBM; later layers read M_{t-1}
-// as the previous layer stored it (4 bytes per element where plane tiles took 6).  Rows past the block's
-// bonds read row 0 of the matrix instead: their accumulator rows are never read (row i of P depends on
-// row i of M only).
+// The first layer's A operand, M_0 = act(inp) (mpn.py:97), formed while staging from the fp32 inp rows
+// (the producer waves of x6_mainloop_ws), so that M_0 never goes through HBM: producer thread t (0..255)
+// stages rows t / 4 and t / 4 + 64 of the block, columns 8 (t % 4) .. +7 of each 32-column chunk,
+// applies the activation and splits into bf16x3 planes.  Rows past the block's bonds read row 0 of the
+// matrix instead: their accumulator rows are never read (row i of P depends on row i of M only).
 template <int BM, int AACT>
 struct MsgAProd {
     static constexpr int U = BM / 64;       // rows per producer thread
@@ -162,12 +160,18 @@ struct MsgAProd {
     }
 };
 
-// The fused layer kernel runs 512 threads for either column-tile width (64 or 80): 4 consumer waves of
-// 32 rows x all BN columns and their 4 producer partners (gemm_x6.hpp x6_mainloop_ws), then all 512
-// threads in the epilogue.  80-column tiles give 4 tiles for Hk = 320 and so exactly one workgroup per
-// CU at the benchmark size (64 blocks x 4 = 256): a grid of 1.25 workgroups per CU left a quarter of
-// the CUs with twice the bytes to stream.
+// The fused layer kernel runs 512 threads.  The first layer (A = act(inp) from fp32 rows) is
+// warp-specialised: 4 MFMA waves of 32 rows x all BN columns and their 4 staging partners
+// (gemm_x6.hpp x6_mainloop_ws).  Later layers read M_{t-1} as plane tiles by LDS-DMA with all 8 waves
+// on MFMA: BN = 64 -> 4 x 2 waves, BN = 80 -> 8 x 1 (each wave 16 rows x all 80 columns; against 2 x 5
+// waves +1.8 % with two batches in flight, profiles/round2_wave_layout_ab.txt).  The epilogue runs on
+// all 512 threads.  80-column tiles give 4 tiles for Hk = 320 and so exactly one workgroup per CU at the
+// benchmark size (64 blocks x 4 = 256): a grid of 1.25 workgroups per CU left a quarter of the CUs with
+// twice the bytes to stream.
 constexpr int MP_THREADS = 512;
+template <int BN> struct MpWaves;
+template <> struct MpWaves<64> { static constexpr int WM = 4, WN = 2; };
+template <> struct MpWaves<80> { static constexpr int WM = 8, WN = 1; };
 
 // mp_layer epilogue: the gather G applied to the P = M_{t-1} W_h^T tile in LDS in the reference's two
 // steps (mpn.py:110-120), then bias, residual, activation, dropout and the plane stores of M_t -- or, in
@@ -271,9 +275,7 @@ struct MpEpilogue {
         }
         __syncthreads();
         const float slope = ACT == ACT_PRELU ? P.slope[0] : 0.f;
-        // M_t: the block's rows of the fp32 message matrix (natural rows), write-through buffer stores
-        const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(
-            LAST ? (void *)P.aplanes : (void *)(P.mnext + (size_t)B.bs * P.kp), 0, B.bn * P.kp * 4, 0x00020000);
+        const __amdgpu_buffer_rsrc_t mrs = x6_block_rsrc<BM>(LAST ? P.aplanes : P.mnext_pl, P.kp, blk);
         float4 ym[LAST ? UPT : 1][2];  // LAST: this thread's M_t units until P is dead
 #pragma unroll
         for (int i = 0; i < UPT; ++i) {
@@ -311,9 +313,7 @@ struct MpEpilogue {
                 ym[i][0] = y0;
                 ym[i][1] = y1;
             } else if (lr < B.bn) {  // rows past the block's bonds are never loaded by the next layer
-                const int o = (lr * P.kp + n0 + c) * 4;
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y0), mrs, o, 0, WD_WT_POL);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, y1), mrs, o + 16, 0, WD_WT_POL);
+                x6_store8_blk<BM>(mrs, lr, n0 + c, y0, y1);
             }
         }
         if constexpr (LAST) {
@@ -369,15 +369,34 @@ __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpL
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
     MpEpilogue<BN, NT, LAST> E;
-    MsgAProd<BM, FIRST ? ACT : -1> ap(P, B);
-    floatx4 acc[BM / 64][BN / 16];
-    x6_mainloop_ws<BM, BN>(P.wh + (size_t)nt * (P.kp >> 5) * (3 * BN * 64), P.kp >> 5, B.bn, lds, acc, ap);
-    // the epilogue's gather lists and ids: loaded now, not during the GEMM (live across the GEMM loop they
-    // pushed the consumers' accumulators and fragments past 128 VGPRs)
-    E.prefetch(P, B);
-    __syncthreads();
     float *Pt = reinterpret_cast<float *>(lds);
-    if (threadIdx.x < 256) x6_acc_to_lds<BM, BN, 4, 1>(acc, Pt);  // (the consumer waves hold the tile)
+    if constexpr (FIRST) {
+        // A = act(inp) from fp32 rows: warp-specialised (4 MFMA waves, 4 staging waves)
+        MsgAProd<BM, ACT> ap(P, B);
+        floatx4 acc[BM / 64][BN / 16];
+        x6_mainloop_ws<BM, BN>(P.wh + (size_t)nt * (P.kp >> 5) * (3 * BN * 64), P.kp >> 5, B.bn, lds, acc, ap);
+        // the epilogue's gather lists and ids: loaded now, not during the GEMM (live across the GEMM loop
+        // they pushed the consumers' accumulators and fragments past 128 VGPRs)
+        E.prefetch(P, B);
+        __syncthreads();
+        if (threadIdx.x < 256) x6_acc_to_lds<BM, BN, 4, 1>(acc, Pt);  // (the consumer waves hold the tile)
+    } else {
+        // A = M_{t-1} plane tiles: LDS-DMA for both operands, all 8 waves on MFMA
+        constexpr int WM = MpWaves<BN>::WM, WN = MpWaves<BN>::WN;
+        auto prefetch = [&](int phase) {
+            if (phase == 0) E.prefetch(P, B);
+        };
+        X6Operands O{};
+        O.a0 = P.mprev_pl; O.nkc0 = P.kp >> 5; O.kc0 = P.kp >> 5;
+        O.a1 = P.mprev_pl; O.nkc1 = P.kp >> 5; O.kc1 = 0;  // no second segment (a non-null alias)
+        O.rb = blk;
+        O.a_rows = B.bn;
+        O.b = P.wh + (size_t)nt * (P.kp >> 5) * (3 * BN * 64);
+        floatx4 acc[BM / WM / 16][BN / WN / 16];
+        x6_mainloop<BM, BN, WM, WN, S, CPS, true>(O, lds, acc, prefetch);
+        __syncthreads();
+        x6_acc_to_lds<BM, BN, WM, WN>(acc, Pt);
+    }
     __syncthreads();
     E.template run<ACT>(P, B, blk, n0, Pt);
     // the pad row 0 (bond and atom) belongs to no block: its saved rows are written as zeros, which the

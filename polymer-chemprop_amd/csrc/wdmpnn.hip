@@ -465,7 +465,7 @@ struct FwdLayout {
     std::vector<size_t> Z, M, X;
     size_t packed = 0, A = 0, Zo = 0, h = 0, Zd = 0, hd = 0, total = 0;
     size_t Xp = 0, Ap = 0;  // plane tiles of X_t and A (D.x6)
-    size_t Mb[2] = {0, 0}, Ab = 0;  // fp32 rows of M_t (ping-pong) and molecule-blocked plane tiles of A (D.blocked)
+    size_t Mb[2] = {0, 0}, Ab = 0;  // molecule-blocked plane tiles of M_t (ping-pong) and A (D.blocked)
     size_t Eo = 0;                  // D.blocked: f_atoms W_o[:, :Fa]^T per blocked atom row (compact codes)
     bool own_pack = false;
 };
@@ -485,8 +485,8 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
     }
     L.A = take(atm);
     if (D.blocked) {
-        // fp32 message rows M_t, ping-pong (layer t writes Mb[t & 1]; the first reads inp, the last writes none)
-        for (int i = 0; i < 2 && i < D.T - 2; ++i) L.Mb[1 - i] = take(msg);
+        // M_t plane tiles, ping-pong (layer t writes Mb[t & 1]; the first reads inp, the last writes none)
+        for (int i = 0; i < 2 && i < D.T - 2; ++i) L.Mb[1 - i] = take((size_t)D.nblk * BLK_BONDS * D.Hk * 6);
         L.Ab = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 6);
         L.Eo = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 4);
     } else if (D.x6) {
@@ -707,9 +707,10 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
         int grid;
         launch_multi(jobs, n, Hk / BNf, [&](MpLayerP &Q, const FusedJob &J) {
             const WdGraph *g = J.g;
-            // M_{t-1}: the first layer stages act(inp) itself; then fp32 rows ping-pong
-            Q.mprev = t == 1 ? F(J, J.L.Z[0]) : F(J, J.L.Mb[(t - 1) & 1]);
-            Q.mnext = last ? nullptr : F(J, J.L.Mb[t & 1]);
+            // M_{t-1}: the first layer stages act(inp) itself; then plane tiles ping-pong
+            Q.mprev = F(J, J.L.Z[0]);
+            Q.mprev_pl = (const uint8_t *)(J.ws + J.L.Mb[(t - 1) & 1]);
+            Q.mnext_pl = last ? nullptr : (uint8_t *)(J.ws + J.L.Mb[t & 1]);
             Q.kp = Hk;
             Q.wh = (const uint8_t *)(pk + (bn80 ? PL.WhX80 : PL.WhX)); Q.inp = F(J, J.L.Z[0]);
             Q.bias = p->b_h ? W(PL.bh) : nullptr;

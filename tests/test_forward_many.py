@@ -62,3 +62,22 @@ def test_forward_many_with_gradients_takes_the_one_batch_path():
     assert all(o.requires_grad for o in outs)
     sum(o.sum() for o in outs).backward()
     assert enc.W_h.weight.grad is not None
+
+
+def test_full_block_plan_gives_the_same_outputs():
+    """block_target=1 (forward_many's throughput layout: small batches in full molecule blocks) changes
+    only the block plan: outputs equal the default plan's within fp32 rounding of the same arithmetic
+    (bitwise here: every per-element operation and its order is independent of the blocking), and
+    forward_many on such graphs equals the single calls bitwise."""
+    enc, _ = _enc(hidden_size=300, depth=3)
+    mols = [synthetic.make_batch('qm9', 64, 900 + i) for i in range(6)]
+    sliced = [BatchMolGraph(m, device_bond_features=True) for m in mols]
+    full = [BatchMolGraph(m, device_bond_features=True, block_target=1) for m in mols]
+    assert full[0].molecule_blocks().shape[0] < sliced[0].molecule_blocks().shape[0]
+    with torch.no_grad():
+        a = [enc(g) for g in sliced]
+        b = [enc(g) for g in full]
+        c = enc.forward_many(full)
+    torch.cuda.synchronize()
+    for x, y, z in zip(a, b, c):
+        assert torch.equal(x, y) and torch.equal(y, z)

@@ -24,7 +24,9 @@ for s in "$@"; do
     bench) step bench 600 python bench.py ;;
     benchq) step benchq 300 python bench.py --steps 200 --warmup 20 --no-cpu --no-secondary --stream-graphs 0 --stream-train-graphs 0 ;;
     prof) step rocprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof -o run --output-format csv -- python bench.py --steps 100 --warmup 10 --no-cpu --no-secondary --streams 1 --many 0 --stream-graphs 0 --stream-train-graphs 0 && python tools/kstats.py gpurun_out/rocprof/run_kernel_stats.csv 8 ;;
-    pmc) step pmc 900 bash tools/pmc.sh ;;
+    pmc) step pmc 900 bash tools/pmc.sh && python tools/pmc_summary.py gpurun_out/pmc gpurun_out/pmc_traffic.json > gpurun_out/pmc_summary.txt ;;
+    train) step train 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof_train -o run --output-format csv -- python tools/train_bench.py && python tools/train_trace.py gpurun_out/rocprof_train/run_kernel_trace.csv > gpurun_out/train_trace.txt && tail -3 gpurun_out/train_trace.txt ;;
+    stream) step stream 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rocprof_stream -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu --no-secondary --stream-graphs 200000 --stream-train-graphs 0 && python tools/kstats.py gpurun_out/rocprof_stream/run_kernel_stats.csv 8 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
