@@ -26,6 +26,10 @@
 namespace wd {
 
 constexpr int GB_BONDS = 128, GB_ATOMS = 64, GB_MOLS = 64, GB_ELLW = 8, GB_CSR_PAD = 8;
+// workgroups per block for a full (non-lean) build: slice 0 builds the block's structure (in-lists, CSR,
+// ELL, maps) and every slice writes a quarter of its feature rows and planes -- with one workgroup per
+// block a B = 64 batch (65 workgroups) wrote its ~30 MB from a quarter of the CUs (48 us, 0.08 of HBM)
+constexpr int GB_SLICES = 4;
 
 struct GraphBuildP {
     WdCompact c;
@@ -60,105 +64,14 @@ __device__ __forceinline__ void put_row8(float *row_f32, uint8_t *planes, int ld
     x6_store8<64>(planes, ld, r, c0, lo, hi);
 }
 
-// grid: per batch its n_blocks + 1 workgroups (Multi: up to WD_MULTI batches per launch)
-__global__ __launch_bounds__(256) void graph_build_kernel(const Multi<GraphBuildP> MP) {
-    int k;
-    const GraphBuildP &P = multi_pick(MP, (int)blockIdx.x, k);
-    const int tid = threadIdx.x;
-    const WdCompact &C = P.c;
-    const int Fa = P.Fa, Fb = P.Fb, UA = P.lda / 8, UB = P.ldb / 8;
-    if (k == C.n_blocks) {  // pad rows: atom / bond row 0, the rows up to the padded extents, CSR heads and tails
-        const int V1 = C.n_atoms, E1 = C.n_bonds;
-        const int na_pad = 1 + (P.Vap - V1), nb_pad = 1 + (P.Rbp - E1);
-        const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int u = tid; u < (P.lean ? 0 : na_pad * UA); u += 256) {
-            const int i = u / UA, r = i == 0 ? 0 : V1 + i - 1, c0 = (u % UA) * 8;
-            put_row8(P.f_atoms + (size_t)r * P.lda, P.fa_x6, P.lda, r, c0, z);
-        }
-        for (int u = tid; u < (P.lean ? 0 : nb_pad * UB); u += 256) {
-            const int i = u / UB, r = i == 0 ? 0 : E1 + i - 1, c0 = (u % UB) * 8;
-            put_row8(P.f_bonds + (size_t)r * P.ldb, P.fb_x6, P.ldb, r, c0, z);
-        }
-        for (int i = tid; i < na_pad; i += 256) {
-            const int r = i == 0 ? 0 : V1 + i - 1;
-            P.atom_blk_row[r] = -1;
-            for (int s = 0; s < GB_ELLW; ++s) { P.agg_ell_idx[GB_ELLW * r + s] = 0; P.agg_ell_coef[GB_ELLW * r + s] = 0.f; }
-        }
-        for (int i = tid; i < nb_pad; i += 256) {
-            const int r = i == 0 ? 0 : E1 + i - 1;
-            P.bond_blk_row[r] = -1;
-            P.bond_src_blk[r] = 0;
-            P.bond_tail[r] = 0;
-            if (!P.lean)
-                for (int s = 0; s < GB_ELLW; ++s) { P.msg_ell_idx[GB_ELLW * r + s] = 0; P.msg_ell_coef[GB_ELLW * r + s] = 0.f; }
-        }
-        if (tid < 2) {  // row 0 (pad atom / bond) has no entries
-            P.agg_ptr[tid] = 0;
-            if (!P.lean) { P.msg_ptr[tid] = 0; P.msgt_ptr[tid] = 0; P.aggt_ptr[tid] = 0; }
-        }
-        if (tid == 0) { P.w_atoms[0] = 0.f; P.b2revb[0] = 0; }
-        if (tid < GB_CSR_PAD) {  // readable dummy entries past the end (WdCsr)
-            P.agg_idx[C.nnz_agg + tid] = 0; P.agg_coef[C.nnz_agg + tid] = 0.f;
-            if (!P.lean) {
-                P.msg_idx[C.nnz_msg + tid] = 0; P.msg_coef[C.nnz_msg + tid] = 0.f;
-                P.msgt_idx[C.nnz_msg + tid] = 0; P.msgt_coef[C.nnz_msg + tid] = 0.f;
-                P.aggt_idx[C.nnz_agg + tid] = 0; P.aggt_coef[C.nnz_agg + tid] = 0.f;
-            }
-        }
-        return;
-    }
-
-    __shared__ int s_blk[8];
-    __shared__ int s_mas[GB_MOLS], s_mbs[GB_MOLS];
-    __shared__ WdAtomCode s_code[GB_ATOMS];
-    __shared__ __attribute__((aligned(16))) uint8_t s_src[GB_BONDS], s_dst[GB_BONDS];
-    __shared__ uint8_t s_in[GB_BONDS], s_out[GB_BONDS];
-    __shared__ uint16_t s_tail[GB_BONDS];
-    __shared__ float s_w[GB_BONDS];
-    __shared__ int s_start[GB_ATOMS + 1];  // in(a) = s_in[s_start[a] ..), out(a) = s_out[s_start[a] ..)
-    __shared__ int s_pm[GB_BONDS + 1], s_pt[GB_BONDS + 1], s_pg[GB_BONDS + 1], s_pa[GB_ATOMS + 1];
-    __shared__ int s_off[2];
-    if (tid < 8) s_blk[tid] = C.blocks[8 * k + tid];
-    if (tid < 2) s_off[tid] = C.block_nnz[2 * k + tid];
-    __syncthreads();
-    const int bs = s_blk[0], bn = s_blk[1], as = s_blk[2], an = s_blk[3], ml = s_blk[4], nm = s_blk[5] - s_blk[4];
-    if (bn > GB_BONDS || an > GB_ATOMS || nm > GB_MOLS || nm < 0) return;  // the host plan never does this
-    const int lane = tid & 63, wave = tid >> 6;
-    if (tid < nm) {
-        s_mas[tid] = C.mols[4 * (ml + tid)];
-        s_mbs[tid] = C.mols[4 * (ml + tid) + 2];
-        P.mol_start[ml + tid] = C.mols[4 * (ml + tid)];
-        P.mol_size[ml + tid] = C.mols[4 * (ml + tid) + 1];
-        P.xn[ml + tid] = C.xn[ml + tid];
-    }
-    if (tid < an) {
-        s_code[tid] = C.atoms[as + tid];
-        P.w_atoms[as + tid] = s_code[tid].w;
-        P.atom_blk_row[as + tid] = GB_ATOMS * k + tid;
-    }
-    if (tid < 8) P.blocks[8 * k + tid] = s_blk[tid];
-    if (tid >= bn && tid < GB_BONDS) s_src[tid] = s_dst[tid] = 0xFF;  // never equal to an atom of the block
-    __syncthreads();
-    if (tid < bn) {  // endpoints of bond b = bs + tid
-        const int b = bs + tid;
-        int lo = 0, hi = nm - 1;  // the molecule: last one whose first bond is <= b
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_mbs[mid] <= b) lo = mid; else hi = mid - 1;
-        }
-        const int p = (b - 1) >> 1, dir = (b - 1) & 1;
-        const WdBondPair q = C.pairs[p];
-        const int l1 = s_mas[lo] + q.a1 - as, l2 = s_mas[lo] + q.a2 - as;
-        s_src[tid] = (uint8_t)(dir ? l2 : l1);
-        s_dst[tid] = (uint8_t)(dir ? l1 : l2);
-        s_w[tid] = dir ? q.w21 : q.w12;
-        s_tail[tid] = q.tail;
-        P.b2revb[b] = dir ? b - 1 : b + 1;
-        P.bond_blk_row[b] = GB_BONDS * k + tid;
-        P.bond_src_blk[b] = (uint8_t)(dir ? l2 : l1);
-        P.bond_tail[b] = q.tail;
-    }
-    __syncthreads();
+// the block's in-lists, gather CSRs (+ transposes) and ELL rows (slice 0 of a block's workgroups; the
+// endpoint arrays are in LDS, every thread of the workgroup calls this)
+__device__ __forceinline__ void build_structure(const GraphBuildP &P, int k, int bs, int bn, int as, int an,
+                                                const uint8_t *s_src, const uint8_t *s_dst, uint8_t *s_in,
+                                                uint8_t *s_out, const float *s_w, int *s_start, int *s_pm, int *s_pt,
+                                                int *s_pg, int *s_pa, const int *s_off) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    (void)k;
     // in(a) / out(a) in creation order by counting sort: a bond's slot = start of its atom + the number of
     // earlier bonds with the same endpoint (16-byte broadcast reads of the endpoint arrays: no serial
     // loops over the block's bonds); every pair gives each endpoint one in- and one out-bond, so
@@ -298,9 +211,121 @@ __global__ __launch_bounds__(256) void graph_build_kernel(const Multi<GraphBuild
             P.agg_ell_coef[(size_t)GB_ELLW * a + q] = ecoef[q];
         }
     }
+}
+
+// grid: per batch its n_blocks + 1 workgroups (Multi: up to WD_MULTI batches per launch) x gridDim.y
+// slices (GB_SLICES for full builds, 1 for lean ones)
+__global__ __launch_bounds__(256) void graph_build_kernel(const Multi<GraphBuildP> MP) {
+    int k;
+    const GraphBuildP &P = multi_pick(MP, (int)blockIdx.x, k);
+    const int tid = threadIdx.x, sl = blockIdx.y, nsl = gridDim.y;
+    const WdCompact &C = P.c;
+    const int Fa = P.Fa, Fb = P.Fb, UA = P.lda / 8, UB = P.ldb / 8;
+    if (k == C.n_blocks && sl != 0) return;
+    if (k == C.n_blocks) {  // pad rows: atom / bond row 0, the rows up to the padded extents, CSR heads and tails
+        const int V1 = C.n_atoms, E1 = C.n_bonds;
+        const int na_pad = 1 + (P.Vap - V1), nb_pad = 1 + (P.Rbp - E1);
+        const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int u = tid; u < (P.lean ? 0 : na_pad * UA); u += 256) {
+            const int i = u / UA, r = i == 0 ? 0 : V1 + i - 1, c0 = (u % UA) * 8;
+            put_row8(P.f_atoms + (size_t)r * P.lda, P.fa_x6, P.lda, r, c0, z);
+        }
+        for (int u = tid; u < (P.lean ? 0 : nb_pad * UB); u += 256) {
+            const int i = u / UB, r = i == 0 ? 0 : E1 + i - 1, c0 = (u % UB) * 8;
+            put_row8(P.f_bonds + (size_t)r * P.ldb, P.fb_x6, P.ldb, r, c0, z);
+        }
+        for (int i = tid; i < na_pad; i += 256) {
+            const int r = i == 0 ? 0 : V1 + i - 1;
+            P.atom_blk_row[r] = -1;
+            for (int s = 0; s < GB_ELLW; ++s) { P.agg_ell_idx[GB_ELLW * r + s] = 0; P.agg_ell_coef[GB_ELLW * r + s] = 0.f; }
+        }
+        for (int i = tid; i < nb_pad; i += 256) {
+            const int r = i == 0 ? 0 : E1 + i - 1;
+            P.bond_blk_row[r] = -1;
+            P.bond_src_blk[r] = 0;
+            P.bond_tail[r] = 0;
+            if (!P.lean)
+                for (int s = 0; s < GB_ELLW; ++s) { P.msg_ell_idx[GB_ELLW * r + s] = 0; P.msg_ell_coef[GB_ELLW * r + s] = 0.f; }
+        }
+        if (tid < 2) {  // row 0 (pad atom / bond) has no entries
+            P.agg_ptr[tid] = 0;
+            if (!P.lean) { P.msg_ptr[tid] = 0; P.msgt_ptr[tid] = 0; P.aggt_ptr[tid] = 0; }
+        }
+        if (tid == 0) { P.w_atoms[0] = 0.f; P.b2revb[0] = 0; }
+        if (tid < GB_CSR_PAD) {  // readable dummy entries past the end (WdCsr)
+            P.agg_idx[C.nnz_agg + tid] = 0; P.agg_coef[C.nnz_agg + tid] = 0.f;
+            if (!P.lean) {
+                P.msg_idx[C.nnz_msg + tid] = 0; P.msg_coef[C.nnz_msg + tid] = 0.f;
+                P.msgt_idx[C.nnz_msg + tid] = 0; P.msgt_coef[C.nnz_msg + tid] = 0.f;
+                P.aggt_idx[C.nnz_agg + tid] = 0; P.aggt_coef[C.nnz_agg + tid] = 0.f;
+            }
+        }
+        return;
+    }
+
+    __shared__ int s_blk[8];
+    __shared__ int s_mas[GB_MOLS], s_mbs[GB_MOLS];
+    __shared__ WdAtomCode s_code[GB_ATOMS];
+    __shared__ __attribute__((aligned(16))) uint8_t s_src[GB_BONDS], s_dst[GB_BONDS];
+    __shared__ uint8_t s_in[GB_BONDS], s_out[GB_BONDS];
+    __shared__ uint16_t s_tail[GB_BONDS];
+    __shared__ float s_w[GB_BONDS];
+    __shared__ int s_start[GB_ATOMS + 1];  // in(a) = s_in[s_start[a] ..), out(a) = s_out[s_start[a] ..)
+    __shared__ int s_pm[GB_BONDS + 1], s_pt[GB_BONDS + 1], s_pg[GB_BONDS + 1], s_pa[GB_ATOMS + 1];
+    __shared__ int s_off[2];
+    if (tid < 8) s_blk[tid] = C.blocks[8 * k + tid];
+    if (tid < 2) s_off[tid] = C.block_nnz[2 * k + tid];
+    __syncthreads();
+    const int bs = s_blk[0], bn = s_blk[1], as = s_blk[2], an = s_blk[3], ml = s_blk[4], nm = s_blk[5] - s_blk[4];
+    if (bn > GB_BONDS || an > GB_ATOMS || nm > GB_MOLS || nm < 0) return;  // the host plan never does this
+    const int lane = tid & 63, wave = tid >> 6;
+    const bool head = sl == 0;  // the slice that writes the block's structure
+    if (tid < nm) {
+        s_mas[tid] = C.mols[4 * (ml + tid)];
+        s_mbs[tid] = C.mols[4 * (ml + tid) + 2];
+        if (head) {
+            P.mol_start[ml + tid] = C.mols[4 * (ml + tid)];
+            P.mol_size[ml + tid] = C.mols[4 * (ml + tid) + 1];
+            P.xn[ml + tid] = C.xn[ml + tid];
+        }
+    }
+    if (tid < an) {
+        s_code[tid] = C.atoms[as + tid];
+        if (head) {
+            P.w_atoms[as + tid] = s_code[tid].w;
+            P.atom_blk_row[as + tid] = GB_ATOMS * k + tid;
+        }
+    }
+    if (tid < 8 && head) P.blocks[8 * k + tid] = s_blk[tid];
+    if (tid >= bn && tid < GB_BONDS) s_src[tid] = s_dst[tid] = 0xFF;  // never equal to an atom of the block
+    __syncthreads();
+    if (tid < bn) {  // endpoints of bond b = bs + tid
+        const int b = bs + tid;
+        int lo = 0, hi = nm - 1;  // the molecule: last one whose first bond is <= b
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_mbs[mid] <= b) lo = mid; else hi = mid - 1;
+        }
+        const int p = (b - 1) >> 1, dir = (b - 1) & 1;
+        const WdBondPair q = C.pairs[p];
+        const int l1 = s_mas[lo] + q.a1 - as, l2 = s_mas[lo] + q.a2 - as;
+        s_src[tid] = (uint8_t)(dir ? l2 : l1);
+        s_dst[tid] = (uint8_t)(dir ? l1 : l2);
+        s_w[tid] = dir ? q.w21 : q.w12;
+        s_tail[tid] = q.tail;
+        if (head) {
+            P.b2revb[b] = dir ? b - 1 : b + 1;
+            P.bond_blk_row[b] = GB_BONDS * k + tid;
+            P.bond_src_blk[b] = (uint8_t)(dir ? l2 : l1);
+            P.bond_tail[b] = q.tail;
+        }
+    }
+    __syncthreads();
+    if (head) build_structure(P, k, bs, bn, as, an, s_src, s_dst, s_in, s_out, s_w, s_start, s_pm, s_pt, s_pg, s_pa, s_off);
     if (P.lean) return;
-    // feature rows (8 columns per thread-step): atoms natural + blocked (zero rows past an), bonds natural
-    for (int u = tid; u < GB_ATOMS * UA; u += 256) {
+    // feature rows (8 columns per thread-step, slice sl of them): atoms natural + blocked (zero rows past
+    // an), bonds natural
+    for (int u = tid + 256 * sl; u < GB_ATOMS * UA; u += 256 * nsl) {
         const int la = u / UA, c0 = (u % UA) * 8;
         float v[8];
         if (la < an) {
@@ -315,7 +340,7 @@ __global__ __launch_bounds__(256) void graph_build_kernel(const Multi<GraphBuild
         x6_store8<64>(P.fa_blk_x6, P.lda, GB_ATOMS * k + la, c0, make_float4(v[0], v[1], v[2], v[3]),
                       make_float4(v[4], v[5], v[6], v[7]));
     }
-    for (int u = tid; u < bn * UB; u += 256) {
+    for (int u = tid + 256 * sl; u < bn * UB; u += 256 * nsl) {
         const int lb = u / UB, c0 = (u % UB) * 8;
         const WdAtomCode &cd = s_code[s_src[lb]];
         const int tail = s_tail[lb];

@@ -1281,7 +1281,8 @@ int wdmpnn_build_graph_ex(const WdCompact *c, void *buffer, size_t bytes, WdGrap
     M.n = 1;
     M.t0[0] = 0;
     for (int j = 1; j <= WD_MULTI; ++j) M.t0[j] = c->n_blocks + 1;
-    hipLaunchKernelGGL(graph_build_kernel, dim3(c->n_blocks + 1), dim3(256), 0, (hipStream_t)stream, M);
+    hipLaunchKernelGGL(graph_build_kernel, dim3(c->n_blocks + 1, M.p[0].lean ? 1 : GB_SLICES), dim3(256), 0,
+                       (hipStream_t)stream, M);
     WD_CHECK_LAUNCH("graph_build");
     return 0;
 }
@@ -1361,7 +1362,9 @@ int graph_build_launch(const GraphBuildP *P, int n, hipStream_t st) {
             t += P[j0 + j].c.n_blocks + 1;
         }
         for (int j = M.n; j <= WD_MULTI; ++j) M.t0[j] = t;
-        hipLaunchKernelGGL(graph_build_kernel, dim3(t), dim3(256), 0, st, M);
+        bool lean = true;
+        for (int j = 0; j < M.n; ++j) lean = lean && M.p[j].lean;
+        hipLaunchKernelGGL(graph_build_kernel, dim3(t, lean ? 1 : GB_SLICES), dim3(256), 0, st, M);
         WD_CHECK_LAUNCH("graph_build");
     }
     return 0;
