@@ -278,7 +278,6 @@ __global__ __launch_bounds__(256) void graph_build_kernel(const Multi<GraphBuild
     __syncthreads();
     const int bs = s_blk[0], bn = s_blk[1], as = s_blk[2], an = s_blk[3], ml = s_blk[4], nm = s_blk[5] - s_blk[4];
     if (bn > GB_BONDS || an > GB_ATOMS || nm > GB_MOLS || nm < 0) return;  // the host plan never does this
-    const int lane = tid & 63, wave = tid >> 6;
     const bool head = sl == 0;  // the slice that writes the block's structure
     if (tid < nm) {
         s_mas[tid] = C.mols[4 * (ml + tid)];
