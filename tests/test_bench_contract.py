@@ -46,3 +46,25 @@ def test_bench_prints_one_contract_line():
     st, tr = d['streamed'], d['streamed_training']  # configs[4]: streamed forward and DP training
     assert st['graphs'] == 6400 and st['value'] > 0 and st['h2d_bytes_per_edge'] <= 16
     assert tr['steps_per_rank'] == 10 and tr['value'] > 0
+
+
+def test_batches_in_flight_by_batch_size():
+    """Two batches in flight for polymer / QM9-sized batches, one for ZINC-sized B = 512 (~30 k edges)."""
+    import bench
+    assert bench.default_streams(6164) == 2 and bench.default_streams(900) == 2
+    assert bench.default_streams(30500) == 1
+
+
+def test_usable_cores_respects_affinity_and_quota(monkeypatch, tmp_path):
+    import bench
+    monkeypatch.setattr(os, 'sched_getaffinity', lambda pid: set(range(256)))
+    real_open = open
+
+    def fake_open(path, *a, **k):
+        if path == '/sys/fs/cgroup/cpu.max':
+            f = tmp_path / 'cpu.max'
+            f.write_text('1600000 100000\n')
+            return real_open(f, *a, **k)
+        return real_open(path, *a, **k)
+    monkeypatch.setattr('builtins.open', fake_open)
+    assert bench._usable_cores(16) == (16, 256, 16)
