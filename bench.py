@@ -160,11 +160,12 @@ def forward_roofline(graphs, a, t_fwd):
 
 
 def default_streams(edges_per_batch):
-    """Batches in flight per GPU for a batch size: two (one per HIP stream) while a batch's layer grid
-    leaves CUs idle in its ramp and epilogue (polymer / QM9-sized batches), one for large batches whose
-    grids fill the chip on their own (ZINC-sized B = 512: two streams measured 50.5 vs 52.6 M edges/s,
-    BENCH_r02.json)."""
-    return 2 if edges_per_batch < 16384 else 1
+    """Batches in flight per GPU for a batch size: three (one per HIP stream) while a batch's launches
+    leave CUs idle in their ramps, barriers and epilogues (polymer / QM9-sized batches: 2 / 3 / 4 in flight
+    measured 155-158 / 172-173 / 173-175 M edges/s on one box, profiles/round3_streams_ab.txt), one for
+    large batches whose grids fill the chip on their own (ZINC-sized B = 512: two streams measured 50.5 vs
+    52.6 M edges/s, BENCH_r02.json).  Every step is still one full, independent batch."""
+    return 3 if edges_per_batch < 16384 else 1
 
 
 def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_batches=8, streams=None, many=8):
