@@ -161,10 +161,13 @@ def forward_roofline(graphs, a, t_fwd):
 
 def default_streams(edges_per_batch):
     """Batches in flight per GPU for a batch size: three (one per HIP stream) while a batch's launches
-    leave CUs idle in their ramps, barriers and epilogues (polymer / QM9-sized batches: 2 / 3 / 4 in flight
-    measured 155-158 / 172-173 / 173-175 M edges/s on one box, profiles/round3_streams_ab.txt), one for
+    leave CUs idle in their ramps, barriers and epilogues (polymer-sized batches: 2 / 3 / 4 in flight
+    measured 155-158 / 172-173 / 173-175 M edges/s on one box, profiles/round3_streams_ab.txt), two for
+    QM9-sized batches (tiny grids: a third in flight contends, 50 vs 26.5 us per forward), one for
     large batches whose grids fill the chip on their own (ZINC-sized B = 512: two streams measured 50.5 vs
     52.6 M edges/s, BENCH_r02.json).  Every step is still one full, independent batch."""
+    if edges_per_batch < 2048:  # QM9-sized (~900 edges): three in flight measured 50 us per forward, two 26.5
+        return 2
     return 3 if edges_per_batch < 16384 else 1
 
 
