@@ -332,13 +332,14 @@ def streamed_training(device, rank, world, graphs_per_rank, batch=128, producers
     gen = torch.Generator().manual_seed(rank)
     targets = [torch.randn(batch, 1, generator=gen).tolist() for _ in range(8)]
     steps = -(-graphs_per_rank // batch)
-    for i, g in enumerate(NativeFeed('polymer', batch, 10, seed=77, device=device, rank=rank, producers=producers)):
+    for i, g in enumerate(NativeFeed('polymer', batch, 10, seed=77, device=device, rank=rank, producers=producers,
+                                     planes=False)):
         train_step(model, [g], targets[i % 8], loss_func, opt, bucket=bucket)
     barrier()
     t0 = time.perf_counter()
     edges = 0
     for i, g in enumerate(NativeFeed('polymer', batch, steps, seed=4048, device=device, rank=rank,
-                                     producers=producers)):
+                                     producers=producers, planes=False)):
         train_step(model, [g], targets[i % 8], loss_func, opt, bucket=bucket)
         edges += g.n_bonds - 1
     barrier()

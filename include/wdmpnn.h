@@ -308,6 +308,10 @@ int wdmpnn_build_graph(const WdCompact *c, void *buffer, size_t bytes, WdGraph *
  * then serves only the fused inference forward (categorical codes) -- anything else returns
  * WD_ERR_UNSUPPORTED. */
 #define WDMPNN_GRAPH_LEAN 1
+/* WDMPNN_GRAPH_NO_PLANES: skip only the bf16 plane tiles of the feature rows (f_atoms_x6, f_bonds_x6,
+ * f_atoms_blk_x6 stay NULL).  The fused forward and backward of a categorical-code graph never read them
+ * (training streams); unblocked paths fall back to their register-split GEMMs. */
+#define WDMPNN_GRAPH_NO_PLANES 2
 int wdmpnn_build_graph_ex(const WdCompact *c, void *buffer, size_t bytes, WdGraph *g, int32_t flags, void *stream);
 
 /* index_select_ND (nn_utils.py:50-67): out[i, :] = src[index[i], :], row_len floats per row.
@@ -380,7 +384,7 @@ typedef struct WdFeedSpec {
     int32_t producers;      /* generator threads (>= 1) */
     int32_t slots;          /* batches in flight: host and device slots (>= 2) */
     int32_t target_blocks;  /* molecule-block plan target (>= 1) */
-    int32_t flags;          /* WDMPNN_GRAPH_LEAN: inference-only device graphs */
+    int32_t flags;          /* WDMPNN_GRAPH_LEAN: inference-only device graphs; WDMPNN_GRAPH_NO_PLANES */
     int32_t atom_fdim, bond_fdim;
     void *pinned;           /* caller-owned pinned host memory: slots x host slot bytes */
     void *device;           /* caller-owned device memory: slots x device slot bytes, 256-byte aligned */

@@ -23,6 +23,7 @@ ACT_IDENTITY = 6
 AGGREGATIONS = {'mean': 0, 'sum': 1, 'norm': 2}
 ABI_VERSION = 7
 GRAPH_LEAN = 1  # WDMPNN_GRAPH_LEAN
+GRAPH_NO_PLANES = 2  # WDMPNN_GRAPH_NO_PLANES
 ERR_UNSUPPORTED = -1003  # WD_ERR_UNSUPPORTED
 
 EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace_bytes',

@@ -195,7 +195,8 @@ class NativeFeed:
 
     def __init__(self, kind: str, batch_size: int, n_batches: int, seed: int, device, rank: int = 0,
                  producers: int = 4, slots: Optional[int] = None, lean: bool = False,
-                 target_blocks: int = BLK_TARGET, atom_fdim: int = 133, bond_fdim: int = 147):
+                 target_blocks: int = BLK_TARGET, atom_fdim: int = 133, bond_fdim: int = 147,
+                 planes: bool = True):
         from . import _native
         if kind not in KINDS:
             raise ValueError(f'unknown kind {kind!r}')
@@ -213,7 +214,9 @@ class NativeFeed:
         spec.kind, spec.batch, spec.n_batches = KINDS[kind], self.B, self.n
         spec.seed = (int(seed) + (int(rank) << 32)) & 0xFFFFFFFFFFFFFFFF
         spec.producers, spec.slots, spec.target_blocks = max(1, int(producers)), self.R, int(target_blocks)
-        spec.flags = _native.GRAPH_LEAN if lean else 0
+        # planes=False: no bf16 plane tiles of the feature rows (WDMPNN_GRAPH_NO_PLANES) -- the fused forward
+        # and backward of these categorical-code graphs never read them (training streams)
+        spec.flags = (_native.GRAPH_LEAN if lean else 0) | (0 if planes else _native.GRAPH_NO_PLANES)
         spec.atom_fdim, spec.bond_fdim = atom_fdim, bond_fdim
         spec.pinned, spec.device = self.pinned.data_ptr(), base
         self.lean = bool(lean)

@@ -44,7 +44,8 @@ struct GraphBuildP {
     float *msg_ell_coef, *agg_ell_coef;
     int32_t *msg_ptr, *msg_idx, *agg_ptr, *agg_idx, *msgt_ptr, *msgt_idx, *aggt_ptr, *aggt_idx;
     float *msg_coef, *agg_coef, *msgt_coef, *aggt_coef;
-    int lean;  // 1: no dense feature rows / planes and no transposed gathers (inference-only graph)
+    int lean;    // 1: no dense feature rows / planes and no transposed gathers (inference-only graph)
+    int planes;  // 0: no plane tiles of the feature rows (WDMPNN_GRAPH_NO_PLANES)
 };
 
 // value of f_atoms column c for an atom code (c < Fa)
@@ -56,12 +57,12 @@ __device__ __forceinline__ float code_value(const WdAtomCode &a, int c, int Fa) 
     return hit ? 1.f : 0.f;
 }
 
-// 8 consecutive columns c0 .. c0 + 7 of a natural fp32 row + its plane tiles (BR 64)
+// 8 consecutive columns c0 .. c0 + 7 of a natural fp32 row + its plane tiles (BR 64; planes null: none)
 __device__ __forceinline__ void put_row8(float *row_f32, uint8_t *planes, int ld, int r, int c0, const float (&v)[8]) {
     const float4 lo = make_float4(v[0], v[1], v[2], v[3]), hi = make_float4(v[4], v[5], v[6], v[7]);
     st4(row_f32 + c0, lo);
     st4(row_f32 + c0 + 4, hi);
-    x6_store8<64>(planes, ld, r, c0, lo, hi);
+    if (planes) x6_store8<64>(planes, ld, r, c0, lo, hi);
 }
 
 // the block's in-lists, gather CSRs (+ transposes) and ELL rows (slice 0 of a block's workgroups; the
@@ -336,8 +337,9 @@ __global__ __launch_bounds__(256) void graph_build_kernel(const Multi<GraphBuild
 #pragma unroll
             for (int q = 0; q < 8; ++q) v[q] = 0.f;
         }
-        x6_store8<64>(P.fa_blk_x6, P.lda, GB_ATOMS * k + la, c0, make_float4(v[0], v[1], v[2], v[3]),
-                      make_float4(v[4], v[5], v[6], v[7]));
+        if (P.fa_blk_x6)
+            x6_store8<64>(P.fa_blk_x6, P.lda, GB_ATOMS * k + la, c0, make_float4(v[0], v[1], v[2], v[3]),
+                          make_float4(v[4], v[5], v[6], v[7]));
     }
     for (int u = tid + 256 * sl; u < bn * UB; u += 256 * nsl) {
         const int lb = u / UB, c0 = (u % UB) * 8;

@@ -1291,8 +1291,9 @@ int wdmpnn_build_graph_ex(const WdCompact *c, void *buffer, size_t bytes, WdGrap
 
 // the build parameters and the WdGraph of a compact batch in `buffer` (no launch)
 int graph_build_prepare(const WdCompact *c, void *buffer, size_t bytes, int32_t flags, GraphBuildP &P, WdGraph &Gout) {
-    if (flags & ~WDMPNN_GRAPH_LEAN) return fail(WD_ERR_ARG, "unknown graph build flags 0x%x", flags);
-    const bool lean = flags & WDMPNN_GRAPH_LEAN;
+    if (flags & ~(WDMPNN_GRAPH_LEAN | WDMPNN_GRAPH_NO_PLANES))
+        return fail(WD_ERR_ARG, "unknown graph build flags 0x%x", flags);
+    const bool lean = flags & WDMPNN_GRAPH_LEAN, planes = !lean && !(flags & WDMPNN_GRAPH_NO_PLANES);
     GraphLayout L;
     WD_TRY(graph_layout(c, L));
     if (!buffer) return fail(WD_ERR_ARG, "null buffer");
@@ -1309,7 +1310,8 @@ int graph_build_prepare(const WdCompact *c, void *buffer, size_t bytes, int32_t 
     P.c = *c;
     P.Fa = c->atom_fdim; P.Fb = c->bond_fdim; P.lda = L.lda; P.ldb = L.ldb; P.Vap = L.Vap; P.Rbp = L.Rbp;
     P.f_atoms = F(L.f_atoms); P.f_bonds = F(L.f_bonds);
-    P.fa_x6 = U(L.fa_x6); P.fb_x6 = U(L.fb_x6); P.fa_blk_x6 = U(L.fa_blk_x6);
+    P.fa_x6 = planes ? U(L.fa_x6) : nullptr; P.fb_x6 = planes ? U(L.fb_x6) : nullptr;
+    P.fa_blk_x6 = planes ? U(L.fa_blk_x6) : nullptr;
     P.w_atoms = F(L.w_atoms); P.xn = F(L.xn); P.mol_start = I(L.mol_start); P.mol_size = I(L.mol_size);
     P.b2revb = I(L.b2revb); P.blocks = I(L.blocks); P.bond_blk_row = I(L.bond_blk_row);
     P.atom_blk_row = I(L.atom_blk_row);
@@ -1321,6 +1323,7 @@ int graph_build_prepare(const WdCompact *c, void *buffer, size_t bytes, int32_t 
     P.msgt_ptr = I(L.csr[2][0]); P.msgt_idx = I(L.csr[2][1]); P.msgt_coef = F(L.csr[2][2]);
     P.aggt_ptr = I(L.csr[3][0]); P.aggt_idx = I(L.csr[3][1]); P.aggt_coef = F(L.csr[3][2]);
     P.lean = lean;
+    P.planes = planes;
     WdGraph G{};
     G.n_atoms = c->n_atoms; G.n_bonds = c->n_bonds; G.n_mols = c->n_mols;
     G.atom_fdim = c->atom_fdim; G.bond_fdim = c->bond_fdim; G.ld_atoms = L.lda; G.ld_bonds = L.ldb; G.bond_col0 = 0;
@@ -1405,7 +1408,7 @@ int wdmpnn_feed_create(const WdFeedSpec *spec, void **feed) {
     if (!spec || !feed) return fail(WD_ERR_ARG, "feed: null argument");
     const WdFeedSpec &S = *spec;
     if (S.kind < 0 || S.kind > 2 || S.batch < 1 || S.n_batches < 0 || S.producers < 1 || S.slots < 2 ||
-        S.target_blocks < 1 || (S.flags & ~WDMPNN_GRAPH_LEAN) || !S.pinned || !S.device || ((uintptr_t)S.device & 255))
+        S.target_blocks < 1 || (S.flags & ~(WDMPNN_GRAPH_LEAN | WDMPNN_GRAPH_NO_PLANES)) || !S.pinned || !S.device || ((uintptr_t)S.device & 255))
         return fail(WD_ERR_ARG, "feed: bad spec");
     Feed *F = new Feed();
     F->spec = S;

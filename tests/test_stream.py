@@ -156,7 +156,8 @@ def test_native_feed_training_matches_python_stream():
     targets = [[[float(x)] for x in rng.standard_normal(16)] for _ in range(6)]
     res = []
     for make in (lambda: StreamedBatches('polymer', 16, 6, seed=5, device=DEV),
-                 lambda: NativeFeed('polymer', 16, 6, seed=5, device=DEV, slots=4)):
+                 lambda: NativeFeed('polymer', 16, 6, seed=5, device=DEV, slots=4),
+                 lambda: NativeFeed('polymer', 16, 6, seed=5, device=DEV, slots=4, planes=False)):
         torch.manual_seed(0)
         m = MoleculeModel(args)
         initialize_weights(m)
@@ -164,8 +165,9 @@ def test_native_feed_training_matches_python_stream():
         opt = build_optimizer(m, 1e-3)
         losses = [float(train_step(m, [g], t, get_loss_func('regression'), opt)) for g, t in zip(make(), targets)]
         res.append((losses, [q.detach().cpu() for q in m.parameters()]))
-    assert res[0][0] == res[1][0]
-    assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+    for r in res[1:]:  # (the third: graphs without plane tiles, WDMPNN_GRAPH_NO_PLANES)
+        assert res[0][0] == r[0]
+        assert all(torch.equal(a, b) for a, b in zip(res[0][1], r[1]))
 
 
 def test_native_feed_bad_spec_raises():
