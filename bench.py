@@ -238,6 +238,31 @@ def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_b
                                      '(BatchMolGraph(block_target=1))'}}
 
 
+def unblocked_workload(device, steps=50, warmup=5):
+    """The reference's ``atom_messages`` mode (mpn.py:47-53, 93-94, 104-108, 126-128) on the bench's polymer
+    batches (B = 64, depth 3, hidden 300): the unblocked multi-launch path (gather kernels + split-plane
+    GEMMs; the fused molecule-blocked kernels serve bond messages only), eval forward, one in flight."""
+    args = TrainArgs(hidden_size=300, depth=3, device=device, atom_messages=True)
+    torch.manual_seed(0)
+    enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim(atom_messages=True))
+    initialize_weights(enc)
+    enc = enc.to(device).eval()
+    graphs = [BatchMolGraph(synthetic.make_batch('polymer', 64, 6000 + i)) for i in range(4)]
+    with torch.no_grad():
+        for i in range(warmup):
+            enc(graphs[i % 4])
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            enc(graphs[i % 4])
+        torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    E = sum(graphs[i % 4].n_bonds - 1 for i in range(steps))
+    return {'workload': 'atom_messages=True (mpn.py:47-53): polymer batches of 64, depth 3, hidden 300, unblocked '
+                        'multi-launch path', 'value': E / dt, 'unit': 'edges/s', 'ms_per_step': dt / steps * 1e3,
+            'steps': steps}
+
+
 def training_workload(device, batch=128, steps=100, warmup=10):
     """BASELINE.json configs[2] shape (copolymer batches of 128 with weighted edges, full training
     step): MoleculeModel (encoder + FFN, regression, one task) forward + loss + backward (the
@@ -609,7 +634,7 @@ def main():
             log('[bench] secondary workloads (qm9, zinc, training step)')
             line['secondary'] = [secondary_workload(device, 'qm9', 64, 3, 300, 200),
                                  secondary_workload(device, 'zinc', 512, 5, 512, 30),
-                                 training_workload(device)]
+                                 training_workload(device), unblocked_workload(device)]
         if not a.no_cpu and world == 1:  # the CPU leg is timed at N=1 only
             log(f'[bench] CPU baseline (~{a.cpu_seconds:.0f} s + a one-thread sample)')
             cpu = cpu_baseline(TrainArgs(hidden_size=H, depth=a.depth, device=torch.device('cpu')), graphs[0],
