@@ -210,5 +210,12 @@ def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
 
 
+_RAW_STREAM = getattr(torch._C, '_cuda_getCurrentRawStream', None)
+
+
 def current_stream(device) -> int:
+    """The raw hipStream_t of ``device``'s current stream (torch's raw accessor: no Stream object is built,
+    a few us less host time per call on the training step's path)."""
+    if _RAW_STREAM is not None and isinstance(device, torch.device) and device.index is not None:
+        return _RAW_STREAM(device.index)
     return torch.cuda.current_stream(device).cuda_stream

@@ -96,43 +96,41 @@ class HipAdam(Optimizer):
             with torch.enable_grad():
                 loss = closure()
         L = _native.lib()
+        state = self.state
         for group in self.param_groups:
-            ps = [p for p in group['params'] if p.grad is not None]
+            ps = [(p, state[p]) for p in group['params'] if p.grad is not None]
             if not ps:
                 continue
             # torch's Adam keeps one step count per parameter: a parameter that had no gradient on some
             # steps lags behind the others, so the launches are grouped by step count (usually one group)
             by_step = {}
-            for p in ps:
-                st = self.state[p]
+            for p, st in ps:
                 if 'exp_avg' not in st:
                     if p.device.type != 'cuda' or p.dtype != torch.float32 or not p.is_contiguous():
                         raise TypeError('HipAdam expects contiguous float32 CUDA parameters')
                     st['step'] = 0
                     st['exp_avg'] = torch.zeros_like(p)
                     st['exp_avg_sq'] = torch.zeros_like(p)
-                by_step.setdefault(int(st['step']) + 1, []).append(p)
+                by_step.setdefault(int(st['step']) + 1, []).append((p, st))
             for step, sub in by_step.items():
-                key = tuple(p.data_ptr() for p in sub)
-                ent = self._tables.get(key)
-                if ent is None:
+                key = tuple(p.data_ptr() for p, _ in sub)
+                tab = self._tables.get(key)
+                if tab is None:
                     tab = (_native.WdAdamTensor * len(sub))()
-                    for k, p in enumerate(sub):
-                        st = self.state[p]
+                    for k, (p, st) in enumerate(sub):
                         tab[k].param, tab[k].exp_avg, tab[k].exp_avg_sq = p.data_ptr(), st['exp_avg'].data_ptr(), \
                             st['exp_avg_sq'].data_ptr()
                         tab[k].numel = p.numel()
-                    ent = self._tables[key] = tab
-                tab = ent
-                for k, p in enumerate(sub):
+                    self._tables[key] = tab
+                for k, (p, st) in enumerate(sub):
                     g = p.grad
                     if g.is_sparse or g.dtype != torch.float32 or not g.is_contiguous():
                         raise TypeError('HipAdam expects dense contiguous float32 gradients')
                     tab[k].grad = g.data_ptr()
-                    self.state[p]['step'] = step
+                    st['step'] = step
                 h = _native.WdAdamHyper(float(group['lr']), float(group['betas'][0]), float(group['betas'][1]),
                                         float(group['eps']), float(group['weight_decay']), step, int(self.decoupled))
-                _native.check(L.wdmpnn_adam_step(tab, len(sub), ctypes.byref(h), _native.current_stream(sub[0].device)),
+                _native.check(L.wdmpnn_adam_step(tab, len(sub), ctypes.byref(h), _native.current_stream(sub[0][0].device)),
                               'adam step')
         return loss
 
@@ -159,9 +157,12 @@ def build_optimizer(model: nn.Module, args=1e-4, weight_decay: float = 0.0) -> O
     return Adam(groups)
 
 
-# pinned host tables of batch_loss, reused per (device, shape): allocating pinned memory every step costs
-# more than the rest of the loss; the event of a table's last copy is waited on before refilling it
+# pinned host tables of batch_loss, a ring of _PINNED_RING per (device, shape): allocating pinned memory
+# every step costs more than the rest of the loss.  A buffer is refilled after the event of its last copy,
+# which with a ring is several steps old (one buffer made every step wait for the previous step's forward:
+# the host could not run ahead of the GPU)
 _PINNED_TABLES = {}
+_PINNED_RING = 4
 
 
 def _host_table(rows: np.ndarray, dev: torch.device) -> torch.Tensor:
@@ -169,17 +170,20 @@ def _host_table(rows: np.ndarray, dev: torch.device) -> torch.Tensor:
     if dev.type != 'cuda':
         return torch.from_numpy(rows).to(dev)
     key = (dev, rows.shape)
-    ent = _PINNED_TABLES.get(key)
+    ring = _PINNED_TABLES.get(key)
+    if ring is None:
+        ring = _PINNED_TABLES[key] = [0, [None] * _PINNED_RING]
+    i = ring[0]
+    ring[0] = (i + 1) % _PINNED_RING
+    ent = ring[1][i]
     if ent is None:
-        buf = torch.empty(rows.shape, dtype=torch.float32, pin_memory=True)
-        ev = torch.cuda.Event()
+        ent = ring[1][i] = (torch.empty(rows.shape, dtype=torch.float32, pin_memory=True), torch.cuda.Event())
     else:
-        buf, ev = ent
-        ev.synchronize()  # (the previous step's copy: long finished)
+        ent[1].synchronize()  # (this buffer's copy, _PINNED_RING steps ago)
+    buf, ev = ent
     buf.numpy()[...] = rows
     table = buf.to(dev, non_blocking=True)
     ev.record(torch.cuda.current_stream(dev))
-    _PINNED_TABLES[key] = (buf, ev)
     return table
 
 
@@ -189,11 +193,22 @@ def _loss_table(target_batch, target_weights, data_weights, dev):
     n_b = len(target_batch)
     n_t = len(target_batch[0]) if n_b else 0
     # missing targets are None (train.py:47-48); numpy's float conversion would turn them into NaN, so the
-    # mask comes from an object array (a NaN target stays a NaN, as in the reference)
-    obj = np.array(target_batch, dtype=object).reshape(n_b, n_t)
-    present = obj != None  # noqa: E711 (elementwise)
-    tgt = np.where(present, obj, 0.0).astype(np.float64)
-    mask = present.astype(np.float64)
+    # mask comes from an object array (a NaN target stays a NaN, as in the reference).  Fast path: a batch
+    # that converts to floats without any NaN had neither (mask of ones, the same table)
+    tgt = None
+    try:
+        tgt = np.asarray(target_batch, dtype=np.float64)
+        if tgt.shape != (n_b, n_t) or np.isnan(tgt).any():
+            tgt = None
+    except (TypeError, ValueError):
+        tgt = None
+    if tgt is not None:
+        mask = np.ones((n_b, n_t))
+    else:
+        obj = np.array(target_batch, dtype=object).reshape(n_b, n_t)
+        present = obj != None  # noqa: E711 (elementwise)
+        tgt = np.where(present, obj, 0.0).astype(np.float64)
+        mask = present.astype(np.float64)
     tw = np.ones(n_t) if target_weights is None else np.asarray(target_weights, dtype=np.float64)
     dw = np.ones(n_b) if data_weights is None else np.asarray(data_weights, dtype=np.float64)
     # targets and W travel as one host table (one pinned, asynchronous copy: pageable copies would each
@@ -347,9 +362,21 @@ def _direct_encoder(model: nn.Module, mol_batch, features_batch):
         return None
     if type(mol_batch[0]).__name__ != 'BatchMolGraph':
         return None
-    if any(not p.requires_grad for n, p in model.named_parameters() if not n.endswith('cached_zero_vector')):
+    if not _all_trainable(model, enc.cached_zero_vector):
         return None
     return enc
+
+
+def _all_trainable(mod: nn.Module, skip) -> bool:
+    """Every parameter of ``mod`` and its submodules (but ``skip``) requires grad: ``named_parameters``'s
+    test on the raw module dicts (its generators and memo sets cost tens of us per step)."""
+    for p in mod._parameters.values():
+        if p is not None and p is not skip and not p.requires_grad:
+            return False
+    for m in mod._modules.values():
+        if m is not None and not _all_trainable(m, skip):
+            return False
+    return True
 
 
 def _direct_step(model, enc, graph, head, target_batch, target_weights, data_weights) -> torch.Tensor:

@@ -63,4 +63,5 @@ for i in range(50):
     train_step(model, *batches[i % 4], lf, opt)
 torch.cuda.synchronize()
 pr.disable()
-pstats.Stats(pr).sort_stats('tottime').print_stats(25)
+pstats.Stats(pr).sort_stats('tottime').print_stats(30)
+pstats.Stats(pr).sort_stats('cumulative').print_stats(40)

@@ -45,13 +45,22 @@ for i in range(STEPS):
     host += time.perf_counter() - h
 torch.cuda.synchronize()
 res['resident'] = {'ms_per_step': (time.perf_counter() - t0) / STEPS * 1e3, 'host_train_step_ms': host / STEPS * 1e3}
+# pure host cost: the GPU drained before each step, so nothing in the step waits on it
+host = 0.0
+for i in range(100):
+    torch.cuda.synchronize()
+    h = time.perf_counter()
+    train_step(model, [graphs[i % 4]], targets[i % 8], loss, opt)
+    host += time.perf_counter() - h
+torch.cuda.synchronize()
+res['resident']['host_idle_gpu_ms'] = host / 100 * 1e3
 
 for planes in (False,):
     for i, g in enumerate(NativeFeed('polymer', B, 20, seed=77, device=dev, planes=planes)):
         train_step(model, [g], targets[i % 8], loss, opt)
     torch.cuda.synchronize()
     host = nxt = 0.0
-    it = iter(NativeFeed('polymer', B, STEPS, seed=4048, device=dev, planes=planes))
+    it = iter(NativeFeed('polymer', B, STEPS + 100, seed=4048, device=dev, planes=planes))
     t0 = time.perf_counter()
     for i in range(STEPS):
         h = time.perf_counter()
@@ -62,10 +71,52 @@ for planes in (False,):
         nxt += n - h
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    hi = ni = 0.0
+    for i in range(100):
+        torch.cuda.synchronize()
+        h = time.perf_counter()
+        g = next(it)
+        n = time.perf_counter()
+        train_step(model, [g], targets[i % 8], loss, opt)
+        hi += time.perf_counter() - n
+        ni += n - h
+    torch.cuda.synchronize()
     try:
         next(it)
     except StopIteration:
         pass
     res[f'streamed_planes{int(planes)}'] = {'ms_per_step': dt / STEPS * 1e3, 'host_train_step_ms': host / STEPS * 1e3,
-                                            'host_next_ms': nxt / STEPS * 1e3}
+                                            'host_next_ms': nxt / STEPS * 1e3, 'host_idle_gpu_ms': hi / 100 * 1e3,
+                                            'next_idle_gpu_ms': ni / 100 * 1e3}
+# variants of the streamed loop: one producer thread; slots for every batch (no slot reuse: the feed runs
+# ahead freely)
+for tag, kw in (('slots_all', dict(slots=STEPS + 2)),):
+    it = iter(NativeFeed('polymer', B, STEPS, seed=4048, device=dev, planes=False, **kw))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i, g in enumerate(it):
+        train_step(model, [g], targets[i % 8], loss, opt)
+    torch.cuda.synchronize()
+    res[tag] = {'ms_per_step': (time.perf_counter() - t0) / STEPS * 1e3}
+# the same streamed graphs, all built before the timed loop (slots for every batch: nothing of the feed
+# runs while the steps do)
+N2 = 200
+it = iter(NativeFeed('polymer', B, N2, seed=4048, device=dev, planes=False, slots=N2 + 2))
+pre = [next(it) for _ in range(N2)]
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for i, g in enumerate(pre):
+    train_step(model, [g], targets[i % 8], loss, opt)
+torch.cuda.synchronize()
+res['prebuilt_streamed'] = {'ms_per_step': (time.perf_counter() - t0) / N2 * 1e3}
+t0 = time.perf_counter()
+for i in range(N2):
+    train_step(model, [pre[i % 4]], targets[i % 8], loss, opt)
+torch.cuda.synchronize()
+res['prebuilt_4_cycled'] = {'ms_per_step': (time.perf_counter() - t0) / N2 * 1e3}
+del pre
+try:
+    next(it)
+except StopIteration:
+    pass
 print(json.dumps(res))
