@@ -171,6 +171,19 @@ def default_streams(edges_per_batch):
     return 3 if edges_per_batch < 16384 else 1
 
 
+_STREAMS = []
+
+
+def bench_streams(device, n):
+    """n streams for batches in flight: the current stream + extra HIP streams shared by every workload of
+    the run.  The HIP runtime binds streams to a handful of hardware queues (GPU_MAX_HW_QUEUES = 4 on the
+    box); streams created after the native feed's own stream came to share a queue with a busy one, and
+    two QM9-sized batches in flight took 75 instead of 27 us per forward (same box, profiles/round3_*)"""
+    while len(_STREAMS) < n - 1:
+        _STREAMS.append(torch.cuda.Stream(device))
+    return [torch.cuda.current_stream(device)] + _STREAMS[:n - 1]
+
+
 def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_batches=8, streams=None, many=8):
     """Other BASELINE.json configs' shapes (configs[1]: QM9-like molecules, batch 64, depth 3, hidden
     300; configs[3]: ZINC-like molecules, batch 512, depth 5, hidden 512), timed like the headline:
@@ -184,7 +197,7 @@ def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_b
         g.device_graph(device, False, get_bond_fdim())
     if streams is None:
         streams = default_streams(sum(g.n_bonds - 1 for g in graphs) / len(graphs))
-    ss = [torch.cuda.current_stream(device)] + [torch.cuda.Stream(device) for _ in range(streams - 1)]
+    ss = bench_streams(device, streams)
 
     def timed(n_streams):
         def fwd(i):
@@ -449,7 +462,7 @@ def main():
 
     # independent batches in flight on a.streams HIP streams (round-robin): the kernels of one batch's
     # forward overlap another's ramp / drain / epilogue on the same GPU (graphs are independent units)
-    streams = [torch.cuda.current_stream(device)] + [torch.cuda.Stream(device) for _ in range(a.streams - 1)]
+    streams = bench_streams(device, max(a.streams, 3))[:a.streams]
 
     def step(i, prof=None):
         enc._prof = prof
