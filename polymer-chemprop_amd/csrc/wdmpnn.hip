@@ -672,10 +672,7 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
     if (codes) {
         // 40-column tiles when they divide Hk: twice the workgroups of the layer tiling (two per CU at the
         // benchmark size, 37 KB of LDS each), so one's staging overlaps the other's sums
-#ifndef WD_EMBED_BN40
-#define WD_EMBED_BN40 1
-#endif
-        const bool bn40 = WD_EMBED_BN40 && Hk % 40 == 0;
+        const bool bn40 = Hk % 40 == 0;
         const int nt = Hk / (bn40 ? 40 : BNf);
         Multi<EmbedP> M;
         int grid;
