@@ -402,7 +402,8 @@ int wdmpnn_feed_create(const WdFeedSpec *spec, void **feed);
  * stream is exhausted, 0 on success, < 0 on error (a producer's error included). */
 int wdmpnn_feed_next(void *feed, void *stream, WdGraph *g, WdFeedBatch *info);
 /* Every batch handed out so far is finished when `stream` reaches this point: their slots are reused
- * after it (the feed stream waits on the GPU; the host does not block). */
+ * after it (the feed's own thread waits for that point before refilling a slot; the caller's thread
+ * does not block, and no stream waits on `stream`). */
 int wdmpnn_feed_release(void *feed, void *stream);
 /* Workspace of wdmpnn_feed_forward for up to k batches of this feed. */
 int wdmpnn_feed_forward_workspace_bytes(void *feed, const WdParams *p, const WdConfig *c, int32_t k, size_t *bytes);
