@@ -63,20 +63,8 @@ def _cpu_model():
 
 
 def _usable_cores(fallback):
-    """CPUs this process may run on: its affinity set, capped by the cgroup v2 CPU quota (a GPU box
-    shares its host: the affinity set can list every CPU of the machine while the quota is its share)."""
-    try:
-        affinity = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        affinity = os.cpu_count() or fallback
-    quota = None
-    try:
-        q, period = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
-        if q != 'max':
-            quota = max(1, int(-(-int(q) // int(period))))
-    except (OSError, ValueError):
-        pass
-    return (min(affinity, quota) if quota else affinity), affinity, quota
+    from chemprop_amd.stream import usable_cores
+    return usable_cores(fallback)
 
 
 def cpu_baseline(args, graph, seconds):
@@ -346,7 +334,7 @@ def streamed_workload(device, args, rank, world, graphs_per_rank, batch=64, prod
             h2d += up
         barrier()
         dt = time.perf_counter() - t0
-    return dt, edges, n * batch, h2d
+    return dt, edges, n * batch, h2d, {'producers': feed.producers, 'seed_range': feed.seed_range}
 
 
 def streamed_training(device, rank, world, graphs_per_rank, batch=128, producers=4, barrier=None):
@@ -434,7 +422,9 @@ def main():
     ap.add_argument('--variant', type=int, default=0, help='WdConfig.gemm_variant (0 = default path; 9 = f32 MFMA)')
     ap.add_argument('--stream-graphs', type=int, default=10_000_000 // 8,
                     help='configs[4]: polymer graphs streamed per rank (default 10 M / 8 GPUs); 0 = skip')
-    ap.add_argument('--producers', type=int, default=12, help='native generator threads of the streamed workloads')
+    ap.add_argument('--producers', type=int, default=0,
+                    help='native generator threads per rank of the streamed workloads (0 = the cap: max(2, usable '
+                         'cores // ranks per node - 2), chemprop_amd.stream.producer_cap; larger requests are capped)')
     ap.add_argument('--stream-train-graphs', type=int, default=131_072,
                     help='configs[4] as DP training: streamed graphs per rank (batches of 128); 0 = skip')
     a = ap.parse_args()
@@ -445,6 +435,9 @@ def main():
     from chemprop_amd.dp import init_distributed
     env = init_distributed(os.environ.get('BENCH_BACKEND', 'nccl'), device='cuda')
     world, rank, device = env.world_size, env.rank, env.device
+    from chemprop_amd.stream import producer_cap
+    cap = producer_cap()
+    a.producers = min(a.producers, cap) if a.producers > 0 else cap
     args = TrainArgs(hidden_size=a.hidden, depth=a.depth, device=device)
 
     # inputs: packed + resident in HBM before timing (featurization.py:757-813 equivalent on host)
@@ -539,12 +532,18 @@ def main():
     # configs[4]: streamed graphs (generation + upload + device build + forward, all timed), then the
     # same stream as data-parallel training with one gradient all-reduce per step
     st_dt = st_edges = st_graphs = st_h2d = tr_dt = tr_edges = tr_steps = 0
+    st_info = None
     if a.stream_graphs > 0:
         if rank == 0:
             log(f'[bench] streamed workload: {a.stream_graphs} graphs per rank')
-        st_dt, st_edges, st_graphs, st_h2d = streamed_workload(device, args, rank, world, a.stream_graphs,
-                                                               producers=a.producers,
-                                                               barrier=barrier)
+        st_dt, st_edges, st_graphs, st_h2d, st_info = streamed_workload(device, args, rank, world, a.stream_graphs,
+                                                                         producers=a.producers, barrier=barrier)
+        if world > 1:  # every rank's shard (batch seed range) and producer count, for the report
+            infos = [None] * world
+            dist.all_gather_object(infos, st_info)
+            st_info = infos
+        else:
+            st_info = [st_info]
     if a.stream_train_graphs > 0:
         if rank == 0:
             log(f'[bench] streamed training: {a.stream_train_graphs} graphs per rank')
@@ -632,7 +631,9 @@ def main():
                             'inside the timed region), disjoint seeds per rank, no data-path collective',
                 'graphs': st_graphs, 'graphs_per_rank': a.stream_graphs, 'n_gpus': world,
                 'value': st_edges / st_dt, 'unit': 'edges/s', 'graphs_per_s': st_graphs / st_dt, 'seconds': st_dt,
-                'h2d_bytes_per_edge': st_h2d / st_edges, 'scaling': 'weak'}
+                'h2d_bytes_per_edge': st_h2d / st_edges, 'scaling': 'weak',
+                'producers_per_rank': [i['producers'] for i in st_info], 'producer_cap': cap,
+                'shard_seed_ranges': [list(i['seed_range']) for i in st_info]}
         if tr_dt > 0:
             line['streamed_training'] = {
                 'workload': 'configs[4] as DP training: MoleculeModel (depth 3, hidden 300, regression, Adam) on '

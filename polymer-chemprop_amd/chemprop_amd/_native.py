@@ -158,23 +158,18 @@ def lib() -> ctypes.CDLL:
                                              c_int32, c_void_p, c_int32, c_void_p]
     L.wdmpnn_build_graph_ex.argtypes = [POINTER(WdCompact), c_void_p, c_size_t, POINTER(WdGraph), c_int32, c_void_p]
     L.wdmpnn_head_mse.argtypes = [POINTER(WdHead), c_void_p]
-    # (an experiment library of an older ABI, WDMPNN_LIB, may lack the newest entry points)
-    newest = hasattr(L, 'wdmpnn_forward_many')
-    if newest:
-        L.wdmpnn_forward_many.argtypes = [c_int32, POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig),
-                                          POINTER(c_void_p), POINTER(c_size_t), POINTER(c_void_p), c_void_p]
-    feed = hasattr(L, 'wdmpnn_feed_create')
-    if feed:
-        L.wdmpnn_feed_slot_bytes.argtypes = [c_int32, c_int32, c_int32, c_int32, POINTER(c_size_t), POINTER(c_size_t)]
-        L.wdmpnn_feed_create.argtypes = [POINTER(WdFeedSpec), POINTER(c_void_p)]
-        L.wdmpnn_feed_next.argtypes = [c_void_p, c_void_p, POINTER(WdGraph), POINTER(WdFeedBatch)]
-        L.wdmpnn_feed_release.argtypes = [c_void_p, c_void_p]
-        L.wdmpnn_feed_forward_workspace_bytes.argtypes = [c_void_p, POINTER(WdParams), POINTER(WdConfig), c_int32,
-                                                          POINTER(c_size_t)]
-        L.wdmpnn_feed_forward.argtypes = [c_void_p, c_int32, POINTER(WdParams), POINTER(WdConfig), c_void_p, c_size_t,
-                                          c_void_p, c_int64, c_void_p, POINTER(c_int32), POINTER(c_int64),
-                                          POINTER(c_int64), POINTER(c_int64)]
-        L.wdmpnn_feed_destroy.argtypes = [c_void_p]
+    L.wdmpnn_forward_many.argtypes = [c_int32, POINTER(WdGraph), POINTER(WdParams), POINTER(WdConfig),
+                                      POINTER(c_void_p), POINTER(c_size_t), POINTER(c_void_p), c_void_p]
+    L.wdmpnn_feed_slot_bytes.argtypes = [c_int32, c_int32, c_int32, c_int32, POINTER(c_size_t), POINTER(c_size_t)]
+    L.wdmpnn_feed_create.argtypes = [POINTER(WdFeedSpec), POINTER(c_void_p)]
+    L.wdmpnn_feed_next.argtypes = [c_void_p, c_void_p, POINTER(WdGraph), POINTER(WdFeedBatch)]
+    L.wdmpnn_feed_release.argtypes = [c_void_p, c_void_p]
+    L.wdmpnn_feed_forward_workspace_bytes.argtypes = [c_void_p, POINTER(WdParams), POINTER(WdConfig), c_int32,
+                                                      POINTER(c_size_t)]
+    L.wdmpnn_feed_forward.argtypes = [c_void_p, c_int32, POINTER(WdParams), POINTER(WdConfig), c_void_p, c_size_t,
+                                      c_void_p, c_int64, c_void_p, POINTER(c_int32), POINTER(c_int64),
+                                      POINTER(c_int64), POINTER(c_int64)]
+    L.wdmpnn_feed_destroy.argtypes = [c_void_p]
     L.wdmpnn_scale.argtypes = [POINTER(c_void_p), POINTER(c_int64), c_int32, c_void_p, c_void_p]
     L.wdmpnn_adam_step.argtypes = [POINTER(WdAdamTensor), c_int32, POINTER(WdAdamHyper), c_void_p]
     L.wdmpnn_event_pool_create.argtypes = [c_int32, POINTER(c_void_p)]
@@ -184,12 +179,12 @@ def lib() -> ctypes.CDLL:
                'wdmpnn_workspace_bytes', 'wdmpnn_backward_workspace_bytes', 'wdmpnn_forward', 'wdmpnn_backward',
                'wdmpnn_index_select_rows', 'wdmpnn_plane_bytes', 'wdmpnn_split_planes', 'wdmpnn_split_planes_rows',
                'wdmpnn_build_bond_features', 'wdmpnn_adam_step', 'wdmpnn_head_mse', 'wdmpnn_scale', 'wdmpnn_build_graph_ex') + \
-            (('wdmpnn_forward_many',) if newest else ()) + \
-            (('wdmpnn_feed_slot_bytes', 'wdmpnn_feed_create', 'wdmpnn_feed_next', 'wdmpnn_feed_release',
-              'wdmpnn_feed_forward_workspace_bytes', 'wdmpnn_feed_forward', 'wdmpnn_feed_destroy') if feed else ()):
+            ('wdmpnn_forward_many', 'wdmpnn_feed_slot_bytes', 'wdmpnn_feed_create', 'wdmpnn_feed_next',
+             'wdmpnn_feed_release', 'wdmpnn_feed_forward_workspace_bytes', 'wdmpnn_feed_forward',
+             'wdmpnn_feed_destroy'):
         getattr(L, fn).restype = c_int
     v = L.wdmpnn_abi_version()
-    if v != ABI_VERSION and not ('WDMPNN_LIB' in os.environ and v == 6):
+    if v != ABI_VERSION:
         raise NativeError(f'libwdmpnn ABI {v} != expected {ABI_VERSION}; rebuild the library')
     _LIB = L
     return L

@@ -117,20 +117,33 @@ class GradBucket:
             yield self.buffer[off:off + p.numel()].view_as(p)
             off += p.numel()
 
-    def allreduce_mean(self) -> None:
-        """Sum the bucket over ranks (one collective) and divide by the world size."""
+    def start_allreduce(self) -> None:
+        """Launch the sum of the bucket over ranks (one collective, async_op) as soon as the backward's last
+        gradient kernel is enqueued; :meth:`finish_allreduce` waits for it (on the stream, not the host,
+        with RCCL) and divides by the world size.  In between the host keeps enqueueing."""
         for p, v in zip(self.params, self._views()):
             if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
                 v.copy_(p.grad)  # autograd created a fresh tensor: fold it into the bucket
                 p.grad = v
+        self._work = None
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             if self.buffer.is_cuda and dist.get_backend() == 'gloo':
                 # gloo stages CUDA tensors through host memory; measured on ROCm: without draining the
                 # producing stream first it can read the bucket before the backward kernels have written
                 # it (RCCL orders the collective after the stream's work by itself)
                 torch.cuda.current_stream(self.buffer.device).synchronize()
-            dist.all_reduce(self.buffer, op=dist.ReduceOp.SUM)
+            self._work = dist.all_reduce(self.buffer, op=dist.ReduceOp.SUM, async_op=True)
+
+    def finish_allreduce(self) -> None:
+        work, self._work = getattr(self, '_work', None), None
+        if work is not None:
+            work.wait()  # (RCCL: the current stream waits for the collective's stream)
             self.buffer.div_(dist.get_world_size())
+
+    def allreduce_mean(self) -> None:
+        """Sum the bucket over ranks (one collective) and divide by the world size."""
+        self.start_allreduce()
+        self.finish_allreduce()
 
     @property
     def nbytes(self) -> int:

@@ -298,9 +298,11 @@ class MPNEncoder(nn.Module):
         dgs = [g.device_graph(device, False, d['bond_fdim']) for g in graphs]
         for dg in dgs:
             dg.use_on(stream)
+        # one cached plan, for a repeated call on the same graphs (it holds their DeviceGraphs: a cache of
+        # many would keep the device memory of graphs the caller has dropped)
         key = (ckey, tuple(id(dg) for dg in dgs))
-        many = self.__dict__.setdefault('_many_plans', {})
-        plan = many.get(key)
+        last = d.get('_many_plan')
+        plan = last[1] if last is not None and last[0] == key else None
         if plan is None or any(a is not b for a, b in zip(plan[0], dgs)):
             cfg = self._config(False)
             structs = (_native.WdGraph * len(dgs))()
@@ -320,9 +322,7 @@ class MPNEncoder(nn.Module):
                 rows.append(gs.n_mols)
             plan = (dgs, structs, cfg, (ctypes.c_size_t * len(dgs))(*sizes), offs, max(total, 256), rows,
                     np.cumsum([0] + rows).tolist())
-            if len(many) > 64:
-                many.clear()
-            many[key] = plan
+            d['_many_plan'] = (key, plan)
         dgs_, structs, cfg, sizes, offs, total, rows, row0 = plan
         pstruct, _ = self._packed_params(structs[0], cfg, params, device, stream=stream)
         ws = torch.empty(total, dtype=torch.uint8, device=device)

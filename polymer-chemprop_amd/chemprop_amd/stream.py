@@ -22,8 +22,9 @@ form (include/wdmpnn.h "Compact graphs": ~14 bytes per directed edge) and expand
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
-from typing import Iterator, Optional
+from typing import Iterator, Optional, Tuple
 
 import torch
 
@@ -31,6 +32,34 @@ from .featurization import BLK_TARGET, BatchMolGraph, _packer, upload_compact
 
 KINDS = {'polymer': 0, 'qm9': 1, 'zinc': 2}
 _MAX_ATOMS = {'polymer': 48, 'qm9': 9, 'zinc': 37}
+
+
+def usable_cores(fallback: int = 1) -> Tuple[int, int, Optional[int]]:
+    """(usable, affinity, quota): the CPUs this process may run on -- its affinity set, capped by the
+    cgroup v2 CPU quota (a GPU box shares its host: the affinity set can list every CPU of the machine
+    while the quota is its share)."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or fallback
+    quota = None
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            q, period = f.read().split()[:2]
+        if q != 'max':
+            quota = max(1, int(-(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return (min(affinity, quota) if quota else affinity), affinity, quota
+
+
+def producer_cap(local_world: Optional[int] = None) -> int:
+    """Generator threads one rank may run: max(2, usable cores // ranks on this node - 2) (the ranks of a
+    node share its cores; two stay for the rank's feeder and Python threads).  A rank's stream saturates
+    at ~4 producers (profiles/round3_stream_sweep.txt), so the cap only bites on small CPU shares."""
+    if local_world is None:
+        local_world = int(os.environ.get('LOCAL_WORLD_SIZE', '1'))
+    return max(2, usable_cores()[0] // max(1, local_world) - 2)
 
 
 def stage_capacity(kind: str, batch_size: int) -> int:
@@ -150,7 +179,9 @@ def _device_batch(dg, info, arrays) -> BatchMolGraph:
 
 class _FeedGraph:
     """DeviceGraph of a batch handed out by a NativeFeed: device memory owned by the feed's slot (valid
-    until the feed reuses the slot, after the consumer's release), already waited for on ``home``."""
+    until the feed reuses the slot, after the consumer's release), already waited for on ``home``.  The
+    feed marks it expired when it releases the slot: any later use raises instead of reading a slot that
+    may hold another batch."""
 
     def __init__(self, struct, info, device, home):
         self.struct = struct
@@ -168,8 +199,12 @@ class _FeedGraph:
         self.built_on_device = True
         self.lean = False
         self.index = info.index
+        self.expired = False
 
     def use_on(self, stream) -> None:
+        if self.expired:
+            raise RuntimeError(f'streamed batch {self.index} was released: a NativeFeed batch is valid only until '
+                               'the next one is requested (encode it inside the loop, or copy what you keep)')
         sid = stream.cuda_stream
         if sid in self._streams:
             return
@@ -189,7 +224,9 @@ class NativeFeed:
 
     * iteration yields device-resident ``BatchMolGraph`` objects in order; the batch handed out last is
       released (its slot may be reused) when the next one is requested, after the work enqueued for it on
-      the current stream;
+      the current stream -- a batch kept past that point (``list(feed)``, a look-ahead) raises on use;
+    * the feed's threads write its pinned and device buffers from creation on: iterate it to the end, or
+      ``close()`` it (a ``with`` block, or garbage collection, does so) before dropping it;
     * :meth:`encode` runs the whole stream through an encoder's fused inference forward, ``k`` batches
       per launch set (``wdmpnn_feed_forward``)."""
 
@@ -203,7 +240,8 @@ class NativeFeed:
         self.L = L = _native.lib()
         self.device = torch.device(device)
         self.kind, self.B, self.n = kind, int(batch_size), int(n_batches)
-        self.R = max(int(slots or 0), max(1, int(producers)) + 2, 4)
+        self.producers = min(max(1, int(producers)), producer_cap())  # (threads per rank: producer_cap)
+        self.R = max(int(slots or 0), self.producers + 2, 4)
         hb, db = ctypes.c_size_t(), ctypes.c_size_t()
         _native.check(L.wdmpnn_feed_slot_bytes(KINDS[kind], self.B, atom_fdim, bond_fdim, ctypes.byref(hb),
                                                ctypes.byref(db)), 'feed slot bytes')
@@ -213,7 +251,7 @@ class NativeFeed:
         spec = _native.WdFeedSpec()
         spec.kind, spec.batch, spec.n_batches = KINDS[kind], self.B, self.n
         spec.seed = (int(seed) + (int(rank) << 32)) & 0xFFFFFFFFFFFFFFFF
-        spec.producers, spec.slots, spec.target_blocks = max(1, int(producers)), self.R, int(target_blocks)
+        spec.producers, spec.slots, spec.target_blocks = self.producers, self.R, int(target_blocks)
         # planes=False: no bf16 plane tiles of the feature rows (WDMPNN_GRAPH_NO_PLANES) -- the fused forward
         # and backward of these categorical-code graphs never read them (training streams)
         spec.flags = (_native.GRAPH_LEAN if lean else 0) | (0 if planes else _native.GRAPH_NO_PLANES)
@@ -221,15 +259,31 @@ class NativeFeed:
         spec.pinned, spec.device = self.pinned.data_ptr(), base
         self.lean = bool(lean)
         self.fdims = (atom_fdim, bond_fdim)
+        self.seed_range = (spec.seed, spec.seed + self.n)  # batch i: seed_range[0] + i
         self.handle = ctypes.c_void_p()
         _native.check(L.wdmpnn_feed_create(ctypes.byref(spec), ctypes.byref(self.handle)), 'feed create')
         self._native = _native
 
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # (interpreter shutdown)
+            pass
+
     def __iter__(self) -> Iterator[BatchMolGraph]:
         L, check = self.L, self._native.check
+        prev = None
         try:
             while True:
                 stream = torch.cuda.current_stream(self.device)
+                if prev is not None:
+                    prev.expired = True
                 check(L.wdmpnn_feed_release(self.handle, stream.cuda_stream), 'feed release')
                 g = self._native.WdGraph()
                 info = self._native.WdFeedBatch()
@@ -237,7 +291,7 @@ class NativeFeed:
                 if rc == 1:
                     return
                 check(rc, 'feed next')
-                dg = _FeedGraph(g, info, self.device, stream.cuda_stream)
+                dg = prev = _FeedGraph(g, info, self.device, stream.cuda_stream)
                 dg.lean = self.lean
                 yield _device_batch(dg, ((True,), (info.n_mols, info.n_atoms, info.n_bonds)), None)
         finally:
@@ -248,21 +302,21 @@ class NativeFeed:
         Yields (out [rows, H] tensor, batches, directed edges, H2D bytes) per call."""
         nat = self._native
         L = self.L
-        params = enc._param_tuple()
-        stream = torch.cuda.current_stream(self.device)
-        cfg = enc._config(False)
-        dummy = nat.WdGraph()  # sizes only: the packed-parameter layout depends on the feature widths
-        dummy.n_atoms = dummy.n_bonds = 1
-        dummy.atom_fdim, dummy.bond_fdim = self.fdims
-        dummy.ld_atoms = dummy.ld_bonds = -(-max(self.fdims) // 32) * 32
-        dummy.f_atoms = dummy.f_bonds = self.arena.data_ptr() & ~255
-        pstruct, _ = enc._packed_params(dummy, cfg, tuple(t for t in params), self.device, stream=stream)
-        wsb = ctypes.c_size_t()
-        nat.check(L.wdmpnn_feed_forward_workspace_bytes(self.handle, ctypes.byref(pstruct), ctypes.byref(cfg), k,
-                                                        ctypes.byref(wsb)), 'feed workspace')
-        H = enc.hidden_size
-        got, rows, edges, h2d = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
-        try:
+        try:  # (the setup too: a failure there still stops the feed's threads)
+            params = enc._param_tuple()
+            stream = torch.cuda.current_stream(self.device)
+            cfg = enc._config(False)
+            dummy = nat.WdGraph()  # sizes only: the packed-parameter layout depends on the feature widths
+            dummy.n_atoms = dummy.n_bonds = 1
+            dummy.atom_fdim, dummy.bond_fdim = self.fdims
+            dummy.ld_atoms = dummy.ld_bonds = -(-max(self.fdims) // 32) * 32
+            dummy.f_atoms = dummy.f_bonds = self.arena.data_ptr() & ~255
+            pstruct, _ = enc._packed_params(dummy, cfg, tuple(t for t in params), self.device, stream=stream)
+            wsb = ctypes.c_size_t()
+            nat.check(L.wdmpnn_feed_forward_workspace_bytes(self.handle, ctypes.byref(pstruct), ctypes.byref(cfg), k,
+                                                            ctypes.byref(wsb)), 'feed workspace')
+            H = enc.hidden_size
+            got, rows, edges, h2d = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
             while True:
                 ws = torch.empty(wsb.value, dtype=torch.uint8, device=self.device)
                 out = torch.empty((k * self.B, H), dtype=torch.float32, device=self.device)
@@ -277,7 +331,9 @@ class NativeFeed:
             self.close()
 
     def close(self) -> None:
-        if self.handle:
+        """Stop the feed's threads and free its native state (idempotent).  The pinned and device buffers
+        stay referenced by this object until then, so nothing native writes freed memory."""
+        if getattr(self, 'handle', None):
             torch.cuda.current_stream(self.device).synchronize()  # the slots' last readers
             self.L.wdmpnn_feed_destroy(self.handle)
             self.handle = ctypes.c_void_p()

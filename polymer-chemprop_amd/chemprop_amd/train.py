@@ -346,9 +346,10 @@ def _grad_buffer(p: torch.Tensor) -> torch.Tensor:
     return g
 
 
-def _direct_encoder(model: nn.Module, mol_batch, features_batch):
+def _direct_encoder(model: nn.Module, mol_batch, features_batch, head):
     """The MPNEncoder when the step can skip autograd: one molecule per input, no extra features or
-    descriptors, depth >= 2, every parameter trainable; else None."""
+    descriptors, depth >= 2, every parameter trainable and written by the direct step (the encoder's
+    native gradients and the fused head's); else None."""
     from .model import MoleculeModel
     from .mpn import MPNEncoder
     if not isinstance(model, MoleculeModel) or type(model).forward is not MoleculeModel.forward:
@@ -362,19 +363,30 @@ def _direct_encoder(model: nn.Module, mol_batch, features_batch):
         return None
     if type(mol_batch[0]).__name__ != 'BatchMolGraph':
         return None
-    if not _all_trainable(model, enc.cached_zero_vector):
+    ids = []
+    if not _all_trainable(model, enc.cached_zero_vector, ids):
+        return None
+    # the direct step skips zero_grad and overwrites only the gradients it computes: any other trainable
+    # parameter (a future addition to the model) would keep a stale gradient, so it must not exist
+    l1, l2, _ = head
+    written = {id(t) for _, t in enc._direct_names()} | {id(t) for t in (l1.weight, l1.bias, l2.weight, l2.bias)
+                                                          if t is not None}
+    if len(ids) != len(written) or not written.issuperset(ids):
         return None
     return enc
 
 
-def _all_trainable(mod: nn.Module, skip) -> bool:
-    """Every parameter of ``mod`` and its submodules (but ``skip``) requires grad: ``named_parameters``'s
-    test on the raw module dicts (its generators and memo sets cost tens of us per step)."""
+def _all_trainable(mod: nn.Module, skip, ids: list) -> bool:
+    """Every parameter of ``mod`` and its submodules (but ``skip``) requires grad (their ids appended to
+    ``ids``): ``named_parameters``'s test on the raw module dicts (its generators and memo sets cost tens of
+    us per step)."""
     for p in mod._parameters.values():
-        if p is not None and p is not skip and not p.requires_grad:
-            return False
+        if p is not None and p is not skip:
+            if not p.requires_grad:
+                return False
+            ids.append(id(p))
     for m in mod._modules.values():
-        if m is not None and not _all_trainable(m, skip):
+        if m is not None and not _all_trainable(m, skip, ids):
             return False
     return True
 
@@ -427,7 +439,7 @@ def train_step(model: nn.Module, mol_batch, target_batch, loss_func: Callable, o
     if not model.training:  # (module.train() walks every submodule: the reference sets it once per epoch)
         model.train()
     head = _fusable_head(model, loss_func, dataset_type) if fused_head else None
-    enc = _direct_encoder(model, mol_batch, features_batch) if head is not None and direct else None
+    enc = _direct_encoder(model, mol_batch, features_batch, head) if head is not None and direct else None
     if enc is not None:
         # every trainable parameter's gradient is overwritten: no zeroing, no autograd
         if bucket is not None:
@@ -447,8 +459,9 @@ def train_step(model: nn.Module, mol_batch, target_batch, loss_func: Callable, o
         loss = batch_loss(preds, target_batch, loss_func, dataset_type, target_weights, data_weights)
     if enc is None:
         loss.backward()
-    if bucket is not None:
-        bucket.allreduce_mean()
+    if bucket is not None:  # launched behind the last gradient kernel, waited for before the update
+        bucket.start_allreduce()
+        bucket.finish_allreduce()
     if grad_clip:
         nn.utils.clip_grad_norm_(model.parameters(), grad_clip)
     optimizer.step()

@@ -85,6 +85,24 @@ __device__ __forceinline__ float dropout_scale(uint64_t seed, uint32_t layer, ui
     return u >= p ? 1.0f / (1.0f - p) : 0.0f;
 }
 
+// WD_STAMPS (experiment builds only): per-workgroup phase timestamps of the fused layer kernel, from the
+// chip-wide 100 MHz clock (s_memrealtime), written by one lane with a vector store; read back with
+// wdmpnn_debug_stamps (tools/stamps_layer.py)
+#ifndef WD_STAMPS
+#define WD_STAMPS 0
+#endif
+#if WD_STAMPS
+constexpr int WD_STAMP_SLOTS = 16, WD_STAMP_WG = 8192;
+__device__ uint64_t g_wd_stamps[WD_STAMP_WG * WD_STAMP_SLOTS];
+__device__ __forceinline__ void wd_stamp(int slot) {
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0 && blockIdx.x < WD_STAMP_WG)
+        __hip_atomic_store(&g_wd_stamps[blockIdx.x * WD_STAMP_SLOTS + slot], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#else
+__device__ __forceinline__ void wd_stamp(int) {}
+#endif
+
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
 __device__ __forceinline__ void fma4(float4 &acc, float c, const float4 &v) {

@@ -8,9 +8,11 @@
 // Batch i is generated from seed + i (the caller mixes the rank into the seed: disjoint shards), goes
 // through host slot i % R and device slot i % R, and is handed out in order.  A host slot is rewritten
 // only after the H2D that read it has completed (its copy event, waited on by the producer); a device
-// slot only after the consumer's work on its previous batch (the release event, waited on by the feed
-// stream on the GPU: the host never blocks on the consumer's kernels).  No Python, no GIL: the caller's
-// thread only takes finished graphs.
+// slot only after the consumer's work on its previous batch (the release event, waited on by the feeder
+// thread with hipEventSynchronize: the feeder runs several batches ahead, so the host wait costs nothing,
+// while a feed-stream wait on the consumer's event cost the consumer's stream ~60 us per training step).
+// The caller's thread never blocks on either.  No Python, no GIL: the caller's thread only takes
+// finished graphs.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -127,11 +129,20 @@ struct Feed {
         try {
             std::vector<GraphBuildP> P;
             std::vector<WdGraph> G;
+#ifndef WD_FEED_GROUP
+#define WD_FEED_GROUP 0
+#endif
+            // WD_FEED_GROUP (experiment): a group of grp batches per build launch while the consumer has two
+            // or more built batches in hand (waking for every staged batch gives launches of one batch)
+            const int64_t grp = WD_FEED_GROUP ? std::min<int64_t>(WD_MULTI, std::max<int64_t>(1, R / 2)) : 1;
             for (int64_t i = 0; i < spec.n_batches;) {
                 int64_t n = 0;
                 {
                     std::unique_lock<std::mutex> lk(mu);
-                    cv.wait(lk, [&] { return stop || feedable(i); });
+                    cv.wait(lk, [&] {
+                        return stop || (feedable(i) && (grp == 1 || i + grp > spec.n_batches || feedable(i + grp - 1) ||
+                                                        i - handed < 2));
+                    });
                     if (stop) return;
                     while (n < WD_MULTI && i + n < spec.n_batches && feedable(i + n)) ++n;
                 }

@@ -76,11 +76,17 @@ __device__ __forceinline__ void lds_term(const float *T, int j, int c, float w, 
 }
 
 struct MpLayerP {
-    const float *mprev;         // the first layer: inp, fp32 natural bond rows [Rp][kp] (A = act(inp))
-    const uint8_t *mprev_pl;    // later layers: M_{t-1} as blocked bond plane tiles [nblk * 128][kp]
-    uint8_t *mnext_pl;          // M_t, the same layout (not written by the last layer)
+    const float *zin;           // Z_{t-1}: fp32 natural bond rows [Rp][kp] (the first layer: inp, mpn.py:95); the
+                                // GEMM operand is M_{t-1} = dropout(act(Z_{t-1})) (mpn.py:97, 123-124), formed
+                                // while staging
+    const uint32_t *amax_in;    // its scale words (planes.hpp h2): [nblk][amax_in_n] maxima of |M_{t-1}|,
+    int amax_in_n;              // published per (block, tile) by the embed or by layer t - 1
+    float p_drop_in;            // the dropout of M_{t-1} (0 for M_0: mpn.py:97 drops nothing)
+    float *zout;                // Z_t, same layout (null in the last layer)
+    uint32_t *amax_out;         // [nblk][n_tiles]: max |dropout(act(Z_t))| of each workgroup (not the last layer)
     int kp;                     // Hk
-    const uint8_t *wh;          // W_h plane tiles [Hk][Hk] with BN-row blocks
+    const uint8_t *wh;          // W_h h2 plane tiles [Hk][Hk] with BN-row blocks
+    const uint32_t *wh_amax;    // their scale word (max |W_h|, wdmpnn_pack_params)
     const float *inp;           // fp32 [Rp][Hk] natural rows (mpn.py:95 input)
     const float *bias;          // b_h (padded) or null
     const int32_t *blocks;
@@ -90,92 +96,107 @@ struct MpLayerP {
     int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;
     const int32_t *aptr, *aidx; const float *acoef;  // atom gather (natural atom rows -> natural bond rows)
     const uint8_t *aell_idx; const float *aell_coef; // its first ELLW entries per row, block-local (WdGraph)
-    uint8_t *aplanes;           // A: blocked atom plane tiles [nblk * 64][kp]
+    uint8_t *aplanes;           // A: blocked atom plane tiles [nblk * 64][kp] (the last layer)
     int n_tiles;                // Hk / BN
-    // training forward (save_for_backward) or null: the pre-activation Z_t (mpn.py:123) as fp32 natural
-    // bond rows [Rp][kp]; the last layer also the atom aggregate A (mpn.py:126-131) as fp32 natural atom
-    // rows [Vap][kp] (the backward's operands)
+    // training forward (save_for_backward) or null, the last layer only (the others' Z_t is zout): its
+    // pre-activation Z_t (mpn.py:123) as fp32 natural bond rows [Rp][kp] and the atom aggregate A
+    // (mpn.py:126-131) as fp32 natural atom rows [Vap][kp] (the backward's operands)
     float *zsave, *asave;
 };
 
-// The first layer's A operand, M_0 = act(inp) (mpn.py:97), formed while staging from the fp32 inp rows
-// (the producer waves of x6_mainloop_ws), so that M_0 never goes through HBM: producer thread t (0..255)
-// stages rows t / 4 and t / 4 + 64 of the block, columns 8 (t % 4) .. +7 of each 32-column chunk,
-// applies the activation and splits into bf16x3 planes.  Rows past the block's bonds read row 0 of the
-// matrix instead: their accumulator rows are never read (row i of P depends on row i of M only).
+// The GEMM operand M_{t-1} = dropout(act(Z_{t-1})), formed while staging from the fp32 Z rows (the
+// producer waves of h2_mainloop_ws), so that no message tensor goes through HBM in split form: producer
+// thread t (0..255) stages rows t / 8 + 32 i (i < 4) of the block, columns 4 (t % 8) .. +3 of each
+// 32-column chunk, applies the activation and dropout, scales and splits into fp16 hi / lo.  Rows past
+// the block's bonds read row 0 of the matrix instead: their accumulator rows are never read (row i of P
+// depends on row i of M only).
+#ifndef WD_H2_SETS
+#define WD_H2_SETS 3
+#endif
+// WD_PROD_LINE: 8 producer lanes per row, each 16 bytes of the 128-byte row chunk (one wave-instruction
+// reads 8 whole lines); else 4 lanes per row, two 16-byte loads each (16 half lines per instruction)
+#ifndef WD_PROD_LINE
+#define WD_PROD_LINE 1
+#endif
 template <int BM, int AACT>
-struct MsgAProd {
-    static constexpr int U = BM / 64;       // rows per producer thread
-    static constexpr int LOADS = 2 * U;     // global loads per register set
+struct H2Prod {
+    static constexpr int LPR = WD_PROD_LINE ? 8 : 4;     // lanes per row
+    static constexpr int U = BM * LPR / 256;             // rows per producer thread
+    static constexpr int H = 8 / LPR;                    // 16-byte loads per row
+    static constexpr int SETS = WD_H2_SETS;              // register sets (chunks in flight)
     const float *row[U];
+    uint32_t grow[U];                       // natural bond row (dropout counter)
     int r0, u;
-    float slope;
-    u32x4 v[2][U][2];                       // two register sets (raw fp32 bits)
-    __device__ __forceinline__ MsgAProd(const MpLayerP &P, const BlockRow &B) {
+    float slope, scale, pd;
+    uint64_t seed;
+    uint32_t layer;
+    u32x4 v[SETS][U][H];                    // register sets (raw fp32 bits)
+    __device__ __forceinline__ H2Prod(const MpLayerP &P, const BlockRow &B, int blk) {
         const int t = threadIdx.x & 255;
-        r0 = t >> 2; u = t & 3;
+        r0 = t / LPR; u = t % LPR;
 #pragma unroll
         for (int i = 0; i < U; ++i) {
-            const int r = r0 + 64 * i;
-            row[i] = P.mprev + (r < B.bn ? (size_t)(B.bs + r) * P.kp : 0) + 8 * u;
+            const int r = r0 + (256 / LPR) * i;
+            grow[i] = r < B.bn ? B.bs + r : 0;
+            row[i] = P.zin + (size_t)grow[i] * P.kp + (32 / LPR) * u;
         }
         slope = AACT == ACT_PRELU ? P.slope[0] : 0.f;
+        scale = h2_scale(max_words(P.amax_in + (size_t)blk * P.amax_in_n, P.amax_in_n));
+        pd = P.p_drop_in;
+        seed = P.seed;
+        layer = P.layer - 1;
     }
-    // The loads are inline asm, so that the compiler does not track them: across the mainloop's
-    // back-edge its waitcnt analysis lost their order and waited for the newest set as well.  wait<N>()
-    // is the matching s_waitcnt vmcnt(N), tied to the set's registers so that no use moves above it.
     template <typename S>
     __device__ __forceinline__ void load(S, int kc) {
 #pragma unroll
         for (int i = 0; i < U; ++i)
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
-                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v[S::value][i][h]) : "v"(row[i] + 32 * kc + 4 * h)
-                             : "memory");
-    }
-    template <int N, typename S>
-    __device__ __forceinline__ void wait(S) {
-        static_assert(U == 2, "four registers tied");
-        asm volatile("s_waitcnt vmcnt(%4)" : "+v"(v[S::value][0][0]), "+v"(v[S::value][0][1]), "+v"(v[S::value][1][0]),
-                     "+v"(v[S::value][1][1]) : "n"(N) : "memory");
+            for (int h = 0; h < H; ++h) v[S::value][i][h] = *reinterpret_cast<const u32x4 *>(row[i] + 32 * kc + 4 * h);
     }
     template <typename S>
-    __device__ __forceinline__ void store(S, uint8_t *st) {
+    __device__ __forceinline__ void store(S, int kc, uint8_t *st) {
 #pragma unroll
         for (int i = 0; i < U; ++i) {
-            const u32x4 a = v[S::value][i][0], b = v[S::value][i][1];
-            float x[8] = {__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w),
-                          __uint_as_float(b.x), __uint_as_float(b.y), __uint_as_float(b.z), __uint_as_float(b.w)};
-            if constexpr (AACT >= 0)
+            float x[4 * H];
 #pragma unroll
-                for (int q = 0; q < 8; ++q) x[q] = act_fwd(AACT, x[q], slope);
-            uint32_t h[4], m[4], l[4];
+            for (int h = 0; h < H; ++h) {
+                const u32x4 a = v[S::value][i][h];
+                x[4 * h] = __uint_as_float(a.x); x[4 * h + 1] = __uint_as_float(a.y);
+                x[4 * h + 2] = __uint_as_float(a.z); x[4 * h + 3] = __uint_as_float(a.w);
+            }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) split_pair(x[2 * q], x[2 * q + 1], h[q], m[q], l[q]);
-            uint8_t *d = st + x6_slot(r0 + 64 * i, u);
-            *reinterpret_cast<u32x4 *>(d) = u32x4{h[0], h[1], h[2], h[3]};
-            *reinterpret_cast<u32x4 *>(d + BM * 64) = u32x4{m[0], m[1], m[2], m[3]};
-            *reinterpret_cast<u32x4 *>(d + 2 * BM * 64) = u32x4{l[0], l[1], l[2], l[3]};
+            for (int q = 0; q < 4 * H; ++q) x[q] = act_fwd(AACT, x[q], slope);
+            if (pd > 0.f)
+#pragma unroll
+                for (int q = 0; q < 4 * H; ++q)
+                    x[q] *= dropout_scale(seed, layer, grow[i], 32 * kc + (32 / LPR) * u + q, pd);
+            uint32_t hh[2 * H], ll[2 * H];
+#pragma unroll
+            for (int q = 0; q < 2 * H; ++q) split_h2(x[2 * q], x[2 * q + 1], scale, hh[q], ll[q]);
+            const int r = r0 + (256 / LPR) * i;
+            if constexpr (H == 2) {
+                uint8_t *d = st + x6_slot(r, u);
+                *reinterpret_cast<u32x4 *>(d) = u32x4{hh[0], hh[1], hh[2], hh[3]};
+                *reinterpret_cast<u32x4 *>(d + BM * 64) = u32x4{ll[0], ll[1], ll[2], ll[3]};
+            } else {  // 8 bytes: half of 16-byte unit u / 2
+                uint8_t *d = st + x6_slot(r, u >> 1) + 8 * (u & 1);
+                *reinterpret_cast<uint2 *>(d) = make_uint2(hh[0], hh[1]);
+                *reinterpret_cast<uint2 *>(d + BM * 64) = make_uint2(ll[0], ll[1]);
+            }
         }
     }
 };
 
-// The fused layer kernel runs 512 threads.  The first layer (A = act(inp) from fp32 rows) is
-// warp-specialised: 4 MFMA waves of 32 rows x all BN columns and their 4 staging partners
-// (gemm_x6.hpp x6_mainloop_ws).  Later layers read M_{t-1} as plane tiles by LDS-DMA with all 8 waves
-// on MFMA: BN = 64 -> 4 x 2 waves, BN = 80 -> 8 x 1 (each wave 16 rows x all 80 columns; against 2 x 5
-// waves +1.8 % with two batches in flight, profiles/round2_wave_layout_ab.txt).  The epilogue runs on
-// all 512 threads.  80-column tiles give 4 tiles for Hk = 320 and so exactly one workgroup per CU at the
-// benchmark size (64 blocks x 4 = 256): a grid of 1.25 workgroups per CU left a quarter of the CUs with
-// twice the bytes to stream.
+// The fused layer kernel runs 512 threads, warp-specialised: 4 MFMA waves of 32 rows x all BN columns and
+// their 4 staging partners (gemm_x6.hpp h2_mainloop_ws); the epilogue runs on all 512.  80-column tiles
+// give 4 tiles for Hk = 320 and so exactly one workgroup per CU at the benchmark size (64 blocks x 4 =
+// 256): a grid of 1.25 workgroups per CU left a quarter of the CUs with twice the bytes to stream.
 constexpr int MP_THREADS = 512;
-template <int BN> struct MpWaves;
-template <> struct MpWaves<64> { static constexpr int WM = 4, WN = 2; };
-template <> struct MpWaves<80> { static constexpr int WM = 8, WN = 1; };
 
 // mp_layer epilogue: the gather G applied to the P = M_{t-1} W_h^T tile in LDS in the reference's two
-// steps (mpn.py:110-120), then bias, residual, activation, dropout and the plane stores of M_t -- or, in
-// the last layer, the atom aggregate of M_t (mpn.py:126-131):
+// steps (mpn.py:110-120), then bias, residual and the fp32 stores of Z_t (with the maximum of
+// dropout(act(Z_t)) published for the next layer's scale) -- or, in the last layer, activation, dropout
+// and the atom aggregate of M_t (mpn.py:126-131):
 //     (undirected: P <- (P + P[rev]) / 2, mpn.py:101-102)
 //     A[a] = sum_{b into a} w_b P[b]      (the block's atoms, slot order, into LDS)
 //     X[b] = A[src(b)] - P[rev(b)]
@@ -263,6 +284,7 @@ struct MpEpilogue {
             }
             __syncthreads();
         }
+        wd_stamp(4 + 8 * LAST);
         // A[a] = sum_{b into a} w_b P[b] (mpn.py:112-118)
 #pragma unroll
         for (int i = 0; i < AUPT; ++i) {
@@ -274,9 +296,14 @@ struct MpEpilogue {
             st4(At + la * LDC + c + 4, s1);
         }
         __syncthreads();
+        wd_stamp(5 + 8 * LAST);
         const float slope = ACT == ACT_PRELU ? P.slope[0] : 0.f;
-        const __amdgpu_buffer_rsrc_t mrs = x6_block_rsrc<BM>(LAST ? P.aplanes : P.mnext_pl, P.kp, blk);
         float4 ym[LAST ? UPT : 1][2];  // LAST: this thread's M_t units until P is dead
+        // Z_t rows of this block (the training forward's save in the last layer)
+        float *zr = LAST ? P.zsave : P.zout;
+        const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc(zr ? (void *)(zr + (size_t)B.bs * P.kp) : (void *)P.inp, 0,
+                                                                            BM * P.kp * 4, 0x00020000);
+        uint32_t mx = 0;               // max |dropout(act(Z_t))| of this thread's units (not LAST)
 #pragma unroll
         for (int i = 0; i < UPT; ++i) {
             const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
@@ -296,25 +323,32 @@ struct MpEpilogue {
                 const float b8[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
                 for (int q = 0; q < 8; ++q) z[q] = r8[q] + (z[q] + b8[q]);  // mpn.py:122-123
-                if (P.zsave) {
-                    float *zr = P.zsave + (size_t)b * P.kp + n0 + c;
-                    st4(zr, make_float4(z[0], z[1], z[2], z[3]));
-                    st4(zr + 4, make_float4(z[4], z[5], z[6], z[7]));
+                if (zr) {  // (16-byte buffer stores, write-through: 8-byte atomic stores cost 4 us per launch)
+                    const int o = (lr * P.kp + n0 + c) * 4;
+                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(z[0]), __float_as_uint(z[1]),
+                                                                 __float_as_uint(z[2]), __float_as_uint(z[3])}, zrs, o, 0, WD_WT_POL);
+                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(z[4]), __float_as_uint(z[5]),
+                                                                 __float_as_uint(z[6]), __float_as_uint(z[7])}, zrs, o + 16, 0, WD_WT_POL);
                 }
 #pragma unroll
                 for (int q = 0; q < 8; ++q) z[q] = act_fwd(ACT, z[q], slope);
                 if (P.p_drop > 0.f)
 #pragma unroll
                     for (int q = 0; q < 8; ++q) z[q] *= dropout_scale(P.seed, P.layer, b, n0 + c + q, P.p_drop);
+                if constexpr (!LAST)
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) mx = max(mx, absbits(z[q]));
                 y0 = make_float4(z[0], z[1], z[2], z[3]);
                 y1 = make_float4(z[4], z[5], z[6], z[7]);
             }
             if constexpr (LAST) {
                 ym[i][0] = y0;
                 ym[i][1] = y1;
-            } else if (lr < B.bn) {  // rows past the block's bonds are never loaded by the next layer
-                x6_store8_blk<BM>(mrs, lr, n0 + c, y0, y1);
             }
+        }
+        if constexpr (!LAST) {
+            __shared__ uint32_t red[MP_THREADS / 64];
+            publish_max(mx, P.amax_out + (size_t)blk * P.n_tiles + n0 / BN, red);
         }
         if constexpr (LAST) {
             __syncthreads();  // every read of P done: M_t replaces it
@@ -347,62 +381,54 @@ struct MpEpilogue {
 };
 
 // grid = nblk * n_tiles (XCD-grouped: the column tiles of a block share an XCD), MP_THREADS threads.
-// LDS: two GEMM stages, reused by the epilogue as P [128][BN + 4] fp32; the last layer then
-// overwrites P with M_t (held in registers across a barrier) for the atom aggregate.
-// ACT: the activation (one instantiation each: the epilogue and, in the first layer (FIRST), the A
-// staging of M_0 = act(inp) fold it to straight-line code).
-template <int BN, bool LAST, int ACT, bool FIRST>
+// LDS: two GEMM stages, reused by the epilogue as P [128][BN + 4] fp32 + the atom sums; the last layer
+// then overwrites P with M_t (held in registers across a barrier) for the atom aggregate.
+// ACT: the activation (one instantiation each: the staging of M_{t-1} and the epilogue fold it to
+// straight-line code).
+template <int BN, bool LAST, int ACT>
 // (__launch_bounds__ min 4 waves per SIMD: <= 128 VGPRs, so that two layer workgroups -- batches in flight
-// on two streams -- co-reside on a CU, 2 x 78 KB of LDS)
+// on two streams -- co-reside on a CU)
 __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpLayerP> MP) {
-    constexpr int BM = BLK_BONDS, NT = MP_THREADS;
-    constexpr int S = 2, CPS = 1;  // two stages of one chunk
-    // (<= 80 KB: two workgroups fit one CU's 160 KB, so layers of batches in flight on other
-    // streams co-reside)
-    constexpr int EPI_BYTES = MpEpilogue<BN, NT, LAST>::LDS_FLOATS * 4;  // P tile + the atom sums
-    constexpr int LDS_BYTES = EPI_BYTES > S * CPS * x6_stage_bytes<BM, BN>() ? EPI_BYTES
-                                                                              : S * CPS * x6_stage_bytes<BM, BN>();
+    constexpr int BM = BLK_BONDS;
+    constexpr int EPI_BYTES = MpEpilogue<BN, MP_THREADS, LAST>::LDS_FLOATS * 4;  // P tile + the atom sums
+    constexpr int STG_BYTES = h2_lds_bytes<BM, BN>();
+    constexpr int LDS_BYTES = EPI_BYTES > STG_BYTES ? EPI_BYTES : STG_BYTES;
     static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU");
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
     int tile;
+    wd_stamp(0 + 8 * LAST);
     const MpLayerP &P = multi_pick(MP, xcd_tile(blockIdx.x, gridDim.x), tile);
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
-    MpEpilogue<BN, NT, LAST> E;
+    MpEpilogue<BN, MP_THREADS, LAST> E;
     float *Pt = reinterpret_cast<float *>(lds);
-    if constexpr (FIRST) {
-        // A = act(inp) from fp32 rows: warp-specialised (4 MFMA waves, 4 staging waves)
-        MsgAProd<BM, ACT> ap(P, B);
-        floatx4 acc[BM / 64][BN / 16];
-        x6_mainloop_ws<BM, BN>(P.wh + (size_t)nt * (P.kp >> 5) * (3 * BN * 64), P.kp >> 5, B.bn, lds, acc, ap);
-        // the epilogue's gather lists and ids: loaded now, not during the GEMM (live across the GEMM loop
-        // they pushed the consumers' accumulators and fragments past 128 VGPRs)
-        E.prefetch(P, B);
-        __syncthreads();
-        if (threadIdx.x < 256) x6_acc_to_lds<BM, BN, 4, 1>(acc, Pt);  // (the consumer waves hold the tile)
-    } else {
-        // A = M_{t-1} plane tiles: LDS-DMA for both operands, all 8 waves on MFMA
-        constexpr int WM = MpWaves<BN>::WM, WN = MpWaves<BN>::WN;
-        auto prefetch = [&](int phase) {
-            if (phase == 0) E.prefetch(P, B);
-        };
-        X6Operands O{};
-        O.a0 = P.mprev_pl; O.nkc0 = P.kp >> 5; O.kc0 = P.kp >> 5;
-        O.a1 = P.mprev_pl; O.nkc1 = P.kp >> 5; O.kc1 = 0;  // no second segment (a non-null alias)
-        O.rb = blk;
-        O.a_rows = B.bn;
-        O.b = P.wh + (size_t)nt * (P.kp >> 5) * (3 * BN * 64);
-        floatx4 acc[BM / WM / 16][BN / WN / 16];
-        x6_mainloop<BM, BN, WM, WN, S, CPS, true>(O, lds, acc, prefetch);
-        __syncthreads();
-        x6_acc_to_lds<BM, BN, WM, WN>(acc, Pt);
-    }
+    H2Prod<BM, ACT> ap(P, B, blk);
+    wd_stamp(1 + 8 * LAST);
+    const float ia = h2_inv_scale(max_words(P.amax_in + (size_t)blk * P.amax_in_n, P.amax_in_n));
+    const float iw = h2_inv_scale(*P.wh_amax);
+    floatx4 acc[BM / 64][BN / 16];
+#if WD_EXP_NOGEMM  // experiment: epilogue + launch only
+    for (int a = 0; a < BM / 64; ++a)
+        for (int b = 0; b < BN / 16; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    (void)ap;
+#else
+    h2_mainloop_ws<BM, BN>(P.wh + (size_t)nt * (P.kp >> 5) * (2 * BN * 64), P.kp >> 5, B.bn, lds, acc, ap);
+#endif
+    // the epilogue's gather lists and ids: loaded now, not during the GEMM (live across the GEMM loop
+    // they pushed the consumers' accumulators and fragments past 128 VGPRs)
+    wd_stamp(2 + 8 * LAST);
+    E.prefetch(P, B);
+    __syncthreads();
+    wd_stamp(3 + 8 * LAST);
+    if (threadIdx.x < 256) x6_acc_to_lds_scaled<BM, BN, 4, 1>(acc, Pt, ia, iw);  // (the consumer waves hold the tile)
     __syncthreads();
     E.template run<ACT>(P, B, blk, n0, Pt);
-    // the pad row 0 (bond and atom) belongs to no block: its saved rows are written as zeros, which the
-    // backward multiplies by its zero gradients (an uninitialised NaN would poison them)
+    wd_stamp(6 + 8 * LAST);
+    // the pad row 0 (bond and atom) belongs to no block: its Z rows are written as zeros (the backward
+    // multiplies them by its zero gradients, where an uninitialised NaN would poison them)
     if (blk == 0 && threadIdx.x < BN / 4) {
-        if (P.zsave) st4(P.zsave + n0 + 4 * threadIdx.x, f4zero());
+        float *zr = LAST ? P.zsave : P.zout;
+        if (zr) st4(zr + n0 + 4 * threadIdx.x, f4zero());
         if (LAST && P.asave) st4(P.asave + n0 + 4 * threadIdx.x, f4zero());
     }
 }
@@ -432,6 +458,8 @@ struct EmbedP {
     const int32_t *blocks;
     int Fa, Fb, Hk, n_tiles;
     float *inp;                  // [Rp][Hk]
+    const float *slope;          // PReLU slope (or null)
+    uint32_t *amax;              // [nblk][n_tiles]: max |act(inp)| per workgroup (the first layer's scale, planes.hpp h2)
 };
 
 // s = sum_{c in code} T[c][c4 .. c4+3] + last * T[Fa - 1][c4 ..] (ascending columns, then the mass column:
@@ -449,7 +477,7 @@ __device__ __forceinline__ float4 code_sum(const WdAtomCode &cd, const float *T,
     return s;
 }
 
-template <int BN>
+template <int BN, int ACT>
 __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP> MP) {
     constexpr int NT = 512, LDC = BN + 4, C4 = BN / 4, U8 = BN / 8, MAXK = 160, PER = (MAXK * C4 + NT - 1) / NT;
     constexpr int BU = (BLK_BONDS * U8 + NT - 1) / NT;  // bond units (8 columns of a row) per thread
@@ -514,6 +542,8 @@ __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP> MP) {
         st4(ea + la * LDC + c, code_sum<BN>(code[la], wt, P.Fa, c));
     }
     __syncthreads();
+    const float slope = ACT == ACT_PRELU ? P.slope[0] : 0.f;
+    uint32_t mx = 0;
 #pragma unroll
     for (int u = 0; u < BU; ++u) {
         const int v = tid + NT * u, lb = v / U8, c = 8 * (v % U8), b = B.bs + lb;
@@ -532,8 +562,13 @@ __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP> MP) {
         float *zr = P.inp + (size_t)b * P.Hk + n0 + c;
         st4(zr, z0);
         st4(zr + 4, z1);
+        const float zz[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) mx = max(mx, absbits(act_fwd(ACT, zz[q], slope)));
     }
     if (blk == 0 && tid < C4) st4(P.inp + n0 + 4 * tid, f4zero());  // pad row 0 (Z_0 of the backward)
+    __shared__ uint32_t red[NT / 64];
+    publish_max(mx, P.amax + (size_t)blk * P.n_tiles + nt, red);
 }
 
 constexpr int WO_MAXK = 160;  // f_atoms / f_bonds columns embed_kernel stages (Fa, Fb <= 160)

@@ -412,6 +412,18 @@ __device__ __forceinline__ void glds16(const void *g, uint8_t *lds_wave_base) {
     __builtin_amdgcn_global_load_lds(g, (lds_void_t *)lds_wave_base, 16, 0, 0);
 }
 
+// The same copy issued from inline asm: the compiler does not see it, so it inserts no vmcnt wait for it
+// in front of LDS reads of the other stage (for the builtin it waited at every chunk's first fragment
+// read, exposing the copy's latency); the caller's explicit vmcnt wait + barrier protocol orders it.  It
+// writes no register, so nothing the compiler moves can be overwritten late.  (M0 = the wave's LDS base,
+// saved and restored around the copy.)
+__device__ __forceinline__ void glds16_untracked(const void *g, uint8_t *lds_wave_base) {
+    const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t *)lds_wave_base);
+    uint32_t saved;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(saved) : "s"(l), "v"(g) : "memory");
+}
+
 struct X6Operands {
     const uint8_t *a0; int nkc0, kc0;   // A segment 0: base of the matrix, its 32-column chunks per row block,
                                         // chunks used (K extent / 32)
@@ -450,6 +462,15 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // chunks each.  Uses lds[0 .. S * CPS * x6_stage_bytes<BM, BN>()); on return every DMA has landed and
 // all waves are past their last LDS read (the caller may reuse the LDS after one __syncthreads()).
 struct NoHook { __device__ void operator()(int) const {} };
+
+// f(std::integral_constant<int, i>) for i = 0 .. N - 1
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<N, I + 1>(f);
+    }
+}
 
 // f(std::integral_constant<int, n>) for a wave-uniform runtime n in [0, N]
 template <int N, typename F>
@@ -624,74 +645,77 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
 }
 
 // ---------------------------------------------------------------------------------------------
-// Warp-specialised split-plane GEMM core (the message-passing layer): acc (+)= A · Bᵀ for a BM x BN
-// tile on 512 threads, two LDS stages of one 32-column chunk, one s_barrier per chunk:
+// Warp-specialised fp16-pair GEMM core (the message-passing layer, planes.hpp "h2"): acc (+)= A · Bᵀ
+// for a BM x BN tile on 512 threads, two LDS stages of one 32-column chunk, one s_barrier per chunk:
 //   waves 0-3 (consumers, one per SIMD) multiply: wave w owns rows 32 w .. 32 w + 31 and all BN
-//             columns (2 x BN/16 accumulators), so every B fragment read from LDS feeds two row tiles
-//             (84 KB of fragment reads per chunk where 16-row wave tiles read 144 KB); before chunk kc's
-//             MFMAs they issue the LDS-DMA of chunk kc + 1's B (plane tiles, no registers);
+//             columns (2 x BN/16 accumulators), so every B fragment read from LDS feeds two row tiles;
+//             three v_mfma_f32_16x16x32_f16 per tile and chunk (hi hi, hi lo, lo hi); before chunk kc's
+//             MFMAs they issue the LDS-DMA of chunk kc + 1's B (h2 plane tiles, no registers);
 //   waves 4-7 (producers, the consumers' SIMD partners) stage A through registers (AProd: fp32 rows,
-//             loads, activation, bf16x3 split, ds_write), two chunks ahead: chunk c lives in register
-//             set c & 1 from its loads (issued while chunk c - 2 is multiplied) to its LDS write (while
-//             chunk c - 1 is multiplied).
+//             loads, activation, dropout, scale, fp16 hi / lo split, ds_write), SETS chunks ahead: chunk c
+//             lives in register set c % SETS from its loads (issued while chunk c - SETS is multiplied) to
+//             its LDS write (while chunk c - 1 is multiplied).
 // The two roles run separate loops with the same barrier count, so the register allocator can give the
 // producer's staging sets the registers that hold the consumer's accumulators (a shared loop keeps both
 // live at once; aliasing them by hand made the compiler wait for the producer's loads inside the
 // consumer's MFMAs).
-// AProd interface (producer thread t = threadIdx.x & 255): LOADS (global loads per set); load(set, kc)
-// issues chunk kc's loads into register set `set`; store(set, stage) writes the stage's A image
-// (3 x BM x 64 B, x6_slot layout) from it.
+// AProd interface (producer thread t = threadIdx.x & 255): SETS (register sets: chunks in flight); load(set,
+// kc) issues chunk kc's loads into register set `set`; store(set, kc, stage) writes the stage's A image
+// (2 x BM x 64 B: hi plane, lo plane, x6_slot layout) from it.
 // On return every wave is past its last LDS access of the stages; the consumers' acc holds the tile
 // (the producers' acc is left undefined: the caller reads it in threads 0..255 only).
 // ---------------------------------------------------------------------------------------------
+// B (W_h) copies run WD_B_AHEAD chunks ahead of the chunk multiplied: WD_B_AHEAD + 1 B stages, two A stages
+#ifndef WD_B_AHEAD
+#define WD_B_AHEAD 1
+#endif
+// WD_ALLB: a consumer reads all of a chunk's fragments before its first MFMA (else: the next column
+// tile's B fragments behind each tile's products)
+#ifndef WD_ALLB
+#define WD_ALLB 1
+#endif
+template <int BM, int BN>
+constexpr int h2_lds_bytes() { return 2 * (2 * BM * 64) + (WD_B_AHEAD + 1) * (2 * BN * 64); }
+
 template <int BM, int BN, typename AProd>
-__device__ __forceinline__ void x6_mainloop_ws(const uint8_t *bsrc_base, int nchunks, int a_rows, uint8_t *lds,
+__device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nchunks, int a_rows, uint8_t *lds,
                                                floatx4 (&acc)[BM / 64][BN / 16], AProd &ap) {
     static_assert(BM == 128, "four consumer waves of 32 rows");
     constexpr int TM = BM / 64, TN = BN / 16;
-    constexpr int APL = BM * 64, BPL = BN * 64, STAGE = x6_stage_bytes<BM, BN>();
-    constexpr int BP = 3 * BN / 16, BPW = (BP + 3) / 4;  // B: 1 KB DMA pieces per chunk, per consumer wave
-    constexpr int VM = AProd::LOADS;
-    static_assert(VM <= 15, "vmcnt immediate");
+    constexpr int APL = BM * 64, BPL = BN * 64;
+    constexpr int ASTAGE = 2 * APL, BSTAGE = 2 * BPL, NB = WD_B_AHEAD + 1;  // A stages [2], then B stages [NB]
+    constexpr int BP = 2 * BN / 16, BPW = (BP + 3) / 4;  // B: 1 KB DMA pieces per chunk, per consumer wave
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int w4 = wave & 3, g = lane >> 4, i16 = lane & 15;
-    using S0 = std::integral_constant<int, 0>;
-    using S1 = std::integral_constant<int, 1>;
 
-    if (wave >= 4) {  // ---- producers
-        ap.load(S0{}, 0);
-        if (nchunks > 1) {
-            ap.load(S1{}, 1);
-            ap.template wait<VM>(S0{});  // chunk 0 landed
-        } else {
-            ap.template wait<0>(S0{});
-        }
-        ap.store(S0{}, lds);
-        if (nchunks > 2) ap.load(S0{}, 2);
-        auto produce = [&](int kc, auto set) {  // set = (kc + 1) & 1 holds chunk kc + 1
+    if (wave >= 4) {  // ---- producers: chunk c in register set c % NS, loaded NS chunks ahead of its store
+        // (compiler-visible loads, issued unconditionally -- past the last chunk they reload it -- so that the
+        // compiler's own vmcnt waits before each store are exact: all but the NS - 1 younger sets)
+        constexpr int NS = AProd::SETS;
+        static_for<NS>([&](auto i) { ap.load(i, min((int)decltype(i)::value, nchunks - 1)); });
+        ap.store(std::integral_constant<int, 0>{}, 0, lds);
+        ap.load(std::integral_constant<int, 0>{}, min(NS, nchunks - 1));
+        auto produce = [&](int kc, auto set) {  // set = (kc + 1) % NS holds chunk kc + 1
             if (kc + 1 >= nchunks) return;
-            if (kc + 2 < nchunks) ap.template wait<VM>(set);  // all but the newest set landed
-            else ap.template wait<0>(set);
-            ap.store(set, lds + ((kc + 1) & 1) * STAGE);
-            if (kc + 3 < nchunks) ap.load(set, kc + 3);
+#if !WD_EXP_NOPROD  // experiment: no staging work (the consumers multiply stale LDS)
+            ap.store(set, kc + 1, lds + ((kc + 1) & 1) * ASTAGE);
+            ap.load(set, min(kc + 1 + NS, nchunks - 1));
+#endif
         };
         int kc = 0;
-        for (; kc + 1 < nchunks; kc += 2) {
-            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's stage writes done
-            __builtin_amdgcn_s_barrier();
-            produce(kc, S1{});
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            __builtin_amdgcn_s_barrier();
-            produce(kc + 1, S0{});
-        }
-        if (kc < nchunks) {
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            __builtin_amdgcn_s_barrier();
-            produce(kc, S1{});
-        }
-        // every load landed before the registers go to other values (the asm loads' late writes)
-        ap.template wait<0>(S0{});
-        ap.template wait<0>(S1{});
+        for (; kc + NS <= nchunks; kc += NS)
+            static_for<NS>([&](auto j) {
+                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's stage writes done
+                __builtin_amdgcn_s_barrier();
+                produce(kc + decltype(j)::value, std::integral_constant<int, (decltype(j)::value + 1) % NS>{});
+            });
+        static_for<NS>([&](auto j) {
+            if (kc + decltype(j)::value < nchunks) {
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+                __builtin_amdgcn_s_barrier();
+                produce(kc + decltype(j)::value, std::integral_constant<int, (decltype(j)::value + 1) % NS>{});
+            }
+        });
         __builtin_amdgcn_s_waitcnt(0xc07f);
         return;
     }
@@ -700,52 +724,69 @@ __device__ __forceinline__ void x6_mainloop_ws(const uint8_t *bsrc_base, int nch
     int bsrc[BPW];
 #pragma unroll
     for (int j = 0; j < BPW; ++j) {
-        const int q = 64 * (4 * j + w4) + lane, p = (q / (BN * 4)) % 3, r = (q >> 2) % BN, sl = q & 3;
+        const int q = 64 * (4 * j + w4) + lane, p = (q / (BN * 4)) % 2, r = (q >> 2) % BN, sl = q & 3;
         bsrc[j] = p * BPL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
     }
     auto issue_b = [&](int kc) {
-        const uint8_t *bblk = bsrc_base + (size_t)kc * (3 * BPL);
-        uint8_t *st = lds + (kc & 1) * STAGE + 3 * APL;
+        const uint8_t *bblk = bsrc_base + (size_t)kc * (2 * BPL);
+        uint8_t *st = lds + 2 * ASTAGE + (kc % NB) * BSTAGE;
 #pragma unroll
         for (int j = 0; j < BPW; ++j)
-            if (BP % 4 == 0 || 4 * j + w4 < BP) glds16(bblk + bsrc[j], st + 1024 * (4 * j + w4));
+            if (BP % 4 == 0 || 4 * j + w4 < BP) glds16_untracked(bblk + bsrc[j], st + 1024 * (4 * j + w4));
     };
     int ao[TM], bo[TN];
 #pragma unroll
     for (int a = 0; a < TM; ++a) ao[a] = x6_slot(32 * w4 + 16 * a + i16, g);
 #pragma unroll
-    for (int b = 0; b < TN; ++b) bo[b] = 3 * APL + x6_slot(16 * b + i16, g);
+    for (int b = 0; b < TN; ++b) bo[b] = x6_slot(16 * b + i16, g);
     const int na = min(TM, max(0, (a_rows - 32 * w4 + 15) >> 4));
-    auto compute_n = [&](const uint8_t *st, auto na_c) {
+    auto compute_n = [&](const uint8_t *st, const uint8_t *sb, auto na_c) {
         constexpr int NA = decltype(na_c)::value;
-        constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};  // hh hm mh hl lh mm
-        bf16x8 af[TM][3], bq[2][3];
+        if constexpr (WD_ALLB) {
+            f16x8 af[TM][2], bf[TN][2];
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
+            for (int p = 0; p < 2; ++p)
 #pragma unroll
-            for (int a = 0; a < NA; ++a) af[a][p] = *reinterpret_cast<const bf16x8 *>(st + p * APL + ao[a]);
-            bq[0][p] = *reinterpret_cast<const bf16x8 *>(st + p * BPL + bo[0]);
+                for (int a = 0; a < NA; ++a) af[a][p] = *reinterpret_cast<const f16x8 *>(st + p * APL + ao[a]);
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+#pragma unroll
+                for (int p = 0; p < 2; ++p) bf[b][p] = *reinterpret_cast<const f16x8 *>(sb + p * BPL + bo[b]);
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+#pragma unroll
+                for (int a = 0; a < NA; ++a) {
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][0], bf[b][0], acc[a][b], 0, 0, 0);
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][0], bf[b][1], acc[a][b], 0, 0, 0);
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][1], bf[b][0], acc[a][b], 0, 0, 0);
+                }
+            return;
         }
-        // column tile b: three products, the next tile's fragment reads, the other three products -- pinned
-        // in that order (left to itself the scheduler issued each tile's reads just before their use, and
-        // its LDS wait then also covered the reads issued after them)
+        f16x8 af[TM][2], bq[2][2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+#pragma unroll
+            for (int a = 0; a < NA; ++a) af[a][p] = *reinterpret_cast<const f16x8 *>(st + p * APL + ao[a]);
+            bq[0][p] = *reinterpret_cast<const f16x8 *>(sb + p * BPL + bo[0]);
+        }
+        // column tile b: hi hi, the next tile's fragment reads, hi lo and lo hi -- pinned in that order (left
+        // to itself the scheduler issued each tile's reads just before their use, and its LDS wait then also
+        // covered the reads issued after them)
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
 #pragma unroll
-            for (int t = 0; t < 3; ++t)
-#pragma unroll
-                for (int a = 0; a < NA; ++a)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][PA[t]], bq[b & 1][PB[t]], acc[a][b], 0, 0, 0);
+            for (int a = 0; a < NA; ++a)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][0], bq[b & 1][0], acc[a][b], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
             if (b + 1 < TN)
 #pragma unroll
-                for (int p = 0; p < 3; ++p) bq[(b + 1) & 1][p] = *reinterpret_cast<const bf16x8 *>(st + p * BPL + bo[b + 1]);
+                for (int p = 0; p < 2; ++p) bq[(b + 1) & 1][p] = *reinterpret_cast<const f16x8 *>(sb + p * BPL + bo[b + 1]);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int t = 3; t < 6; ++t)
-#pragma unroll
-                for (int a = 0; a < NA; ++a)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][PA[t]], bq[b & 1][PB[t]], acc[a][b], 0, 0, 0);
+            for (int a = 0; a < NA; ++a) {
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][0], bq[b & 1][1], acc[a][b], 0, 0, 0);
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][1], bq[b & 1][0], acc[a][b], 0, 0, 0);
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -753,13 +794,27 @@ __device__ __forceinline__ void x6_mainloop_ws(const uint8_t *bsrc_base, int nch
     for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
-    issue_b(0);
+    // this wave's copies per chunk (uniform)
+    int mine = 0;
+#pragma unroll
+    for (int j = 0; j < BPW; ++j) mine += BP % 4 == 0 || 4 * j + w4 < BP;
+#pragma unroll
+    for (int c = 0; c < WD_B_AHEAD; ++c)
+        if (c < nchunks) issue_b(c);
     for (int kc = 0; kc < nchunks; ++kc) {
-        __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): this wave's B DMA landed, its reads done
+        // chunk kc's B landed for this wave (the WD_B_AHEAD - 1 younger chunks may stay in flight), this
+        // wave's fragment reads done; then for every wave: A chunk kc staged, B stage (kc + WD_B_AHEAD) % NB
+        // read by all (at kc - 1)
+        wait_vmcnt(min(WD_B_AHEAD - 1, nchunks - 1 - kc) * mine);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (kc + 1 < nchunks) issue_b(kc + 1);
-        const uint8_t *st = lds + (kc & 1) * STAGE;
-        dispatch_upto<TM>(na, [&](auto c) { compute_n(st, c); });
+        if (kc + WD_B_AHEAD < nchunks) issue_b(kc + WD_B_AHEAD);
+        const uint8_t *st = lds + (kc & 1) * ASTAGE, *sb = lds + 2 * ASTAGE + (kc % NB) * BSTAGE;
+#if !WD_EXP_NOMFMA  // experiment: no fragment reads / MFMAs
+        dispatch_upto<TM>(na, [&](auto c) { compute_n(st, sb, c); });
+#else
+        (void)st; (void)sb;
+#endif
     }
     __builtin_amdgcn_s_waitcnt(0x0070);
 }
@@ -777,6 +832,23 @@ __device__ __forceinline__ void x6_acc_to_lds(const floatx4 (&acc)[BM / WM / 16]
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 cl[(wi * (BM / WM) + a * 16 + 4 * g + r) * LDC + wj * (BN / WN) + b * 16 + i16] = acc[a][b][r];
+}
+
+// the same with every value multiplied by sa and then sb (the h2 operands' inverse scales: powers of two,
+// exact unless the result is subnormal)
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void x6_acc_to_lds_scaled(const floatx4 (&acc)[BM / WM / 16][BN / WN / 16], float *cl,
+                                                     float sa, float sb) {
+    constexpr int TM = BM / WM / 16, TN = BN / WN / 16, LDC = BN + 4;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wi = wave / WN, wj = wave % WN, g = lane >> 4, i16 = lane & 15;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                cl[(wi * (BM / WM) + a * 16 + 4 * g + r) * LDC + wj * (BN / WN) + b * 16 + i16] = acc[a][b][r] * sa * sb;
 }
 
 struct X6PParams {

@@ -292,12 +292,14 @@ struct PackJob {
     const float *src; int ld_src;
     int transpose, nrows, nseg;
     int dc0[2], sc0[2], K[2];
+    uint32_t *amax;  // or null: max |dst| of workgroup x -> amax[x] (the h2 scale of split_h2_kernel)
 };
 struct PackJobs { PackJob j[16]; int n; };
 
 __global__ __launch_bounds__(256) void pack_kernel(PackJobs J) {
     const PackJob &P = J.j[blockIdx.y];
     const size_t total = (size_t)P.rows_p * P.cols_p;
+    uint32_t mx = 0;
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
         const int r = (int)(t / P.cols_p), c = (int)(t % P.cols_p);
         float v = 0.f;
@@ -310,7 +312,31 @@ __global__ __launch_bounds__(256) void pack_kernel(PackJobs J) {
             }
         }
         P.dst[t] = v;
+        mx = max(mx, absbits(v));
     }
+    if (P.amax) {  // (uniform per workgroup)
+        __shared__ uint32_t red[4];
+        publish_max(mx, P.amax + blockIdx.x, red);
+    }
+}
+
+// per molecule block (WdGraph.blocks row {bond_start, bond_count, ...}, workgroup = block): max |act(x)|
+// over the block's rows of x [.][ld], columns [0, cols) -> out[block] (the first fused layer's operand
+// scale when the input layer ran as a GEMM instead of the embed)
+template <int ACT>
+__global__ __launch_bounds__(256) void absmax_blocks_kernel(const float *x, int ld, int cols, const int32_t *blocks,
+                                                            const float *slope_p, uint32_t *out) {
+    const float slope = ACT == ACT_PRELU ? slope_p[0] : 0.f;
+    const int bs = blocks[8 * blockIdx.x], bn = blocks[8 * blockIdx.x + 1];
+    const int c4 = cols / 4;
+    uint32_t mx = 0;
+    for (int t = threadIdx.x; t < bn * c4; t += blockDim.x) {
+        const float4 v = ld4(x + (size_t)(bs + t / c4) * ld + 4 * (t % c4));
+        mx = max(mx, max(max(absbits(act_fwd(ACT, v.x, slope)), absbits(act_fwd(ACT, v.y, slope))),
+                         max(absbits(act_fwd(ACT, v.z, slope)), absbits(act_fwd(ACT, v.w, slope)))));
+    }
+    __shared__ uint32_t red[4];
+    publish_max(mx, out + blockIdx.x, red);
 }
 
 // ---------------------------------------------------------------------------------------------

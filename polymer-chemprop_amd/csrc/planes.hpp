@@ -169,4 +169,91 @@ __global__ __launch_bounds__(256) void split_tiles_batch_kernel(SplitJobs J) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp16 hi / lo pairs ("h2"): the message-passing layer's GEMM operands (fused_mp.hpp).
+//
+// With a power-of-two scale s that puts max |x| s in [2^14, 2^15) (the max over the rows one GEMM tile
+// multiplies), x s = hi + lo + r with hi = rne_f16(x s), lo = rne_f16(x s - hi) and |r| <= 2^-22 |x s|
+// (values far below the max go subnormal in lo and keep an absolute error <= 2^-25 of the scaled unit,
+// 2^-39 of the max).  A
+// product is hi_a hi_b + hi_a lo_b + lo_a hi_b (each exact in fp32, accumulated in fp32 by
+// v_mfma_f32_16x16x32_f16); the dropped lo_a lo_b is <= 2^-22 |ab|.  Three MFMAs per fp32 product
+// instead of the planes' six, 4 bytes per value instead of 6; the whole encoder stays at the error of
+// an fp32 GEMM against fp64 (tools/split_precision_sim.py: 1.2-2.9e-7 normwise, fp32 1.1-2.6e-7).
+//
+// The scale comes from the maximum of the rows one GEMM tile multiplies.  Producers publish partial
+// maxima as plain u32 words (absolute-value bits), one per producing workgroup, into slot arrays that
+// each forward overwrites completely: the embed and the message layers one word per (molecule block,
+// column tile), so the consumer of a block reads that block's few words (a per-block scale: the A tile
+// of a fused layer workgroup is one block); the weight packer one word per workgroup, folded into one
+// word by split_h2_kernel.  No atomics, no reset, deterministic.
+// ---------------------------------------------------------------------------------------------
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t absbits(float x) { return __float_as_uint(x) & 0x7fffffffu; }
+// the scale s and its inverse for max |x| (its bits m): s = 2^(141 - e) with e the biased exponent of m
+// (max |x| s in [2^14, 2^15)), both normal floats (clamped for all-zero / subnormal / non-finite maxima)
+__device__ __forceinline__ int h2_sexp(uint32_t m) {
+    const int se = 268 - (int)(m >> 23);
+    return se < 1 ? 1 : (se > 253 ? 253 : se);
+}
+__device__ __forceinline__ float h2_scale(uint32_t m) { return __uint_as_float((uint32_t)h2_sexp(m) << 23); }
+__device__ __forceinline__ float h2_inv_scale(uint32_t m) { return __uint_as_float((uint32_t)(254 - h2_sexp(m)) << 23); }
+// max of n words at a workgroup-uniform address
+__device__ __forceinline__ uint32_t max_words(const uint32_t *w, int n) {
+    uint32_t m = 0;
+    for (int i = 0; i < n; ++i) m = max(m, w[i]);
+    return m;
+}
+// (a, b) scaled by s -> packed fp16 hi pair and lo pair (element 0 in the low half)
+__device__ __forceinline__ void split_h2(float a, float b, float s, uint32_t &hi, uint32_t &lo) {
+    const f16x2v h = __builtin_convertvector((f32x2v){a * s, b * s}, f16x2v);  // v_cvt_pk_f16_f32 (RNE)
+    const float ra = fmaf(a, s, -(float)h[0]), rb = fmaf(b, s, -(float)h[1]);  // exact residuals
+    hi = __builtin_bit_cast(uint32_t, h);
+    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){ra, rb}, f16x2v));
+}
+
+// workgroup max of a u32 -> one plain store by thread 0 (red: >= blockDim.x / 64 words of LDS; every
+// thread of the workgroup must call it)
+__device__ __forceinline__ void publish_max(uint32_t m, uint32_t *slot, uint32_t *red) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint32_t o = __shfl_xor(m, off, 64);
+        m = o > m ? o : m;
+    }
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[wave] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < nw; ++w) m = red[w] > m ? red[w] : m;
+        *slot = m;
+    }
+}
+
+// fp32 [rows][ld] (first kp columns) -> h2 plane tiles with BR-row blocks: block (r / BR, k / 32) of 2 x
+// BR x 64 bytes (hi plane, then lo), row r % BR, columns k % 32 at 64 (r % BR) + 2 (k % 32) -- the bf16
+// plane-tile layout with two planes.  Scaled by the max of the nw words of `words` (pack_kernel's
+// per-workgroup maxima), which workgroup 0 also folds into words[nw] for the consumers.
+__global__ __launch_bounds__(256) void split_h2_kernel(const float *__restrict__ src, int ld, int rows, int kp, int br,
+                                                       uint8_t *__restrict__ dst, uint32_t *words, int nw) {
+    const uint32_t m = max_words(words, nw);
+    const float s = h2_scale(m);
+    if (blockIdx.x == 0 && threadIdx.x == 0) words[nw] = m;
+    const int q8 = kp >> 3;
+    const size_t total = (size_t)rows * q8;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+        const int r = (int)(t / q8), k = (int)(t % q8) * 8;
+        const float4 lo4 = ld4(src + (size_t)r * ld + k), hi4 = ld4(src + (size_t)r * ld + k + 4);
+        uint32_t h[4], l[4];
+        split_h2(lo4.x, lo4.y, s, h[0], l[0]);
+        split_h2(lo4.z, lo4.w, s, h[1], l[1]);
+        split_h2(hi4.x, hi4.y, s, h[2], l[2]);
+        split_h2(hi4.z, hi4.w, s, h[3], l[3]);
+        uint8_t *d = dst + ((size_t)(r / br) * (kp >> 5) + (k >> 5)) * (2 * br * 64) + (r % br) * 64 + 2 * (k & 31);
+        *reinterpret_cast<u32x4 *>(d) = u32x4{h[0], h[1], h[2], h[3]};
+        *reinterpret_cast<u32x4 *>(d + br * 64) = u32x4{l[0], l[1], l[2], l[3]};
+    }
+}
+
 }  // namespace wd

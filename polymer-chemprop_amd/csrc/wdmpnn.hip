@@ -63,6 +63,8 @@ int fail(int code, const char *fmt, ...) {
     } while (0)
 
 inline int rup(int x, int m) { return (x + m - 1) / m * m; }
+
+
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
@@ -114,7 +116,8 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     // natural rows for the backward)
     // (an embed-capable graph -- categorical codes -- needs no feature planes)
     const bool codes = g->atom_codes && g->bond_src_blk && g->bond_tail && D.Fb <= WO_MAXK && D.Fa <= WO_MAXK;
-    D.blocked = D.x6 && !D.desc && D.T >= 2 && g->n_blocks > 0 && g->blocks && g->bond_blk_row &&
+    // (Hk <= 2560: at most 64 column tiles of 40 per block, the h2 scale words' capacity)
+    D.blocked = D.x6 && !D.desc && D.T >= 2 && D.Hk <= 2560 && g->n_blocks > 0 && g->blocks && g->bond_blk_row &&
                 (codes || (g->f_atoms_blk_x6 && g->f_bonds_x6)) && g->bond_src_blk && g->b2revb &&
                 g->atom_ell_idx && g->atom_ell_coef;
     D.nblk = D.blocked ? g->n_blocks : 0;
@@ -145,7 +148,13 @@ struct PackLayout {
     size_t WhX80 = 0, WoX80 = 0;       // the same with 80-row blocks (fused forward, Hk % 80 == 0)
     size_t WiT = 0, WoaT = 0;          // W_i^T [Kink][Hk] and W_o[:, :Fa]^T [Fak][Hk]: weight columns as rows
                                        // (the categorical-code embedding of the fused forward)
+    size_t WhH = 0;                    // h2 plane tiles of W_h (fused layers; BN-row blocks, BN = fused_bn)
+    size_t amax = 0;                   // W_h's h2 scale: pack_kernel's 64 per-workgroup maxima + their max (u32)
 };
+
+// column tile of the fused kernels: 80 when it divides Hk (Hk = 320: 4 tiles, one workgroup per CU at the
+// benchmark size), else 64
+int fused_bn(int Hk) { return Hk % 80 == 0 ? 80 : 64; }
 
 PackLayout pack_layout(const Dims &D) {
     PackLayout L;
@@ -168,6 +177,8 @@ PackLayout pack_layout(const Dims &D) {
         L.WhX80 = take((size_t)D.Hk * D.ldx * 3 / 2);
         L.WoX80 = take((size_t)D.Hk * D.Ko * 3 / 2);
     }
+    L.WhH = take((size_t)D.Hk * D.Hk);  // 2 fp16 per value
+    L.amax = take(65);
     if (D.desc) {
         L.Wd = take((size_t)D.Hdk * D.Kd);
         L.bd = take(D.Hdk);
@@ -204,10 +215,12 @@ int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
     auto add = [&](const PackJob &j) { J.j[J.n++] = j; };
     add(job_plain(F(L.Wi), D.Hk, D.Kink, p->W_i, D.Kin, H, {{0, 0, D.Kin}}));
     add(job_plain(F(L.bi), 1, D.Hk, p->b_i, H, 1, {{0, 0, H}}));
+    uint32_t *wh_amax = (uint32_t *)(base + L.amax);
     if (D.atom)
         add(job_plain(F(L.Wh), D.Hk, D.ldx, p->W_h, H + D.Fb, H, {{0, 0, H}, {D.Hk, H, D.Fb}}));
     else
         add(job_plain(F(L.Wh), D.Hk, D.ldx, p->W_h, H, H, {{0, 0, H}}));
+    J.j[J.n - 1].amax = wh_amax;  // (pack_kernel's grid: 64 workgroups per job)
     add(job_plain(F(L.bh), 1, D.Hk, p->b_h, H, 1, {{0, 0, H}}));
     add(job_plain(F(L.Wo), D.Hk, D.Ko, p->W_o, D.Fa + H, H, {{0, 0, D.Fa}, {D.Fak, D.Fa, H}}));
     add(job_plain(F(L.bo), 1, D.Hk, p->b_o, H, 1, {{0, 0, H}}));
@@ -240,6 +253,10 @@ int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
     const int kmax = std::max(D.Kink, std::max(D.ldx, D.Ko));
     hipLaunchKernelGGL(split_tiles_batch_kernel, dim3(ew_blocks((size_t)D.Hk * kmax / 8), X.n), dim3(256), 0, st, X);
     WD_CHECK_LAUNCH("pack_params planes");
+    // fp16 hi / lo tiles of W_h[:, :Hk] for the fused layers, scaled by its published maximum
+    hipLaunchKernelGGL(split_h2_kernel, dim3(ew_blocks((size_t)D.Hk * D.Hk / 8)), dim3(256), 0, st, (const float *)F(L.Wh),
+                       D.ldx, D.Hk, D.Hk, fused_bn(D.Hk), (uint8_t *)(base + L.WhH), wh_amax, 64);
+    WD_CHECK_LAUNCH("pack_params h2");
     return 0;
 }
 
@@ -465,7 +482,8 @@ struct FwdLayout {
     std::vector<size_t> Z, M, X;
     size_t packed = 0, A = 0, Zo = 0, h = 0, Zd = 0, hd = 0, total = 0;
     size_t Xp = 0, Ap = 0;  // plane tiles of X_t and A (D.x6)
-    size_t Mb[2] = {0, 0}, Ab = 0;  // molecule-blocked plane tiles of M_t (ping-pong) and A (D.blocked)
+    size_t Zb[2] = {0, 0}, Ab = 0;  // D.blocked inference: Z_t fp32 rows (ping-pong); A as blocked plane tiles
+    size_t amax[2] = {0, 0};        // D.blocked: h2 scale words of M_t, ping-pong [nblk][tiles] (planes.hpp)
     size_t Eo = 0;                  // D.blocked: f_atoms W_o[:, :Fa]^T per blocked atom row (compact codes)
     bool own_pack = false;
 };
@@ -485,8 +503,11 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
     }
     L.A = take(atm);
     if (D.blocked) {
-        // M_t plane tiles, ping-pong (layer t writes Mb[t & 1]; the first reads inp, the last writes none)
-        for (int i = 0; i < 2 && i < D.T - 2; ++i) L.Mb[1 - i] = take((size_t)D.nblk * BLK_BONDS * D.Hk * 6);
+        // Z_t, ping-pong (layer t writes Zb[t & 1]; the first reads inp, the last writes none; a training
+        // forward writes L.Z[t] instead)
+        if (!D.save)
+            for (int i = 0; i < 2 && i < D.T - 2; ++i) L.Zb[1 - i] = take(msg);
+        for (int i = 0; i < 2; ++i) L.amax[i] = take((size_t)D.nblk * 64 * 4);  // (<= 64 tiles per block)
         L.Ab = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 6);
         L.Eo = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 4);
     } else if (D.x6) {
@@ -669,11 +690,14 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
         if (fused_codes(jobs[j].g, jobs[j].D) != codes || jobs[j].D.Hk != Hk || jobs[j].D.T != D0.T ||
             jobs[j].D.Fa != D0.Fa || jobs[j].D.Fb != D0.Fb || jobs[j].D.save != D0.save)
             return fail(WD_ERR_UNSUPPORTED, "fused forward: batches of one launch differ in layout");
+    // h2 scale words of M_t (written by the embed for t = 0, by layer t after): [nblk][tiles of the producer]
+    auto slot = [&](const FusedJob &J, int t) { return (uint32_t *)(J.ws + J.L.amax[t & 1]); };
+    // 40-column tiles for the embed when they divide Hk: twice the workgroups of the layer tiling (two per
+    // CU at the benchmark size, 37 KB of LDS each), so one's staging overlaps the other's sums
+    const bool bn40 = Hk % 40 == 0;
+    const int embed_tiles = Hk / (bn40 ? 40 : BNf);
     if (codes) {
-        // 40-column tiles when they divide Hk: twice the workgroups of the layer tiling (two per CU at the
-        // benchmark size, 37 KB of LDS each), so one's staging overlaps the other's sums
-        const bool bn40 = Hk % 40 == 0;
-        const int nt = Hk / (bn40 ? 40 : BNf);
+        const int nt = embed_tiles;
         Multi<EmbedP> M;
         int grid;
         launch_multi(jobs, n, nt, [&](EmbedP &E, const FusedJob &J) {
@@ -683,10 +707,14 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
             E.blocks = g->blocks;
             E.Fa = J.D.Fa; E.Fb = J.D.Fb; E.Hk = Hk; E.n_tiles = nt;
             E.inp = F(J, J.L.Z[0]);
+            E.slope = p->prelu; E.amax = slot(J, 0);
         }, M, grid);
-        if (bn40) hipLaunchKernelGGL(embed_kernel<40>, dim3(grid), dim3(512), 0, st, M);
-        else if (bn80) hipLaunchKernelGGL(embed_kernel<80>, dim3(grid), dim3(512), 0, st, M);
-        else hipLaunchKernelGGL(embed_kernel<64>, dim3(grid), dim3(512), 0, st, M);
+        host_with_act(c->activation, [&](auto act_c) {
+            constexpr int A = decltype(act_c)::value;
+            if (bn40) hipLaunchKernelGGL((embed_kernel<40, A>), dim3(grid), dim3(512), 0, st, M);
+            else if (bn80) hipLaunchKernelGGL((embed_kernel<80, A>), dim3(grid), dim3(512), 0, st, M);
+            else hipLaunchKernelGGL((embed_kernel<64, A>), dim3(grid), dim3(512), 0, st, M);
+        });
         WD_CHECK_LAUNCH("embed");
     } else {
         for (int j = 0; j < n; ++j) {
@@ -695,6 +723,11 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
             Epi e = epi_act(ACT_IDENTITY, nullptr, W(PL.bi), nullptr, F(J, J.L.Z[0]), nullptr, Hk, c, 0);
             if (!x6g_eligible(e)) return fail(WD_ERR_SHAPE, "fused forward: unaligned buffers");
             WD_TRY(gemm_x6g(J.g->f_bonds_x6, J.g->ld_bonds, J.D.Kink, nullptr, 0, 0, pk + PL.WiX, J.D.Rp, Hk, e, st));
+            host_with_act(c->activation, [&](auto act_c) {
+                hipLaunchKernelGGL(absmax_blocks_kernel<decltype(act_c)::value>, dim3(J.D.nblk), dim3(256), 0, st,
+                                   (const float *)F(J, J.L.Z[0]), Hk, Hk, J.g->blocks, p->prelu, slot(J, 0));
+            });
+            WD_CHECK_LAUNCH("absmax");
         }
     }
     const int T = D0.T;
@@ -704,12 +737,18 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
         int grid;
         launch_multi(jobs, n, Hk / BNf, [&](MpLayerP &Q, const FusedJob &J) {
             const WdGraph *g = J.g;
-            // M_{t-1}: the first layer stages act(inp) itself; then plane tiles ping-pong
-            Q.mprev = F(J, J.L.Z[0]);
-            Q.mprev_pl = (const uint8_t *)(J.ws + J.L.Mb[(t - 1) & 1]);
-            Q.mnext_pl = last ? nullptr : (uint8_t *)(J.ws + J.L.Mb[t & 1]);
+            // Z_{t-1} in, Z_t out (the last layer: none): a training forward keeps every Z_t (L.Z), inference
+            // ping-pongs two buffers after inp
+            auto zbuf = [&](int k) { return k == 0 || J.D.save ? F(J, J.L.Z[k]) : F(J, J.L.Zb[k & 1]); };
+            Q.zin = zbuf(t - 1);
+            Q.amax_in = slot(J, t - 1);
+            Q.amax_in_n = t > 1 ? Hk / BNf : (codes ? embed_tiles : 1);
+            Q.p_drop_in = t - 1 == 0 ? 0.f : c->dropout;
+            Q.zout = last ? nullptr : zbuf(t);
+            Q.amax_out = last ? nullptr : slot(J, t);
             Q.kp = Hk;
-            Q.wh = (const uint8_t *)(pk + (bn80 ? PL.WhX80 : PL.WhX)); Q.inp = F(J, J.L.Z[0]);
+            Q.wh = (const uint8_t *)(pk + PL.WhH); Q.wh_amax = (const uint32_t *)(pk + PL.amax) + 64;
+            Q.inp = F(J, J.L.Z[0]);
             Q.bias = p->b_h ? W(PL.bh) : nullptr;
             Q.blocks = g->blocks;
             Q.rev = g->b2revb; Q.src_blk = g->bond_src_blk; Q.undirected = J.D.undirected;
@@ -718,30 +757,23 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
             Q.aell_idx = g->atom_ell_idx; Q.aell_coef = g->atom_ell_coef;
             Q.aplanes = (uint8_t *)(J.ws + J.L.Ab);
             Q.n_tiles = Hk / BNf;
-            Q.zsave = J.D.save ? F(J, J.L.Z[t]) : nullptr;
+            Q.zsave = J.D.save && last ? F(J, J.L.Z[t]) : nullptr;
             Q.asave = J.D.save && last ? F(J, J.L.A) : nullptr;
         }, M, grid);
         if (t == 1) WD_TRY(record_prof(c, 0, 0, st));  // one pair around all the layers
-        // one instantiation per (tile width, last layer, activation, first layer)
-        auto go = [&](auto bn_c, auto last_c, auto first_c) {
+        // one instantiation per (tile width, last layer, activation)
+        auto go = [&](auto bn_c, auto last_c) {
             constexpr int BN = decltype(bn_c)::value;
-            constexpr bool LAST = decltype(last_c)::value, FIRST = decltype(first_c)::value;
-            const dim3 blk(MP_THREADS);
+            constexpr bool LAST = decltype(last_c)::value;
             host_with_act(c->activation, [&](auto act_c) {
-                hipLaunchKernelGGL((mp_layer_kernel<BN, LAST, decltype(act_c)::value, FIRST>), dim3(grid), blk, 0, st, M);
+                hipLaunchKernelGGL((mp_layer_kernel<BN, LAST, decltype(act_c)::value>), dim3(grid), dim3(MP_THREADS), 0,
+                                   st, M);
             });
         };
         using I80 = std::integral_constant<int, 80>;
         using I64 = std::integral_constant<int, 64>;
-        using BT = std::true_type;
-        using BF = std::false_type;
-        if (bn80) {
-            if (t == 1) { if (last) go(I80{}, BT{}, BT{}); else go(I80{}, BF{}, BT{}); }
-            else { if (last) go(I80{}, BT{}, BF{}); else go(I80{}, BF{}, BF{}); }
-        } else {
-            if (t == 1) { if (last) go(I64{}, BT{}, BT{}); else go(I64{}, BF{}, BT{}); }
-            else { if (last) go(I64{}, BT{}, BF{}); else go(I64{}, BF{}, BF{}); }
-        }
+        if (bn80) { if (last) go(I80{}, std::true_type{}); else go(I80{}, std::false_type{}); }
+        else { if (last) go(I64{}, std::true_type{}); else go(I64{}, std::false_type{}); }
         WD_CHECK_LAUNCH("mp_layer");
         if (last) WD_TRY(record_prof(c, 0, 1, st));
     }
@@ -789,6 +821,19 @@ int graph_build_launch(const GraphBuildP *P, int n, hipStream_t st);
 extern "C" {
 
 int wdmpnn_abi_version(void) { return WDMPNN_ABI_VERSION; }
+
+// experiment builds (WD_STAMPS): copy the layer kernel's phase stamps of the last launch to the host
+int wdmpnn_debug_stamps(void *host, size_t bytes) {
+#if WD_STAMPS
+    if (hipDeviceSynchronize() != hipSuccess) return fail(WD_ERR_ARG, "sync");
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wd_stamps), std::min(bytes, sizeof(g_wd_stamps))) != hipSuccess)
+        return fail(WD_ERR_ARG, "stamps copy");
+    return 0;
+#else
+    (void)host; (void)bytes;
+    return fail(WD_ERR_UNSUPPORTED, "library built without WD_STAMPS");
+#endif
+}
 
 
 
@@ -1459,6 +1504,7 @@ int wdmpnn_feed_next(void *feed, void *stream, WdGraph *g, WdFeedBatch *info) {
         info->h2d_bytes = S.total;
     }
     F->handed = i + 1;
+    if (WD_FEED_GROUP) F->cv.notify_all();  // (the feeder groups its builds while the consumer holds built batches)
     return 0;
 }
 

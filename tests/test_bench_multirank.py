@@ -1,6 +1,6 @@
 """bench.py's multi-rank path (process group, per-rank disjoint shards, MAX / SUM reductions of the
-timings and counters, streamed DP training with one gradient all-reduce per step), run here as two ranks
-on cuda:0 over gloo: the 8-GPU node runs the same code with backend 'nccl' (chemprop_amd.dp
+timings and counters, per-rank producer cap, streamed DP training with one gradient all-reduce per step),
+run here as four ranks on cuda:0 over gloo: the 8-GPU node runs the same code with backend 'nccl' (chemprop_amd.dp
 .init_distributed is the only initialisation path).  The launcher starts in a fresh child process,
 before any GPU call in that child."""
 import json
@@ -24,10 +24,10 @@ def _free_port():
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
-def test_bench_two_ranks_gloo_on_one_gpu():
+def test_bench_four_ranks_gloo_on_one_gpu():
     per_rank = 1280
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
-           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), 'bench.py', '--gpus', '2',
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '4',
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), 'bench.py', '--gpus', '4',
            '--steps', '5', '--warmup', '1', '--n-batches', '2', '--no-cpu', '--no-secondary',
            '--stream-graphs', str(per_rank), '--stream-train-graphs', '512']
     env = dict(os.environ, BENCH_BACKEND='gloo', MASTER_ADDR='127.0.0.1', OMP_NUM_THREADS='4')
@@ -36,8 +36,17 @@ def test_bench_two_ranks_gloo_on_one_gpu():
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
     assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints the one JSON line
     d = json.loads(lines[0])
-    assert d['n_gpus'] == 2 and d['config']['global_batch'] == 128
+    assert d['n_gpus'] == 4 and d['config']['global_batch'] == 256
     assert d['value'] > 0 and d['ms_per_step'] > 0
-    assert d['streamed']['graphs'] == 2 * per_rank and d['streamed']['n_gpus'] == 2
-    assert d['streamed_training']['n_gpus'] == 2 and d['streamed_training']['steps_per_rank'] == 4
+    st = d['streamed']
+    assert st['graphs'] == 4 * per_rank and st['n_gpus'] == 4
+    # producers per rank capped by the node's usable cores shared over its 4 ranks
+    from chemprop_amd.stream import producer_cap
+    assert st['producer_cap'] == producer_cap(4)
+    assert st['producers_per_rank'] == [st['producer_cap']] * 4
+    # disjoint shards: rank r streams batch seeds [lo_r, hi_r), pairwise disjoint
+    rng = sorted(tuple(r) for r in st['shard_seed_ranges'])
+    assert len(rng) == 4 and all(hi - lo == per_rank // 64 for lo, hi in rng)
+    assert all(rng[i][1] <= rng[i + 1][0] for i in range(3))
+    assert d['streamed_training']['n_gpus'] == 4 and d['streamed_training']['steps_per_rank'] == 4
     assert d['roofline']['launches_timed'] == 5 * 2

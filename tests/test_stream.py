@@ -176,3 +176,24 @@ def test_native_feed_bad_spec_raises():
         NativeFeed('protein', 8, 1, seed=0, device=DEV)
     f = NativeFeed('qm9', 8, 0, seed=0, device=DEV)
     assert list(f) == []
+
+
+def test_native_feed_released_batch_raises_and_close_is_safe():
+    """A NativeFeed batch used after the next one was requested raises (its slot may hold another batch);
+    a feed dropped or closed before or during iteration stops its threads (context manager, close twice,
+    garbage collection)."""
+    import gc
+    from chemprop_amd.stream import NativeFeed
+    enc = _encoder(hidden=64)
+    with torch.no_grad(), NativeFeed('polymer', 8, 4, seed=2, device=DEV, slots=4) as f:
+        it = iter(f)
+        g1 = next(it)
+        out1 = enc(g1)
+        g2 = next(it)
+        with pytest.raises(RuntimeError, match='released'):
+            enc(g1)
+        assert enc(g2).shape == out1.shape
+    f.close()  # idempotent
+    NativeFeed('polymer', 8, 50, seed=2, device=DEV, slots=4)  # dropped unread
+    gc.collect()
+    torch.cuda.synchronize()

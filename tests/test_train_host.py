@@ -76,3 +76,19 @@ def test_build_optimizer_follows_reference_args():
     opt = build_optimizer(m, TrainArgs(optimizer='adamw', device=torch.device('cpu')))
     assert type(opt) is torch.optim.AdamW and opt.param_groups[0]['lr'] == 1e-4
     assert build_optimizer(m, 2e-3).param_groups[0]['lr'] == 2e-3
+
+
+def test_direct_step_requires_every_trainable_parameter_written():
+    """the direct step skips zero_grad and writes only the encoder's native gradients and the
+    fused head's; a model with any other trainable parameter must take the autograd path."""
+    from chemprop_amd import MoleculeModel, TrainArgs, synthetic
+    from chemprop_amd.featurization import BatchMolGraph
+    from chemprop_amd.train import _direct_encoder
+    model = MoleculeModel(TrainArgs(hidden_size=32, depth=3, device=torch.device('cpu')))
+    head = (model.ffn[1], model.ffn[4], 0)
+    batch = [BatchMolGraph(synthetic.make_batch('polymer', 2, 0))]
+    assert _direct_encoder(model, batch, None, head) is model.encoder.encoder[0]
+    model.extra = torch.nn.Parameter(torch.zeros(3))  # trainable, but no direct-step gradient
+    assert _direct_encoder(model, batch, None, head) is None
+    model.extra.requires_grad_(False)  # frozen parameters stop the direct path as before
+    assert _direct_encoder(model, batch, None, head) is None
