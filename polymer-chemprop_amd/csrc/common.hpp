@@ -99,8 +99,17 @@ __device__ __forceinline__ void wd_stamp(int slot) {
     if (threadIdx.x == 0 && blockIdx.x < WD_STAMP_WG)
         __hip_atomic_store(&g_wd_stamps[blockIdx.x * WD_STAMP_SLOTS + slot], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// per-chunk loop stamps (shader clock, s_memtime): [WG][chunk < 16][slot < 8], one lane of the calling wave
+constexpr int WD_LSTAMP_WG = 512;
+__device__ uint64_t g_wd_lstamps[WD_LSTAMP_WG * 16 * 8];
+__device__ __forceinline__ void wd_lstamp(int chunk, int slot) {
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < WD_LSTAMP_WG && chunk < 16)
+        __hip_atomic_store(&g_wd_lstamps[(blockIdx.x * 16 + chunk) * 8 + slot], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 #else
 __device__ __forceinline__ void wd_stamp(int) {}
+__device__ __forceinline__ void wd_lstamp(int, int) {}
 #endif
 
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }

@@ -20,7 +20,7 @@ for s in "$@"; do
     testsv) step pytest_gpu 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     lab) step lab_mainloop 150 ./tools/gemm_lab 200 mainloop ;;
-    ab) step ab 600 bash tools/ab_lib.sh ;;
+    ab) step ab 600 bash tools/ab_libs.sh ${AB:-base cur} ;;
     ab3) step ab3 900 bash tools/ab3.sh ${AB3:-cur base} ;;
     bench) step bench 600 python bench.py ;;
     benchq) step benchq 300 python bench.py --steps 200 --warmup 20 --no-cpu --no-secondary --stream-graphs 0 --stream-train-graphs 0 ;;

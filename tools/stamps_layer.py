@@ -48,3 +48,20 @@ with torch.no_grad():
             print('   phase p50 (us): ' + '  '.join(f'{n} {np.median(dur[:, k]) / 1e3:.2f}' for k, n in enumerate(names)))
             print('   phase p90 (us): ' + '  '.join(f'{n} {np.percentile(dur[:, k], 90) / 1e3:.2f}' for k, n in enumerate(names)))
         buf[:] = 0
+
+# per-chunk loop stamps of the last launch (the last layer): consumer wave 0 (0 before its B wait, 1 after,
+# 2 after the barrier, 3 after its MFMAs) and producer wave 4 (4 before a store, 5 after it), shader clock
+buf2 = np.zeros(8192 * 16 + 512 * 16 * 8, dtype=np.uint64)
+with torch.no_grad():
+    torch.cuda.synchronize()
+    enc(g)
+    torch.cuda.synchronize()
+    _native.check(L.wdmpnn_debug_stamps(buf2.ctypes.data, buf2.nbytes), 'stamps')
+ls = buf2[8192 * 16:].reshape(512, 16, 8).astype(np.int64)[:256]
+print('chunk  Bwait  barrier  mfma(w0)  period | prod store  (cycles, median over WGs)')
+for kc in range(10):
+    c = ls[:, kc]
+    nxt = ls[:, kc + 1, 0] if kc < 9 else c[:, 3]
+    print(f'{kc:5d} {np.median(c[:, 1] - c[:, 0]):6.0f} {np.median(c[:, 2] - c[:, 1]):8.0f} '
+          f'{np.median(c[:, 3] - c[:, 2]):9.0f} {np.median(nxt - c[:, 0]):7.0f} | '
+          f'{np.median(c[:, 5] - c[:, 4]) if kc < 9 else 0:10.0f}')
