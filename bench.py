@@ -35,9 +35,9 @@ from chemprop_amd.mpn import MPNEncoder  # noqa: E402
 from chemprop_amd.nn_utils import initialize_weights  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
-BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 (the split-plane GEMMs issue 6 bf16 products per fp32 product)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 / fp16 (the layer issues 3 fp16 products per fp32 product, W_o 6 bf16)
 HBM_PEAK_GBS = 8000.0
-PMC_TRAFFIC = "round3_pmc_traffic.json"  # per-kernel HBM bytes per launch (tools/pmc_summary.py)
+PMC_TRAFFIC = "round4_pmc_traffic.json"  # per-kernel HBM bytes per launch (tools/pmc_summary.py)
 
 
 def log(*a):
@@ -591,8 +591,9 @@ def main():
             'scaling': 'weak',
             'vs_baseline': None,
             'dtype': 'fp32',
-            'arith': 'fp32-accurate GEMMs as exact bf16x3 operand splits on bf16 MFMA (6 products, fp32 '
-                     'accumulate); gathers, residual, activations and readout in fp32',
+            'arith': 'fp32-accurate GEMMs: message-passing layers as fp16 hi/lo operand pairs with per-block '
+                     'power-of-two scales on fp16 MFMA (3 products, fp32 accumulate), W_o as exact bf16x3 '
+                     'splits (6 products); gathers, residual, activations and readout in fp32',
             'data': 'synthetic',
             'config': {'workload': f'MPNEncoder.forward on synthetic {a.kind} batches of {a.batch} graphs '
                                    f'(avg E={E_avg:.0f} directed edges), depth={a.depth}, hidden={H}, '
@@ -611,13 +612,13 @@ def main():
                                       'call share one grid per kernel; every batch a full B=64 forward'}
                              if many_dt else None),
             'roofline': {'bound': 'mfma',
-                         'kernel': 'mp_layer_kernel: one message-passing layer, W_h split-plane GEMM + in-block CSR '
+                         'kernel': 'mp_layer_kernel: one message-passing layer, W_h fp16-pair GEMM + in-block CSR '
                                    'gather + residual/activation (mpn.py:110-124)',
                          'achieved': achieved, 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                          'frac': achieved / FP32_MFMA_PEAK_TFLOPS if achieved else None, 'traffic': traffic,
                          'traffic_source': traffic_src,
-                         'peak_note': 'fp32 dense MFMA peak; the kernel issues bf16 MFMAs, whose fp32-product '
-                                      f'equivalent peak is {BF16_MFMA_PEAK_TFLOPS / 6:.0f} TFLOP/s',
+                         'peak_note': 'fp32 dense MFMA peak; the kernel issues fp16 MFMAs (3 per fp32 product), whose '
+                                      f'fp32-product equivalent peak is {BF16_MFMA_PEAK_TFLOPS / 3:.0f} TFLOP/s',
                          'avg_launch_us': avg_launch_s * 1e6, 'flops_per_launch': flops_launch,
                          'bytes_per_launch': bytes_launch, 'hbm_gbs': hbm,
                          'hbm_frac': hbm / HBM_PEAK_GBS if hbm else None,

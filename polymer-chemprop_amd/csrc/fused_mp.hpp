@@ -96,9 +96,7 @@ struct MpLayerP {
     int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;
     const int32_t *aptr, *aidx; const float *acoef;  // atom gather (natural atom rows -> natural bond rows)
     const uint8_t *aell_idx; const float *aell_coef; // its first ELLW entries per row, block-local (WdGraph)
-    uint8_t *aplanes;           // A (the last layer): blocked atom plane tiles [nblk * 64][kp], or with WD_WO_H2
-                                // fp32 blocked atom rows [nblk * 64][kp]
-    uint32_t *amax_a;           // WD_WO_H2: [nblk][n_tiles] max |A| of each last-layer workgroup (W_o's scale)
+    uint8_t *aplanes;           // A: blocked atom plane tiles [nblk * 64][kp] (the last layer)
     int n_tiles;                // Hk / BN
     // training forward (save_for_backward) or null, the last layer only (the others' Z_t is zout): its
     // pre-activation Z_t (mpn.py:123) as fp32 natural bond rows [Rp][kp] and the atom aggregate A
@@ -108,42 +106,38 @@ struct MpLayerP {
 
 // The GEMM operand M_{t-1} = dropout(act(Z_{t-1})), formed while staging from the fp32 Z rows (the
 // producer waves of h2_mainloop_ws), so that no message tensor goes through HBM in split form: producer
-// thread t (0..255) stages rows t / 8 + 32 i (i < 4) of the block, columns 4 (t % 8) .. +3 of each
-// 32-column chunk, applies the activation and dropout, scales and splits into fp16 hi / lo.  Rows past
-// the block's bonds read row 0 of the matrix instead: their accumulator rows are never read (row i of P
-// depends on row i of M only).
-#ifndef WD_H2_SETS
-#define WD_H2_SETS 3
-#endif
-// WD_PROD_LINE: 8 producer lanes per row, each 16 bytes of the 128-byte row chunk (one wave-instruction
-// reads 8 whole lines); else 4 lanes per row, two 16-byte loads each (16 half lines per instruction)
-#ifndef WD_PROD_LINE
-#define WD_PROD_LINE 0
-#endif
+// thread t (0..255) stages rows t / 4 and t / 4 + 64 of the block, columns 8 (t % 4) .. +7 of each
+// 32-column chunk, applies the activation and dropout, scales and splits into fp16 hi / lo.  The rows are
+// read through a buffer resource that ends at the block's last bond: rows past it come back as zeros
+// without touching memory (a QM9 block holds ~14 of the 128 rows), with the same instruction stream in
+// every wave, so the compiler's vmcnt waits stay exact; only the 16-row tiles the consumers multiply are
+// converted and stored.  (8 lanes per row, one 16-byte load each, measured +0.5 us per launch.)
 template <int BM, int AACT>
 struct H2Prod {
-    static constexpr int LPR = WD_PROD_LINE ? 8 : 4;     // lanes per row
-    static constexpr int U = BM * LPR / 256;             // rows per producer thread
-    static constexpr int H = 8 / LPR;                    // 16-byte loads per row
-    static constexpr int SETS = WD_H2_SETS;              // register sets (chunks in flight)
-    const float *row[U];
+    static constexpr int U = BM / 64;                    // rows per producer thread
+    static constexpr int SETS = 3;                       // register sets (chunks in flight)
+    __amdgpu_buffer_rsrc_t rs;              // the block's Z rows
+    int off[U];                             // byte offset of this thread's columns in row r0 + 64 i
     uint32_t grow[U];                       // natural bond row (dropout counter)
-    int r0, u;
+    int r0, u, live16;                      // live16: rows of the 16-row tiles holding bonds
     float slope, scale, pd;
     uint64_t seed;
     uint32_t layer;
     const uint32_t *sw; int sn;             // the scale's words
-    u32x4 v[SETS][U][H];                    // register sets (raw fp32 bits)
+    u32x4 v[SETS][U][2];                    // register sets (raw fp32 bits)
     __device__ __forceinline__ void init() { scale = h2_scale(max_words(sw, sn)); }
     __device__ __forceinline__ H2Prod(const MpLayerP &P, const BlockRow &B, int blk) {
         const int t = threadIdx.x & 255;
-        r0 = t / LPR; u = t % LPR;
+        r0 = t >> 2; u = t & 3;
+        rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(P.zin + (size_t)B.bs * P.kp), 0, B.bn * P.kp * 4,
+                                               0x00020000);
 #pragma unroll
         for (int i = 0; i < U; ++i) {
-            const int r = r0 + (256 / LPR) * i;
+            const int r = r0 + 64 * i;
             grow[i] = r < B.bn ? B.bs + r : 0;
-            row[i] = P.zin + (size_t)grow[i] * P.kp + (32 / LPR) * u;
+            off[i] = (r * P.kp + 8 * u) * 4;
         }
+        live16 = (B.bn + 15) & ~15;
         slope = AACT == ACT_PRELU ? P.slope[0] : 0.f;
         sw = P.amax_in + (size_t)blk * P.amax_in_n; sn = P.amax_in_n;
         scale = 1.f;
@@ -153,102 +147,44 @@ struct H2Prod {
     }
     template <typename S>
     __device__ __forceinline__ void load(S, int kc) {
-#if WD_EXP_NOLOAD  // experiment: stale registers (one load per set, the first time)
-        if (kc >= SETS) return;
-#endif
 #pragma unroll
         for (int i = 0; i < U; ++i)
 #pragma unroll
-            for (int h = 0; h < H; ++h) v[S::value][i][h] = *reinterpret_cast<const u32x4 *>(row[i] + 32 * kc + 4 * h);
+            for (int h = 0; h < 2; ++h)
+                v[S::value][i][h] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off[i] + 128 * kc + 16 * h, 0, 0));
     }
     template <typename S>
     __device__ __forceinline__ void store(S, int kc, uint8_t *st) {
 #pragma unroll
         for (int i = 0; i < U; ++i) {
-            float x[4 * H];
+            const int r = r0 + 64 * i;
+            if (r >= live16) continue;  // (the consumers skip those 16-row tiles)
+            float x[8];
 #pragma unroll
-            for (int h = 0; h < H; ++h) {
+            for (int h = 0; h < 2; ++h) {
                 const u32x4 a = v[S::value][i][h];
                 x[4 * h] = __uint_as_float(a.x); x[4 * h + 1] = __uint_as_float(a.y);
                 x[4 * h + 2] = __uint_as_float(a.z); x[4 * h + 3] = __uint_as_float(a.w);
             }
 #pragma unroll
-            for (int q = 0; q < 4 * H; ++q) x[q] = act_fwd(AACT, x[q], slope);
+            for (int q = 0; q < 8; ++q) x[q] = act_fwd(AACT, x[q], slope);
             if (pd > 0.f)
 #pragma unroll
-                for (int q = 0; q < 4 * H; ++q)
-                    x[q] *= dropout_scale(seed, layer, grow[i], 32 * kc + (32 / LPR) * u + q, pd);
-            uint32_t hh[2 * H], ll[2 * H];
-#if WD_EXP_NOCONV  // experiment: raw bits, no activation / split work
+                for (int q = 0; q < 8; ++q) x[q] *= dropout_scale(seed, layer, grow[i], 32 * kc + 8 * u + q, pd);
+            uint32_t hh[4], ll[4];
 #pragma unroll
-            for (int q = 0; q < 2 * H; ++q) { hh[q] = v[S::value][i][q / 4][q % 4]; ll[q] = hh[q]; }
-#else
-#pragma unroll
-            for (int q = 0; q < 2 * H; ++q) split_h2(x[2 * q], x[2 * q + 1], scale, hh[q], ll[q]);
-#endif
-#if WD_EXP_NOSTORE  // experiment: no LDS stores (keeps the values live)
-            if (__builtin_expect(hh[0] == 0x7fc00001u && ll[1] == 0x7fc00001u, 0)) {
-#endif
-            const int r = r0 + (256 / LPR) * i;
-            if constexpr (H == 2) {
-                uint8_t *d = st + x6_slot(r, u);
-                *reinterpret_cast<u32x4 *>(d) = u32x4{hh[0], hh[1], hh[2], hh[3]};
-                *reinterpret_cast<u32x4 *>(d + BM * 64) = u32x4{ll[0], ll[1], ll[2], ll[3]};
-            } else {  // 8 bytes: half of 16-byte unit u / 2
-                uint8_t *d = st + x6_slot(r, u >> 1) + 8 * (u & 1);
-                *reinterpret_cast<uint2 *>(d) = make_uint2(hh[0], hh[1]);
-                *reinterpret_cast<uint2 *>(d + BM * 64) = make_uint2(ll[0], ll[1]);
-            }
-#if WD_EXP_NOSTORE
-            }
-#endif
+            for (int q = 0; q < 4; ++q) split_h2(x[2 * q], x[2 * q + 1], scale, hh[q], ll[q]);
+            uint8_t *d = st + x6_slot(r, u);
+            *reinterpret_cast<u32x4 *>(d) = u32x4{hh[0], hh[1], hh[2], hh[3]};
+            *reinterpret_cast<u32x4 *>(d + BM * 64) = u32x4{ll[0], ll[1], ll[2], ll[3]};
         }
     }
 };
 
-// The same conversion for h2d_mainloop (WD_LAYER_DMA): each MFMA wave converts its own A fragment (8
-// consecutive columns of one row) from the DMA-staged fp32 rows
-template <int AACT>
-struct H2Conv {
-    float slope, scale, pd;
-    uint64_t seed;
-    uint32_t layer;
-    int bs, bn;
-    // an operand without activation or dropout (W_o's A)
-    __device__ __forceinline__ H2Conv(float scale_) : slope(0.f), scale(scale_), pd(0.f), seed(0), layer(0), bs(0), bn(0) {}
-    __device__ __forceinline__ H2Conv(const MpLayerP &P, const BlockRow &B, int blk) {
-        slope = AACT == ACT_PRELU ? P.slope[0] : 0.f;
-        scale = h2_scale(max_words(P.amax_in + (size_t)blk * P.amax_in_n, P.amax_in_n));
-        pd = P.p_drop_in;
-        seed = P.seed;
-        layer = P.layer - 1;
-        bs = B.bs; bn = B.bn;
-    }
-    __device__ __forceinline__ void convert(float (&x)[8], int r, int col, f16x8 &hi, f16x8 &lo) const {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) x[q] = act_fwd(AACT, x[q], slope);
-        if (pd > 0.f) {
-            const uint32_t row = r < bn ? bs + r : 0;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) x[q] *= dropout_scale(seed, layer, row, col + q, pd);
-        }
-        uint32_t h[4], l[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) split_h2(x[2 * q], x[2 * q + 1], scale, h[q], l[q]);
-        hi = __builtin_bit_cast(f16x8, u32x4{h[0], h[1], h[2], h[3]});
-        lo = __builtin_bit_cast(f16x8, u32x4{l[0], l[1], l[2], l[3]});
-    }
-};
-
-// WD_LAYER_DMA: the layer's GEMM on h2d_mainloop (fp32 rows by LDS-DMA, all 8 waves on MFMA, three
-// stages) instead of h2_mainloop_ws (producer / consumer waves)
-#ifndef WD_LAYER_DMA
-#define WD_LAYER_DMA 0
-#endif
-// WD_WO_H2: W_o's A operand as fp32 rows with per-(block, tile) maxima, multiplied on h2d_mainloop
-// (fp16 pairs); else bf16x3 plane tiles on x6_mainloop
-#ifndef WD_WO_H2
-#define WD_WO_H2 0
+// cache policy of the Z_t row stores: default write-back.  Write-through, as the planes use, measured
+// slower on the first polymer layer (17.46 us against 16.50, same box)
+#ifndef WD_ZWT
+#define WD_ZWT 0
 #endif
 
 // The fused layer kernel runs 512 threads, warp-specialised: 4 MFMA waves of 32 rows x all BN columns and
@@ -390,9 +326,9 @@ struct MpEpilogue {
                 if (zr) {  // (16-byte buffer stores, write-through: 8-byte atomic stores cost 4 us per launch)
                     const int o = (lr * P.kp + n0 + c) * 4;
                     __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(z[0]), __float_as_uint(z[1]),
-                                                                 __float_as_uint(z[2]), __float_as_uint(z[3])}, zrs, o, 0, WD_WT_POL);
+                                                                 __float_as_uint(z[2]), __float_as_uint(z[3])}, zrs, o, 0, WD_ZWT);
                     __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(z[4]), __float_as_uint(z[5]),
-                                                                 __float_as_uint(z[6]), __float_as_uint(z[7])}, zrs, o + 16, 0, WD_WT_POL);
+                                                                 __float_as_uint(z[6]), __float_as_uint(z[7])}, zrs, o + 16, 0, WD_ZWT);
                 }
 #pragma unroll
                 for (int q = 0; q < 8; ++q) z[q] = act_fwd(ACT, z[q], slope);
@@ -426,40 +362,20 @@ struct MpEpilogue {
             }
             __syncthreads();
             // atom aggregate of this column tile: A[a] = sum_{b into a} w_b M_t[b] (mpn.py:126-131)
-#if WD_WO_H2
-            const __amdgpu_buffer_rsrc_t ars = __builtin_amdgcn_make_buffer_rsrc(
-                P.aplanes + (size_t)blk * BLK_ATOMS * P.kp * 4, 0, BLK_ATOMS * P.kp * 4, 0x00020000);
-            uint32_t amx = 0;
-#else
             const __amdgpu_buffer_rsrc_t ars = x6_block_rsrc<BLK_ATOMS>(P.aplanes, P.kp, blk);
-#endif
 #pragma unroll
             for (int i = 0; i < AUPT; ++i) {
                 const int v = tid + NT * i, la = v / UPR, c = 8 * (v % UPR);
                 if (v >= AUNITS || la >= B.an) break;  // rows past the block's atoms are never loaded
                 float4 s0, s1;
                 atom_sum(P, B, aell[i], la, c, Mt, s0, s1);
-#if WD_WO_H2
-                const int o = (la * P.kp + n0 + c) * 4;
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(s0.x), __float_as_uint(s0.y),
-                                                             __float_as_uint(s0.z), __float_as_uint(s0.w)}, ars, o, 0, WD_WT_POL);
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(s1.x), __float_as_uint(s1.y),
-                                                             __float_as_uint(s1.z), __float_as_uint(s1.w)}, ars, o + 16, 0, WD_WT_POL);
-                amx = max(amx, max(max(max(absbits(s0.x), absbits(s0.y)), max(absbits(s0.z), absbits(s0.w))),
-                                   max(max(absbits(s1.x), absbits(s1.y)), max(absbits(s1.z), absbits(s1.w)))));
-#else
                 x6_store8_blk<BLK_ATOMS>(ars, la, n0 + c, s0, s1);
-#endif
                 if (P.asave) {
                     float *ar = P.asave + (size_t)(B.as + la) * P.kp + n0 + c;
                     st4(ar, s0);
                     st4(ar + 4, s1);
                 }
             }
-#if WD_WO_H2
-            __shared__ uint32_t red[MP_THREADS / 64];
-            publish_max(amx, P.amax_a + (size_t)blk * P.n_tiles + n0 / BN, red);
-#endif
         }
     }
 };
@@ -475,7 +391,7 @@ template <int BN, bool LAST, int ACT>
 __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpLayerP> MP) {
     constexpr int BM = BLK_BONDS;
     constexpr int EPI_BYTES = MpEpilogue<BN, MP_THREADS, LAST>::LDS_FLOATS * 4;  // P tile + the atom sums
-    constexpr int STG_BYTES = WD_LAYER_DMA ? 3 * h2d_stage_bytes<BM, BN>() : h2_lds_bytes<BM, BN>();
+    constexpr int STG_BYTES = h2_lds_bytes<BM, BN>();
     constexpr int LDS_BYTES = EPI_BYTES > STG_BYTES ? EPI_BYTES : STG_BYTES;
     static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU");
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
@@ -486,30 +402,10 @@ __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpL
     const BlockRow B = load_block(P.blocks, blk);
     MpEpilogue<BN, MP_THREADS, LAST> E;
     float *Pt = reinterpret_cast<float *>(lds);
-#if WD_LAYER_DMA
-    const float ia = h2_inv_scale(max_words(P.amax_in + (size_t)blk * P.amax_in_n, P.amax_in_n));
-    const float iw = h2_inv_scale(*P.wh_amax);
-    H2Conv<ACT> cv(P, B, blk);
-    wd_stamp(1 + 8 * LAST);
-    floatx4 acc[1][BN / 16];
-    h2d_mainloop<BM, BN, 3>(P.zin + (size_t)B.bs * P.kp, P.kp, B.bn, P.wh + (size_t)nt * (P.kp >> 5) * (2 * BN * 64),
-                            P.kp >> 5, lds, acc, cv, P.zin);
-    wd_stamp(2 + 8 * LAST);
-    E.prefetch(P, B);
-    __syncthreads();
-    wd_stamp(3 + 8 * LAST);
-    x6_acc_to_lds_scaled<BM, BN, 8, 1>(acc, Pt, ia, iw);
-#else
     H2Prod<BM, ACT> ap(P, B, blk);
     wd_stamp(1 + 8 * LAST);
     floatx4 acc[BM / 64][BN / 16];
-#if WD_EXP_NOGEMM  // experiment: epilogue + launch only
-    for (int a = 0; a < BM / 64; ++a)
-        for (int b = 0; b < BN / 16; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
-    (void)ap;
-#else
     h2_mainloop_ws<BM, BN>(P.wh + (size_t)nt * (P.kp >> 5) * (2 * BN * 64), P.kp >> 5, B.bn, lds, acc, ap);
-#endif
     // the epilogue's gather lists and ids: loaded now, not during the GEMM (live across the GEMM loop
     // they pushed the consumers' accumulators and fragments past 128 VGPRs)
     wd_stamp(2 + 8 * LAST);
@@ -519,7 +415,6 @@ __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpL
     const float ia = h2_inv_scale(max_words(P.amax_in + (size_t)blk * P.amax_in_n, P.amax_in_n));
     const float iw = h2_inv_scale(*P.wh_amax);
     if (threadIdx.x < 256) x6_acc_to_lds_scaled<BM, BN, 4, 1>(acc, Pt, ia, iw);  // (the consumer waves hold the tile)
-#endif
     __syncthreads();
     E.template run<ACT>(P, B, blk, n0, Pt);
     wd_stamp(6 + 8 * LAST);
@@ -689,10 +584,6 @@ struct WoReadoutP {
     const float *eo;
     int Hk;
     float *zosave;  // training forward or null: the W_o pre-activation (mpn.py:133) as fp32 natural atom rows [Vap][Hk]
-    // WD_WO_H2: A as fp32 blocked atom rows [nblk * 64][Hk] with its scale words [nblk][amax_n] (the last
-    // layer's), W_o[:, Fa:] as h2 plane tiles [Hk][Hk] (BN-row blocks) and their scale word
-    const float *ag32; const uint32_t *amax_a; int amax_n;
-    const uint8_t *woh; const uint32_t *wo_amax;
 };
 
 template <int BN> struct WoWaves;
@@ -705,17 +596,15 @@ template <> struct WoWaves<80> { static constexpr int WM = 2, WN = 5; };
 // workgroups queue per CU; CPS 1 (55 KB of LDS) for one batch, whose 256 workgroups then co-reside
 // with the layer kernels of batches in flight on other streams (+5 % with two streams, same-box A/B,
 // profiles/round3_*).  64-column tiles: CPS 1.
-// H2 (WD_WO_H2): the A half on h2d_mainloop (fp32 rows by LDS-DMA, fp16 pairs, 4 waves of 16 rows x BN,
-// three stages), the f_atoms half from eo (always precomputed then).
-template <int BN, int CPS, bool H2 = false>
-__global__ __launch_bounds__(H2 ? 256 : 64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_readout_kernel(const Multi<WoReadoutP> MP) {
+template <int BN, int CPS>
+__global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_readout_kernel(const Multi<WoReadoutP> MP) {
     constexpr int BM = BLK_ATOMS, LDC = BN + 4, WM = WoWaves<BN>::WM, WN = WoWaves<BN>::WN;
-    constexpr int NT = H2 ? 256 : 64 * WM * WN;
+    constexpr int NT = 64 * WM * WN;
     // (deeper single-chunk pipelines, with the mainloop hook's loads ordered ahead of the partial vmcnt
     // waits, measured slower: three / four stages 15.1 / 14.8 us here, 12.8 / 11.8 against 9.7 us on
     // QM9-shaped batches)
     constexpr int WS = 2;  // LDS stages
-    constexpr int LDS_BYTES = H2 ? 3 * h2d_stage_bytes<BM, BN>() : WS * CPS * x6_stage_bytes<BM, BN>();
+    constexpr int LDS_BYTES = WS * CPS * x6_stage_bytes<BM, BN>();
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
     int tile;
     const WoReadoutP &P = multi_pick(MP, xcd_tile(blockIdx.x, gridDim.x), tile);
@@ -733,7 +622,7 @@ __global__ __launch_bounds__(H2 ? 256 : 64 * WoWaves<BN>::WM * WoWaves<BN>::WN) 
     // prefetched during the GEMM (mainloop hook): this thread's bias columns, the block's atom weights
     // (thread a < an: w_atoms[as + a]) and its molecules' scope / Xn (thread i < nm)
     constexpr int C4 = BN / 4;
-    static_assert(BM <= NT, "one atom weight per thread");
+    static_assert(NT % C4 == 0 && BM <= NT, "one bias group per thread, one atom weight per thread");
     const int nm = min(B.mh - B.ml, BLK_MOLS);  // (the packer never exceeds BLK_MOLS)
     if (P.zosave && blk == 0 && tid < BN / 4) st4(P.zosave + n0 + 4 * tid, f4zero());  // pad atom row 0
     float4 bb = f4zero();
@@ -758,22 +647,10 @@ __global__ __launch_bounds__(H2 ? 256 : 64 * WoWaves<BN>::WM * WoWaves<BN>::WN) 
         }
     };
     float *H = reinterpret_cast<float *>(lds);
-    if constexpr (H2) {
-        prefetch(0);
-        const uint32_t am = max_words(P.amax_a + (size_t)blk * P.amax_n, P.amax_n);
-        const float ia = h2_inv_scale(am), iw = h2_inv_scale(*P.wo_amax);
-        const H2Conv<ACT_IDENTITY> cv(h2_scale(am));
-        floatx4 acc[1][BN / 16];
-        h2d_mainloop<BM, BN, 3>(P.ag32 + (size_t)blk * BM * P.Hk, P.Hk, B.an, P.woh + (size_t)nt * (P.Hk >> 5) * (2 * BN * 64),
-                                P.Hk >> 5, lds, acc, cv, P.ag32);
-        __syncthreads();
-        x6_acc_to_lds_scaled<BM, BN, 4, 1>(acc, H, ia, iw);
-    } else {
-        floatx4 acc[BM / WM / 16][BN / WN / 16];
-        x6_mainloop<BM, BN, WM, WN, WS, CPS>(O, lds, acc, prefetch);
-        __syncthreads();
-        x6_acc_to_lds<BM, BN, WM, WN>(acc, H);
-    }
+    floatx4 acc[BM / WM / 16][BN / WN / 16];
+    x6_mainloop<BM, BN, WM, WN, WS, CPS>(O, lds, acc, prefetch);
+    __syncthreads();
+    x6_acc_to_lds<BM, BN, WM, WN>(acc, H);
     float *Wl = H + BM * LDC;           // [BM] atom weights of the block
     float *Ml = Wl + BM;                // [3][BLK_MOLS] per molecule: start (as float bits), size, Xn
     static_assert((BM * LDC + BM + 3 * BLK_MOLS) * 4 <= LDS_BYTES, "readout staging fits");
@@ -796,8 +673,7 @@ __global__ __launch_bounds__(H2 ? 256 : 64 * WoWaves<BN>::WM * WoWaves<BN>::WN) 
             const int la = v / C4, c = 4 * (v % C4);
             float4 hv = ld4(H + la * LDC + c);
             hv.x += eo[j].x; hv.y += eo[j].y; hv.z += eo[j].z; hv.w += eo[j].w;  // (0 without codes)
-            const float4 bq = NT % C4 == 0 ? bb : ld4(P.bias + n0 + c);  // (one bias group per thread when it fits)
-            float z[4] = {hv.x + bq.x, hv.y + bq.y, hv.z + bq.z, hv.w + bq.w};
+            float z[4] = {hv.x + bb.x, hv.y + bb.y, hv.z + bb.z, hv.w + bb.w};
             if (P.zosave && la < B.an) st4(P.zosave + (size_t)(B.as + la) * P.Hk + n0 + c, make_float4(z[0], z[1], z[2], z[3]));
 #pragma unroll
             for (int q = 0; q < 4; ++q) z[q] = act_fwd(ACT, z[q], slope);

@@ -665,22 +665,13 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
 // On return every wave is past its last LDS access of the stages; the consumers' acc holds the tile
 // (the producers' acc is left undefined: the caller reads it in threads 0..255 only).
 // ---------------------------------------------------------------------------------------------
-// B (W_h) copies run WD_B_AHEAD chunks ahead of the chunk multiplied (WD_B_AHEAD + 1 B stages); the
-// producers store A WD_A_STAGES - 1 chunks ahead (WD_A_STAGES A stages): with three, one late wave no longer
-// holds every barrier
-#ifndef WD_B_AHEAD
-#define WD_B_AHEAD 1
-#endif
-#ifndef WD_A_STAGES
-#define WD_A_STAGES 2
-#endif
-// WD_ALLB: a consumer reads all of a chunk's fragments before its first MFMA (else: the next column
-// tile's B fragments behind each tile's products)
-#ifndef WD_ALLB
-#define WD_ALLB 0
-#endif
+// The B (W_h) copies run H2_B_AHEAD chunks ahead of the chunk multiplied (H2_B_AHEAD + 1 B stages); the
+// producers store A H2_A_STAGES - 1 chunks ahead (H2_A_STAGES A stages).  (Measured, same box: three A
+// stages +1.3 us per launch, B two chunks ahead +0.4 us, all of a chunk's fragments read before its first
+// MFMA +0.4 us, 3 / 4 / 6 register sets in flight 16.6 / 17.5 / 22.4 us: tools/prof_libs.sh variants.)
+constexpr int H2_B_AHEAD = 1, H2_A_STAGES = 2;
 template <int BM, int BN>
-constexpr int h2_lds_bytes() { return WD_A_STAGES * (2 * BM * 64) + (WD_B_AHEAD + 1) * (2 * BN * 64); }
+constexpr int h2_lds_bytes() { return H2_A_STAGES * (2 * BM * 64) + (H2_B_AHEAD + 1) * (2 * BN * 64); }
 
 template <int BM, int BN, typename AProd>
 __device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nchunks, int a_rows, uint8_t *lds,
@@ -688,7 +679,7 @@ __device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nch
     static_assert(BM == 128, "four consumer waves of 32 rows");
     constexpr int TM = BM / 64, TN = BN / 16;
     constexpr int APL = BM * 64, BPL = BN * 64;
-    constexpr int ASTAGE = 2 * APL, BSTAGE = 2 * BPL, NA = WD_A_STAGES, NB = WD_B_AHEAD + 1;  // A stages [NA], B [NB]
+    constexpr int ASTAGE = 2 * APL, BSTAGE = 2 * BPL, NA = H2_A_STAGES, NB = H2_B_AHEAD + 1;  // A stages [NA], B [NB]
     constexpr int BP = 2 * BN / 16, BPW = (BP + 3) / 4;  // B: 1 KB DMA pieces per chunk, per consumer wave
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int w4 = wave & 3, g = lane >> 4, i16 = lane & 15;
@@ -709,11 +700,9 @@ __device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nch
             const int cs = kc + NA - 1;
             if (cs >= nchunks) return;
             if (WD_STAMPS && wave == 4) wd_lstamp(kc, 4);
-#if !WD_EXP_NOPROD  // experiment: no staging work (the consumers multiply stale LDS)
             ap.store(set, cs, lds + (cs % NA) * ASTAGE);
             if (WD_STAMPS && wave == 4) { __builtin_amdgcn_s_waitcnt(0xc07f); wd_lstamp(kc, 5); }
             ap.load(set, min(cs + NS, nchunks - 1));
-#endif
         };
         int kc = 0;
         for (; kc + NS <= nchunks; kc += NS)
@@ -755,26 +744,6 @@ __device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nch
     const int na = min(TM, max(0, (a_rows - 32 * w4 + 15) >> 4));
     auto compute_n = [&](const uint8_t *st, const uint8_t *sb, auto na_c) {
         constexpr int NA = decltype(na_c)::value;
-        if constexpr (WD_ALLB) {
-            f16x8 af[TM][2], bf[TN][2];
-#pragma unroll
-            for (int p = 0; p < 2; ++p)
-#pragma unroll
-                for (int a = 0; a < NA; ++a) af[a][p] = *reinterpret_cast<const f16x8 *>(st + p * APL + ao[a]);
-#pragma unroll
-            for (int b = 0; b < TN; ++b)
-#pragma unroll
-                for (int p = 0; p < 2; ++p) bf[b][p] = *reinterpret_cast<const f16x8 *>(sb + p * BPL + bo[b]);
-#pragma unroll
-            for (int b = 0; b < TN; ++b)
-#pragma unroll
-                for (int a = 0; a < NA; ++a) {
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][0], bf[b][0], acc[a][b], 0, 0, 0);
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][0], bf[b][1], acc[a][b], 0, 0, 0);
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][1], bf[b][0], acc[a][b], 0, 0, 0);
-                }
-            return;
-        }
         f16x8 af[TM][2], bq[2][2];
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
@@ -812,129 +781,27 @@ __device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nch
 #pragma unroll
     for (int j = 0; j < BPW; ++j) mine += BP % 4 == 0 || 4 * j + w4 < BP;
 #pragma unroll
-    for (int c = 0; c < WD_B_AHEAD; ++c)
+    for (int c = 0; c < H2_B_AHEAD; ++c)
         if (c < nchunks) issue_b(c);
     for (int kc = 0; kc < nchunks; ++kc) {
-        // chunk kc's B landed for this wave (the WD_B_AHEAD - 1 younger chunks may stay in flight), this
-        // wave's fragment reads done; then for every wave: A chunk kc staged, B stage (kc + WD_B_AHEAD) % NB
+        // chunk kc's B landed for this wave (the H2_B_AHEAD - 1 younger chunks may stay in flight), this
+        // wave's fragment reads done; then for every wave: A chunk kc staged, B stage (kc + H2_B_AHEAD) % NB
         // read by all (at kc - 1)
         if (WD_STAMPS && wave == 0) wd_lstamp(kc, 0);
-        wait_vmcnt(min(WD_B_AHEAD - 1, nchunks - 1 - kc) * mine);
+        wait_vmcnt(min(H2_B_AHEAD - 1, nchunks - 1 - kc) * mine);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (WD_STAMPS && wave == 0) wd_lstamp(kc, 1);
         __builtin_amdgcn_s_barrier();
         if (WD_STAMPS && wave == 0) wd_lstamp(kc, 2);
-        if (kc + WD_B_AHEAD < nchunks) issue_b(kc + WD_B_AHEAD);
+        if (kc + H2_B_AHEAD < nchunks) issue_b(kc + H2_B_AHEAD);
         const uint8_t *st = lds + (kc % NA) * ASTAGE, *sb = lds + NA * ASTAGE + (kc % NB) * BSTAGE;
-#if !WD_EXP_NOMFMA  // experiment: no fragment reads / MFMAs
         dispatch_upto<TM>(na, [&](auto c) { compute_n(st, sb, c); });
-#else
-        (void)st; (void)sb;
-#endif
         if (WD_STAMPS && wave == 0) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             wd_lstamp(kc, 3);
         }
     }
     __builtin_amdgcn_s_waitcnt(0x0070);
-}
-
-// ---------------------------------------------------------------------------------------------
-// fp16-pair GEMM core with the A operand as fp32 rows (the message-passing layer, planes.hpp "h2"):
-// acc (+)= conv(A) · Bᵀ for a BM x BN tile, every wave on MFMA (wave w: rows 16 w .. 16 w + 15, all BN
-// columns), S stages of one 32-column chunk, each stage = A chunk [BM][32] fp32 (128-byte rows, 16-byte
-// unit u of row r at slot u ^ ((r >> 1) & 7): conflict-free fragment reads) + B chunk (h2 plane tiles
-// [2][BN][32]); both copied by LDS-DMA, S - 1 chunks in flight, no staging registers.  Each wave converts
-// its own A fragment (8 fp32 per lane per chunk) in the MFMA shadow: AConv::convert(x[8], local row,
-// column) applies the activation / dropout / scale and returns the fp16 hi and lo fragments.
-// The copies are issued from inline asm (glds16_untracked): the explicit vmcnt wait + barrier per chunk
-// orders them, the compiler adds no waits of its own.
-// ---------------------------------------------------------------------------------------------
-template <int BM, int BN>
-constexpr int h2d_stage_bytes() { return BM * 128 + 2 * BN * 64; }
-
-template <int BM, int BN, int S, typename AConv>
-__device__ __forceinline__ void h2d_mainloop(const float *arow0, int lda, int a_rows, const uint8_t *bsrc_base,
-                                             int nchunks, uint8_t *lds, floatx4 (&acc)[1][BN / 16], const AConv &conv,
-                                             const float *afallback) {
-    constexpr int NW = BM / 16, TN = BN / 16;
-    constexpr int STAGE = h2d_stage_bytes<BM, BN>(), AB = BM * 128, BPL = BN * 64;
-    constexpr int AP = BM / 8, BP = 2 * BN / 16;                       // 1 KB pieces per chunk
-    constexpr int APW = (AP + NW - 1) / NW, BPW = (BP + NW - 1) / NW;  // per wave (the last ones predicated)
-    static_assert(S >= 2 && S <= 4, "stages");
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
-    // A piece c (rows 8c .. 8c + 7): lane l writes LDS unit 64 c + l = (row 8c + l / 8, slot l % 8), whose
-    // source is unit (l % 8) ^ ((r >> 1) & 7) of that row; rows past the block read row 0 of the matrix
-    const float *asrc[APW];
-#pragma unroll
-    for (int j = 0; j < APW; ++j) {
-        const int c = j * NW + wave, r = 8 * c + (lane >> 3), sl = lane & 7;
-        asrc[j] = (r < a_rows ? arow0 + (size_t)r * lda : afallback) + 4 * (sl ^ ((r >> 1) & 7));
-    }
-    int bsrc[BPW];
-#pragma unroll
-    for (int j = 0; j < BPW; ++j) {
-        const int q = 64 * (j * NW + wave) + lane, p = (q / (BN * 4)) % 2, r = (q >> 2) % BN, sl = q & 3;
-        bsrc[j] = p * BPL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
-    }
-    auto issue = [&](int kc, int stage) {
-        uint8_t *st = lds + stage * STAGE;
-#pragma unroll
-        for (int j = 0; j < APW; ++j) {
-            const int c = j * NW + wave;
-            if ((AP % NW == 0 || c < AP) && 8 * c < a_rows) glds16_untracked(asrc[j] + 32 * kc, st + 1024 * c);
-        }
-        const uint8_t *bblk = bsrc_base + (size_t)kc * (2 * BPL);
-#pragma unroll
-        for (int j = 0; j < BPW; ++j)
-            if (BP % NW == 0 || j * NW + wave < BP) glds16_untracked(bblk + bsrc[j], st + AB + 1024 * (j * NW + wave));
-    };
-    int mine = 0;  // this wave's copies per chunk
-#pragma unroll
-    for (int j = 0; j < APW; ++j) {
-        const int c = j * NW + wave;
-        mine += (AP % NW == 0 || c < AP) && 8 * c < a_rows;
-    }
-#pragma unroll
-    for (int j = 0; j < BPW; ++j) mine += BP % NW == 0 || j * NW + wave < BP;
-    // this lane's A fragment: row 16 wave + i16, columns 8 g .. 8 g + 7 = units 2 g, 2 g + 1
-    const int ar = 16 * wave + i16;
-    const int a0 = ar * 128 + 16 * ((2 * g) ^ ((ar >> 1) & 7)), a1 = ar * 128 + 16 * ((2 * g + 1) ^ ((ar >> 1) & 7));
-    int bo[TN];
-#pragma unroll
-    for (int b = 0; b < TN; ++b) bo[b] = AB + x6_slot(16 * b + i16, g);
-    const bool live = 16 * wave < a_rows;
-#pragma unroll
-    for (int b = 0; b < TN; ++b) acc[0][b] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < S - 1; ++c)
-        if (c < nchunks) issue(c, c);
-    for (int kc = 0; kc < nchunks; ++kc) {
-        // chunk kc landed for this wave (the younger ones may stay in flight), then for every wave; every
-        // wave is past its reads of stage (kc + S - 1) % S (read at kc - 1)
-        wait_vmcnt(min(S - 2, nchunks - 1 - kc) * mine);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (kc + S - 1 < nchunks) issue(kc + S - 1, (kc + S - 1) % S);
-        if (!live) continue;
-        const uint8_t *st = lds + (kc % S) * STAGE;
-        const float4 x0 = *reinterpret_cast<const float4 *>(st + a0), x1 = *reinterpret_cast<const float4 *>(st + a1);
-        f16x8 bf[TN][2];
-#pragma unroll
-        for (int b = 0; b < TN; ++b)
-#pragma unroll
-            for (int p = 0; p < 2; ++p) bf[b][p] = *reinterpret_cast<const f16x8 *>(st + p * BPL + bo[b]);
-        float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        f16x8 ah, al;
-        conv.convert(x, ar, 32 * kc + 8 * g, ah, al);
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-            acc[0][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf[b][0], acc[0][b], 0, 0, 0);
-            acc[0][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bf[b][1], acc[0][b], 0, 0, 0);
-            acc[0][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bf[b][0], acc[0][b], 0, 0, 0);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
 // acc tile -> LDS fp32 [BM][BN + 4] (C/D map of 16x16: col = lane & 15, row = 4 (lane >> 4) + reg)

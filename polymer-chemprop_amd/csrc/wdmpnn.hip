@@ -150,7 +150,6 @@ struct PackLayout {
                                        // (the categorical-code embedding of the fused forward)
     size_t WhH = 0;                    // h2 plane tiles of W_h (fused layers; BN-row blocks, BN = fused_bn)
     size_t amax = 0;                   // W_h's h2 scale: pack_kernel's 64 per-workgroup maxima + their max (u32)
-    size_t WoH = 0, amax_o = 0;        // the same for W_o[:, Fa:] (WD_WO_H2: the W_o + readout kernel's A half)
 };
 
 // column tile of the fused kernels: 80 when it divides Hk (Hk = 320: 4 tiles, one workgroup per CU at the
@@ -180,8 +179,6 @@ PackLayout pack_layout(const Dims &D) {
     }
     L.WhH = take((size_t)D.Hk * D.Hk);  // 2 fp16 per value
     L.amax = take(65);
-    L.WoH = take((size_t)D.Hk * D.Hk);
-    L.amax_o = take(65);
     if (D.desc) {
         L.Wd = take((size_t)D.Hdk * D.Kd);
         L.bd = take(D.Hdk);
@@ -226,8 +223,6 @@ int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
     J.j[J.n - 1].amax = wh_amax;  // (pack_kernel's grid: 64 workgroups per job)
     add(job_plain(F(L.bh), 1, D.Hk, p->b_h, H, 1, {{0, 0, H}}));
     add(job_plain(F(L.Wo), D.Hk, D.Ko, p->W_o, D.Fa + H, H, {{0, 0, D.Fa}, {D.Fak, D.Fa, H}}));
-    uint32_t *wo_amax = (uint32_t *)(base + L.amax_o);
-    J.j[J.n - 1].amax = wo_amax;  // (a max over all of W_o: a valid scale for its A half)
     add(job_plain(F(L.bo), 1, D.Hk, p->b_o, H, 1, {{0, 0, H}}));
     // transposes for dX = dZ W_h[:, :H] and dA = dZo W_o[:, Fa:]
     add(job_transpose(F(L.WhT), D.Hk, D.Hk, p->W_h, D.atom ? H + D.Fb : H, 0, H, H));
@@ -262,9 +257,6 @@ int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
     hipLaunchKernelGGL(split_h2_kernel, dim3(ew_blocks((size_t)D.Hk * D.Hk / 8)), dim3(256), 0, st, (const float *)F(L.Wh),
                        D.ldx, D.Hk, D.Hk, fused_bn(D.Hk), (uint8_t *)(base + L.WhH), wh_amax, 64);
     WD_CHECK_LAUNCH("pack_params h2");
-    hipLaunchKernelGGL(split_h2_kernel, dim3(ew_blocks((size_t)D.Hk * D.Hk / 8)), dim3(256), 0, st,
-                       (const float *)F(L.Wo) + D.Fak, D.Ko, D.Hk, D.Hk, fused_bn(D.Hk), (uint8_t *)(base + L.WoH), wo_amax, 64);
-    WD_CHECK_LAUNCH("pack_params h2 W_o");
     return 0;
 }
 
@@ -330,9 +322,8 @@ int gemm_nt(const float *a0, int lda0, int ka0, const float *a1, int lda1, int k
 // first ka_i columns of a [Mp][kp_i] plane-tile matrix, B a [Np][ka0 + ka1] one.
 bool x6g_eligible(const Epi &epi) { return epi_aligned(epi); }
 
-// kpb: B's K extent per row when larger than the K multiplied (leading chunks of each row block only)
 int gemm_x6g(const void *a0, int kp0, int ka0, const void *a1, int kp1, int ka1, const void *b, int Mp, int Np,
-             const Epi &epi, hipStream_t st, int kpb = 0) {
+             const Epi &epi, hipStream_t st) {
     if (Mp <= 0 || Np <= 0) return 0;
     if (Mp % 64 || Np % 64 || ka0 <= 0 || ka0 % 32 || ka1 % 32 || kp0 % 32 || (ka1 && kp1 % 32) || ka0 > kp0 ||
         ka1 > kp1 || !x6g_eligible(epi))
@@ -340,7 +331,7 @@ int gemm_x6g(const void *a0, int kp0, int ka0, const void *a1, int kp1, int ka1,
     X6PParams X{};
     X.a0 = (const uint8_t *)a0; X.kp0 = kp0; X.ka0 = ka0;
     X.a1 = (const uint8_t *)(a1 ? a1 : a0); X.kp1 = a1 ? kp1 : kp0; X.ka1 = ka1;
-    X.b = (const uint8_t *)b; X.kpb = kpb > 0 ? kpb : ka0 + ka1;
+    X.b = (const uint8_t *)b; X.kpb = ka0 + ka1;
     X.M = Mp; X.N = Np; X.epi = epi; X.tiles_m = Mp / 64; X.tiles_n = Np / X6_BN;
     hipLaunchKernelGGL(gemm_x6g_kernel, dim3(X.tiles_m * X.tiles_n), dim3(512), 0, st, X);
     WD_CHECK_LAUNCH("gemm_x6g");
@@ -703,7 +694,10 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
     auto slot = [&](const FusedJob &J, int t) { return (uint32_t *)(J.ws + J.L.amax[t & 1]); };
     // 40-column tiles for the embed when they divide Hk: twice the workgroups of the layer tiling (two per
     // CU at the benchmark size, 37 KB of LDS each), so one's staging overlaps the other's sums
-    const bool bn40 = Hk % 40 == 0;
+#ifndef WD_EMBED40
+#define WD_EMBED40 1
+#endif
+    const bool bn40 = WD_EMBED40 && Hk % 40 == 0;
     const int embed_tiles = Hk / (bn40 ? 40 : BNf);
     if (codes) {
         const int nt = embed_tiles;
@@ -765,7 +759,6 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
             Q.aptr = g->atom_gather.ptr; Q.aidx = g->atom_gather.idx; Q.acoef = g->atom_gather.coef;
             Q.aell_idx = g->atom_ell_idx; Q.aell_coef = g->atom_ell_coef;
             Q.aplanes = (uint8_t *)(J.ws + J.L.Ab);
-            Q.amax_a = last ? slot(J, t) : nullptr;  // (the other word buffer than this launch reads)
             Q.n_tiles = Hk / BNf;
             Q.zsave = J.D.save && last ? F(J, J.L.Z[t]) : nullptr;
             Q.asave = J.D.save && last ? F(J, J.L.A) : nullptr;
@@ -806,23 +799,8 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
         R.act = c->activation; R.slope = p->prelu; R.p_drop = c->dropout; R.seed = c->seed; R.layer = J.D.T;
         R.out = J.out; R.ncols = J.D.H; R.n_tiles = Hk / BNf;
         R.zosave = J.D.save ? F(J, J.L.Zo) : nullptr;
-        if (WD_WO_H2) {
-            R.eo = F(J, J.L.Eo); R.kca = 0;  // (the f_atoms half precomputed, below for graphs without codes)
-            R.ag32 = F(J, J.L.Ab); R.amax_a = slot(J, T - 1); R.amax_n = Hk / BNf;
-            R.woh = (const uint8_t *)(pk + PL.WoH); R.wo_amax = (const uint32_t *)(pk + PL.amax_o) + 64;
-        }
     }, M, grid);
-    if (WD_WO_H2 && !codes)  // Eo = f_atoms W_o[:, :Fa]^T on the blocked f_atoms planes (a GEMM segment of W_o)
-        for (int j = 0; j < n; ++j) {
-            const FusedJob &J = jobs[j];
-            WD_TRY(gemm_x6g(J.g->f_atoms_blk_x6, J.g->ld_atoms, J.D.Fak, nullptr, 0, 0, pk + PL.WoX, J.D.nblk * BLK_ATOMS,
-                            Hk, epi_store(F(J, J.L.Eo), Hk), st, J.D.Ko));
-        }
-    if (grid > 0 && WD_WO_H2) {
-        if (bn80) hipLaunchKernelGGL((wo_readout_kernel<80, 1, true>), dim3(grid), dim3(256), 0, st, M);
-        else hipLaunchKernelGGL((wo_readout_kernel<64, 1, true>), dim3(grid), dim3(256), 0, st, M);
-        WD_CHECK_LAUNCH("wo_readout");
-    } else if (grid > 0) {
+    if (grid > 0) {
         // one batch: single-chunk stages (55 KB, co-resident with other streams' layers); several: two
         if (bn80 && n > 1)
             hipLaunchKernelGGL((wo_readout_kernel<80, 2>), dim3(grid), dim3(64 * WoWaves<80>::WM * WoWaves<80>::WN), 0, st, M);
