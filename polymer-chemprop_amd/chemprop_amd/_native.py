@@ -205,6 +205,23 @@ def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
 
 
+_HIP = None
+
+
+def host_device_ptr(p: int) -> int:
+    """Device address of pinned host memory at ``p`` (hipHostGetDevicePointer on the HIP runtime torch
+    loaded), 0 if that memory is not mapped for the device: a kernel may then read it over PCIe directly."""
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL('libamdhip64.so.7')
+        _HIP.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
+        _HIP.hipHostGetDevicePointer.restype = ctypes.c_int
+    d = ctypes.c_void_p()
+    if _HIP.hipHostGetDevicePointer(ctypes.byref(d), ctypes.c_void_p(p), 0) != 0:
+        return 0
+    return d.value or 0
+
+
 _RAW_STREAM = getattr(torch._C, '_cuda_getCurrentRawStream', None)
 
 

@@ -165,10 +165,13 @@ _PINNED_TABLES = {}
 _PINNED_RING = 4
 
 
-def _host_table(rows: np.ndarray, dev: torch.device) -> torch.Tensor:
-    """rows (float32 [B][2T]) -> device tensor through a reused pinned buffer (asynchronous copy)."""
+def _host_table(rows: np.ndarray, dev: torch.device, zero_copy: bool = False):
+    """rows (float32 [B][2T]) -> device tensor through a reused pinned buffer (asynchronous copy).
+    ``zero_copy``: no copy; returns (device address of the pinned buffer, its event) or None when the
+    buffer is not mapped for the device -- the caller's kernel reads the rows over PCIe, and the caller
+    records the event after that kernel's launch (the buffer is refilled only after it)."""
     if dev.type != 'cuda':
-        return torch.from_numpy(rows).to(dev)
+        return None if zero_copy else torch.from_numpy(rows).to(dev)
     key = (dev, rows.shape)
     ring = _PINNED_TABLES.get(key)
     if ring is None:
@@ -177,17 +180,21 @@ def _host_table(rows: np.ndarray, dev: torch.device) -> torch.Tensor:
     ring[0] = (i + 1) % _PINNED_RING
     ent = ring[1][i]
     if ent is None:
-        ent = ring[1][i] = (torch.empty(rows.shape, dtype=torch.float32, pin_memory=True), torch.cuda.Event())
+        buf = torch.empty(rows.shape, dtype=torch.float32, pin_memory=True)
+        from . import _native
+        ent = ring[1][i] = (buf, torch.cuda.Event(), _native.host_device_ptr(buf.data_ptr()))
     else:
-        ent[1].synchronize()  # (this buffer's copy, _PINNED_RING steps ago)
-    buf, ev = ent
+        ent[1].synchronize()  # (this buffer's last reader, _PINNED_RING steps ago)
+    buf, ev, dptr = ent
     buf.numpy()[...] = rows
+    if zero_copy:
+        return (dptr, ev) if dptr else None
     table = buf.to(dev, non_blocking=True)
     ev.record(torch.cuda.current_stream(dev))
     return table
 
 
-def _loss_table(target_batch, target_weights, data_weights, dev):
+def _loss_table(target_batch, target_weights, data_weights, dev, zero_copy: bool = False):
     """train.py:46-74's targets and weights as one device table [B][2T] (targets | w = target weight *
     data weight * mask, rounded once to fp32) and the host count mask.sum()."""
     n_b = len(target_batch)
@@ -214,6 +221,8 @@ def _loss_table(target_batch, target_weights, data_weights, dev):
     # targets and W travel as one host table (one pinned, asynchronous copy: pageable copies would each
     # stall the host until the forward has drained)
     rows = np.concatenate([tgt, tw[None, :] * dw[:, None] * mask], axis=1).astype(np.float32)
+    if zero_copy:
+        return _host_table(rows, dev, True), n_t, int(mask.sum()), rows.shape
     return _host_table(rows, dev), n_t, int(mask.sum())
 
 
@@ -400,11 +409,18 @@ def _direct_step(model, enc, graph, head, target_batch, target_weights, data_wei
     from . import _native
     l1, l2, act = head
     out, state = enc._train_forward(graph)
-    table, n_t, n_mask = _loss_table(target_batch, target_weights, data_weights, out.device)
+    # the loss table read by the head kernel straight from its pinned host buffer (no copy launch in the
+    # step: the copy kernel and its gap were ~10 us, profiles/round4_train_kernel_trace_v1.txt)
+    zc, n_t, n_mask, tshape = _loss_table(target_batch, target_weights, data_weights, out.device, zero_copy=True)
+    if zc is None:
+        table, n_t, n_mask = _loss_table(target_batch, target_weights, data_weights, out.device)
+        tab_ptr, tshape = table.data_ptr(), tuple(table.shape)
+    else:
+        tab_ptr = zc[0]
     if n_t != l2.out_features:
         raise ValueError(f'{n_t} targets per row for {l2.out_features} outputs')
-    if table.shape[0] != out.shape[0] or out.shape[1] != l1.in_features:
-        raise ValueError(f'{table.shape[0]} target rows for encodings of shape {tuple(out.shape)} '
+    if tshape[0] != out.shape[0] or out.shape[1] != l1.in_features:
+        raise ValueError(f'{tshape[0]} target rows for encodings of shape {tuple(out.shape)} '
                          f'(FFN input {l1.in_features})')
     inv_n = 1.0 / n_mask if n_mask else float('inf')
     dev = out.device
@@ -418,10 +434,12 @@ def _direct_step(model, enc, graph, head, target_batch, target_weights, data_wei
     db2 = _grad_buffer(l2.bias) if l2.bias is not None else None
     ptr = _native.ptr
     sp = scratch.data_ptr()
-    h = _native.WdHead(ptr(out), F, B, F, Hf, T, ptr(l1.weight), ptr(l1.bias), ptr(l2.weight), ptr(l2.bias), ptr(table),
-                       table.shape[1], float(inv_n), act, sp, sp + 4 * B * Hf, sp + 8 * B * Hf, sp + 4 * B * (2 * Hf + T),
+    h = _native.WdHead(ptr(out), F, B, F, Hf, T, ptr(l1.weight), ptr(l1.bias), ptr(l2.weight), ptr(l2.bias), tab_ptr,
+                       tshape[1], float(inv_n), act, sp, sp + 4 * B * Hf, sp + 8 * B * Hf, sp + 4 * B * (2 * Hf + T),
                        ptr(dx), ptr(dW1), ptr(db1), ptr(dW2), ptr(db2), ptr(loss))
     _native.check(_native.lib().wdmpnn_head_mse(ctypes.byref(h), _native.current_stream(dev)), 'FFN head + loss')
+    if zc is not None:
+        zc[1].record(torch.cuda.current_stream(dev))  # (the pinned buffer's last reader)
     enc._train_backward(state, dx, {n: _grad_buffer(p) for n, p in enc._direct_names()})
     return loss
 

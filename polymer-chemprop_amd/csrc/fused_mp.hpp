@@ -123,10 +123,10 @@ struct H2Prod {
     float slope, scale, pd;
     uint64_t seed;
     uint32_t layer;
-    const uint32_t *sw; int sn;             // the scale's words
+    uint32_t wv;                            // this lane's scale word (lane_word, loaded by the caller)
     u32x4 v[SETS][U][2];                    // register sets (raw fp32 bits)
-    __device__ __forceinline__ void init() { scale = h2_scale(max_words(sw, sn)); }
-    __device__ __forceinline__ H2Prod(const MpLayerP &P, const BlockRow &B, int blk) {
+    __device__ __forceinline__ void init() { scale = h2_scale(wave_max_u32(wv)); }
+    __device__ __forceinline__ H2Prod(const MpLayerP &P, const BlockRow &B, uint32_t words) {
         const int t = threadIdx.x & 255;
         r0 = t >> 2; u = t & 3;
         rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(P.zin + (size_t)B.bs * P.kp), 0, B.bn * P.kp * 4,
@@ -139,7 +139,7 @@ struct H2Prod {
         }
         live16 = (B.bn + 15) & ~15;
         slope = AACT == ACT_PRELU ? P.slope[0] : 0.f;
-        sw = P.amax_in + (size_t)blk * P.amax_in_n; sn = P.amax_in_n;
+        wv = words;
         scale = 1.f;
         pd = P.p_drop_in;
         seed = P.seed;
@@ -155,6 +155,12 @@ struct H2Prod {
     }
     template <typename S>
     __device__ __forceinline__ void store(S, int kc, uint8_t *st) {
+        // (a use of every register of the set outside the row branch below: the compiler otherwise sank
+        // the first set's second-row loads into that branch, right in front of their use)
+#pragma unroll
+        for (int i = 0; i < U; ++i)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) asm volatile("" ::"v"(v[S::value][i][h]));
 #pragma unroll
         for (int i = 0; i < U; ++i) {
             const int r = r0 + 64 * i;
@@ -402,7 +408,11 @@ __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpL
     const BlockRow B = load_block(P.blocks, blk);
     MpEpilogue<BN, MP_THREADS, LAST> E;
     float *Pt = reinterpret_cast<float *>(lds);
-    H2Prod<BM, ACT> ap(P, B, blk);
+    // the block's scale words of M_{t-1} (<= 64, one per lane) and W_h's: loaded before the GEMM's first
+    // loads, reduced by the producers before their first stage and by the consumers after the GEMM
+    const uint32_t wv = lane_word(P.amax_in + (size_t)blk * P.amax_in_n, P.amax_in_n);
+    const uint32_t whm = *P.wh_amax;
+    H2Prod<BM, ACT> ap(P, B, wv);
     wd_stamp(1 + 8 * LAST);
     floatx4 acc[BM / 64][BN / 16];
     h2_mainloop_ws<BM, BN>(P.wh + (size_t)nt * (P.kp >> 5) * (2 * BN * 64), P.kp >> 5, B.bn, lds, acc, ap);
@@ -412,8 +422,8 @@ __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpL
     E.prefetch(P, B);
     __syncthreads();
     wd_stamp(3 + 8 * LAST);
-    const float ia = h2_inv_scale(max_words(P.amax_in + (size_t)blk * P.amax_in_n, P.amax_in_n));
-    const float iw = h2_inv_scale(*P.wh_amax);
+    const float ia = h2_inv_scale(wave_max_u32(wv));
+    const float iw = h2_inv_scale(whm);
     if (threadIdx.x < 256) x6_acc_to_lds_scaled<BM, BN, 4, 1>(acc, Pt, ia, iw);  // (the consumer waves hold the tile)
     __syncthreads();
     E.template run<ACT>(P, B, blk, n0, Pt);

@@ -205,6 +205,103 @@ __global__ __launch_bounds__(256) void readout_bwd_kernel(ReadoutP P, const floa
     }
 }
 
+// The readout backward fused with the backward of the W_o activation (mpn.py:133-134, 145-171) when the
+// readout reads h directly (no descriptor layer):
+//     dZo[a] = (dout[i] Xn_i w_a (1/sum w | 1 | 1/norm)) * dropout_scale * act'(Zo[a])
+// the same arithmetic, in the same order, as readout_bwd_kernel + act_bwd_kernel, without dh's round trip
+// through HBM and without its memset: workgroups (i < B, y) write molecule i's atom rows (all ld columns,
+// zeros past ncols; the (atom, float4) units strided over the RO_ACT_Y workgroups of the molecule), the
+// workgroups (B, y) the rows of no molecule (the pad row 0 and [rows, rows_p)).  Each thread loads its
+// RO_ACT_U units' Zo before computing any (the loop of load-then-store units waited one memory latency per
+// unit).  grid = (B + 1, RO_ACT_Y), 256 threads; ld <= RO_ACT_MAXLD, a multiple of 4.
+struct RoActBwd {
+    const float *Z; int ld;                 // Zo [rows_p][ld]
+    int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;
+    float *out;                             // dZo [rows_p][ld]
+    int rows, rows_p;
+    float *prelu_part;                      // [gridDim.x * gridDim.y] or null
+};
+constexpr int RO_ACT_MAXLD = 2560, RO_ACT_Y = 4, RO_ACT_U = 4;
+
+__global__ __launch_bounds__(256) void readout_act_bwd_kernel(ReadoutP P, const float *__restrict__ dout, RoActBwd A) {
+    constexpr int NT = 256, U = RO_ACT_U;
+    __shared__ float red[NT];
+    __shared__ float4 gsl[RO_ACT_MAXLD / 4];
+    const int tid = threadIdx.x, i = blockIdx.x, Q = A.ld / 4;
+    const int t0 = blockIdx.y * NT + tid, ts = NT * gridDim.y;  // this thread's units t0, t0 + ts, ...
+    const float slope = A.act == ACT_PRELU ? A.slope[0] : 0.f;
+    float ppart = 0.f;
+    if (i == (int)gridDim.x - 1) {
+        const int extra = A.rows_p - A.rows;
+        for (int t = t0; t < (1 + extra) * Q; t += ts) {
+            const int k = t / Q, q = t % Q, r = k == 0 ? 0 : A.rows + k - 1;
+            st4(A.out + (size_t)r * A.ld + 4 * q, f4zero());
+        }
+    } else if (P.mol_size[i] > 0) {
+        const int a0 = P.mol_start[i], n = P.mol_size[i];
+        float w = 0.f;  // sum w_a: the tree of readout_bwd_kernel
+        for (int a = tid; a < n; a += NT) w += P.w_atoms[a0 + a];
+        red[tid] = w;
+        __syncthreads();
+        for (int k = NT / 2; k > 0; k >>= 1) {
+            if (tid < k) red[tid] += red[tid + k];
+            __syncthreads();
+        }
+        const float wsum = red[0], x = P.xn[i];
+        for (int q = tid; q < Q; q += NT) {
+            float gs[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int c = 4 * q + e;
+                const float g = c < P.ncols ? dout[(size_t)i * P.ncols + c] * x : 0.f;
+                gs[e] = P.agg == 0 ? g / wsum : (P.agg == 2 ? g / P.norm : g);
+            }
+            gsl[q] = make_float4(gs[0], gs[1], gs[2], gs[3]);
+        }
+        __syncthreads();
+        for (int tb = t0; tb < n * Q; tb += U * ts) {
+            float4 z4[U];
+            float wa[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = tb + u * ts, a = t / Q, q = t % Q;
+                z4[u] = f4zero();
+                wa[u] = 0.f;
+                if (t < n * Q) {
+                    z4[u] = ld4(A.Z + (size_t)(a0 + a) * A.ld + 4 * q);
+                    wa[u] = P.w_atoms[a0 + a];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = tb + u * ts, a = t / Q, q = t % Q, r = a0 + a;
+                if (t >= n * Q) break;
+                const float4 g4 = gsl[q];
+                const float g[4] = {g4.x * wa[u], g4.y * wa[u], g4.z * wa[u], g4.w * wa[u]};
+                const float z[4] = {z4[u].x, z4[u].y, z4[u].z, z4[u].w};
+                float dz[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float s = A.p_drop > 0.f ? dropout_scale(A.seed, A.layer, r, 4 * q + e, A.p_drop) : 1.f;
+                    dz[e] = g[e] * s * act_grad(A.act, z[e], slope);
+                    if (A.act == ACT_PRELU && !(z[e] > 0.f)) ppart += z[e] * g[e] * s;
+                }
+                st4(A.out + (size_t)r * A.ld + 4 * q, make_float4(dz[0], dz[1], dz[2], dz[3]));
+            }
+        }
+    }
+    if (A.prelu_part) {
+        __syncthreads();
+        red[tid] = ppart;
+        __syncthreads();
+        for (int s = NT / 2; s > 0; s >>= 1) {
+            if (tid < s) red[tid] += red[tid + s];
+            __syncthreads();
+        }
+        if (tid == 0) A.prelu_part[blockIdx.y * gridDim.x + blockIdx.x] = red[0];
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Backward of one activation layer, fused with the gather that produces its incoming gradient:
 //   g   = sum_e coef[e] * G[idx[e]]  (csr) | (G[r] + G[rev[r]]) / 2 (sym) | G[r] (dense)
@@ -242,12 +339,31 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(ActBwd P) {
         if (r < P.rows) {
             fv g;
             if (P.ptr) {
+                // the first GE entries' ids and weights fetched together (WdCsr lists are readable 8 entries
+                // past their end; dead entries read row 0 and are not added), then all their rows: three
+                // dependent hops per row instead of two per entry; entries added in CSR order
+                constexpr int GE = 4;
                 g = (fv)0.f;
-                const int e1 = P.ptr[r + 1];
-                for (int e = P.ptr[r]; e < e1; ++e) {
-                    const float w = P.coef ? P.coef[e] : 1.f;
-                    const fv x = *(const fv *)(P.G + (size_t)P.idx[e] * P.ldg + c);
-                    for (int q = 0; q < V; ++q) g[q] = fmaf(w, x[q], g[q]);
+                const int e0 = P.ptr[r], e1 = P.ptr[r + 1];
+                int j[GE];
+                float w[GE];
+#pragma unroll
+                for (int k = 0; k < GE; ++k) {
+                    const int jj = P.idx[e0 + k];
+                    j[k] = e0 + k < e1 ? jj : 0;
+                    w[k] = P.coef ? P.coef[e0 + k] : 1.f;
+                }
+                fv x[GE];
+#pragma unroll
+                for (int k = 0; k < GE; ++k) x[k] = *(const fv *)(P.G + (size_t)j[k] * P.ldg + c);
+#pragma unroll
+                for (int k = 0; k < GE; ++k)
+                    if (e0 + k < e1)
+                        for (int q = 0; q < V; ++q) g[q] = fmaf(w[k], x[k][q], g[q]);
+                for (int e = e0 + GE; e < e1; ++e) {
+                    const float we = P.coef ? P.coef[e] : 1.f;
+                    const fv xe = *(const fv *)(P.G + (size_t)P.idx[e] * P.ldg + c);
+                    for (int q = 0; q < V; ++q) g[q] = fmaf(we, xe[q], g[q]);
                 }
             } else if (P.sym_rev) {
                 const fv a = *(const fv *)(P.G + (size_t)r * P.ldg + c);
@@ -524,68 +640,95 @@ struct SmallGemm {
     float *C; long long ldc;
     int M, N, K;
 };
-__device__ __forceinline__ void small_gemm_tile(const SmallGemm &G, int tile, float (*as)[33], float (*bs)[33]) {
+// 32 x 32 output tile per workgroup of 4 waves: both operands' K-slices of SG_KC staged k-major in LDS
+// (every load of the stage in flight at once: these GEMMs are load-latency-bound, 128 x 300 x 300), wave w
+// multiplies the w-th quarter of the stage's K (lane: 4 x 4 outputs from two float4 reads per k), and the
+// four partial tiles are added in wave order (deterministic).
+constexpr int SG_KC = 320, SG_LD = 36;  // (row stride 36: float4-aligned, 4-way bank spread for the staging)
+struct SmallGemmLds { float as[SG_KC][SG_LD]; float bs[SG_KC][SG_LD]; };
+// AK: A's k index contiguous (sak == 1, else sai == 1); BJ: B's j index contiguous (sbj == 1, else sbk == 1)
+template <bool AK, bool BJ>
+__device__ __forceinline__ void small_gemm_tile_t(const SmallGemm &G, int tile, SmallGemmLds &L) {
     const int tn = (G.N + 31) / 32, i0 = (tile / tn) * 32, j0 = (tile % tn) * 32;
-    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
-    float c[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
-    // staging: consecutive lanes along each operand's contiguous index (coalesced loads; the padded rows
-    // keep the transposed LDS writes conflict-free); the next chunk is loaded into registers while this
-    // one is multiplied (these GEMMs are load-latency-bound: 128 x 300 x 300)
-    float ra[4], rb[4];
-    auto load = [&](int k0) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, ri = 4 * (lane >> 3), cj = 4 * (lane & 7);
+    constexpr int PER = 32 * SG_KC / 256;
+    float c[4][4] = {};
+    float ra[PER], rb[PER];
+    auto load = [&](int k0) {  // consecutive lanes along each operand's contiguous index (coalesced)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = tid + 256 * q, hi = e >> 5, lo = e & 31;
-            const int ar = G.sak == 1 ? hi : lo, ac = G.sak == 1 ? lo : hi;  // (i, k) of A
-            const int ia = i0 + ar, ka = k0 + ac;
+        for (int q = 0; q < PER; ++q) {
+            const int e = tid + 256 * q;
+            const int ia = i0 + (AK ? e / SG_KC : e % 32), ka = k0 + (AK ? e % SG_KC : e / 32);
             ra[q] = ia < G.M && ka < G.K ? G.A[ia * G.sai + ka * G.sak] : 0.f;
-            const int br = G.sbj == 1 ? hi : lo, bc = G.sbj == 1 ? lo : hi;  // (k, j) of B
-            const int kb = k0 + br, jb = j0 + bc;
+            const int kb = k0 + (BJ ? e / 32 : e % SG_KC), jb = j0 + (BJ ? e % 32 : e / SG_KC);
             rb[q] = kb < G.K && jb < G.N ? G.B[kb * G.sbk + jb * G.sbj] : 0.f;
         }
     };
     auto store = [&]() {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int e = tid + 256 * q, hi = e >> 5, lo = e & 31;
-            as[G.sak == 1 ? hi : lo][G.sak == 1 ? lo : hi] = ra[q];
-            bs[G.sbj == 1 ? hi : lo][G.sbj == 1 ? lo : hi] = rb[q];
+        for (int q = 0; q < PER; ++q) {
+            const int e = tid + 256 * q;
+            if (AK) L.as[e % SG_KC][e / SG_KC] = ra[q];
+            else L.as[e / 32][e % 32] = ra[q];
+            if (BJ) L.bs[e / 32][e % 32] = rb[q];
+            else L.bs[e % SG_KC][e / SG_KC] = rb[q];
         }
     };
     load(0);
-    for (int k0 = 0; k0 < G.K; k0 += 32) {
+    for (int k0 = 0; k0 < G.K; k0 += SG_KC) {
         store();
         __syncthreads();
-        if (k0 + 32 < G.K) load(k0 + 32);
-#pragma unroll 8
-        for (int k = 0; k < 32; ++k) {
-            const float a0 = as[2 * ty][k], a1 = as[2 * ty + 1][k], b0 = bs[k][2 * tx], b1 = bs[k][2 * tx + 1];
-            c[0][0] = fmaf(a0, b0, c[0][0]); c[0][1] = fmaf(a0, b1, c[0][1]);
-            c[1][0] = fmaf(a1, b0, c[1][0]); c[1][1] = fmaf(a1, b1, c[1][1]);
+        if (k0 + SG_KC < G.K) load(k0 + SG_KC);
+        const int kn = min(SG_KC, G.K - k0), kq = (kn + 3) / 4, kb = wave * kq, ke = min(kn, kb + kq);
+#pragma unroll 4
+        for (int k = kb; k < ke; ++k) {
+            const float4 a = *reinterpret_cast<const float4 *>(&L.as[k][ri]);
+            const float4 b = *reinterpret_cast<const float4 *>(&L.bs[k][cj]);
+            const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) c[x][y] = fmaf(av[x], bv[y], c[x][y]);
         }
         __syncthreads();
     }
+    // the four waves' partial tiles (in as, free after the last barrier), added in wave order
+    float *part = &L.as[0][0];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int x = 0; x < 4; ++x)
+        *reinterpret_cast<float4 *>(part + wave * 1024 + (ri + x) * 32 + cj) = make_float4(c[x][0], c[x][1], c[x][2], c[x][3]);
+    __syncthreads();
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            const int i = i0 + 2 * ty + a, j = j0 + 2 * tx + b;
-            if (i < G.M && j < G.N) G.C[i * G.ldc + j] = c[a][b] + (G.bias ? G.bias[j] : 0.f);
-        }
+    for (int q = 0; q < 4; ++q) {
+        const int o = tid + 256 * q, i = i0 + o / 32, j = j0 + o % 32;
+        const float v = ((part[o] + part[1024 + o]) + part[2048 + o]) + part[3072 + o];
+        if (i < G.M && j < G.N) G.C[i * G.ldc + j] = v + (G.bias ? G.bias[j] : 0.f);
+    }
 }
-// sum_{r < B} x[r * ld] (+ fma with y[r * ldy] when y): rows in order, eight loads in flight
+__device__ __forceinline__ void small_gemm_tile(const SmallGemm &G, int tile, SmallGemmLds &L) {
+    if (G.sak == 1) {
+        if (G.sbj == 1) small_gemm_tile_t<true, true>(G, tile, L);
+        else small_gemm_tile_t<true, false>(G, tile, L);
+    } else {
+        if (G.sbj == 1) small_gemm_tile_t<false, true>(G, tile, L);
+        else small_gemm_tile_t<false, false>(G, tile, L);
+    }
+}
+
+// sum_{r < B} x[r * ld] (+ fma with y[r * ldy] when y): rows in order, RU loads in flight
 __device__ __forceinline__ float row_sum(const float *x, long long ld, const float *y, long long ldy, int B) {
     float s = 0.f;
     int r = 0;
-    for (; r + 8 <= B; r += 8) {
-        float v[8], w[8];
+    constexpr int RU = 32;  // rows in flight (8 paid a memory latency per 8 rows: B = 128 -> 16 in a row)
+    for (; r + RU <= B; r += RU) {
+        float v[RU], w[RU];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
+        for (int q = 0; q < RU; ++q) {
             v[q] = x[(r + q) * ld];
             w[q] = y ? y[(r + q) * ldy] : 1.f;
         }
 #pragma unroll
-        for (int q = 0; q < 8; ++q) s = y ? fmaf(v[q], w[q], s) : s + v[q];
+        for (int q = 0; q < RU; ++q) s = y ? fmaf(v[q], w[q], s) : s + v[q];
     }
     for (; r < B; ++r) s = y ? fmaf(x[r * ld], y[r * ldy], s) : s + x[r * ld];
     return s;
@@ -594,9 +737,9 @@ __device__ __forceinline__ int small_gemm_tiles(const SmallGemm &G) { return ((G
 
 // head step 1: H = X W1^T + b1 -> P.a (pre-activation, [B][Hf])
 __global__ __launch_bounds__(256) void head_h_kernel(WdHead P) {
-    __shared__ float as[32][33], bs[32][33];
+    __shared__ SmallGemmLds L;
     SmallGemm G{P.x, P.ld_x, 1, P.W1, 1, P.F, P.b1, P.a, P.Hf, P.B, P.Hf, P.F};
-    small_gemm_tile(G, blockIdx.x, as, bs);
+    small_gemm_tile(G, blockIdx.x, L);
 }
 
 // head step 2, one wave per row: out = W2 act(h) + b2, the row's loss terms, dout = 2 w (out - y) / n,
@@ -636,13 +779,13 @@ __global__ __launch_bounds__(256) void head_rows_kernel(WdHead P) {
 // head step 3: dX = dH W1 (tiles 0 .. n1), dW1 = dH^T X (next n2 tiles), then db1, dW2, db2 and the loss
 // (one thread per element, rows summed in order)
 __global__ __launch_bounds__(256) void head_grads_kernel(WdHead P) {
-    __shared__ float as[32][33], bs[32][33];
+    __shared__ SmallGemmLds L;
     const SmallGemm GX{P.dh, P.Hf, 1, P.W1, P.F, 1, nullptr, P.dx, P.ld_x, P.B, P.F, P.Hf};
     const SmallGemm GW{P.dh, 1, P.Hf, P.x, P.ld_x, 1, nullptr, P.dW1, P.F, P.Hf, P.F, P.B};
     const int n1 = small_gemm_tiles(GX), n2 = small_gemm_tiles(GW);
     const int b = blockIdx.x;
-    if (b < n1) { small_gemm_tile(GX, b, as, bs); return; }
-    if (b < n1 + n2) { small_gemm_tile(GW, b - n1, as, bs); return; }
+    if (b < n1) { small_gemm_tile(GX, b, L); return; }
+    if (b < n1 + n2) { small_gemm_tile(GW, b - n1, L); return; }
     const int Hf = P.Hf, T = P.T, B = P.B;
     const long long q = (long long)(b - n1 - n2) * 256 + threadIdx.x;
     if (q < Hf) {

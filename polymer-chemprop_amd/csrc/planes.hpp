@@ -200,12 +200,24 @@ __device__ __forceinline__ int h2_sexp(uint32_t m) {
 }
 __device__ __forceinline__ float h2_scale(uint32_t m) { return __uint_as_float((uint32_t)h2_sexp(m) << 23); }
 __device__ __forceinline__ float h2_inv_scale(uint32_t m) { return __uint_as_float((uint32_t)(254 - h2_sexp(m)) << 23); }
-// max of n words at a workgroup-uniform address
-__device__ __forceinline__ uint32_t max_words(const uint32_t *w, int n) {
-    uint32_t m = 0;
-    for (int i = 0; i < n; ++i) m = max(m, w[i]);
-    return m;
+// Max of n <= 64 words at a workgroup-uniform address, in two steps so that the load can be issued early
+// and waited for late: lane_word (lane i loads word i: one load, all words in flight at once; a loop of
+// dependent loads cost one memory latency per word), then wave_max_u32 (every lane of the wave active):
+// DPP max within each 16-lane row, then the four rows' maxima read into scalars.
+__device__ __forceinline__ uint32_t lane_word(const uint32_t *w, int n) {
+    const int l = threadIdx.x & 63;
+    return l < n ? w[l] : 0u;
 }
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t m) {
+    m = max(m, (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    m = max(m, (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    m = max(m, (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0x124, 0xF, 0xF, false));  // row_ror:4
+    m = max(m, (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0x128, 0xF, 0xF, false));  // row_ror:8
+    const uint32_t a = __builtin_amdgcn_readlane(m, 0), b = __builtin_amdgcn_readlane(m, 16);
+    const uint32_t c = __builtin_amdgcn_readlane(m, 32), d = __builtin_amdgcn_readlane(m, 48);
+    return max(max(a, b), max(c, d));
+}
+__device__ __forceinline__ uint32_t max_words(const uint32_t *w, int n) { return wave_max_u32(lane_word(w, n)); }
 // (a, b) scaled by s -> packed fp16 hi pair and lo pair (element 0 in the low half)
 __device__ __forceinline__ void split_h2(float a, float b, float s, uint32_t &hi, uint32_t &lo) {
     const f16x2v h = __builtin_convertvector((f32x2v){a * s, b * s}, f16x2v);  // v_cvt_pk_f16_f32 (RNE)
@@ -217,11 +229,7 @@ __device__ __forceinline__ void split_h2(float a, float b, float s, uint32_t &hi
 // workgroup max of a u32 -> one plain store by thread 0 (red: >= blockDim.x / 64 words of LDS; every
 // thread of the workgroup must call it)
 __device__ __forceinline__ void publish_max(uint32_t m, uint32_t *slot, uint32_t *red) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const uint32_t o = __shfl_xor(m, off, 64);
-        m = o > m ? o : m;
-    }
+    m = wave_max_u32(m);
     const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     if ((threadIdx.x & 63) == 0) red[wave] = m;
     __syncthreads();
@@ -234,7 +242,7 @@ __device__ __forceinline__ void publish_max(uint32_t m, uint32_t *slot, uint32_t
 // fp32 [rows][ld] (first kp columns) -> h2 plane tiles with BR-row blocks: block (r / BR, k / 32) of 2 x
 // BR x 64 bytes (hi plane, then lo), row r % BR, columns k % 32 at 64 (r % BR) + 2 (k % 32) -- the bf16
 // plane-tile layout with two planes.  Scaled by the max of the nw words of `words` (pack_kernel's
-// per-workgroup maxima), which workgroup 0 also folds into words[nw] for the consumers.
+// per-workgroup maxima, nw <= 64), which workgroup 0 also folds into words[nw] for the consumers.
 __global__ __launch_bounds__(256) void split_h2_kernel(const float *__restrict__ src, int ld, int rows, int kp, int br,
                                                        uint8_t *__restrict__ dst, uint32_t *words, int nw) {
     const uint32_t m = max_words(words, nw);

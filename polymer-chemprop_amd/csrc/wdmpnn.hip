@@ -1055,11 +1055,24 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
         return P;
     };
 
-    // readout backward -> dH [Vap][Hk or Hdk]
+    // readout backward -> dH [Vap][Hk or Hdk]; without descriptors fused with the W_o activation's backward
+    // (readout_act_bwd_kernel: dZo straight from dout, no dH and no memset)
     const int ldH = D.desc ? D.Hdk : Hk;
     float *dH = S(Bl.dH);
-    if (hipMemsetAsync(dH, 0, (size_t)D.Vap * ldH * 4, st) != hipSuccess) return fail(WD_ERR_ARG, "memset failed");
-    if (D.B > 0) {
+    const int ro_wgs = (D.B + 1) * RO_ACT_Y;
+    const bool ro_fused = !D.desc && Hk <= RO_ACT_MAXLD && (!prelu || prelu_used + ro_wgs <= (int)Bl.prelu_floats);
+    if (ro_fused) {
+        RoActBwd A{};
+        A.Z = F(L.Zo); A.ld = Hk; A.act = c->activation; A.slope = p->prelu; A.p_drop = c->dropout;
+        A.seed = c->seed; A.layer = D.T; A.out = S(Bl.dZo); A.rows = D.Va; A.rows_p = D.Vap;
+        if (prelu) { A.prelu_part = prelu_part + prelu_used; prelu_used += ro_wgs; }
+        hipLaunchKernelGGL(readout_act_bwd_kernel, dim3(D.B + 1, RO_ACT_Y), dim3(256), 0, st,
+                           readout_params(g, p, c, nullptr, Hk, D.Hd, nullptr), dout, A);
+        WD_CHECK_LAUNCH("readout_act_bwd");
+    } else if (hipMemsetAsync(dH, 0, (size_t)D.Vap * ldH * 4, st) != hipSuccess) {
+        return fail(WD_ERR_ARG, "memset failed");
+    }
+    if (D.B > 0 && !ro_fused) {
         hipLaunchKernelGGL(readout_bwd_kernel, dim3(D.B, (D.Hd + RO_BWD_COLS - 1) / RO_BWD_COLS), dim3(256), 0, st,
                            readout_params(g, p, c, nullptr, ldH, D.Hd, nullptr), dout, dH);
         WD_CHECK_LAUNCH("readout_bwd");
@@ -1082,9 +1095,11 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
     }
     // W_o layer
     {
-        ActBwd P = base_bwd(F(L.Zo), D.T, c->activation, D.Va, D.Vap, Hk, S(Bl.dZo));
-        P.G = dh; P.ldg = Hk;
-        WD_TRY(act_bwd(P));
+        if (!ro_fused) {
+            ActBwd P = base_bwd(F(L.Zo), D.T, c->activation, D.Va, D.Vap, Hk, S(Bl.dZo));
+            P.G = dh; P.ldg = Hk;
+            WD_TRY(act_bwd(P));
+        }
         Src dZ = make_src(D.Va, {seg_dense(S(Bl.dZo), Hk, Hk)});
         Src X = x_o(g, D, F(L.A));
         TnPlan tp = tn_plan(Hk, X, D.Va);
