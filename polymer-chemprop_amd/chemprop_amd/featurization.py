@@ -512,7 +512,15 @@ class BatchMolGraph:
             msg, feat = self.bond_message_gather(), None
             msg_rows = self.n_bonds
         agg = self.atom_aggregate_gather(atom_messages)
-        blocks = None if atom_messages else self.molecule_blocks()
+        blocks = self.molecule_blocks()
+        msg_blk = msg
+        if atom_messages and blocks is not None and len(blocks):
+            # the fused atom-message layers (wdmpnn.hip get_dims: bias-free models only) gather a2a neighbours
+            # inside the block: their ELL lists drop the pad slots (atom 0, whose message is zero without
+            # biases); msg keeps each row's real entries first, so a longer row continues in msg past the
+            # ELL width (the kernel skips its pad entry)
+            rows, j = self._entries_of_in(np.arange(self.n_atoms, dtype=np.int64))
+            msg_blk = Csr.from_rows(rows, self._np['b2a'][j], np.ones(len(rows), np.float32), self.n_atoms)
         if blocks is not None and len(blocks):
             # every gather of a block's rows must stay inside the block (block-diagonal batches)
             bond_blk = np.full(fb_p.shape[0], -1, np.int32)
@@ -526,9 +534,12 @@ class BatchMolGraph:
                 rows = np.repeat(start, count) + within
                 blk_row[rows] = cap * k + within
                 blk_of[rows] = k
-            for c, rb in ((msg, blk_of_bond), (agg, blk_of_atom)):
+            # (bond mode: msg rows are bonds gathering bonds, agg rows atoms gathering bonds; atom mode: both
+            # gather atoms into atom rows)
+            src_of = blk_of_atom if atom_messages else blk_of_bond
+            for c, rb in ((msg_blk, blk_of_atom if atom_messages else blk_of_bond), (agg, blk_of_atom)):
                 row = np.repeat(np.arange(len(c.ptr) - 1), np.diff(c.ptr))
-                if len(row) and not np.array_equal(rb[row], blk_of_bond[c.idx]):
+                if len(row) and not np.array_equal(rb[row], src_of[c.idx]):
                     blocks = None
                     break
         if atom_messages:
@@ -543,10 +554,10 @@ class BatchMolGraph:
             arrays.append(('b2a', b2a_p))
         if blocks is not None and len(blocks):
             arrays += [('blocks', blocks), ('bond_blk_row', bond_blk), ('atom_blk_row', atom_blk)]
-            bstart = np.zeros(len(blocks) + 1, np.int64)
-            bstart[:-1] = blocks[:, 0]
-            for name, c, rows_p, rb in (('msg_ell', msg, fb_p.shape[0], blk_of_bond), ('agg_ell', agg, fa_p.shape[0],
-                                                                                     blk_of_atom)):
+            bstart = np.zeros(len(blocks) + 1, np.int64)  # first row of the gathered kind per block (-1: row 0)
+            bstart[:-1] = blocks[:, 2] if atom_messages else blocks[:, 0]
+            mrows, mblk = (fa_p.shape[0], blk_of_atom) if atom_messages else (fb_p.shape[0], blk_of_bond)
+            for name, c, rows_p, rb in (('msg_ell', msg_blk, mrows, mblk), ('agg_ell', agg, fa_p.shape[0], blk_of_atom)):
                 ell_idx, ell_coef = ell_rows(c, rows_p, bstart[rb[:len(c.ptr) - 1]])
                 arrays += [(name + '_idx', ell_idx), (name + '_coef', ell_coef)]
             # per bond row: its source atom (b2a) as a block-local atom index (the fused layer's X[b] =
@@ -626,7 +637,8 @@ class BatchMolGraph:
                 s.n_blocks, s.blocks, s.bond_blk_row = len(blocks), P('blocks'), P('bond_blk_row')
                 s.msg_ell_idx, s.msg_ell_coef = P('msg_ell_idx'), P('msg_ell_coef')
                 s.atom_ell_idx, s.atom_ell_coef = P('agg_ell_idx'), P('agg_ell_coef')
-                s.bond_src_blk = P('bond_src_blk')
+                if not atom_messages:
+                    s.bond_src_blk = P('bond_src_blk')
                 s.f_atoms_blk_x6 = planes.data_ptr()
         dg = DeviceGraph(buf, views, s)
         dg.finish()

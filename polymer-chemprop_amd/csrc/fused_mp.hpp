@@ -102,6 +102,15 @@ struct MpLayerP {
     // pre-activation Z_t (mpn.py:123) as fp32 natural bond rows [Rp][kp] and the atom aggregate A
     // (mpn.py:126-131) as fp32 natural atom rows [Vap][kp] (the backward's operands)
     float *zsave, *asave;
+    // atom-message mode (mpn.py:47-53, 93-94, 104-108; the template's ATOM): the message rows are the
+    // block's atoms, inp is the residual inp + (sum over a2b of the bond features) W_h[:, H:]^T, and the
+    // gather is the a2a neighbour sum X[a] = sum_{a' in nbr(a)} P[a'] (no reverse term), from these lists
+    // (block-local ELL over atom rows); aptr / aell above stay the final
+    // aggregate (mpn.py:126-131).  The ELL lists drop the a2a pad slots (atom 0, whose message is zero
+    // without biases); rows longer than the ELL width continue in the CSR list msg_gather, whose pad-slot
+    // entry (atom 0, outside every block) is skipped
+    const uint8_t *mell_idx; const float *mell_coef;
+    const int32_t *mptr, *midx; const float *mcoef;
 };
 
 // The GEMM operand M_{t-1} = dropout(act(Z_{t-1})), formed while staging from the fp32 Z rows (the
@@ -126,18 +135,19 @@ struct H2Prod {
     uint32_t wv;                            // this lane's scale word (lane_word, loaded by the caller)
     u32x4 v[SETS][U][2];                    // register sets (raw fp32 bits)
     __device__ __forceinline__ void init() { scale = h2_scale(wave_max_u32(wv)); }
-    __device__ __forceinline__ H2Prod(const MpLayerP &P, const BlockRow &B, uint32_t words) {
+    // rows rs .. rs + rn - 1 of zin (the block's bonds, or its atoms in atom-message mode)
+    __device__ __forceinline__ H2Prod(const MpLayerP &P, int rs0, int rn, uint32_t words) {
         const int t = threadIdx.x & 255;
         r0 = t >> 2; u = t & 3;
-        rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(P.zin + (size_t)B.bs * P.kp), 0, B.bn * P.kp * 4,
+        rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(P.zin + (size_t)rs0 * P.kp), 0, rn * P.kp * 4,
                                                0x00020000);
 #pragma unroll
         for (int i = 0; i < U; ++i) {
             const int r = r0 + 64 * i;
-            grow[i] = r < B.bn ? B.bs + r : 0;
+            grow[i] = r < rn ? rs0 + r : 0;
             off[i] = (r * P.kp + 8 * u) * 4;
         }
-        live16 = (B.bn + 15) & ~15;
+        live16 = (rn + 15) & ~15;
         slope = AACT == ACT_PRELU ? P.slope[0] : 0.f;
         wv = words;
         scale = 1.f;
@@ -210,49 +220,66 @@ constexpr int MP_THREADS = 512;
 // registers: with <= 128 VGPRs two layer workgroups co-reside on a CU -- one's epilogue beside the
 // other's GEMM when batches are in flight on two streams); the residual rows are loaded when the
 // epilogue starts and land behind the atom sums.
-template <int BN, int NT, bool LAST>
+template <int BN, int NT, bool LAST, bool ATOM = false>
 struct MpEpilogue {
     static constexpr int BM = BLK_BONDS, LDC = BN + 4;
     static constexpr int UPR = BN / 8, UNITS = BM * UPR, UPT = (UNITS + NT - 1) / NT;  // 8-column units
     static constexpr int AUNITS = BLK_ATOMS * UPR, AUPT = (AUNITS + NT - 1) / NT;
     static constexpr int LDS_FLOATS = (BM + BLK_ATOMS) * LDC;  // P tile, then the atom sums
-    EllRow aell[AUPT];
-    int32_t rv[UPT];
-    uint32_t sa[UPT];
+    static constexpr int YPT = ATOM ? AUPT : UPT;              // units of M_t per thread (rows: atoms | bonds)
+    EllRow aell[AUPT];               // bond mode: the atom gather; atom mode: the a2a neighbour lists
+    EllRow gell[ATOM && LAST ? AUPT : 1];  // atom mode, last layer: the final aggregate's lists
+    int32_t rv[ATOM ? 1 : UPT];
+    uint32_t sa[ATOM ? 1 : UPT];
 
-    // during the GEMM: the atom gather rows of this thread's atom units (unit v = tid + NT i: atom v / UPR)
-    // and the source / reverse ids of its bond units (unit v: row v / UPR) -- loads only, no arithmetic on
-    // what they return (that would wait for them inside the GEMM)
+    // during the GEMM: the gather rows of this thread's atom units (unit v = tid + NT i: atom v / UPR) and,
+    // in bond mode, the source / reverse ids of its bond units (unit v: row v / UPR) -- loads only, no
+    // arithmetic on what they return (that would wait for them inside the GEMM)
     __device__ __forceinline__ void prefetch(const MpLayerP &P, const BlockRow &B) {
         const int tid = threadIdx.x;
 #pragma unroll
         for (int i = 0; i < AUPT; ++i) {
             const int v = tid + NT * i;
+            const bool ok = v < AUNITS && v / UPR < B.an;
             aell[i] = ell_zero();
-            if (v < AUNITS && v / UPR < B.an) aell[i] = ell_load(P.aell_idx, P.aell_coef, (size_t)B.as + v / UPR);
-        }
-#pragma unroll
-        for (int i = 0; i < UPT; ++i) {
-            const int v = tid + NT * i, lr = v / UPR;
-            rv[i] = 0;
-            sa[i] = 0;
-            if (v < UNITS && lr < B.bn) {
-                rv[i] = P.rev[B.bs + lr];
-                sa[i] = P.src_blk[B.bs + lr];
+            if (ok) aell[i] = ATOM ? ell_load(P.mell_idx, P.mell_coef, (size_t)B.as + v / UPR)
+                                   : ell_load(P.aell_idx, P.aell_coef, (size_t)B.as + v / UPR);
+            if constexpr (ATOM && LAST) {
+                gell[i] = ell_zero();
+                if (ok) gell[i] = ell_load(P.aell_idx, P.aell_coef, (size_t)B.as + v / UPR);
             }
         }
+        if constexpr (!ATOM)
+#pragma unroll
+            for (int i = 0; i < UPT; ++i) {
+                const int v = tid + NT * i, lr = v / UPR;
+                rv[i] = 0;
+                sa[i] = 0;
+                if (v < UNITS && lr < B.bn) {
+                    rv[i] = P.rev[B.bs + lr];
+                    sa[i] = P.src_blk[B.bs + lr];
+                }
+            }
     }
 
-    // A[la][c..c+7] = sum over the atom's in-bonds (ELL slots, then the CSR rest) of w * T[bond]
-    __device__ __forceinline__ void atom_sum(const MpLayerP &P, const BlockRow &B, const EllRow &E, int la, int c,
-                                             const float *T, float4 &s0, float4 &s1) {
+    // s = sum over the row's entries (ELL slots, then the CSR rest: natural ids, base = the block's first
+    // row of the gathered kind; entries below it -- the atom-message pad slot -- skipped) of w * T[entry][c .. c + 7]
+    __device__ __forceinline__ void row_sum(const int32_t *ptr, const int32_t *idx, const float *coef, int row, int base,
+                                            const EllRow &E, int c, const float *T, float4 &s0, float4 &s1) {
         s0 = s1 = f4zero();
 #pragma unroll
         for (int k = 0; k < ELLW; ++k)
             if (E.w[k] != 0.f) lds_term<LDC>(T, ell_idx(E, k), c, E.w[k], s0, s1);
         if (ell_more(E))
-            for (int q = P.aptr[B.as + la] + ELLW; q < P.aptr[B.as + la + 1]; ++q)
-                lds_term<LDC>(T, P.aidx[q] - B.bs, c, P.acoef ? P.acoef[q] : 1.0f, s0, s1);
+            for (int q = ptr[row] + ELLW; q < ptr[row + 1]; ++q) {
+                const int li = idx[q] - base;
+                if (li >= 0) lds_term<LDC>(T, li, c, coef ? coef[q] : 1.0f, s0, s1);
+            }
+    }
+    // A[la][c..c+7] = sum over the atom's in-bonds of w * T[bond] (bond mode's atom gather)
+    __device__ __forceinline__ void atom_sum(const MpLayerP &P, const BlockRow &B, const EllRow &E, int la, int c,
+                                             const float *T, float4 &s0, float4 &s1) {
+        row_sum(P.aptr, P.aidx, P.acoef, B.as + la, ATOM ? B.as : B.bs, E, c, T, s0, s1);
     }
 
     // Pt: the P tile [BM][LDC] fp32 in LDS (every write of it done and synchronised); At = Pt + BM * LDC
@@ -260,68 +287,83 @@ struct MpEpilogue {
     __device__ __forceinline__ void run(const MpLayerP &P, const BlockRow &B, int blk, int n0, float *Pt) {
         const int tid = threadIdx.x;
         float *At = Pt + BM * LDC;
-        // residual rows (mpn.py:123 input): issued now, consumed after the atom sums
-        float4 res[UPT][2];
+        // message rows of this block: bonds, or atoms in atom-message mode
+        const int rs = ATOM ? B.as : B.bs, rn = ATOM ? B.an : B.bn;
+        constexpr int NU = ATOM ? AUNITS : UNITS, PT = ATOM ? AUPT : UPT;
+        // residual rows (mpn.py:123 input): issued now, consumed after the gathers
+        float4 res[PT][2];
 #pragma unroll
-        for (int i = 0; i < UPT; ++i) {
+        for (int i = 0; i < PT; ++i) {
             const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
             res[i][0] = res[i][1] = f4zero();
-            if (v < UNITS && lr < B.bn) {
-                const float *s = P.inp + (size_t)(B.bs + lr) * P.kp + n0 + c;
+            if (v < NU && lr < rn) {
+                const float *s = P.inp + (size_t)(rs + lr) * P.kp + n0 + c;
                 res[i][0] = ld4(s);
                 res[i][1] = ld4(s + 4);
             }
         }
-        if (P.undirected) {  // P <- (P + P[rev]) / 2, one thread per reverse pair (the lower row)
+        if constexpr (!ATOM) {
+            if (P.undirected) {  // P <- (P + P[rev]) / 2, one thread per reverse pair (the lower row)
 #pragma unroll
-            for (int i = 0; i < UPT; ++i) {
-                const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
-                const int rl = rv[i] - B.bs;
-                if (v < UNITS && lr < B.bn && lr < rl) {
-                    float4 p0 = ld4(Pt + lr * LDC + c), p1 = ld4(Pt + lr * LDC + c + 4);
-                    const float4 q0 = ld4(Pt + rl * LDC + c), q1 = ld4(Pt + rl * LDC + c + 4);
-                    p0.x = (p0.x + q0.x) / 2.0f; p0.y = (p0.y + q0.y) / 2.0f;
-                    p0.z = (p0.z + q0.z) / 2.0f; p0.w = (p0.w + q0.w) / 2.0f;
-                    p1.x = (p1.x + q1.x) / 2.0f; p1.y = (p1.y + q1.y) / 2.0f;
-                    p1.z = (p1.z + q1.z) / 2.0f; p1.w = (p1.w + q1.w) / 2.0f;
-                    st4(Pt + lr * LDC + c, p0); st4(Pt + lr * LDC + c + 4, p1);
-                    st4(Pt + rl * LDC + c, p0); st4(Pt + rl * LDC + c + 4, p1);
+                for (int i = 0; i < UPT; ++i) {
+                    const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
+                    const int rl = rv[i] - B.bs;
+                    if (v < UNITS && lr < B.bn && lr < rl) {
+                        float4 p0 = ld4(Pt + lr * LDC + c), p1 = ld4(Pt + lr * LDC + c + 4);
+                        const float4 q0 = ld4(Pt + rl * LDC + c), q1 = ld4(Pt + rl * LDC + c + 4);
+                        p0.x = (p0.x + q0.x) / 2.0f; p0.y = (p0.y + q0.y) / 2.0f;
+                        p0.z = (p0.z + q0.z) / 2.0f; p0.w = (p0.w + q0.w) / 2.0f;
+                        p1.x = (p1.x + q1.x) / 2.0f; p1.y = (p1.y + q1.y) / 2.0f;
+                        p1.z = (p1.z + q1.z) / 2.0f; p1.w = (p1.w + q1.w) / 2.0f;
+                        st4(Pt + lr * LDC + c, p0); st4(Pt + lr * LDC + c + 4, p1);
+                        st4(Pt + rl * LDC + c, p0); st4(Pt + rl * LDC + c + 4, p1);
+                    }
                 }
+                __syncthreads();
+            }
+            wd_stamp(4 + 8 * LAST);
+            // A[a] = sum_{b into a} w_b P[b] (mpn.py:112-118)
+#pragma unroll
+            for (int i = 0; i < AUPT; ++i) {
+                const int v = tid + NT * i, la = v / UPR, c = 8 * (v % UPR);
+                if (v >= AUNITS || la >= B.an) break;
+                float4 s0, s1;
+                atom_sum(P, B, aell[i], la, c, Pt, s0, s1);
+                st4(At + la * LDC + c, s0);
+                st4(At + la * LDC + c + 4, s1);
             }
             __syncthreads();
+            wd_stamp(5 + 8 * LAST);
         }
-        wd_stamp(4 + 8 * LAST);
-        // A[a] = sum_{b into a} w_b P[b] (mpn.py:112-118)
-#pragma unroll
-        for (int i = 0; i < AUPT; ++i) {
-            const int v = tid + NT * i, la = v / UPR, c = 8 * (v % UPR);
-            if (v >= AUNITS || la >= B.an) break;
-            float4 s0, s1;
-            atom_sum(P, B, aell[i], la, c, Pt, s0, s1);
-            st4(At + la * LDC + c, s0);
-            st4(At + la * LDC + c + 4, s1);
-        }
-        __syncthreads();
-        wd_stamp(5 + 8 * LAST);
         const float slope = ACT == ACT_PRELU ? P.slope[0] : 0.f;
-        float4 ym[LAST ? UPT : 1][2];  // LAST: this thread's M_t units until P is dead
+        float4 ym[LAST ? YPT : 1][2];  // LAST: this thread's M_t units until P is dead
         // Z_t rows of this block (the training forward's save in the last layer)
         float *zr = LAST ? P.zsave : P.zout;
-        const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc(zr ? (void *)(zr + (size_t)B.bs * P.kp) : (void *)P.inp, 0,
+        const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc(zr ? (void *)(zr + (size_t)rs * P.kp) : (void *)P.inp, 0,
                                                                             BM * P.kp * 4, 0x00020000);
         uint32_t mx = 0;               // max |dropout(act(Z_t))| of this thread's units (not LAST)
 #pragma unroll
-        for (int i = 0; i < UPT; ++i) {
+        for (int i = 0; i < PT; ++i) {
             const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
-            if (v >= UNITS) break;
+            if (v >= NU) break;
             float4 y0 = f4zero(), y1 = f4zero();
-            if (lr < B.bn) {
-                const int b = B.bs + lr, rl = rv[i] - B.bs, a = (int)sa[i];
-                // X[b] = A[src(b)] - P[rev(b)] (mpn.py:119-120)
-                const float4 a0 = ld4(At + a * LDC + c), a1 = ld4(At + a * LDC + c + 4);
-                const float4 q0 = ld4(Pt + rl * LDC + c), q1 = ld4(Pt + rl * LDC + c + 4);
-                float z[8] = {a0.x - q0.x, a0.y - q0.y, a0.z - q0.z, a0.w - q0.w,
-                              a1.x - q1.x, a1.y - q1.y, a1.z - q1.z, a1.w - q1.w};
+            if (lr < rn) {
+                const int b = rs + lr;
+                float z[8];
+                if constexpr (ATOM) {
+                    // X[a] = sum_{a' in nbr(a)} P[a'] (mpn.py:104-108, the W_h[:, :H] part; the bond-feature
+                    // part is in the residual)
+                    float4 s0, s1;
+                    row_sum(P.mptr, P.midx, P.mcoef, b, B.as, aell[i], c, Pt, s0, s1);
+                    z[0] = s0.x; z[1] = s0.y; z[2] = s0.z; z[3] = s0.w; z[4] = s1.x; z[5] = s1.y; z[6] = s1.z; z[7] = s1.w;
+                } else {
+                    const int rl = rv[i] - B.bs, a = (int)sa[i];
+                    // X[b] = A[src(b)] - P[rev(b)] (mpn.py:119-120)
+                    const float4 a0 = ld4(At + a * LDC + c), a1 = ld4(At + a * LDC + c + 4);
+                    const float4 q0 = ld4(Pt + rl * LDC + c), q1 = ld4(Pt + rl * LDC + c + 4);
+                    z[0] = a0.x - q0.x; z[1] = a0.y - q0.y; z[2] = a0.z - q0.z; z[3] = a0.w - q0.w;
+                    z[4] = a1.x - q1.x; z[5] = a1.y - q1.y; z[6] = a1.z - q1.z; z[7] = a1.w - q1.w;
+                }
                 float4 b0 = f4zero(), b1 = f4zero();
                 if (P.bias) { b0 = ld4(P.bias + n0 + c); b1 = ld4(P.bias + n0 + c + 4); }
                 const float r8[8] = {res[i][0].x, res[i][0].y, res[i][0].z, res[i][0].w,
@@ -329,7 +371,7 @@ struct MpEpilogue {
                 const float b8[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
                 for (int q = 0; q < 8; ++q) z[q] = r8[q] + (z[q] + b8[q]);  // mpn.py:122-123
-                if (zr) {  // (16-byte buffer stores, write-through: 8-byte atomic stores cost 4 us per launch)
+                if (zr) {  // (16-byte buffer stores)
                     const int o = (lr * P.kp + n0 + c) * 4;
                     __builtin_amdgcn_raw_buffer_store_b128(u32x4{__float_as_uint(z[0]), __float_as_uint(z[1]),
                                                                  __float_as_uint(z[2]), __float_as_uint(z[3])}, zrs, o, 0, WD_ZWT);
@@ -360,21 +402,23 @@ struct MpEpilogue {
             __syncthreads();  // every read of P done: M_t replaces it
             float *Mt = Pt;
 #pragma unroll
-            for (int i = 0; i < UPT; ++i) {
+            for (int i = 0; i < PT; ++i) {
                 const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
-                if (v >= UNITS) break;
+                if (v >= NU) break;
                 st4(Mt + lr * LDC + c, ym[i][0]);
                 st4(Mt + lr * LDC + c + 4, ym[i][1]);
             }
             __syncthreads();
-            // atom aggregate of this column tile: A[a] = sum_{b into a} w_b M_t[b] (mpn.py:126-131)
+            // atom aggregate of this column tile: A[a] = sum_{x into a} w M_t[x] (mpn.py:126-131; x: the
+            // atom's in-bonds, or its a2a neighbours in atom-message mode)
             const __amdgpu_buffer_rsrc_t ars = x6_block_rsrc<BLK_ATOMS>(P.aplanes, P.kp, blk);
 #pragma unroll
             for (int i = 0; i < AUPT; ++i) {
                 const int v = tid + NT * i, la = v / UPR, c = 8 * (v % UPR);
                 if (v >= AUNITS || la >= B.an) break;  // rows past the block's atoms are never loaded
                 float4 s0, s1;
-                atom_sum(P, B, aell[i], la, c, Mt, s0, s1);
+                if constexpr (ATOM) atom_sum(P, B, gell[i], la, c, Mt, s0, s1);
+                else atom_sum(P, B, aell[i], la, c, Mt, s0, s1);
                 x6_store8_blk<BLK_ATOMS>(ars, la, n0 + c, s0, s1);
                 if (P.asave) {
                     float *ar = P.asave + (size_t)(B.as + la) * P.kp + n0 + c;
@@ -391,12 +435,12 @@ struct MpEpilogue {
 // then overwrites P with M_t (held in registers across a barrier) for the atom aggregate.
 // ACT: the activation (one instantiation each: the staging of M_{t-1} and the epilogue fold it to
 // straight-line code).
-template <int BN, bool LAST, int ACT>
+template <int BN, bool LAST, int ACT, bool ATOM = false>
 // (__launch_bounds__ min 4 waves per SIMD: <= 128 VGPRs, so that two layer workgroups -- batches in flight
 // on two streams -- co-reside on a CU)
 __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpLayerP> MP) {
     constexpr int BM = BLK_BONDS;
-    constexpr int EPI_BYTES = MpEpilogue<BN, MP_THREADS, LAST>::LDS_FLOATS * 4;  // P tile + the atom sums
+    constexpr int EPI_BYTES = MpEpilogue<BN, MP_THREADS, LAST, ATOM>::LDS_FLOATS * 4;  // P tile + the atom sums
     constexpr int STG_BYTES = h2_lds_bytes<BM, BN>();
     constexpr int LDS_BYTES = EPI_BYTES > STG_BYTES ? EPI_BYTES : STG_BYTES;
     static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU");
@@ -406,16 +450,17 @@ __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpL
     const MpLayerP &P = multi_pick(MP, xcd_tile(blockIdx.x, gridDim.x), tile);
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
-    MpEpilogue<BN, MP_THREADS, LAST> E;
+    MpEpilogue<BN, MP_THREADS, LAST, ATOM> E;
     float *Pt = reinterpret_cast<float *>(lds);
     // the block's scale words of M_{t-1} (<= 64, one per lane) and W_h's: loaded before the GEMM's first
     // loads, reduced by the producers before their first stage and by the consumers after the GEMM
     const uint32_t wv = lane_word(P.amax_in + (size_t)blk * P.amax_in_n, P.amax_in_n);
     const uint32_t whm = *P.wh_amax;
-    H2Prod<BM, ACT> ap(P, B, wv);
+    const int rs = ATOM ? B.as : B.bs, rn = ATOM ? B.an : B.bn;  // the block's message rows
+    H2Prod<BM, ACT> ap(P, rs, rn, wv);
     wd_stamp(1 + 8 * LAST);
     floatx4 acc[BM / 64][BN / 16];
-    h2_mainloop_ws<BM, BN>(P.wh + (size_t)nt * (P.kp >> 5) * (2 * BN * 64), P.kp >> 5, B.bn, lds, acc, ap);
+    h2_mainloop_ws<BM, BN>(P.wh + (size_t)nt * (P.kp >> 5) * (2 * BN * 64), P.kp >> 5, rn, lds, acc, ap);
     // the epilogue's gather lists and ids: loaded now, not during the GEMM (live across the GEMM loop
     // they pushed the consumers' accumulators and fragments past 128 VGPRs)
     wd_stamp(2 + 8 * LAST);

@@ -441,9 +441,10 @@ __global__ __launch_bounds__(256) void pack_kernel(PackJobs J) {
 // scale when the input layer ran as a GEMM instead of the embed)
 template <int ACT>
 __global__ __launch_bounds__(256) void absmax_blocks_kernel(const float *x, int ld, int cols, const int32_t *blocks,
-                                                            const float *slope_p, uint32_t *out) {
+                                                            const float *slope_p, uint32_t *out, int atom_rows) {
     const float slope = ACT == ACT_PRELU ? slope_p[0] : 0.f;
-    const int bs = blocks[8 * blockIdx.x], bn = blocks[8 * blockIdx.x + 1];
+    // the block's bond rows (or its atom rows: atom-message mode)
+    const int bs = blocks[8 * blockIdx.x + 2 * atom_rows], bn = blocks[8 * blockIdx.x + 1 + 2 * atom_rows];
     const int c4 = cols / 4;
     uint32_t mx = 0;
     for (int t = threadIdx.x; t < bn * c4; t += blockDim.x) {

@@ -117,9 +117,16 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     // (an embed-capable graph -- categorical codes -- needs no feature planes)
     const bool codes = g->atom_codes && g->bond_src_blk && g->bond_tail && D.Fb <= WO_MAXK && D.Fa <= WO_MAXK;
     // (Hk <= 2560: at most 64 column tiles of 40 per block, the h2 scale words' capacity)
-    D.blocked = D.x6 && !D.desc && D.T >= 2 && D.Hk <= 2560 && g->n_blocks > 0 && g->blocks && g->bond_blk_row &&
-                (codes || (g->f_atoms_blk_x6 && g->f_bonds_x6)) && g->bond_src_blk && g->b2revb &&
-                g->atom_ell_idx && g->atom_ell_coef;
+    const bool blk_common = !D.desc && D.T >= 2 && D.Hk <= 2560 && g->n_blocks > 0 && g->blocks &&
+                            g->atom_ell_idx && g->atom_ell_coef;
+    // atom-message mode (inference): the a2a gather's pad slots read atom 0, whose message is act(b_i) and
+    // later act(b_i + W_h(...)) -- zero without biases, so the block-local lists drop them; with biases,
+    // or for training, the unblocked path runs
+    const bool atom_blk = D.atom && !D.f32 && !D.save && !D.undirected && !p->b_i && !p->b_h && g->f_atoms_x6 &&
+                          g->f_atoms_blk_x6 && g->bond_feat_gather.ptr && g->msg_ell_idx && g->msg_ell_coef &&
+                          g->msg_gather.ptr && D.Fbk == 32;
+    D.blocked = blk_common && (atom_blk || (D.x6 && g->bond_blk_row && (codes || (g->f_atoms_blk_x6 && g->f_bonds_x6)) &&
+                                            g->bond_src_blk && g->b2revb));
     D.nblk = D.blocked ? g->n_blocks : 0;
     if (D.atom && D.undirected)
         return fail(WD_ERR_UNSUPPORTED, "undirected with atom_messages (the reference indexes atom messages "
@@ -485,6 +492,8 @@ struct FwdLayout {
     size_t Zb[2] = {0, 0}, Ab = 0;  // D.blocked inference: Z_t fp32 rows (ping-pong); A as blocked plane tiles
     size_t amax[2] = {0, 0};        // D.blocked: h2 scale words of M_t, ping-pong [nblk][tiles] (planes.hpp)
     size_t Eo = 0;                  // D.blocked: f_atoms W_o[:, :Fa]^T per blocked atom row (compact codes)
+    size_t Fs = 0, Res = 0;         // D.blocked atom-message mode: per atom the sum of its in-bonds' features
+                                    // [Vap][Fbk], and the layers' residual inp + Fs W_h[:, H:]^T [Vap][Hk]
     bool own_pack = false;
 };
 
@@ -510,6 +519,10 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
         for (int i = 0; i < 2; ++i) L.amax[i] = take((size_t)D.nblk * 64 * 4);  // (<= 64 tiles per block)
         L.Ab = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 6);
         L.Eo = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 4);
+        if (D.atom) {
+            L.Fs = take((size_t)D.Vap * D.Fbk * 4);
+            L.Res = take(msg);
+        }
     } else if (D.x6) {
         if (D.T > 1) L.Xp = take((size_t)D.Rp * D.Hk * 6);
         L.Ap = take((size_t)D.Vap * D.Hk * 6);
@@ -688,6 +701,7 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
     const bool codes = fused_codes(jobs[0].g, D0);
     for (int j = 1; j < n; ++j)
         if (fused_codes(jobs[j].g, jobs[j].D) != codes || jobs[j].D.Hk != Hk || jobs[j].D.T != D0.T ||
+            jobs[j].D.atom != D0.atom ||
             jobs[j].D.Fa != D0.Fa || jobs[j].D.Fb != D0.Fb || jobs[j].D.save != D0.save)
             return fail(WD_ERR_UNSUPPORTED, "fused forward: batches of one launch differ in layout");
     // h2 scale words of M_t (written by the embed for t = 0, by layer t after): [nblk][tiles of the producer]
@@ -723,14 +737,26 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
         for (int j = 0; j < n; ++j) {
             const FusedJob &J = jobs[j];
             // inp only: the first layer stages M_0 = act(inp) itself
-            Epi e = epi_act(ACT_IDENTITY, nullptr, W(PL.bi), nullptr, F(J, J.L.Z[0]), nullptr, Hk, c, 0);
+            Epi e = epi_act(ACT_IDENTITY, nullptr, p->b_i ? W(PL.bi) : nullptr, nullptr, F(J, J.L.Z[0]), nullptr, Hk, c, 0);
             if (!x6g_eligible(e)) return fail(WD_ERR_SHAPE, "fused forward: unaligned buffers");
-            WD_TRY(gemm_x6g(J.g->f_bonds_x6, J.g->ld_bonds, J.D.Kink, nullptr, 0, 0, pk + PL.WiX, J.D.Rp, Hk, e, st));
+            if (J.D.atom)  // inp = f_atoms W_i^T (mpn.py:93)
+                WD_TRY(gemm_x6g(J.g->f_atoms_x6, J.g->ld_atoms, J.D.Kink, nullptr, 0, 0, pk + PL.WiX, J.D.Rp, Hk, e, st));
+            else
+                WD_TRY(gemm_x6g(J.g->f_bonds_x6, J.g->ld_bonds, J.D.Kink, nullptr, 0, 0, pk + PL.WiX, J.D.Rp, Hk, e, st));
             host_with_act(c->activation, [&](auto act_c) {
                 hipLaunchKernelGGL(absmax_blocks_kernel<decltype(act_c)::value>, dim3(J.D.nblk), dim3(256), 0, st,
-                                   (const float *)F(J, J.L.Z[0]), Hk, Hk, J.g->blocks, p->prelu, slot(J, 0));
+                                   (const float *)F(J, J.L.Z[0]), Hk, Hk, J.g->blocks, p->prelu, slot(J, 0), (int)J.D.atom);
             });
             WD_CHECK_LAUNCH("absmax");
+            if (J.D.atom) {
+                // the bond-feature half of every layer's W_h (mpn.py:105-107), the same in each layer: per atom
+                // Fs = sum of its in-bonds' feature rows, Res = inp + Fs W_h[:, H:]^T -- the layers' residual
+                WD_TRY(gather8(J.g->f_bonds, J.g->ld_bonds, J.D.Fbk, J.g->bond_feat_gather, nullptr, F(J, J.L.Fs), J.D.Fbk,
+                               nullptr, 0, 0, J.D.R, J.D.Rp, st));
+                WD_TRY(gemm_nt(F(J, J.L.Fs), J.D.Fbk, J.D.Fbk, nullptr, 0, 0, W(PL.Wh) + Hk, J.D.ldx, J.D.Rp, Hk,
+                               epi_act(ACT_IDENTITY, nullptr, nullptr, F(J, J.L.Z[0]), nullptr, F(J, J.L.Res), Hk, c, 0),
+                               st, true));
+            }
         }
     }
     const int T = D0.T;
@@ -751,8 +777,10 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
             Q.amax_out = last ? nullptr : slot(J, t);
             Q.kp = Hk;
             Q.wh = (const uint8_t *)(pk + PL.WhH); Q.wh_amax = (const uint32_t *)(pk + PL.amax) + 64;
-            Q.inp = F(J, J.L.Z[0]);
+            Q.inp = J.D.atom ? F(J, J.L.Res) : F(J, J.L.Z[0]);
             Q.bias = p->b_h ? W(PL.bh) : nullptr;
+            Q.mell_idx = g->msg_ell_idx; Q.mell_coef = g->msg_ell_coef;
+            Q.mptr = g->msg_gather.ptr; Q.midx = g->msg_gather.idx; Q.mcoef = g->msg_gather.coef;
             Q.blocks = g->blocks;
             Q.rev = g->b2revb; Q.src_blk = g->bond_src_blk; Q.undirected = J.D.undirected;
             Q.act = c->activation; Q.slope = p->prelu; Q.p_drop = c->dropout; Q.seed = c->seed; Q.layer = t;
@@ -769,8 +797,11 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
             constexpr int BN = decltype(bn_c)::value;
             constexpr bool LAST = decltype(last_c)::value;
             host_with_act(c->activation, [&](auto act_c) {
-                hipLaunchKernelGGL((mp_layer_kernel<BN, LAST, decltype(act_c)::value>), dim3(grid), dim3(MP_THREADS), 0,
-                                   st, M);
+                constexpr int A = decltype(act_c)::value;
+                if (D0.atom)
+                    hipLaunchKernelGGL((mp_layer_kernel<BN, LAST, A, true>), dim3(grid), dim3(MP_THREADS), 0, st, M);
+                else
+                    hipLaunchKernelGGL((mp_layer_kernel<BN, LAST, A, false>), dim3(grid), dim3(MP_THREADS), 0, st, M);
             });
         };
         using I80 = std::integral_constant<int, 80>;

@@ -302,6 +302,51 @@ def test_blocked_fused_forward(kind, b, hidden, depth, extra):
     assert golden_io.normwise(out.cpu().numpy(), ref.numpy()) <= TOL
 
 
+def _runs_blocked(enc, g):
+    """True when the native forward of ``enc`` on ``g`` takes the molecule-blocked fused path: its
+    workspace (fwd_layout) differs from the same graph's with the blocks withheld."""
+    import ctypes
+    from chemprop_amd import _native
+    dg = g.device_graph(DEV, enc.atom_messages, enc.bond_fdim)
+    gs = enc._graph_struct(dg)
+    cfg = enc._config(False)
+    params = tuple(t.detach().float() if t is not None else None for t in enc._param_tuple())
+    pstruct, _ = enc._packed_params(gs, cfg, params, DEV)
+    sizes = []
+    for nb in (gs.n_blocks, 0):
+        g2 = _native.WdGraph.from_buffer_copy(gs)
+        g2.n_blocks = nb
+        n = ctypes.c_size_t()
+        _native.check(_native.lib().wdmpnn_workspace_bytes(ctypes.byref(g2), ctypes.byref(pstruct), ctypes.byref(cfg),
+                                                           ctypes.byref(n)), 'workspace')
+        sizes.append(n.value)
+    return sizes[0] != sizes[1]
+
+
+@pytest.mark.parametrize('kind,b,hidden,depth,extra', [
+    ('polymer', 64, 300, 3, {}),                                        # the bench's atom_messages secondary
+    ('qm9', 32, 64, 2, dict(activation='tanh')),
+    ('zinc', 24, 128, 4, dict(activation='PReLU')),
+    ('polymer', 8, 96, 3, dict(activation='ELU', aggregation='sum')),
+])
+def test_blocked_atom_messages_forward(kind, b, hidden, depth, extra):
+    """atom_messages=True without biases runs the molecule-blocked fused layers (a2a neighbour sums in the
+    layer epilogue, the bond-feature half of W_h folded into the residual) and matches the fp32 oracle at
+    1e-5 normwise; with a bias the same batch falls back to the unblocked path, also at 1e-5."""
+    for bias in (False, True):
+        args = TrainArgs(hidden_size=hidden, depth=depth, atom_messages=True, bias=bias, **extra)
+        g = BatchMolGraph(synthetic.make_batch(kind, b, 900 + b))
+        enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim(atom_messages=True))
+        synthetic.fill_parameters(enc, 21)
+        p = {n: t.detach().clone() for n, t in enc.named_parameters()}
+        ref = mpn_ref.encoder_forward(p, g, args)
+        enc = enc.to(DEV).eval()
+        assert _runs_blocked(enc, g) == (not bias)
+        with torch.no_grad():
+            out = enc(g)
+        assert golden_io.normwise(out.cpu().numpy(), ref.numpy()) <= TOL
+
+
 def test_blocked_forward_edge_cases_and_fallback():
     """Empty / single-atom molecules in blocks, and a 130-leaf hub molecule that exceeds a block (the
     forward falls back to the unblocked plane-tile path)."""
