@@ -239,7 +239,7 @@ def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_b
                                      '(BatchMolGraph(block_target=1))'}}
 
 
-def unblocked_workload(device, steps=50, warmup=5):
+def atom_messages_workload(device, steps=50, warmup=5):
     """The reference's ``atom_messages`` mode (mpn.py:47-53, 93-94, 104-108, 126-128) on the bench's polymer
     batches (B = 64, depth 3, hidden 300, the reference's default bias=False): the molecule-blocked fused
     layers over atom rows (a2a neighbour sums in the layer epilogue), eval forward, one in flight."""
@@ -650,7 +650,7 @@ def main():
             log('[bench] secondary workloads (qm9, zinc, training step)')
             line['secondary'] = [secondary_workload(device, 'qm9', 64, 3, 300, 200),
                                  secondary_workload(device, 'zinc', 512, 5, 512, 30),
-                                 training_workload(device), unblocked_workload(device)]
+                                 training_workload(device), atom_messages_workload(device)]
         if not a.no_cpu and world == 1:  # the CPU leg is timed at N=1 only
             log(f'[bench] CPU baseline (~{a.cpu_seconds:.0f} s + a one-thread sample)')
             cpu = cpu_baseline(TrainArgs(hidden_size=H, depth=a.depth, device=torch.device('cpu')), graphs[0],

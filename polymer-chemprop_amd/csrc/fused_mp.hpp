@@ -80,7 +80,10 @@ struct MpLayerP {
                                 // GEMM operand is M_{t-1} = dropout(act(Z_{t-1})) (mpn.py:97, 123-124), formed
                                 // while staging
     const uint32_t *amax_in;    // its scale words (planes.hpp h2): [nblk][amax_in_n] maxima of |M_{t-1}|,
-    int amax_in_n;              // published per (block, tile) by the embed or by layer t - 1
+    int amax_in_n;              // published per (block, tile) by the embed or by layer t - 1; amax_rt > 0:
+    int amax_rt;                //   per (amax_rt-row tile of zin, column tile) by the input GEMM (gemm_x6g's
+                                //   Epi.amax): the words of the row tiles the block's rows overlap
+    int ldz, ldr;               // row strides of zin and of the residual inp (Hk, or wider for column slices)
     float p_drop_in;            // the dropout of M_{t-1} (0 for M_0: mpn.py:97 drops nothing)
     float *zout;                // Z_t, same layout (null in the last layer)
     uint32_t *amax_out;         // [nblk][n_tiles]: max |dropout(act(Z_t))| of each workgroup (not the last layer)
@@ -139,13 +142,13 @@ struct H2Prod {
     __device__ __forceinline__ H2Prod(const MpLayerP &P, int rs0, int rn, uint32_t words) {
         const int t = threadIdx.x & 255;
         r0 = t >> 2; u = t & 3;
-        rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(P.zin + (size_t)rs0 * P.kp), 0, rn * P.kp * 4,
-                                               0x00020000);
+        rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(P.zin + (size_t)rs0 * P.ldz), 0,
+                                               rn > 0 ? ((rn - 1) * P.ldz + P.kp) * 4 : 0, 0x00020000);
 #pragma unroll
         for (int i = 0; i < U; ++i) {
             const int r = r0 + 64 * i;
             grow[i] = r < rn ? rs0 + r : 0;
-            off[i] = (r * P.kp + 8 * u) * 4;
+            off[i] = (r * P.ldz + 8 * u) * 4;
         }
         live16 = (rn + 15) & ~15;
         slope = AACT == ACT_PRELU ? P.slope[0] : 0.f;
@@ -297,7 +300,7 @@ struct MpEpilogue {
             const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
             res[i][0] = res[i][1] = f4zero();
             if (v < NU && lr < rn) {
-                const float *s = P.inp + (size_t)(rs + lr) * P.kp + n0 + c;
+                const float *s = P.inp + (size_t)(rs + lr) * P.ldr + n0 + c;
                 res[i][0] = ld4(s);
                 res[i][1] = ld4(s + 4);
             }
@@ -452,11 +455,17 @@ __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpL
     const BlockRow B = load_block(P.blocks, blk);
     MpEpilogue<BN, MP_THREADS, LAST, ATOM> E;
     float *Pt = reinterpret_cast<float *>(lds);
+    const int rs = ATOM ? B.as : B.bs, rn = ATOM ? B.an : B.bn;  // the block's message rows
     // the block's scale words of M_{t-1} (<= 64, one per lane) and W_h's: loaded before the GEMM's first
     // loads, reduced by the producers before their first stage and by the consumers after the GEMM
-    const uint32_t wv = lane_word(P.amax_in + (size_t)blk * P.amax_in_n, P.amax_in_n);
+    int w0 = blk * P.amax_in_n, wn = P.amax_in_n;
+    if (P.amax_rt > 0) {  // (the row tiles of the block's rows)
+        const int t0 = rs / P.amax_rt, t1 = (rs + max(rn, 1) - 1) / P.amax_rt;
+        w0 = t0 * P.amax_in_n;
+        wn = (t1 - t0 + 1) * P.amax_in_n;
+    }
+    const uint32_t wv = lane_word(P.amax_in + w0, wn);
     const uint32_t whm = *P.wh_amax;
-    const int rs = ATOM ? B.as : B.bs, rn = ATOM ? B.an : B.bn;  // the block's message rows
     H2Prod<BM, ACT> ap(P, rs, rn, wv);
     wd_stamp(1 + 8 * LAST);
     floatx4 acc[BM / 64][BN / 16];
@@ -467,7 +476,7 @@ __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpL
     E.prefetch(P, B);
     __syncthreads();
     wd_stamp(3 + 8 * LAST);
-    const float ia = h2_inv_scale(wave_max_u32(wv));
+    const float ia = h2_inv_scale(wave_max_u32(wv));  // (the producers' scale)
     const float iw = h2_inv_scale(whm);
     if (threadIdx.x < 256) x6_acc_to_lds_scaled<BM, BN, 4, 1>(acc, Pt, ia, iw);  // (the consumer waves hold the tile)
     __syncthreads();
@@ -502,7 +511,7 @@ struct EmbedP {
     const uint16_t *tail;        // per natural bond row: bond columns as bits
     const float *wt;             // W_i^T [>= Fb][Hk] (fp32, packed)
     const float *woat;           // W_o[:, :Fa]^T [>= Fa][Hk] (fp32, packed)
-    float *eo;                   // [nblk * 64][Hk]
+    float *eo;                   // [atom rows][Hk] (natural rows)
     const float *bias;           // b_i (padded) or null
     const int32_t *blocks;
     int Fa, Fb, Hk, n_tiles;
@@ -576,7 +585,7 @@ __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP> MP) {
     // Eo[a] = sum_{c in code(a)} W_o[:, c] + last(a) W_o[:, Fa-1] (the f_atoms half of W_o)
     for (int v = tid; v < B.an * C4; v += NT) {
         const int la = v / C4, c = 4 * (v % C4);
-        st4(P.eo + ((size_t)blk * BLK_ATOMS + la) * P.Hk + n0 + c, code_sum<BN>(code[la], wt, P.Fa, c));
+        st4(P.eo + (size_t)(B.as + la) * P.Hk + n0 + c, code_sum<BN>(code[la], wt, P.Fa, c));
     }
     __syncthreads();  // every read of the W_o tile done
 #pragma unroll
@@ -634,10 +643,11 @@ struct WoReadoutP {
     int act; const float *slope; float p_drop; uint64_t seed; uint32_t layer;
     float *out; int ncols;                   // out [B][ncols] (ncols = H)
     int n_tiles;
-    // categorical codes (kca = 0): the f_atoms half of [f_atoms | A] W_o^T, precomputed per atom by
-    // embed_kernel as sums of W_o columns: fp32 [nblk * 64][Hk], blocked atom rows (null: GEMM segment)
+    // kca = 0: the f_atoms half of [f_atoms | A] W_o^T, precomputed per atom (by embed_kernel as sums of
+    // W_o columns, or by the atom-message input GEMM): fp32 natural atom rows, row stride ldeo (null: GEMM
+    // segment)
     const float *eo;
-    int Hk;
+    int Hk, ldeo;
     float *zosave;  // training forward or null: the W_o pre-activation (mpn.py:133) as fp32 natural atom rows [Vap][Hk]
 };
 
@@ -693,7 +703,7 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
 #pragma unroll
         for (int j = 0; j < EPU; ++j) {
             const int v = tid + NT * j, la = v / C4, c = 4 * (v % C4);
-            eo[j] = P.eo && v < BM * C4 && la < B.an ? ld4(P.eo + ((size_t)blk * BM + la) * P.Hk + n0 + c) : f4zero();
+            eo[j] = P.eo && v < BM * C4 && la < B.an ? ld4(P.eo + (size_t)(B.as + la) * P.ldeo + n0 + c) : f4zero();
         }
         if (tid < nm) {
             mstart = P.mol_start[B.ml + tid];

@@ -49,6 +49,11 @@ struct Epi {
     int res_init;
     int rows_valid;        // rows >= rows_valid get dZ = 0
     float *prelu_part;     // per-workgroup PReLU slope partial (indexed by blockIdx.x) or null
+    // EPI_ACT, gemm_x6g only: per (64-row tile, 64-column tile) the max |amax_act(z)| of the output columns
+    // < amax_cols -> amax[row tile * amax_cols / 64 + column tile] (the h2 scale words of a fused layer's
+    // first operand, planes.hpp; slope: PReLU's)
+    uint32_t *amax;
+    int amax_cols, amax_act;
 };
 
 template <int ACT, int TM, int TN>
@@ -123,13 +128,17 @@ struct EpiPrefetch {
     }
 };
 
+// returns this thread's max |amax_act(z)| (Epi.amax; 0 without)
 template <int ACT, int BM, int BN, int NT>
-__device__ __forceinline__ void epilogue_v4_act(const Epi &E, const float *C, int ldc, int m0, int n0, int M, int N,
-                                                const EpiPrefetch<BM, BN, NT> &ep) {
+__device__ __forceinline__ uint32_t epilogue_v4_act(const Epi &E, const float *C, int ldc, int m0, int n0, int M, int N,
+                                                    const EpiPrefetch<BM, BN, NT> &ep) {
     using EP = EpiPrefetch<BM, BN, NT>;
     const int t = threadIdx.x, cl = (t % EP::C4) * 4, j = n0 + cl;
-    if (j >= N) return;
+    uint32_t mx = 0;
+    if (j >= N) return mx;
     const float slope = (E.kind == EPI_ACT && E.act == ACT_PRELU) ? E.slope[0] : 0.f;
+    const bool amx = E.kind == EPI_ACT && E.amax && j < E.amax_cols;
+    const float aslope = amx && E.amax_act == ACT_PRELU ? E.slope[0] : 0.f;
 #pragma unroll
     for (int p = 0; p < EP::NP; ++p) {
         const int rl = t / EP::C4 + p * EP::RS, i = m0 + rl;
@@ -148,6 +157,7 @@ __device__ __forceinline__ void epilogue_v4_act(const Epi &E, const float *C, in
                 float y = act_fwd(ACT, z[q], slope);
                 if (E.p_drop > 0.f) y *= dropout_scale(E.seed, E.layer, i, j + q, E.p_drop);
                 out[q] = y;
+                if (amx) mx = max(mx, absbits(act_fwd(E.amax_act, z[q], aslope)));
             }
             if (j + 4 <= N) {
                 if (E.Z) st4(E.Z + o, make_float4(z[0], z[1], z[2], z[3]));
@@ -176,6 +186,7 @@ __device__ __forceinline__ void epilogue_v4_act(const Epi &E, const float *C, in
             }
         }
     }
+    return mx;
 }
 
 
@@ -242,14 +253,16 @@ __device__ __forceinline__ void epilogue(const Epi &E, floatx16 (&acc)[TM][TN], 
         epilogue_act<ACT_IDENTITY>(E, acc, i0, j0, h, l32, M, N, Y);
 }
 template <int BM, int BN, int NT>
-__device__ __forceinline__ void epilogue_v4(const Epi &E, const float *C, int ldc, int m0, int n0, int M, int N,
-                                            const EpiPrefetch<BM, BN, NT> &ep) {
+__device__ __forceinline__ uint32_t epilogue_v4(const Epi &E, const float *C, int ldc, int m0, int n0, int M, int N,
+                                                const EpiPrefetch<BM, BN, NT> &ep) {
+    uint32_t mx = 0;
     if (E.kind == EPI_ACT)
-        with_act(E.act, [&](auto a) { epilogue_v4_act<decltype(a)::value>(E, C, ldc, m0, n0, M, N, ep); });
+        with_act(E.act, [&](auto a) { mx = epilogue_v4_act<decltype(a)::value>(E, C, ldc, m0, n0, M, N, ep); });
     else if (E.kind == EPI_ACTBWD)
         with_act(E.act, [&](auto a) { epilogue_v4_actbwd<decltype(a)::value, BM, BN, NT>(E, C, ldc, m0, n0, M, N); });
     else
-        epilogue_v4_act<ACT_IDENTITY>(E, C, ldc, m0, n0, M, N, ep);
+        mx = epilogue_v4_act<ACT_IDENTITY>(E, C, ldc, m0, n0, M, N, ep);
+    return mx;
 }
 
 template <int BM, int BN, int WM, int WN>

@@ -870,7 +870,11 @@ __global__ __launch_bounds__(512) void gemm_x6g_kernel(X6PParams P) {
     float *cl = reinterpret_cast<float *>(lds);
     x6_acc_to_lds<BM, 64, 4, 2>(acc, cl);
     __syncthreads();
-    epilogue_v4<BM, X6_BN, NT>(P.epi, cl, 68, m0, n0, P.M, P.N, ep);
+    const uint32_t mx = epilogue_v4<BM, X6_BN, NT>(P.epi, cl, 68, m0, n0, P.M, P.N, ep);
+    if (P.epi.kind == EPI_ACT && P.epi.amax && n0 < P.epi.amax_cols) {  // (workgroup-uniform)
+        __shared__ uint32_t red[NT / 64];
+        publish_max(mx, P.epi.amax + (size_t)mt * (P.epi.amax_cols / X6_BN) + nt, red);
+    }
 }
 
 }  // namespace wd

@@ -409,6 +409,7 @@ struct PackJob {
     int transpose, nrows, nseg;
     int dc0[2], sc0[2], K[2];
     uint32_t *amax;  // or null: max |dst| of workgroup x -> amax[x] (the h2 scale of split_h2_kernel)
+    const float *src1; int ld_src1;  // or null: segment 1's source (plain jobs; else every segment reads src)
 };
 struct PackJobs { PackJob j[16]; int n; };
 
@@ -424,7 +425,10 @@ __global__ __launch_bounds__(256) void pack_kernel(PackJobs J) {
                 if (c < P.K[0]) v = P.src[(size_t)c * P.ld_src + P.sc0[0] + r];
             } else {
                 for (int s = 0; s < P.nseg; ++s)
-                    if (c >= P.dc0[s] && c < P.dc0[s] + P.K[s]) v = P.src[(size_t)r * P.ld_src + P.sc0[s] + c - P.dc0[s]];
+                    if (c >= P.dc0[s] && c < P.dc0[s] + P.K[s]) {
+                        const bool one = s == 1 && P.src1;
+                        v = (one ? P.src1 : P.src)[(size_t)r * (one ? P.ld_src1 : P.ld_src) + P.sc0[s] + c - P.dc0[s]];
+                    }
             }
         }
         P.dst[t] = v;

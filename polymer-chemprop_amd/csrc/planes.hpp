@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void split_tiles_kernel(const float *__restric
 // Several dense splits in one launch (blockIdx.y = job; BR 64 or 80 per job): the weight packing of
 // a training forward splits five small matrices, and five launches cost more than the work.
 struct SplitJob { const float *src; uint8_t *dst; int ld, rows, kp, br; };
-struct SplitJobs { SplitJob j[5]; int n; };
+struct SplitJobs { SplitJob j[6]; int n; };
 
 __global__ __launch_bounds__(256) void split_tiles_batch_kernel(SplitJobs J) {
     const SplitJob S = J.j[blockIdx.y];

@@ -122,7 +122,8 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     // atom-message mode (inference): the a2a gather's pad slots read atom 0, whose message is act(b_i) and
     // later act(b_i + W_h(...)) -- zero without biases, so the block-local lists drop them; with biases,
     // or for training, the unblocked path runs
-    const bool atom_blk = D.atom && !D.f32 && !D.save && !D.undirected && !p->b_i && !p->b_h && g->f_atoms_x6 &&
+    const bool atom_blk = D.atom && !D.f32 && !D.save && !D.undirected && !p->b_i && !p->b_h && D.Hk <= 2048 &&
+                          g->f_atoms_x6 &&
                           g->f_atoms_blk_x6 && g->bond_feat_gather.ptr && g->msg_ell_idx && g->msg_ell_coef &&
                           g->msg_gather.ptr && D.Fbk == 32;
     D.blocked = blk_common && (atom_blk || (D.x6 && g->bond_blk_row && (codes || (g->f_atoms_blk_x6 && g->f_bonds_x6)) &&
@@ -157,6 +158,9 @@ struct PackLayout {
                                        // (the categorical-code embedding of the fused forward)
     size_t WhH = 0;                    // h2 plane tiles of W_h (fused layers; BN-row blocks, BN = fused_bn)
     size_t amax = 0;                   // W_h's h2 scale: pack_kernel's 64 per-workgroup maxima + their max (u32)
+    // atom-message mode: the fused forward's input GEMM [f_atoms | Fs] B^T with B [3 Hk][Fak + Fbk] =
+    // [[W_i, 0], [W_i, W_h[:, H:]], [W_o[:, :Fa], 0]] -> inp | inp + Fs W_h[:, H:]^T | f_atoms W_o[:, :Fa]^T
+    size_t WiA = 0, WiAX = 0;          // fp32, and its bf16x3 plane tiles (64-row blocks)
 };
 
 // column tile of the fused kernels: 80 when it divides Hk (Hk = 320: 4 tiles, one workgroup per CU at the
@@ -186,6 +190,10 @@ PackLayout pack_layout(const Dims &D) {
     }
     L.WhH = take((size_t)D.Hk * D.Hk);  // 2 fp16 per value
     L.amax = take(65);
+    if (D.atom) {
+        L.WiA = take((size_t)3 * D.Hk * (D.Fak + D.Fbk));
+        L.WiAX = take((size_t)3 * D.Hk * (D.Fak + D.Fbk) * 3 / 2);
+    }
     if (D.desc) {
         L.Wd = take((size_t)D.Hdk * D.Kd);
         L.bd = take(D.Hdk);
@@ -237,6 +245,15 @@ int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
     // weight columns as rows for the categorical-code embedding (fused_mp.hpp embed_kernel / wo_readout)
     add(job_transpose(F(L.WiT), D.Kink, D.Hk, p->W_i, D.Kin, 0, D.Kin, H));
     add(job_transpose(F(L.WoaT), D.Fak, D.Hk, p->W_o, D.Fa + H, 0, D.Fa, H));
+    if (D.atom) {
+        const int Kc = D.Fak + D.Fbk;
+        const size_t band = (size_t)D.Hk * Kc;
+        add(job_plain(F(L.WiA), D.Hk, Kc, p->W_i, D.Fa, H, {{0, 0, D.Fa}}));
+        PackJob b1 = job_plain(F(L.WiA) + band, D.Hk, Kc, p->W_i, D.Fa, H, {{0, 0, D.Fa}, {D.Fak, H, D.Fb}});
+        b1.src1 = p->W_h; b1.ld_src1 = H + D.Fb;
+        add(b1);
+        add(job_plain(F(L.WiA) + 2 * band, D.Hk, Kc, p->W_o, D.Fa + H, H, {{0, 0, D.Fa}}));
+    }
     if (D.desc) {
         add(job_plain(F(L.Wd), D.Hdk, D.Kd, p->W_d, D.Hd, D.Hd, {{0, 0, H}, {D.Hk, H, D.d}}));
         add(job_plain(F(L.bd), 1, D.Hdk, p->b_d, D.Hd, 1, {{0, 0, D.Hd}}));
@@ -257,7 +274,12 @@ int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
         split(L.Wh, L.WhX80, D.ldx, 80);
         split(L.Wo, L.WoX80, D.Ko, 80);
     }
-    const int kmax = std::max(D.Kink, std::max(D.ldx, D.Ko));
+    int kmax = std::max(D.Kink, std::max(D.ldx, D.Ko));
+    if (D.atom) {
+        X.j[X.n++] = SplitJob{(const float *)(base + L.WiA), (uint8_t *)(base + L.WiAX), D.Fak + D.Fbk, 3 * D.Hk,
+                              D.Fak + D.Fbk, 64};
+        kmax = std::max(kmax, D.Fak + D.Fbk);
+    }
     hipLaunchKernelGGL(split_tiles_batch_kernel, dim3(ew_blocks((size_t)D.Hk * kmax / 8), X.n), dim3(256), 0, st, X);
     WD_CHECK_LAUNCH("pack_params planes");
     // fp16 hi / lo tiles of W_h[:, :Hk] for the fused layers, scaled by its published maximum
@@ -492,8 +514,9 @@ struct FwdLayout {
     size_t Zb[2] = {0, 0}, Ab = 0;  // D.blocked inference: Z_t fp32 rows (ping-pong); A as blocked plane tiles
     size_t amax[2] = {0, 0};        // D.blocked: h2 scale words of M_t, ping-pong [nblk][tiles] (planes.hpp)
     size_t Eo = 0;                  // D.blocked: f_atoms W_o[:, :Fa]^T per blocked atom row (compact codes)
-    size_t Fs = 0, Res = 0;         // D.blocked atom-message mode: per atom the sum of its in-bonds' features
-                                    // [Vap][Fbk], and the layers' residual inp + Fs W_h[:, H:]^T [Vap][Hk]
+    size_t Fs = 0, In3 = 0;         // D.blocked atom-message mode: per atom the sum of its in-bonds' features
+                                    // (plane tiles [Vap][Fbk]), and the input GEMM's [Vap][3 Hk] output
+                                    // inp | inp + Fs W_h[:, H:]^T (the layers' residual) | Eo
     bool own_pack = false;
 };
 
@@ -516,12 +539,15 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
         // forward writes L.Z[t] instead)
         if (!D.save)
             for (int i = 0; i < 2 && i < D.T - 2; ++i) L.Zb[1 - i] = take(msg);
-        for (int i = 0; i < 2; ++i) L.amax[i] = take((size_t)D.nblk * 64 * 4);  // (<= 64 tiles per block)
+        // (<= 64 tiles per block; the atom-message input GEMM: one word per 64 x 64 tile of inp)
+        const size_t words = std::max((size_t)D.nblk * 64, (size_t)(D.Rp / 64) * (D.Hk / 64));
+        for (int i = 0; i < 2; ++i) L.amax[i] = take(words * 4);
         L.Ab = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 6);
-        L.Eo = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 4);
         if (D.atom) {
-            L.Fs = take((size_t)D.Vap * D.Fbk * 4);
-            L.Res = take(msg);
+            L.Fs = take((size_t)D.Vap * D.Fbk * 6);
+            L.In3 = take((size_t)D.Rp * 3 * D.Hk * 4);
+        } else {
+            L.Eo = take((size_t)D.Vap * D.Hk * 4);
         }
     } else if (D.x6) {
         if (D.T > 1) L.Xp = take((size_t)D.Rp * D.Hk * 6);
@@ -736,27 +762,31 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
     } else {
         for (int j = 0; j < n; ++j) {
             const FusedJob &J = jobs[j];
+            if (J.D.atom) {
+                // atom messages: per atom Fs = the sum of its in-bonds' feature rows (mpn.py:105-107, as plane
+                // tiles), then ONE GEMM [f_atoms | Fs] [[W_i, 0], [W_i, W_h[:, H:]], [W_o[:, :Fa], 0]]^T ->
+                // inp (mpn.py:93) | inp + Fs W_h[:, H:]^T (every layer's residual: the bond-feature half of
+                // W_h is the same in each layer) | f_atoms W_o[:, :Fa]^T (the f_atoms half of W_o), whose
+                // epilogue also publishes the first layer's h2 scale words per 64 x 64 tile of inp
+                WD_TRY(gather8(J.g->f_bonds, J.g->ld_bonds, J.D.Fbk, J.g->bond_feat_gather, nullptr, nullptr, 0,
+                               J.ws + J.L.Fs, J.D.Fbk, 0, J.D.R, J.D.Rp, st));
+                Epi e = epi_act(ACT_IDENTITY, nullptr, nullptr, nullptr, nullptr, F(J, J.L.In3), 3 * Hk, c, 0);
+                e.amax = slot(J, 0); e.amax_cols = Hk; e.amax_act = c->activation; e.slope = p->prelu;
+                if (!x6g_eligible(e)) return fail(WD_ERR_SHAPE, "fused forward: unaligned buffers");
+                WD_TRY(gemm_x6g(J.g->f_atoms_x6, J.g->ld_atoms, J.D.Fak, J.ws + J.L.Fs, J.D.Fbk, J.D.Fbk, pk + PL.WiAX,
+                                J.D.Rp, 3 * Hk, e, st));
+                continue;
+            }
             // inp only: the first layer stages M_0 = act(inp) itself
-            Epi e = epi_act(ACT_IDENTITY, nullptr, p->b_i ? W(PL.bi) : nullptr, nullptr, F(J, J.L.Z[0]), nullptr, Hk, c, 0);
+            Epi e = epi_act(ACT_IDENTITY, nullptr, W(PL.bi), nullptr, F(J, J.L.Z[0]), nullptr, Hk, c, 0);
             if (!x6g_eligible(e)) return fail(WD_ERR_SHAPE, "fused forward: unaligned buffers");
-            if (J.D.atom)  // inp = f_atoms W_i^T (mpn.py:93)
-                WD_TRY(gemm_x6g(J.g->f_atoms_x6, J.g->ld_atoms, J.D.Kink, nullptr, 0, 0, pk + PL.WiX, J.D.Rp, Hk, e, st));
-            else
-                WD_TRY(gemm_x6g(J.g->f_bonds_x6, J.g->ld_bonds, J.D.Kink, nullptr, 0, 0, pk + PL.WiX, J.D.Rp, Hk, e, st));
+            WD_TRY(gemm_x6g(J.g->f_bonds_x6, J.g->ld_bonds, J.D.Kink, nullptr, 0, 0, pk + PL.WiX, J.D.Rp, Hk, e, st));
             host_with_act(c->activation, [&](auto act_c) {
                 hipLaunchKernelGGL(absmax_blocks_kernel<decltype(act_c)::value>, dim3(J.D.nblk), dim3(256), 0, st,
-                                   (const float *)F(J, J.L.Z[0]), Hk, Hk, J.g->blocks, p->prelu, slot(J, 0), (int)J.D.atom);
+                                   (const float *)F(J, J.L.Z[0]), Hk, Hk, J.g->blocks, p->prelu, slot(J, 0), 0);
             });
             WD_CHECK_LAUNCH("absmax");
-            if (J.D.atom) {
-                // the bond-feature half of every layer's W_h (mpn.py:105-107), the same in each layer: per atom
-                // Fs = sum of its in-bonds' feature rows, Res = inp + Fs W_h[:, H:]^T -- the layers' residual
-                WD_TRY(gather8(J.g->f_bonds, J.g->ld_bonds, J.D.Fbk, J.g->bond_feat_gather, nullptr, F(J, J.L.Fs), J.D.Fbk,
-                               nullptr, 0, 0, J.D.R, J.D.Rp, st));
-                WD_TRY(gemm_nt(F(J, J.L.Fs), J.D.Fbk, J.D.Fbk, nullptr, 0, 0, W(PL.Wh) + Hk, J.D.ldx, J.D.Rp, Hk,
-                               epi_act(ACT_IDENTITY, nullptr, nullptr, F(J, J.L.Z[0]), nullptr, F(J, J.L.Res), Hk, c, 0),
-                               st, true));
-            }
+
         }
     }
     const int T = D0.T;
@@ -769,15 +799,19 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
             // Z_{t-1} in, Z_t out (the last layer: none): a training forward keeps every Z_t (L.Z), inference
             // ping-pongs two buffers after inp
             auto zbuf = [&](int k) { return k == 0 || J.D.save ? F(J, J.L.Z[k]) : F(J, J.L.Zb[k & 1]); };
-            Q.zin = zbuf(t - 1);
+            const bool a3 = J.D.atom && t == 1;  // (the atom-message input GEMM's inp columns)
+            Q.zin = a3 ? F(J, J.L.In3) : zbuf(t - 1);
+            Q.ldz = a3 ? 3 * Hk : Hk;
             Q.amax_in = slot(J, t - 1);
-            Q.amax_in_n = t > 1 ? Hk / BNf : (codes ? embed_tiles : 1);
+            Q.amax_in_n = t > 1 ? Hk / BNf : (codes ? embed_tiles : (J.D.atom ? Hk / 64 : 1));
+            Q.amax_rt = a3 ? 64 : 0;
             Q.p_drop_in = t - 1 == 0 ? 0.f : c->dropout;
             Q.zout = last ? nullptr : zbuf(t);
             Q.amax_out = last ? nullptr : slot(J, t);
             Q.kp = Hk;
             Q.wh = (const uint8_t *)(pk + PL.WhH); Q.wh_amax = (const uint32_t *)(pk + PL.amax) + 64;
-            Q.inp = J.D.atom ? F(J, J.L.Res) : F(J, J.L.Z[0]);
+            Q.inp = J.D.atom ? F(J, J.L.In3) + Hk : F(J, J.L.Z[0]);
+            Q.ldr = J.D.atom ? 3 * Hk : Hk;
             Q.bias = p->b_h ? W(PL.bh) : nullptr;
             Q.mell_idx = g->msg_ell_idx; Q.mell_coef = g->msg_ell_coef;
             Q.mptr = g->msg_gather.ptr; Q.midx = g->msg_gather.idx; Q.mcoef = g->msg_gather.coef;
@@ -820,8 +854,9 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
         // segment's non-null base)
         R.fa = g->f_atoms_blk_x6 ? (const uint8_t *)g->f_atoms_blk_x6 : (const uint8_t *)(J.ws + J.L.Ab);
         R.kpa = g->ld_atoms; R.kcw = J.D.Fak / 32;
-        R.kca = codes ? 0 : R.kcw;
-        R.eo = codes ? F(J, J.L.Eo) : nullptr; R.Hk = Hk;
+        R.kca = codes || J.D.atom ? 0 : R.kcw;
+        R.eo = codes ? F(J, J.L.Eo) : (J.D.atom ? F(J, J.L.In3) + 2 * Hk : nullptr); R.Hk = Hk;
+        R.ldeo = J.D.atom ? 3 * Hk : Hk;
         R.ag = (const uint8_t *)(J.ws + J.L.Ab); R.kp = Hk;
         R.wo = (const uint8_t *)(pk + (bn80 ? PL.WoX80 : PL.WoX)); R.bias = W(PL.bo);
         R.blocks = g->blocks;
