@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for round in 1 2; do
+for round in ${ROUNDS:-1 2}; do
   for v in "$@"; do
     export WDMPNN_LIB=$PWD/exp/libwdmpnn_$v.so
     timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu --no-secondary --many 0 --stream-graphs 300000 \
