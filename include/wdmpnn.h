@@ -127,10 +127,13 @@ typedef struct WdGraph {
     const void *f_atoms_blk_x6;
     /* Required with blocks: the first WDMPNN_ELL_WIDTH (W = 8) entries of every msg_gather / atom_gather
      * row in block-local ELL form, so that the fused kernels prefetch a row's list with independent
-     * loads during the GEMM instead of a ptr -> idx chain after it.  *_ell_idx[W r + k] = idx -
-     * bond_start of the row's block (uint8, < 128), *_ell_coef[W r + k] = coef; unused slots coef 0 and
-     * a valid index; bit 7 of slot W - 1 set when the row has more than W entries (the rest are read
-     * from the CSR lists). */
+     * loads during the GEMM instead of a ptr -> idx chain after it.  *_ell_idx[W r + k] = idx - the
+     * first row of the gathered kind in the row's block (bond_start for bond rows; atom_start in
+     * atom-message mode, whose gathers read atom rows), uint8 < 128, *_ell_coef[W r + k] = coef; unused
+     * slots coef 0 and a valid index; bit 7 of slot W - 1 set when the row has more than W entries (the
+     * rest are read from the CSR lists).  Atom-message mode: msg_ell lists only the real a2a entries (the
+     * pad slots' atom 0 is dropped; the fused path runs bias-free models only, whose pad messages are 0),
+     * and the CSR rest of a longer row skips entries outside the block. */
     const uint8_t *msg_ell_idx;
     const float *msg_ell_coef;
     const uint8_t *atom_ell_idx;
