@@ -756,6 +756,10 @@ __global__ __launch_bounds__(256) void head_rows_kernel(WdHead P) {
     const int Hf = P.Hf, T = P.T;
     float *h = P.a + (size_t)row * Hf;
     const float *tab = P.table + (size_t)row * P.ld_table;
+    // the row's targets | weights, one per lane, loaded first: the table may be read from pinned host
+    // memory (train.py's zero-copy loss table), whose latency then overlaps the dot products below
+    const bool tlane = 2 * T <= 64;
+    const float tv = tlane && lane < 2 * T ? tab[lane] : 0.f;
     with_act(P.act, [&](auto act_c) {
         constexpr int ACT = decltype(act_c)::value;
         float l = 0.f;
@@ -764,7 +768,8 @@ __global__ __launch_bounds__(256) void head_rows_kernel(WdHead P) {
             float s = 0.f;
             for (int j = lane; j < Hf; j += 64) s = fmaf(w2[j], act_fwd(ACT, h[j], 0.f), s);
             s = wave_sum(s) + (P.b2 ? P.b2[t] : 0.f);
-            const float r = s - tab[t], w = tab[T + t];
+            const float y = tlane ? __shfl(tv, t, 64) : tab[t], w = tlane ? __shfl(tv, T + t, 64) : tab[T + t];
+            const float r = s - y;
             l = fmaf(w * r, r, l);
             const float d = 2.f * w * r * P.inv_n;
             dsh[wave][t] = d;
