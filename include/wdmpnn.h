@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define WDMPNN_ABI_VERSION 7
+#define WDMPNN_ABI_VERSION 8
 #define WDMPNN_ELL_WIDTH 8
 
 enum WdActivation {     /* nn_utils.py:70-99 get_activation_function */
@@ -146,6 +146,11 @@ typedef struct WdGraph {
     const WdAtomCode *atom_codes;
     const uint8_t *bond_src_blk;
     const uint16_t *bond_tail;
+    /* Optional, atom-message mode (ABI 8): per atom row the sum of its in-bonds' feature rows
+     * (bond_feat_gather applied to f_bonds, mpn.py:105-106 summed over the slots: a function of the graph
+     * alone) as bf16x3 plane tiles [rows of f_atoms][ld_bonds], made with the graph's other planes.  NULL:
+     * the fused forward gathers it in one extra launch. */
+    const void *atom_feat_sum_x6;
 } WdGraph;
 
 /* nn.Module parameters of MPNEncoder (mpn.py:17-64); all device pointers, row-major like nn.Linear. */

@@ -552,6 +552,16 @@ class BatchMolGraph:
                   ('b2revb', self._np['b2revb'].astype(np.int32))]
         if dev_bonds:
             arrays.append(('b2a', b2a_p))
+        if atom_messages and feat is not None:
+            # per atom the sum of its in-bonds' feature rows (mpn.py:105-106 summed over the a2b slots): a
+            # function of the graph alone, made here with the feature planes (WdGraph.atom_feat_sum_x6);
+            # fp32, added in slot order -- the gather kernel's order
+            fs = np.zeros((fa_p.shape[0], fb_p.shape[1]), np.float32)
+            deg = np.diff(feat.ptr)
+            for k in range(int(deg.max(initial=0))):
+                rows_k = np.nonzero(deg > k)[0]
+                fs[rows_k] += fb_p[feat.idx[feat.ptr[rows_k] + k]]
+            arrays.append(('atom_feat_sum', fs))
         if blocks is not None and len(blocks):
             arrays += [('blocks', blocks), ('bond_blk_row', bond_blk), ('atom_blk_row', atom_blk)]
             bstart = np.zeros(len(blocks) + 1, np.int64)  # first row of the gathered kind per block (-1: row 0)
@@ -617,7 +627,10 @@ class BatchMolGraph:
         s.atom_messages = int(bool(atom_messages))
         if device.type == 'cuda':  # bf16x3 plane tiles of the features for the split GEMMs (exact copies)
             L = _native.lib()
-            for name, rows, ld in (('f_atoms', fa_p.shape[0], lda), ('f_bonds', rows_b, ldb)):
+            plane_srcs = [('f_atoms', fa_p.shape[0], lda), ('f_bonds', rows_b, ldb)]
+            if 'atom_feat_sum' in offsets:
+                plane_srcs.append(('atom_feat_sum', fa_p.shape[0], ldb))
+            for name, rows, ld in plane_srcs:
                 nbytes = ctypes.c_size_t()
                 _native.check(L.wdmpnn_plane_bytes(rows, ld, ctypes.byref(nbytes)), 'plane bytes')
                 planes = torch.empty(max(nbytes.value, 256), dtype=torch.uint8, device=device)

@@ -768,12 +768,18 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
                 // inp (mpn.py:93) | inp + Fs W_h[:, H:]^T (every layer's residual: the bond-feature half of
                 // W_h is the same in each layer) | f_atoms W_o[:, :Fa]^T (the f_atoms half of W_o), whose
                 // epilogue also publishes the first layer's h2 scale words per 64 x 64 tile of inp
-                WD_TRY(gather8(J.g->f_bonds, J.g->ld_bonds, J.D.Fbk, J.g->bond_feat_gather, nullptr, nullptr, 0,
-                               J.ws + J.L.Fs, J.D.Fbk, 0, J.D.R, J.D.Rp, st));
+                const void *fs = J.g->atom_feat_sum_x6;  // (built with the graph, or gathered here)
+                int kpf = J.g->ld_bonds;
+                if (!fs) {
+                    kpf = J.D.Fbk;
+                    WD_TRY(gather8(J.g->f_bonds, J.g->ld_bonds, J.D.Fbk, J.g->bond_feat_gather, nullptr, nullptr, 0,
+                                   J.ws + J.L.Fs, J.D.Fbk, 0, J.D.R, J.D.Rp, st));
+                    fs = J.ws + J.L.Fs;
+                }
                 Epi e = epi_act(ACT_IDENTITY, nullptr, nullptr, nullptr, nullptr, F(J, J.L.In3), 3 * Hk, c, 0);
                 e.amax = slot(J, 0); e.amax_cols = Hk; e.amax_act = c->activation; e.slope = p->prelu;
                 if (!x6g_eligible(e)) return fail(WD_ERR_SHAPE, "fused forward: unaligned buffers");
-                WD_TRY(gemm_x6g(J.g->f_atoms_x6, J.g->ld_atoms, J.D.Fak, J.ws + J.L.Fs, J.D.Fbk, J.D.Fbk, pk + PL.WiAX,
+                WD_TRY(gemm_x6g(J.g->f_atoms_x6, J.g->ld_atoms, J.D.Fak, fs, kpf, J.D.Fbk, pk + PL.WiAX,
                                 J.D.Rp, 3 * Hk, e, st));
                 continue;
             }

@@ -345,6 +345,15 @@ def test_blocked_atom_messages_forward(kind, b, hidden, depth, extra):
         with torch.no_grad():
             out = enc(g)
         assert golden_io.normwise(out.cpu().numpy(), ref.numpy()) <= TOL
+        if not bias:  # the same forward with the per-atom bond-feature sums gathered in the forward instead
+            dg = g.device_graph(DEV, True, enc.bond_fdim)
+            assert dg.struct.atom_feat_sum_x6
+            dg.struct.atom_feat_sum_x6 = 0
+            dg.encoder_structs.clear()
+            dg.encoder_plans.clear()
+            with torch.no_grad():
+                out2 = enc(g)
+            assert torch.equal(out, out2)
 
 
 def test_blocked_forward_edge_cases_and_fallback():
