@@ -265,6 +265,49 @@ struct MpEpilogue {
             }
     }
 
+    // The same lists handed over through LDS (WD_EPI_PRE): the staging waves, done one chunk before the MFMA
+    // waves, load them for the whole block while the last chunk is multiplied (fill_pre), and every thread
+    // reads its units' rows from LDS after the barrier (take_pre) -- no memory latency after the GEMM.
+    static constexpr int PRE_ELL = BLK_ATOMS * (int)sizeof(EllRow);
+    static constexpr int PRE_BYTES = PRE_ELL * (ATOM && LAST ? 2 : 1) + (ATOM ? 0 : BM * 8);
+    __device__ __forceinline__ void fill_pre(const MpLayerP &P, const BlockRow &B, uint8_t *pre) {
+        const int t = threadIdx.x - MP_THREADS / 2;  // (staging threads 0 .. 255)
+        if (t < BLK_ATOMS) {
+            EllRow e = ell_zero();
+            if (t < B.an) e = ATOM ? ell_load(P.mell_idx, P.mell_coef, (size_t)B.as + t)
+                                   : ell_load(P.aell_idx, P.aell_coef, (size_t)B.as + t);
+            reinterpret_cast<EllRow *>(pre)[t] = e;
+            if constexpr (ATOM && LAST) {
+                EllRow f = ell_zero();
+                if (t < B.an) f = ell_load(P.aell_idx, P.aell_coef, (size_t)B.as + t);
+                reinterpret_cast<EllRow *>(pre + PRE_ELL)[t] = f;
+            }
+        }
+        if constexpr (!ATOM)
+            if (t < BM) {
+                int2 q = make_int2(0, 0);
+                if (t < B.bn) q = make_int2(P.rev[B.bs + t], (int)P.src_blk[B.bs + t]);
+                reinterpret_cast<int2 *>(pre + PRE_ELL)[t] = q;
+            }
+    }
+    __device__ __forceinline__ void take_pre(const BlockRow &B, const uint8_t *pre) {
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < AUPT; ++i) {
+            const int v = tid + NT * i, la = min(v / UPR, BLK_ATOMS - 1);
+            aell[i] = reinterpret_cast<const EllRow *>(pre)[la];
+            if constexpr (ATOM && LAST) gell[i] = reinterpret_cast<const EllRow *>(pre + PRE_ELL)[la];
+        }
+        if constexpr (!ATOM)
+#pragma unroll
+            for (int i = 0; i < UPT; ++i) {
+                const int v = tid + NT * i, lr = min(v / UPR, BM - 1);
+                const int2 q = reinterpret_cast<const int2 *>(pre + PRE_ELL)[lr];
+                rv[i] = q.x;
+                sa[i] = (uint32_t)q.y;
+            }
+    }
+
     // s = sum over the row's entries (ELL slots, then the CSR rest: natural ids, base = the block's first
     // row of the gathered kind; entries below it -- the atom-message pad slot -- skipped) of w * T[entry][c .. c + 7]
     __device__ __forceinline__ void row_sum(const int32_t *ptr, const int32_t *idx, const float *coef, int row, int base,
@@ -470,11 +513,23 @@ __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpL
     wd_stamp(1 + 8 * LAST);
     floatx4 acc[BM / 64][BN / 16];
     h2_mainloop_ws<BM, BN>(P.wh + (size_t)nt * (P.kp >> 5) * (2 * BN * 64), P.kp >> 5, rn, lds, acc, ap);
-    // the epilogue's gather lists and ids: loaded now, not during the GEMM (live across the GEMM loop
-    // they pushed the consumers' accumulators and fragments past 128 VGPRs)
+    // the epilogue's gather lists and ids: not during the GEMM (live across the GEMM loop they pushed the
+    // consumers' accumulators and fragments past 128 VGPRs); the staging waves load them into LDS while the
+    // MFMA waves finish the last chunk
     wd_stamp(2 + 8 * LAST);
-    E.prefetch(P, B);
+#ifndef WD_EPI_PRE
+#define WD_EPI_PRE 1
+#endif
+    using Epi_ = MpEpilogue<BN, MP_THREADS, LAST, ATOM>;
+    __shared__ __attribute__((aligned(16))) uint8_t pre[WD_EPI_PRE ? Epi_::PRE_BYTES : 16];
+    static_assert(LDS_BYTES + (WD_EPI_PRE ? Epi_::PRE_BYTES : 0) + 64 <= 80 * 1024, "two workgroups per CU");
+    if (WD_EPI_PRE) {
+        if (threadIdx.x >= MP_THREADS / 2) E.fill_pre(P, B, pre);
+    } else {
+        E.prefetch(P, B);
+    }
     __syncthreads();
+    if (WD_EPI_PRE) E.take_pre(B, pre);
     wd_stamp(3 + 8 * LAST);
     const float ia = h2_inv_scale(wave_max_u32(wv));  // (the producers' scale)
     const float iw = h2_inv_scale(whm);
