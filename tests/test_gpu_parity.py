@@ -356,6 +356,23 @@ def test_blocked_atom_messages_forward(kind, b, hidden, depth, extra):
             assert torch.equal(out, out2)
 
 
+def test_blocked_atom_messages_edge_cases():
+    """atom_messages=True on the edge-case batch (empty and single-atom molecules, a hub that still fits a
+    block) and on a 130-leaf hub that exceeds a block (unblocked fallback): fp32 oracle at 1e-5."""
+    args = TrainArgs(hidden_size=64, depth=3, atom_messages=True)
+    for leaves in (20, 130):
+        g = BatchMolGraph(synthetic.edge_case_batch(9, star_leaves=leaves))
+        enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim(atom_messages=True))
+        synthetic.fill_parameters(enc, 5)
+        p = {n: t.detach().clone() for n, t in enc.named_parameters()}
+        ref = mpn_ref.encoder_forward(p, g, args)
+        enc = enc.to(DEV).eval()
+        assert _runs_blocked(enc, g) == (leaves == 20)
+        with torch.no_grad():
+            out = enc(g)
+        assert golden_io.normwise(out.cpu().numpy(), ref.numpy()) <= TOL
+
+
 def test_blocked_forward_edge_cases_and_fallback():
     """Empty / single-atom molecules in blocks, and a 130-leaf hub molecule that exceeds a block (the
     forward falls back to the unblocked plane-tile path)."""
