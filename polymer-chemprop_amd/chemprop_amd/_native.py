@@ -206,16 +206,52 @@ def ptr(t) -> int:
 
 
 _HIP = None
+HIP_HOST_MALLOC_MAPPED = 0x2
+HIP_HOST_MALLOC_COHERENT = 0x40000000
+
+
+def _hip():
+    global _HIP
+    if _HIP is None:
+        h = ctypes.CDLL('libamdhip64.so.7')
+        h.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
+        h.hipHostGetDevicePointer.restype = ctypes.c_int
+        h.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+        h.hipHostMalloc.restype = ctypes.c_int
+        h.hipHostFree.argtypes = [ctypes.c_void_p]
+        h.hipHostFree.restype = ctypes.c_int
+        _HIP = h
+    return _HIP
+
+
+class CoherentHostBuffer:
+    """Pinned host memory that GPU kernels read directly (hipHostMalloc mapped + coherent: the device
+    reads it uncached over PCIe, so a host rewrite between two launches is always seen, without the
+    L2-invalidation assumption a non-coherent pinned buffer would need).  ``array`` is a float32 numpy
+    view, ``device_ptr`` its device address."""
+
+    def __init__(self, shape):
+        import numpy as np
+        n = int(np.prod(shape)) * 4
+        h = _hip()
+        p = ctypes.c_void_p()
+        if h.hipHostMalloc(ctypes.byref(p), max(n, 4), HIP_HOST_MALLOC_MAPPED | HIP_HOST_MALLOC_COHERENT) != 0:
+            raise NativeError('hipHostMalloc (mapped, coherent) failed')
+        self._p = p.value
+        self.array = np.ctypeslib.as_array((ctypes.c_float * max(n // 4, 1)).from_address(self._p))[:n // 4]
+        self.array = self.array.reshape(shape)
+        self.device_ptr = host_device_ptr(self._p)
+
+    def __del__(self):
+        if getattr(self, '_p', None) and _HIP is not None:
+            _HIP.hipHostFree(ctypes.c_void_p(self._p))
+            self._p = None
 
 
 def host_device_ptr(p: int) -> int:
     """Device address of pinned host memory at ``p`` (hipHostGetDevicePointer on the HIP runtime torch
     loaded), 0 if that memory is not mapped for the device: a kernel may then read it over PCIe directly."""
-    global _HIP
-    if _HIP is None:
-        _HIP = ctypes.CDLL('libamdhip64.so.7')
-        _HIP.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
-        _HIP.hipHostGetDevicePointer.restype = ctypes.c_int
+    _hip()
     d = ctypes.c_void_p()
     if _HIP.hipHostGetDevicePointer(ctypes.byref(d), ctypes.c_void_p(p), 0) != 0:
         return 0

@@ -81,15 +81,30 @@ def broadcast_parameters(module: nn.Module, src: int = 0) -> None:
 
 
 class GradBucket:
-    """One flat fp32 gradient buffer for all trainable parameters (grads are views into it)."""
+    """One flat fp32 gradient buffer for all trainable parameters (grads are views into it).
 
-    def __init__(self, module: nn.Module):
-        self.params = [p for p in module.parameters() if p.requires_grad]
-        if not self.params:
+    The buffer has two segments: the *early* parameters first (default: a MoleculeModel's FFN head,
+    whose gradients the direct training step has finished before it enqueues the encoder backward),
+    then the rest.  :meth:`start_early` all-reduces the early segment while the encoder backward still
+    runs on the compute stream (RCCL runs the collective on its own stream, ordered after the work
+    enqueued so far); :meth:`start_allreduce` then launches the rest and :meth:`finish_allreduce` waits
+    for both."""
+
+    def __init__(self, module: nn.Module, early: Sequence[nn.Parameter] = None):
+        params = [p for p in module.parameters() if p.requires_grad]
+        if not params:
             raise ValueError('module has no trainable parameters')
+        if early is None:
+            ffn = getattr(module, 'ffn', None)
+            early = list(ffn.parameters()) if isinstance(ffn, nn.Module) else []
+        ids = {id(p) for p in early}
+        self.params = [p for p in params if id(p) in ids] + [p for p in params if id(p) not in ids]
+        self.n_early = sum(p.numel() for p in self.params if id(p) in ids)
         dev = self.params[0].device
         n = sum(p.numel() for p in self.params)
         self.buffer = torch.zeros(n, dtype=torch.float32, device=dev)
+        self._works = []
+        self._early_started = False
         off = 0
         for p in self.params:
             if p.dtype != torch.float32:
@@ -117,27 +132,43 @@ class GradBucket:
             yield self.buffer[off:off + p.numel()].view_as(p)
             off += p.numel()
 
+    @staticmethod
+    def _multi_rank() -> bool:
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+    def _launch(self, seg: torch.Tensor) -> None:
+        if self.buffer.is_cuda and dist.get_backend() == 'gloo':
+            # gloo stages CUDA tensors through host memory; measured on ROCm: without draining the
+            # producing stream first it can read the bucket before the backward kernels have written
+            # it (RCCL orders the collective after the stream's work by itself)
+            torch.cuda.current_stream(self.buffer.device).synchronize()
+        self._works.append(dist.all_reduce(seg, op=dist.ReduceOp.SUM, async_op=True))
+
+    def start_early(self) -> None:
+        """Launch the early segment's all-reduce (async_op) once its gradients are enqueued: on RCCL it
+        overlaps the rest of the backward.  No-op on one rank or without an early segment."""
+        if self.n_early and not self._early_started and self._multi_rank():
+            self._launch(self.buffer[:self.n_early])
+            self._early_started = True
+
     def start_allreduce(self) -> None:
-        """Launch the sum of the bucket over ranks (one collective, async_op) as soon as the backward's last
-        gradient kernel is enqueued; :meth:`finish_allreduce` waits for it (on the stream, not the host,
-        with RCCL) and divides by the world size.  In between the host keeps enqueueing."""
+        """Launch the sum over ranks of what :meth:`start_early` has not launched (async_op) once the
+        backward's last gradient kernel is enqueued; :meth:`finish_allreduce` waits for every launched
+        collective (on the stream, not the host, with RCCL) and divides by the world size."""
         for p, v in zip(self.params, self._views()):
             if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
+                if self._early_started:
+                    raise RuntimeError('a gradient was replaced after its segment was all-reduced')
                 v.copy_(p.grad)  # autograd created a fresh tensor: fold it into the bucket
                 p.grad = v
-        self._work = None
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            if self.buffer.is_cuda and dist.get_backend() == 'gloo':
-                # gloo stages CUDA tensors through host memory; measured on ROCm: without draining the
-                # producing stream first it can read the bucket before the backward kernels have written
-                # it (RCCL orders the collective after the stream's work by itself)
-                torch.cuda.current_stream(self.buffer.device).synchronize()
-            self._work = dist.all_reduce(self.buffer, op=dist.ReduceOp.SUM, async_op=True)
+        if self._multi_rank():
+            self._launch(self.buffer[self.n_early:] if self._early_started else self.buffer)
 
     def finish_allreduce(self) -> None:
-        work, self._work = getattr(self, '_work', None), None
-        if work is not None:
-            work.wait()  # (RCCL: the current stream waits for the collective's stream)
+        works, self._works, self._early_started = self._works, [], False
+        for w in works:
+            w.wait()  # (RCCL: the current stream waits for the collective's stream)
+        if works:
             self.buffer.div_(dist.get_world_size())
 
     def allreduce_mean(self) -> None:

@@ -145,11 +145,14 @@ class DeviceGraph:
             self._streams.add(st.cuda_stream)
 
     def use_on(self, stream) -> None:
-        """Order ``stream`` after the graph's build and keep its memory alive for that stream's work."""
+        """Order ``stream`` after the graph's build and keep its memory alive for that stream's work.
+        (Callers on a hot path test ``sid in dg._streams`` with the raw stream id first: a repeat costs
+        nothing.)"""
         sid = stream.cuda_stream
         if sid in self._streams:
             return
-        stream.wait_event(self.ready)
+        if self.ready is not None and not self.ready.query():  # (a finished build needs no wait)
+            stream.wait_event(self.ready)
         seen = set()
         for t in [self.buffer] + list(self.views.values()):
             base = t.untyped_storage().data_ptr()
@@ -463,10 +466,17 @@ class BatchMolGraph:
         assert info[0], 'staged image larger than its bound'
         return upload_compact(device, host, info, *self._compact_dims)
 
-    def device_graph(self, device, atom_messages: bool = False, bond_fdim: int = None) -> DeviceGraph:
-        """Pack (once per device/mode) into one device buffer; returns the cached DeviceGraph."""
+    def device_graph(self, device, atom_messages: bool = False, bond_fdim: int = None,
+                     atom_blocks: bool = True) -> DeviceGraph:
+        """Pack (once per device/mode) into one device buffer; returns the cached DeviceGraph.
+        ``atom_blocks`` (atom messages only): also build what the molecule-blocked fused atom-message
+        forward reads (blocks, block-local ELL lists, per-atom bond-feature sums).  Only a bias-free
+        inference forward can take that path (wdmpnn.hip get_dims), so the encoder asks for them only
+        then: a training or biased graph skips their host work and upload."""
         device = torch.device(device)
-        key = (str(device), bool(atom_messages), bond_fdim)
+        atom_blocks = bool(atom_blocks) or not atom_messages
+        key = (str(device), bool(atom_messages), bond_fdim) if atom_blocks else \
+            (str(device), True, bond_fdim, 'no_blocks')
         dg = self._device_cache.get(key)
         if dg is not None:
             return dg
@@ -512,7 +522,7 @@ class BatchMolGraph:
             msg, feat = self.bond_message_gather(), None
             msg_rows = self.n_bonds
         agg = self.atom_aggregate_gather(atom_messages)
-        blocks = self.molecule_blocks()
+        blocks = self.molecule_blocks() if atom_blocks else None
         msg_blk = msg
         if atom_messages and blocks is not None and len(blocks):
             # the fused atom-message layers (wdmpnn.hip get_dims: bias-free models only) gather a2a neighbours
@@ -552,7 +562,7 @@ class BatchMolGraph:
                   ('b2revb', self._np['b2revb'].astype(np.int32))]
         if dev_bonds:
             arrays.append(('b2a', b2a_p))
-        if atom_messages and feat is not None:
+        if atom_messages and feat is not None and blocks is not None and len(blocks):
             # per atom the sum of its in-bonds' feature rows (mpn.py:105-106 summed over the a2b slots): a
             # function of the graph alone, made here with the feature planes (WdGraph.atom_feat_sum_x6);
             # fp32, added in slot order -- the gather kernel's order

@@ -180,6 +180,15 @@ class MPNEncoder(nn.Module):
         self._pack_cache = None  # (parameter-version key, packed weight buffer)
         self._gemm_variant = 0  # WdConfig.gemm_variant (0 = split-plane default; 9 = f32-MFMA A/B)
         self._plan_token = object()  # this encoder's key in DeviceGraph.encoder_plans
+        self._infer_configs = {}  # plan key -> WdConfig of the inference call (_infer)
+
+    def __getstate__(self):
+        """Copies (copy.deepcopy, pickle) drop the device-side caches: packed weights, workspaces, plans."""
+        state = self.__dict__.copy()
+        for k in ('_ws_by_stream', '_many_plan'):
+            state.pop(k, None)
+        state.update(_pack_cache=None, _infer_configs={}, _plan_token=object())
+        return state
 
     def _config(self, save: bool) -> _native.WdConfig:
         c = _native.WdConfig()
@@ -209,10 +218,13 @@ class MPNEncoder(nn.Module):
                 None, act._parameters['weight'] if isinstance(act, nn.PReLU) else None)
 
     def _infer(self, mol_graph: BatchMolGraph):
-        """Inference call path (no autograd, no dropout, no descriptors, no profiling hook): the graph
-        struct, config and workspace size are cached per (graph, encoder configuration) in a plan on the
-        DeviceGraph, so a repeated forward costs two allocations and one C-ABI call.  Returns None when
-        the call needs the general path."""
+        """Inference call path (no autograd, no dropout, no descriptors, no profiling hook).  Everything a
+        call derives from the (graph, encoder configuration) pair -- the graph struct, the config, the
+        workspace size -- is a plan cached on the DeviceGraph, the config itself once per encoder, and the
+        workspace is this encoder's per-stream buffer: a repeated forward costs one output allocation and
+        one C-ABI call, and a graph's first forward, or its first on another stream, little more (bench.py
+        times 20 forwards that are mostly such first uses, predict.py:30-40 only first uses).  Returns None
+        when the call needs the general path."""
         d = self.__dict__
         if d.get('_prof') is not None or '_plan_token' not in d or (self.training and self.dropout > 0):
             return None
@@ -222,29 +234,42 @@ class MPNEncoder(nn.Module):
             return None  # the general path raises
         if params[8] is not None and params[8].numel() != 1:
             return None
-        dg = mol_graph.device_graph(device, d['atom_messages'], d['bond_fdim'])
-        stream = torch.cuda.current_stream(device)
-        dg.use_on(stream)
+        dg = mol_graph.device_graph(device, d['atom_messages'], d['bond_fdim'], not d['bias'])
+        sid = _native.current_stream(device)
+        if sid not in dg._streams:
+            dg.use_on(torch.cuda.current_stream(device))
         ckey = (self._plan_token, d['atom_fdim'], d['bond_fdim'], d['hidden_size'], d['depth'], d['undirected'],
                 d['activation'], d['aggregation'], d['aggregation_norm'], d['_gemm_variant'])
         plan = dg.encoder_plans.get(ckey)
         if plan is None:
             gs = self._graph_struct(dg)
-            cfg = self._config(False)
-            params = tuple(_f32(t) for t in params)
-            pstruct, _ = self._packed_params(gs, cfg, params, device, stream=stream)
+            cfg = self._infer_configs.get(ckey)
+            if cfg is None:
+                cfg = self._infer_configs[ckey] = self._config(False)
+            pstruct, _ = self._packed_params(gs, cfg, params, device, sid=sid)
             nbytes = ctypes.c_size_t()
             _native.check(_native.lib().wdmpnn_workspace_bytes(ctypes.byref(gs), ctypes.byref(pstruct),
                                                                ctypes.byref(cfg), ctypes.byref(nbytes)),
                           'MPNEncoder workspace')
             plan = (ctypes.byref(gs), ctypes.byref(cfg), max(nbytes.value, 256), gs.n_mols, gs, cfg)
             dg.encoder_plans[ckey] = plan
-        pstruct, _ = self._packed_params(plan[4], plan[5], params, device, stream=stream)
-        ws = torch.empty(plan[2], dtype=torch.uint8, device=device)
+        pstruct, _ = self._packed_params(plan[4], plan[5], params, device, sid=sid)
+        ws = self._stream_workspace(sid, plan[2], device)
         out = torch.empty((plan[3], d['hidden_size']), dtype=torch.float32, device=device)
         _native.check(_native.lib().wdmpnn_forward(plan[0], ctypes.byref(pstruct), plan[1], ws.data_ptr(), plan[2],
-                                                   out.data_ptr(), stream.cuda_stream), 'MPNEncoder forward')
+                                                   out.data_ptr(), sid), 'MPNEncoder forward')
         return out
+
+    def _stream_workspace(self, sid: int, nbytes: int, device) -> torch.Tensor:
+        """This encoder's inference workspace for the stream ``sid`` (current at the call), grown to the
+        largest request.  Calls on one stream run in order, so they share one buffer safely; each stream has
+        its own (allocated while it is current: the caching allocator ties the block to it)."""
+        wss = self.__dict__.setdefault('_ws_by_stream', {})
+        ws = wss.get(sid)
+        if ws is None or ws.numel() < nbytes:
+            wss[sid] = ws = None  # (the old buffer is released before the larger one is allocated)
+            wss[sid] = ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        return ws
 
     # ---------------------------------------------------------------- direct training step (train.py)
     def _direct_names(self):
@@ -367,7 +392,9 @@ class MPNEncoder(nn.Module):
         if device.type != 'cuda':
             raise RuntimeError('chemprop_amd.MPNEncoder runs on the MI355X HIP path only: move the model to a '
                                'GPU (model.to("cuda"))')
-        dg = mol_graph.device_graph(device, self.atom_messages, self.bond_fdim)
+        # (atom messages: the fused atom-row path's arrays only for a bias-free inference forward)
+        grad = torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in base)
+        dg = mol_graph.device_graph(device, self.atom_messages, self.bond_fdim, not self.bias and not grad)
         dg.use_on(torch.cuda.current_stream(device))
         # descriptors are per call: their struct is never cached
         gs = self._graph_struct(dg) if atom_descriptors_batch is None else self._new_graph_struct(dg)
@@ -415,23 +442,31 @@ class MPNEncoder(nn.Module):
         bypasses both their version counters and ``torch.optim`` (e.g. ``p.data.copy_(...)``)."""
         self._pack_cache = None
 
-    def _packed_params(self, gs, cfg, params, device, cache=True, stream=None, defer=False):
+    def _packed_params(self, gs, cfg, params, device, cache=True, stream=None, defer=False, sid=None):
         """WdParams + the padded weight copies (wdmpnn_pack_params).  Inference caches them per
         (parameter pointer, version counter, optimizer-step generation): fused optimizers update the
         weights without bumping version counters, so every ``Optimizer.step`` also bumps
-        ``_OPT_STEPS``.  A training forward always repacks and leaves no cache behind."""
+        ``_OPT_STEPS``.  A training forward always repacks and leaves no cache behind.  ``sid``: the raw
+        id of the current stream (the inference path's cheaper alternative to ``stream``)."""
         key = (tuple((t.data_ptr(), t._version) if t is not None else None for t in params), _OPT_STEPS[0],
                self._parameters['cached_zero_vector'].data_ptr(), gs.atom_fdim, gs.bond_fdim, gs.desc_dim,
                gs.atom_messages, device) if cache else None
         cached = self._pack_cache if cache else None
         if cached is not None and cached[0] == key:
-            if stream is None:
-                stream = torch.cuda.current_stream(device)
-            if stream.cuda_stream not in cached[4]:  # packed on another stream: order after the pack and
-                stream.wait_event(cached[3])         # keep the buffer alive for this stream's kernels
+            if sid is None:
+                if stream is None:
+                    stream = torch.cuda.current_stream(device)
+                sid = stream.cuda_stream
+            if sid not in cached[4]:  # packed on another stream: order after the pack and keep the buffer
+                if stream is None:    # alive for this stream's kernels
+                    stream = torch.cuda.current_stream(device)
+                if not cached[3].query():
+                    stream.wait_event(cached[3])
                 cached[1].record_stream(stream)
-                cached[4].add(stream.cuda_stream)
+                cached[4].add(sid)
             return cached[2], cached[1]
+        if sid is not None and stream is None:
+            stream = torch.cuda.current_stream(device)
         params = [_f32(t) for t in params]  # also after model.half() / .double(): never pack other dtypes
         p = _native.WdParams()
         p.hidden = self.hidden_size

@@ -172,7 +172,7 @@ def _host_table(rows: np.ndarray, dev: torch.device, zero_copy: bool = False):
     records the event after that kernel's launch (the buffer is refilled only after it)."""
     if dev.type != 'cuda':
         return None if zero_copy else torch.from_numpy(rows).to(dev)
-    key = (dev, rows.shape)
+    key = (dev, rows.shape, zero_copy)
     ring = _PINNED_TABLES.get(key)
     if ring is None:
         ring = _PINNED_TABLES[key] = [0, [None] * _PINNED_RING]
@@ -180,15 +180,23 @@ def _host_table(rows: np.ndarray, dev: torch.device, zero_copy: bool = False):
     ring[0] = (i + 1) % _PINNED_RING
     ent = ring[1][i]
     if ent is None:
-        buf = torch.empty(rows.shape, dtype=torch.float32, pin_memory=True)
         from . import _native
-        ent = ring[1][i] = (buf, torch.cuda.Event(), _native.host_device_ptr(buf.data_ptr()))
+        if zero_copy:
+            # the kernel reads the rows in place: coherent mapped memory (torch's pinned buffers are
+            # non-coherent, and a rewritten slot read again at the same device address would then rely
+            # on the dispatch invalidating stale L2 lines)
+            cb = _native.CoherentHostBuffer(rows.shape)
+            ent = ring[1][i] = (cb, torch.cuda.Event(), cb.device_ptr)
+        else:
+            buf = torch.empty(rows.shape, dtype=torch.float32, pin_memory=True)
+            ent = ring[1][i] = (buf, torch.cuda.Event(), 0)
     else:
         ent[1].synchronize()  # (this buffer's last reader, _PINNED_RING steps ago)
     buf, ev, dptr = ent
-    buf.numpy()[...] = rows
     if zero_copy:
+        buf.array[...] = rows
         return (dptr, ev) if dptr else None
+    buf.numpy()[...] = rows
     table = buf.to(dev, non_blocking=True)
     ev.record(torch.cuda.current_stream(dev))
     return table
@@ -400,7 +408,7 @@ def _all_trainable(mod: nn.Module, skip, ids: list) -> bool:
     return True
 
 
-def _direct_step(model, enc, graph, head, target_batch, target_weights, data_weights) -> torch.Tensor:
+def _direct_step(model, enc, graph, head, target_batch, target_weights, data_weights, bucket=None) -> torch.Tensor:
     """Forward, loss and every gradient of a fused-head step without the autograd engine: the encoder's
     training forward, wdmpnn_head_mse (loss, d loss / d encoding, the head's gradients) and the encoder's
     backward on that gradient (the incoming gradient of the loss is 1), each written straight into the
@@ -440,6 +448,8 @@ def _direct_step(model, enc, graph, head, target_batch, target_weights, data_wei
     _native.check(_native.lib().wdmpnn_head_mse(ctypes.byref(h), _native.current_stream(dev)), 'FFN head + loss')
     if zc is not None:
         zc[1].record(torch.cuda.current_stream(dev))  # (the pinned buffer's last reader)
+    if bucket is not None:  # the head's gradients are enqueued: their all-reduce overlaps the encoder backward
+        bucket.start_early()
     enc._train_backward(state, dx, {n: _grad_buffer(p) for n, p in enc._direct_names()})
     return loss
 
@@ -462,22 +472,23 @@ def train_step(model: nn.Module, mol_batch, target_batch, loss_func: Callable, o
         # every trainable parameter's gradient is overwritten: no zeroing, no autograd
         if bucket is not None:
             bucket.attach()
-        loss = _direct_step(model, enc, mol_batch[0], head, target_batch, target_weights, data_weights)
-    elif bucket is not None:
-        bucket.zero()
+        loss = _direct_step(model, enc, mol_batch[0], head, target_batch, target_weights, data_weights, bucket)
     else:
-        optimizer.zero_grad(set_to_none=True)  # (the optimizer holds every model parameter: build_optimizer)
-    if enc is not None:
-        pass
-    elif head is not None:  # the default regression head: ffn + loss + their gradients as two HIP launches
-        loss = head_loss(model.encoder(mol_batch, features_batch), head, target_batch, target_weights,
-                         data_weights)
-    else:
-        preds = model(mol_batch, features_batch)
-        loss = batch_loss(preds, target_batch, loss_func, dataset_type, target_weights, data_weights)
-    if enc is None:
+        if bucket is not None:
+            bucket.zero()
+        else:
+            optimizer.zero_grad(set_to_none=True)  # (the optimizer holds every model parameter: build_optimizer)
+        if head is not None:  # the default regression head: ffn + loss + their gradients as two HIP launches
+            loss = head_loss(model.encoder(mol_batch, features_batch), head, target_batch, target_weights,
+                             data_weights)
+        else:
+            preds = model(mol_batch, features_batch)
+            loss = batch_loss(preds, target_batch, loss_func, dataset_type, target_weights, data_weights)
         loss.backward()
-    if bucket is not None:  # launched behind the last gradient kernel, waited for before the update
+    if bucket is not None:
+        # the rest of the bucket behind the last gradient kernel (the direct step launched the head's
+        # segment before the encoder backward, so that one overlaps the backward on the GPU); with RCCL
+        # finish_allreduce makes the compute stream, not the host, wait for both before the update
         bucket.start_allreduce()
         bucket.finish_allreduce()
     if grad_clip:

@@ -200,13 +200,16 @@ __device__ __forceinline__ int h2_sexp(uint32_t m) {
 }
 __device__ __forceinline__ float h2_scale(uint32_t m) { return __uint_as_float((uint32_t)h2_sexp(m) << 23); }
 __device__ __forceinline__ float h2_inv_scale(uint32_t m) { return __uint_as_float((uint32_t)(254 - h2_sexp(m)) << 23); }
-// Max of n <= 64 words at a workgroup-uniform address, in two steps so that the load can be issued early
+// Max of n words at a workgroup-uniform address, in two steps so that the load can be issued early
 // and waited for late: lane_word (lane i loads word i: one load, all words in flight at once; a loop of
-// dependent loads cost one memory latency per word), then wave_max_u32 (every lane of the wave active):
-// DPP max within each 16-lane row, then the four rows' maxima read into scalars.
+// dependent loads cost one memory latency per word; n > 64 -- hidden sizes past 2560 -- folds words
+// i, i + 64, ... into lane i), then wave_max_u32 (every lane of the wave active): DPP max within each
+// 16-lane row, then the four rows' maxima read into scalars.
 __device__ __forceinline__ uint32_t lane_word(const uint32_t *w, int n) {
     const int l = threadIdx.x & 63;
-    return l < n ? w[l] : 0u;
+    uint32_t m = l < n ? w[l] : 0u;
+    for (int i = l + 64; i < n; i += 64) m = max(m, w[i]);
+    return m;
 }
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t m) {
     m = max(m, (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]

@@ -116,13 +116,13 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     // natural rows for the backward)
     // (an embed-capable graph -- categorical codes -- needs no feature planes)
     const bool codes = g->atom_codes && g->bond_src_blk && g->bond_tail && D.Fb <= WO_MAXK && D.Fa <= WO_MAXK;
-    // (Hk <= 2560: at most 64 column tiles of 40 per block, the h2 scale words' capacity)
-    const bool blk_common = !D.desc && D.T >= 2 && D.Hk <= 2560 && g->n_blocks > 0 && g->blocks &&
+    // (any Hk: a consumer folds its block's h2 scale words 64 at a time, planes.hpp lane_word)
+    const bool blk_common = !D.desc && D.T >= 2 && g->n_blocks > 0 && g->blocks &&
                             g->atom_ell_idx && g->atom_ell_coef;
     // atom-message mode (inference): the a2a gather's pad slots read atom 0, whose message is act(b_i) and
     // later act(b_i + W_h(...)) -- zero without biases, so the block-local lists drop them; with biases,
     // or for training, the unblocked path runs
-    const bool atom_blk = D.atom && !D.f32 && !D.save && !D.undirected && !p->b_i && !p->b_h && D.Hk <= 2048 &&
+    const bool atom_blk = D.atom && !D.f32 && !D.save && !D.undirected && !p->b_i && !p->b_h &&
                           g->f_atoms_x6 &&
                           g->f_atoms_blk_x6 && g->bond_feat_gather.ptr && g->msg_ell_idx && g->msg_ell_coef &&
                           g->msg_gather.ptr && D.Fbk == 32;

@@ -53,6 +53,37 @@ def run(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
+class HeadModel(nn.Module):
+    """An encoder part and an ``ffn`` head: GradBucket's default early segment is the head."""
+
+    def __init__(self):
+        super().__init__()
+        self.enc = nn.Linear(6, 16)
+        self.ffn = nn.Sequential(nn.ReLU(), nn.Linear(16, 2))
+
+
+def run_segments(rank, world, port, out_path):
+    """Rank-dependent gradients all-reduced in two segments (start_early: the head, then the rest)."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dp.init_distributed('gloo')
+    torch.manual_seed(0)
+    model = HeadModel()
+    bucket = dp.GradBucket(model)
+    for k, p in enumerate(model.parameters()):
+        p.grad.copy_(torch.full_like(p, float(10 * k + rank + 1)))
+    bucket.start_early()
+    n_early_launched = len(bucket._works)
+    bucket.start_allreduce()
+    bucket.finish_allreduce()
+    if rank == 0:
+        torch.save({'grads': [p.grad.clone() for p in model.parameters()], 'n_early': bucket.n_early,
+                    'early_launched': n_early_launched, 'head_first': bucket.params[0] is model.ffn[1].weight},
+                   out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def run_gpu(rank, world, port, out_path):
     """Two ranks on cuda:0 (gloo process group): MoleculeModel with the HIP encoder, DP training with the
     flat GradBucket all-reduce, fused Adam, on disjoint synthetic polymer shards."""

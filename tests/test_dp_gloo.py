@@ -56,6 +56,18 @@ def test_two_rank_gradient_allreduce_matches_single_process(tmp_path):
     assert res['nbytes'] == 4 * sum(p.numel() for p in model.parameters())
 
 
+def test_two_segment_allreduce_averages_every_gradient(tmp_path):
+    """GradBucket's early segment (the ``ffn`` head, launched by start_early while the encoder backward
+    would still run) and the rest: every gradient ends as the mean over the ranks."""
+    out = str(tmp_path / 'seg.pt')
+    mp.spawn(dp_worker.run_segments, args=(2, free_port(), out), nprocs=2, join=True)
+    res = torch.load(out, weights_only=True)
+    assert res['head_first'] and res['early_launched'] == 1
+    assert res['n_early'] == 16 * 2 + 2
+    for k, g in enumerate(res['grads']):
+        assert torch.equal(g, torch.full_like(g, 10 * k + 1.5)), k
+
+
 @pytest.mark.gpu
 def test_two_rank_molecule_model_on_gpu_matches_single_process(tmp_path):
     """World size 2 on cuda:0 (gloo): the real MoleculeModel with the HIP encoder (its autograd.Function

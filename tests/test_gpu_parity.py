@@ -125,6 +125,7 @@ def _check(res):
     ('polymer', 16, 70, 3, dict(activation='PReLU', bias=True, aggregation='norm')),
     ('polymer', 8, 1100, 2, dict(activation='ELU')),                 # hidden > 1024 (readout backward chunks)
     ('polymer', 6, 2400, 3, dict(bias=True)),                        # the reference hyperopt's largest hidden
+    ('polymer', 3, 2850, 2, {}),  # Hk 2880: 72 embed scale words per block (> 64, folded by lane_word)
 ])
 def test_random_graphs_vs_oracle(kind, b, hidden, depth, extra):
     args = TrainArgs(hidden_size=hidden, depth=depth, **extra)
@@ -502,6 +503,31 @@ def test_direct_training_step_equals_autograd_step(act, bias):
         assert res[0][0] == res[1][0]
         assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
         assert all(torch.equal(a, b) for a, b in zip(res[0][2], res[1][2]))
+
+
+def test_direct_steps_without_host_sync_read_each_steps_targets():
+    """The direct step's head kernel reads its loss table in place from a ring of 4 coherent mapped host
+    buffers.  Ten steps with ten different target sets and NO host sync between them (the losses stay on
+    the device until the end) give bitwise the losses and parameters of the copy path (autograd step,
+    targets copied to the device): every rewritten ring slot is seen by the kernel that reads it."""
+    from chemprop_amd.nn_utils import initialize_weights
+    from chemprop_amd.train import build_optimizer, get_loss_func, train_step
+    args = TrainArgs(hidden_size=48, depth=3, device=DEV)
+    g = BatchMolGraph(synthetic.make_batch('polymer', 12, 40), device_bond_features=True)
+    targets = [[[0.25 * j - 2.0 + 0.7 * i] for j in range(12)] for i in range(10)]
+    res = []
+    for direct in (True, False):
+        torch.manual_seed(0)
+        m = MoleculeModel(args)
+        initialize_weights(m)
+        m = m.to(DEV)
+        opt = build_optimizer(m, 1e-3)
+        losses = [train_step(m, [g], t, get_loss_func('regression'), opt, direct=direct) for t in targets]
+        torch.cuda.synchronize()
+        res.append(([float(x) for x in losses], [q.detach().clone() for q in m.parameters()]))
+    assert len(set(res[0][0])) == 10
+    assert res[0][0] == res[1][0]
+    assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
 
 
 @pytest.mark.parametrize('kind', ['adam', 'adamw'])

@@ -107,6 +107,27 @@ def test_training_on_streamed_batches_matches_host_packed():
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
 
 
+def test_wide_hidden_runs_fused_on_lean_streamed_graphs():
+    """hidden 2850 (Hk 2880: 72 scale words per molecule block, more than one per lane): the streamed lean
+    graphs -- which only the molecule-blocked fused forward can encode -- give the oracle's output, and
+    NativeFeed.encode gives the per-batch forwards bitwise."""
+    from chemprop_amd.stream import NativeFeed
+    from oracle import mpn_ref
+    enc = _encoder(hidden=2850, depth=2, seed=4)
+    p = {n: t.detach().cpu().clone() for n, t in enc.named_parameters()}
+    with torch.no_grad():
+        full = list(StreamedBatches('polymer', 8, 3, seed=31, device=DEV, keep_host=True))
+        ref = [enc(g) for g in full]
+        lean = [enc(g) for g in StreamedBatches('polymer', 8, 3, seed=31, device=DEV, lean=True)]
+        feed = torch.cat([out.clone() for out, *_ in
+                          NativeFeed('polymer', 8, 3, seed=31, device=DEV, producers=2, lean=True).encode(enc, k=2)])
+        torch.cuda.synchronize()
+        want = mpn_ref.encoder_forward(p, full[0], TrainArgs(hidden_size=2850, depth=2))
+    assert golden_io.normwise(ref[0].cpu().numpy(), want.numpy()) <= 1e-5
+    assert all(torch.equal(a, b) for a, b in zip(ref, lean))
+    assert torch.equal(feed, torch.cat(ref))
+
+
 def _molgraphs(g):
     from test_compact import _as_molgraphs
     return _as_molgraphs(g)
