@@ -147,6 +147,15 @@ def forward_roofline(graphs, a, t_fwd):
             'note': 'SURVEY 8(d) formulas; combined = max(bytes/8 TB/s, flops/157.3 TF/s) / measured time'}
 
 
+def device_identity(device):
+    """This rank's GPU as the HIP runtime reports it (ordinal, PCI domain:bus:device, UUID, name): the
+    bench line lists every rank's, so a multi-GPU line shows how many distinct devices ran it."""
+    p = torch.cuda.get_device_properties(device)
+    pci = f'{getattr(p, "pci_domain_id", 0):04x}:{getattr(p, "pci_bus_id", 0):02x}:{getattr(p, "pci_device_id", 0):02x}'
+    return {'ordinal': device.index, 'pci': pci, 'uuid': str(getattr(p, 'uuid', '')), 'name': p.name,
+            'visible_devices': torch.cuda.device_count()}
+
+
 def default_streams(edges_per_batch):
     """Batches in flight per GPU for a batch size: three (one per HIP stream) while a batch's launches
     leave CUs idle in their ramps, barriers and epilogues (polymer-sized batches: 2 / 3 / 4 in flight
@@ -191,14 +200,16 @@ def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_b
         def fwd(i):
             if n_streams == 1:
                 return enc(graphs[i % len(graphs)])
-            with torch.cuda.stream(ss[i % n_streams]):
-                return enc(graphs[i % len(graphs)])
+            torch.cuda.set_stream(ss[i % n_streams])  # (see main(): step)
+            return enc(graphs[i % len(graphs)])
         for i in range(warmup):
             fwd(i)
+        torch.cuda.set_stream(ss[0])
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
         for i in range(steps):
             fwd(i)
+        torch.cuda.set_stream(ss[0])
         torch.cuda.synchronize(device)
         return time.perf_counter() - t0
 
@@ -459,11 +470,17 @@ def main():
     streams = bench_streams(device, max(a.streams, 3))[:a.streams]
 
     def step(i, prof=None):
+        # (torch.cuda.set_stream, not the `with torch.cuda.stream(...)` context manager: that costs ~6 us of
+        # host time per switch against 0.4 us, profiles/round5_host_breakdown.txt; the loops below restore
+        # the default stream when they end)
         enc._prof = prof
         if prof is not None or len(streams) == 1:
             return enc(graphs[i % len(graphs)])
-        with torch.cuda.stream(streams[i % len(streams)]):
-            return enc(graphs[i % len(graphs)])
+        torch.cuda.set_stream(streams[i % len(streams)])
+        return enc(graphs[i % len(graphs)])
+
+    def restore():
+        torch.cuda.set_stream(streams[0])
 
     def barrier():
         torch.cuda.synchronize(device)
@@ -477,10 +494,12 @@ def main():
         barrier()
         for i in range(1, a.warmup):
             step(i)
+        restore()
         barrier()
         t0 = time.perf_counter()
         for i in range(a.steps):
             step(i)
+        restore()
         barrier()
         elapsed = time.perf_counter() - t0
         my_edges = sum(edges[i % len(edges)] for i in range(a.steps))
@@ -521,6 +540,7 @@ def main():
         t1 = time.perf_counter()
         for i in range(a.steps):
             step(i, (pool.value, i))
+        restore()
         barrier()
         elapsed_prof = time.perf_counter() - t1
         enc._prof = None
@@ -551,6 +571,12 @@ def main():
         tr_dt, tr_edges, tr_steps = streamed_training(device, rank, world, a.stream_train_graphs,
                                                       producers=a.producers, barrier=barrier)
 
+    ident = device_identity(device)
+    if world > 1:
+        idents = [None] * world
+        dist.all_gather_object(idents, ident)
+    else:
+        idents = [ident]
     t = torch.tensor([elapsed, elapsed_prof, single or 0.0, st_dt, tr_dt, many_dt or 0.0], dtype=torch.float64,
                      device=device)
     e = torch.tensor([my_edges, st_edges, st_graphs, st_h2d, tr_edges, many_edges if many_dt else 0.0],
@@ -585,6 +611,9 @@ def main():
             'value': total_edges / elapsed,
             'unit': 'edges/s',
             'n_gpus': world,
+            'backend': dist.get_backend() if world > 1 else 'none (one process)',
+            'distinct_devices': len({(d['pci'], d['uuid']) for d in idents}),
+            'rank_devices': idents,
             'steps': a.steps,
             'warmup': a.warmup,
             'ms_per_step': elapsed / a.steps * 1e3,

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define WDMPNN_ABI_VERSION 8
+#define WDMPNN_ABI_VERSION 9
 #define WDMPNN_ELL_WIDTH 8
 
 enum WdActivation {     /* nn_utils.py:70-99 get_activation_function */
@@ -151,6 +151,11 @@ typedef struct WdGraph {
      * alone) as bf16x3 plane tiles [rows of f_atoms][ld_bonds], made with the graph's other planes.  NULL:
      * the fused forward gathers it in one extra launch. */
     const void *atom_feat_sum_x6;
+    /* Optional (ABI 9): the largest bond / atom row counts of any block (0 = unknown).  When every block
+     * holds <= 32 of each (QM9-sized molecules) the fused inference forward runs as ONE launch, a
+     * workgroup carrying its block from the input layer to the readout (small_fwd.hpp). */
+    int32_t blk_max_bonds;
+    int32_t blk_max_atoms;
 } WdGraph;
 
 /* nn.Module parameters of MPNEncoder (mpn.py:17-64); all device pointers, row-major like nn.Linear. */

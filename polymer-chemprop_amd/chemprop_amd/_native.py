@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get('WDMPNN_LIB', os.path.join(HERE, 'libwdmpnn.so'))
 ACTIVATIONS = {'ReLU': 0, 'LeakyReLU': 1, 'PReLU': 2, 'tanh': 3, 'SELU': 4, 'ELU': 5}
 ACT_IDENTITY = 6
 AGGREGATIONS = {'mean': 0, 'sum': 1, 'norm': 2}
-ABI_VERSION = 8
+ABI_VERSION = 9
 GRAPH_LEAN = 1  # WDMPNN_GRAPH_LEAN
 GRAPH_NO_PLANES = 2  # WDMPNN_GRAPH_NO_PLANES
 ERR_UNSUPPORTED = -1003  # WD_ERR_UNSUPPORTED
@@ -54,7 +54,8 @@ class WdGraph(Structure):
                 ('n_blocks', c_int32), ('blocks', c_void_p), ('bond_blk_row', c_void_p), ('f_atoms_blk_x6', c_void_p),
                 ('msg_ell_idx', c_void_p), ('msg_ell_coef', c_void_p), ('atom_ell_idx', c_void_p),
                 ('atom_ell_coef', c_void_p), ('atom_codes', c_void_p), ('bond_src_blk', c_void_p),
-                ('bond_tail', c_void_p), ('atom_feat_sum_x6', c_void_p)]
+                ('bond_tail', c_void_p), ('atom_feat_sum_x6', c_void_p),
+                ('blk_max_bonds', c_int32), ('blk_max_atoms', c_int32)]
 
 
 class WdParams(Structure):

@@ -658,6 +658,7 @@ class BatchMolGraph:
                                                          _native.current_stream(device)), 'blocked f_atoms planes')
                 views['f_atoms_blk_x6'] = planes
                 s.n_blocks, s.blocks, s.bond_blk_row = len(blocks), P('blocks'), P('bond_blk_row')
+                s.blk_max_bonds, s.blk_max_atoms = int(blocks[:, 1].max()), int(blocks[:, 3].max())
                 s.msg_ell_idx, s.msg_ell_coef = P('msg_ell_idx'), P('msg_ell_coef')
                 s.atom_ell_idx, s.atom_ell_coef = P('agg_ell_idx'), P('agg_ell_coef')
                 if not atom_messages:
@@ -696,6 +697,9 @@ def upload_compact(device, staged: torch.Tensor, info, atom_fdim: int, bond_fdim
     _native.check(L.wdmpnn_build_graph_ex(ctypes.byref(c), gbuf.data_ptr(), nbytes.value, ctypes.byref(s),
                                           _native.GRAPH_LEAN if lean else 0, _native.current_stream(device)),
                   'device graph build')
+    if n_blocks:  # the block plan's largest blocks, read from the staged image (WdGraph.blk_max_*)
+        blk = np.frombuffer(staged.numpy(), np.int32, count=8 * n_blocks, offset=off[4]).reshape(n_blocks, 8)
+        s.blk_max_bonds, s.blk_max_atoms = int(blk[:, 1].max()), int(blk[:, 3].max())
     dg = DeviceGraph(gbuf, {'compact': buf}, s)
     dg.finish()
     dg.n_edges = n_bonds - 1

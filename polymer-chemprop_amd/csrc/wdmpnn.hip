@@ -33,6 +33,7 @@
 #include "gemm_x6.hpp"
 #include "graph_build.hpp"
 #include "kernels.hpp"
+#include "small_fwd.hpp"
 #include "wdmpnn.h"
 
 using namespace wd;
@@ -85,6 +86,7 @@ struct Dims {
     bool f32;  // WdConfig.gemm_variant 9: f32-MFMA GEMMs (gemm_nt16_kernel) on the unblocked path
     bool x6;   // plane-tile pipeline: gathers emit bf16x3 plane tiles, GEMMs run gemm_x6g_kernel
     bool blocked;  // molecule-blocked fused inference forward (fused_mp.hpp)
+    bool small;    // ... as ONE launch, a workgroup per block (small_fwd.hpp: blocks <= 32 rows, Hk 320)
     int nblk;
 };
 
@@ -129,6 +131,10 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     D.blocked = blk_common && (atom_blk || (D.x6 && g->bond_blk_row && (codes || (g->f_atoms_blk_x6 && g->f_bonds_x6)) &&
                                             g->bond_src_blk && g->b2revb));
     D.nblk = D.blocked ? g->n_blocks : 0;
+    // QM9-sized blocks, inference: the one-launch forward (WdConfig.gemm_variant 11 keeps the four launches)
+    D.small = D.blocked && codes && !D.atom && !D.save && c->dropout == 0.f && D.Hk == SF_HK && !D.undirected &&
+              c->gemm_variant != 11 && g->blk_max_bonds > 0 && g->blk_max_bonds <= SF_ROWS &&
+              g->blk_max_atoms <= SF_ATOMS && D.Fa <= WO_MAXK && D.Fb <= WO_MAXK && D.Fb - D.Fa <= SF_ROWS;
     if (D.atom && D.undirected)
         return fail(WD_ERR_UNSUPPORTED, "undirected with atom_messages (the reference indexes atom messages "
                                         "with b2revb, mpn.py:101-102)");
@@ -885,6 +891,34 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
     return 0;
 }
 
+// the whole fused inference forward as one launch (small_fwd.hpp): one workgroup per molecule block
+int small_forward(const WdGraph *g, const Dims &D, const WdParams *p, const WdConfig *c, const PackLayout &PL,
+                  const char *pk, float *out, hipStream_t st) {
+    if (D.nblk < 1) return 0;
+    auto W = [&](size_t off) { return (const float *)(pk + off); };
+    const bool bn80 = D.Hk % 80 == 0;
+    SmallFwdP S{};
+    S.blocks = g->blocks; S.codes = g->atom_codes; S.src_blk = g->bond_src_blk; S.tail = g->bond_tail;
+    S.rev = g->b2revb;
+    S.aell_idx = g->atom_ell_idx; S.aell_coef = g->atom_ell_coef;
+    S.aptr = g->atom_gather.ptr; S.aidx = g->atom_gather.idx; S.acoef = g->atom_gather.coef;
+    S.w_atoms = g->w_atoms; S.mol_start = g->mol_start; S.mol_size = g->mol_size; S.xn = g->degree_of_polym;
+    S.wit = W(PL.WiT); S.woat = W(PL.WoaT);
+    S.bi = p->b_i ? W(PL.bi) : nullptr; S.bh = p->b_h ? W(PL.bh) : nullptr; S.bo = W(PL.bo);
+    S.wh = (const uint8_t *)(pk + PL.WhH); S.wh_amax = (const uint32_t *)(pk + PL.amax) + 64; S.whbr = fused_bn(D.Hk);
+    S.wo = (const uint8_t *)(pk + (bn80 ? PL.WoX80 : PL.WoX)); S.wobr = bn80 ? 80 : 64; S.kcw = D.Fak / 32;
+    S.Fa = D.Fa; S.Fb = D.Fb; S.T = D.T; S.undirected = D.undirected; S.agg = c->aggregation; S.norm = c->aggregation_norm;
+    S.zero_vec = p->zero_vec; S.slope = p->prelu;
+    S.out = out; S.ncols = D.H;
+    WD_TRY(record_prof(c, 0, 0, st));
+    host_with_act(c->activation, [&](auto act_c) {
+        hipLaunchKernelGGL(small_forward_kernel<decltype(act_c)::value>, dim3(D.nblk), dim3(SF_THREADS), 0, st, S);
+    });
+    WD_CHECK_LAUNCH("small_forward");
+    WD_TRY(record_prof(c, 0, 1, st));
+    return 0;
+}
+
 }  // namespace
 
 // ================================================================================================
@@ -972,6 +1006,7 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
     const bool split = !D.f32;
     const char *pkb = pk;
 
+    if (D.small) return small_forward(g, D, p, c, PL, pk, out, st);
     if (D.blocked) {
         FusedJob J{g, D, L, ws, out};
         return fused_forward(&J, 1, p, c, PL, pk, st);

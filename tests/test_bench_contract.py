@@ -38,6 +38,7 @@ def test_bench_prints_one_contract_line():
               'vs_baseline', 'dtype', 'data', 'config', 'roofline'):
         assert k in d, k
     assert d['n_gpus'] == 1 and d['steps'] == 5 and d['warmup'] == 1 and d['value'] > 0
+    assert d['distinct_devices'] == 1 and len(d['rank_devices']) == 1 and d['rank_devices'][0]['ordinal'] == 0
     assert d['metric'] == json.load(open(os.path.join(ROOT, 'BASELINE.json')))['metric']
     rf = d['roofline']
     for k in ('bound', 'achieved', 'peak', 'unit', 'frac', 'traffic'):

@@ -37,6 +37,10 @@ def test_bench_four_ranks_gloo_on_one_gpu():
     assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints the one JSON line
     d = json.loads(lines[0])
     assert d['n_gpus'] == 4 and d['config']['global_batch'] == 256
+    # the rehearsal is four ranks on ONE device over gloo, and the line says so (the 8-GPU node's line
+    # must show backend nccl and 8 distinct devices)
+    assert d['backend'] == 'gloo' and d['distinct_devices'] == 1
+    assert len(d['rank_devices']) == 4 and {r['ordinal'] for r in d['rank_devices']} == {0}
     assert d['value'] > 0 and d['ms_per_step'] > 0
     st = d['streamed']
     assert st['graphs'] == 4 * per_rank and st['n_gpus'] == 4

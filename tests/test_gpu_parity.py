@@ -133,6 +133,43 @@ def test_random_graphs_vs_oracle(kind, b, hidden, depth, extra):
     _check(_oracle_vs_hip(graphs, args, seed=b))
 
 
+def _scale_mass(g, factor):
+    """Multiply a molecule's mass feature (the last atom column, featurization.py:210) by ``factor``, in
+    f_atoms and in the f_atoms half of its f_bonds rows: its messages grow by about that much."""
+    for row in g.f_atoms:
+        row[-1] *= factor
+    fa = len(g.f_atoms[0])
+    for b, row in enumerate(g.f_bonds):
+        row[fa - 1] = g.f_atoms[g.b2a[b]][-1]
+    return g
+
+
+@pytest.mark.parametrize('activation', ['ReLU', 'LeakyReLU'])
+def test_per_molecule_accuracy_in_mixed_magnitude_blocks(activation):
+    """The fused layers scale their fp16-pair operand per (molecule block, column tile) from the block's max
+    (planes.hpp h2).  Molecules whose messages are 10^2 - 10^4 x smaller than a block-mate's must still meet
+    1e-5 against the fp64 oracle relative to their OWN row maximum (per-element pair error <= max(2^-22 |x s|,
+    2^-25) in scaled units: no loss until a row is ~2^-18 of the block max).  Full molecule blocks
+    (block_target=1) so that the scaled and unscaled molecules share blocks."""
+    rng_mols = synthetic.make_batch('qm9', 24, 61)
+    for i, f in ((2, 1e2), (9, 1e4), (17, 1e3)):
+        _scale_mass(rng_mols[i], f)
+    g = BatchMolGraph(rng_mols, block_target=1)
+    assert g.device_graph(DEV, False, get_bond_fdim()).struct.n_blocks < 24  # molecules do share blocks
+    args = TrainArgs(hidden_size=300, depth=3, activation=activation)
+    enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim())
+    synthetic.fill_parameters(enc, 8)
+    p = {n: t.detach().to(torch.float64) for n, t in enc.named_parameters()}
+    enc = enc.to(DEV).eval()
+    with torch.no_grad():
+        out = enc(g).cpu().double()
+        ref = mpn_ref.encoder_forward(p, g, args, dtype=torch.float64)
+    mx = ref.abs().max(dim=1).values
+    assert float(mx.max() / mx.min()) > 100  # the magnitudes really are mixed
+    err = (out - ref).abs().max(dim=1).values / mx
+    assert float(err.max()) <= TOL, err.tolist()
+
+
 def test_edge_cases_hub_degree_empty_single_atom():
     args = TrainArgs(hidden_size=64, depth=3, bias=True)
     graphs = BatchMolGraph(synthetic.edge_case_batch(9, star_leaves=130))
@@ -686,3 +723,44 @@ def test_backward_after_the_batch_graph_is_dropped():
         del junk
         grads.append([p.grad.cpu() for p in enc.parameters() if p.grad is not None])
     assert all(torch.equal(a, b) for a, b in zip(*grads))
+
+
+def _small_batch(seed):
+    """QM9-sized molecules plus an empty molecule, a single atom and a molecule with 9 atoms in one
+    ring-closed chain: every block <= 32 bond rows / atoms (the one-launch forward's domain)."""
+    rng = np.random.default_rng(seed)
+    mols = synthetic.make_batch('qm9', 40, seed)
+    mols[5:5] = [synthetic.empty_graph(), synthetic.single_atom_graph(rng)]
+    return mols
+
+
+@pytest.mark.parametrize('act,bias,agg', [('ReLU', False, 'mean'), ('LeakyReLU', True, 'sum'), ('PReLU', True, 'norm'),
+                                          ('tanh', False, 'mean'), ('SELU', True, 'mean'), ('ELU', False, 'sum')])
+def test_one_launch_small_block_forward_is_bitwise_the_four_launch_forward(act, bias, agg):
+    """QM9-sized blocks run the whole inference forward as ONE launch (small_fwd.hpp).  It must give
+    torch.equal outputs to the four-launch fused forward (WdConfig.gemm_variant 11 keeps that path) for
+    every activation, with and without biases, every aggregation, on the default block plan (about one
+    molecule per block) and on blocks of two to three molecules (block_target=20: <= 32 rows), and match the
+    fp32 oracle at 1e-5."""
+    args = TrainArgs(hidden_size=300, depth=3, activation=act, bias=bias, aggregation=agg)
+    enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim())
+    synthetic.fill_parameters(enc, 13)
+    p = {n: t.detach().clone() for n, t in enc.named_parameters()}
+    enc = enc.to(DEV).eval()
+    for target in (None, 20):
+        mols = _small_batch(21)
+        g = BatchMolGraph(mols, device_bond_features=True) if target is None else \
+            BatchMolGraph(mols, device_bond_features=True, block_target=target)
+        dg = g.device_graph(DEV, False, get_bond_fdim())
+        assert 0 < dg.struct.blk_max_bonds <= 32 and dg.struct.blk_max_atoms <= 32
+        assert target is None or dg.struct.n_blocks <= 24  # several molecules per block
+        with torch.no_grad():
+            one = enc(g)
+            enc._gemm_variant = 11
+            four = enc(g)
+            enc._gemm_variant = 0
+        torch.cuda.synchronize()
+        assert torch.equal(one, four), (target, float((one - four).abs().max()))
+        with torch.no_grad():
+            ref = mpn_ref.encoder_forward(p, g, args)
+        assert golden_io.normwise(one.cpu().numpy(), ref.numpy()) <= TOL

@@ -64,6 +64,20 @@ with torch.no_grad():
     timeit('native wdmpnn_workspace_bytes', lambda: L.wdmpnn_workspace_bytes(
         ctypes.byref(gs), ctypes.byref(pstruct), ctypes.byref(cfg), ctypes.byref(nbytes)))
     timeit('ctypes no-op (wdmpnn_last_error)', lambda: L.wdmpnn_last_error())
+    s2 = torch.cuda.Stream(dev)
+
+    def ctx():
+        with torch.cuda.stream(s2):
+            pass
+    timeit('with torch.cuda.stream(s): pass', ctx)
+    timeit('torch.cuda.set_stream x2', lambda: (torch.cuda.set_stream(s2), torch.cuda.set_stream(stream)))
+
+    def ctx_fwd():
+        with torch.cuda.stream(s2):
+            enc(g)
+    timeit('with stream: enc(g)', ctx_fwd)
+    ev = torch.cuda.Event()
+    timeit('event.record', lambda: ev.record(stream))
     torch.cuda.synchronize()
 for k, v in res.items():
     print(f'{k:40s} {v:7.2f} us', flush=True)
