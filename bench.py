@@ -159,12 +159,13 @@ def device_identity(device):
 def default_streams(edges_per_batch):
     """Batches in flight per GPU for a batch size: three (one per HIP stream) while a batch's launches
     leave CUs idle in their ramps, barriers and epilogues (polymer-sized batches: 2 / 3 / 4 in flight
-    measured 155-158 / 172-173 / 173-175 M edges/s on one box, profiles/round3_streams_ab.txt), two for
-    QM9-sized batches (tiny grids: a third in flight contends, 50 vs 26.5 us per forward), one for
+    measured 155-158 / 172-173 / 173-175 M edges/s on one box, profiles/round3_streams_ab.txt), four for
+    QM9-sized batches (each forward one launch of ~64 workgroups: four fill the chip), one for
     large batches whose grids fill the chip on their own (ZINC-sized B = 512: two streams measured 50.5 vs
     52.6 M edges/s, BENCH_r02.json).  Every step is still one full, independent batch."""
-    if edges_per_batch < 2048:  # QM9-sized (~900 edges): three in flight measured 50 us per forward, two 26.5
-        return 2
+    if edges_per_batch < 2048:  # QM9-sized (~900 edges): the one-launch small-block forward (64 workgroups a
+        return 4                # batch): 1 / 2 / 3 / 4 in flight 36.9 / 18.4 / 12.4 / 9.8 us per forward, 5-6
+                                # (past the 4 hardware queues) 12-15 (profiles/round5_qm9_streams.txt)
     return 3 if edges_per_batch < 16384 else 1
 
 
@@ -467,7 +468,9 @@ def main():
 
     # independent batches in flight on a.streams HIP streams (round-robin): the kernels of one batch's
     # forward overlap another's ramp / drain / epilogue on the same GPU (graphs are independent units)
-    streams = bench_streams(device, max(a.streams, 3))[:a.streams]
+    # (every stream a workload uses is created here, before the native feed's stream: a stream created after it
+    # can share its hardware queue)
+    streams = bench_streams(device, max(a.streams, 4))[:a.streams]
 
     def step(i, prof=None):
         # (torch.cuda.set_stream, not the `with torch.cuda.stream(...)` context manager: that costs ~6 us of

@@ -669,7 +669,10 @@ __device__ __forceinline__ void x6_mainloop(const X6Operands &O, uint8_t *lds,
 // producers store A H2_A_STAGES - 1 chunks ahead (H2_A_STAGES A stages).  (Measured, same box: three A
 // stages +1.3 us per launch, B two chunks ahead +0.4 us, all of a chunk's fragments read before its first
 // MFMA +0.4 us, 3 / 4 / 6 register sets in flight 16.6 / 17.5 / 22.4 us: tools/prof_libs.sh variants.)
-constexpr int H2_B_AHEAD = 1, H2_A_STAGES = 2;
+#ifndef WD_H2_B_AHEAD
+#define WD_H2_B_AHEAD 1
+#endif
+constexpr int H2_B_AHEAD = WD_H2_B_AHEAD, H2_A_STAGES = 2;
 template <int BM, int BN>
 constexpr int h2_lds_bytes() { return H2_A_STAGES * (2 * BM * 64) + (H2_B_AHEAD + 1) * (2 * BN * 64); }
 

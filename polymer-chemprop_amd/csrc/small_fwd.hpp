@@ -132,6 +132,24 @@ __device__ __forceinline__ void sf_gemm(const uint8_t *a_img, int rg, const uint
     }
 }
 
+// code_sum over a global (L2-resident) table, branch-free: every slot loads a row (an unused slot row 0,
+// added as +0), so the nine loads of a unit go out together -- the same sums as code_sum
+template <int LDT>
+__device__ __forceinline__ float4 code_sum_g(const WdAtomCode &cd, const float *T, int Fa, int c) {
+    float4 w[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) w[q] = ld4(T + (cd.col[q] == 0xFF ? 0 : (int)cd.col[q]) * LDT + c);
+    const float4 wl = ld4(T + (Fa - 1) * LDT + c);
+    float4 s = f4zero();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const bool ok = cd.col[q] != 0xFF;
+        s.x += ok ? w[q].x : 0.f; s.y += ok ? w[q].y : 0.f; s.z += ok ? w[q].z : 0.f; s.w += ok ? w[q].w : 0.f;
+    }
+    fma4(s, cd.last, wl);
+    return s;
+}
+
 // acc -> fp32 LDS tile T[row][SF_LDI] (x sa x sb, in that order: the fused layer's x6_acc_to_lds_scaled)
 template <bool SCALED>
 __device__ __forceinline__ void sf_acc_store(const floatx4 (&acc)[3][2], float *T, float sa, float sb) {
@@ -248,7 +266,7 @@ __global__ __launch_bounds__(SF_THREADS) void small_forward_kernel(const SmallFw
         st4(ZP + (v / C4) * LDI + 4 * (v % C4), ld4(P.wit + (size_t)(P.Fa + v / C4) * HK + 4 * (v % C4)));
     for (int v = tid; v < B.an * C4; v += NT) {
         const int la = v / C4, c = 4 * (v % C4);
-        st4(X + la * LDI + c, code_sum<HK>(s_code[la], P.wit, P.Fa, c));
+        st4(X + la * LDI + c, code_sum_g<HK>(s_code[la], P.wit, P.Fa, c));
     }
     __syncthreads();
     wd_stamp(2);
@@ -372,7 +390,7 @@ __global__ __launch_bounds__(SF_THREADS) void small_forward_kernel(const SmallFw
     for (int v = tid; v < B.an * C4; v += NT) {
         const int la = v / C4, c = 4 * (v % C4);
         float4 hv = ld4(INP + la * LDI + c);
-        const float4 eo = code_sum<HK>(s_code[la], P.woat, P.Fa, c);
+        const float4 eo = code_sum_g<HK>(s_code[la], P.woat, P.Fa, c);
         const float4 bb = ld4(P.bo + c);
         hv.x += eo.x; hv.y += eo.y; hv.z += eo.z; hv.w += eo.w;
         float z[4] = {hv.x + bb.x, hv.y + bb.y, hv.z + bb.z, hv.w + bb.w};
