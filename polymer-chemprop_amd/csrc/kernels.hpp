@@ -476,9 +476,31 @@ struct SlabReduce {
 // bias is the extra column after the segments).  Every thread sums its column over the splits in
 // split order z = 0, 1, ... (eight independent loads in flight, then eight ordered adds), so the
 // result does not depend on the launch shape.
+// several reductions in one launch (the training backward's W_o, W_h and W_i gradients, each from its own
+// slab area): job k owns the 1-D grid range [blk0[k], blk0[k + 1]), each range a (column groups x row
+// groups) grid of the single-job form
+constexpr int SLAB_MAX = 4;
+struct SlabReduceJobs {
+    SlabReduce j[SLAB_MAX];
+    int cgroups[SLAB_MAX];
+    int blk0[SLAB_MAX + 1];
+    int n;
+};
+
+__device__ __forceinline__ void slab_reduce_elem(const SlabReduce &P, int n, int j);
+
+__global__ __launch_bounds__(256) void slab_reduce_multi_kernel(SlabReduceJobs J) {
+    int k = 0;
+    while (k + 1 < J.n && (int)blockIdx.x >= J.blk0[k + 1]) ++k;
+    const int b = blockIdx.x - J.blk0[k];
+    slab_reduce_elem(J.j[k], (b / J.cgroups[k]) * 4 + (threadIdx.x >> 6), (b % J.cgroups[k]) * 64 + (threadIdx.x & 63));
+}
+
 __global__ __launch_bounds__(256) void slab_reduce_kernel(SlabReduce P) {
-    const int n = blockIdx.y * 4 + (threadIdx.x >> 6);
-    int j = blockIdx.x * 64 + (threadIdx.x & 63);
+    slab_reduce_elem(P, blockIdx.y * 4 + (threadIdx.x >> 6), blockIdx.x * 64 + (threadIdx.x & 63));
+}
+
+__device__ __forceinline__ void slab_reduce_elem(const SlabReduce &P, int n, int j) {
     if (n >= P.rows) return;
     int src = -1;
     float *dst = nullptr;
@@ -581,21 +603,65 @@ __global__ __launch_bounds__(256) void build_bond_features_kernel(const float *_
 // Adam: L2 weight decay folded into the gradient (AdamW: decoupled, on the parameter), moments as
 // beta * m + (1 - beta) * g, denom = sqrt(v) / sqrt(bc2) + eps, p -= (lr / bc1) * m / denom.
 namespace wd {
-constexpr int ADAM_MAX = 16, ADAM_PER_BLOCK = 1024;
+constexpr int ADAM_MAX = 16, ADAM_PER_BLOCK = 1024, ADAM_OUTS = 20;
+// An extra destination of a tensor's updated values (wdmpnn_adam_step_repack: the training step's packed
+// weight copies written by the optimizer itself instead of a repack before the next forward).  Source
+// element (r, c) of a [rows][cols] tensor, for the column segment s holding c (c in [sc0[s], sc0[s] + K[s])):
+//   AO_PLAIN      dst[r * ld + dc0[s] + c - sc0[s]]            (pack_kernel's plain jobs)
+//   AO_TRANSPOSE  dst[(c - sc0[s]) * ld + r]                   (its transposes)
+//   AO_PLANES     bf16x3 plane tiles of the padded plain matrix (row blocks of br, kp padded columns), the
+//                 value split exactly as split_pair / x6_store8 split it
+enum { AO_PLAIN = 0, AO_TRANSPOSE = 1, AO_PLANES = 2 };
+struct AdamOut {
+    void *dst;
+    int kind, ld, nseg, br;
+    int sc0[2], dc0[2], K[2];
+};
 struct AdamLaunch {
     WdAdamTensor t[ADAM_MAX];
     int blk0[ADAM_MAX + 1];
     int n;
     float beta1, beta2, eps, wd, lr, step_size, bc2_sqrt;
     int decoupled;
+    // repack (optional): tensor k's outputs out[o0[k] .. o0[k + 1]), its column count, and where its
+    // workgroups publish max |p| (one word per workgroup, or null)
+    AdamOut out[ADAM_OUTS];
+    int o0[ADAM_MAX + 1];
+    int cols[ADAM_MAX];
+    uint32_t *amax[ADAM_MAX];
 };
 
+__device__ __forceinline__ void adam_out(const AdamOut &O, int64_t r, int c, float v) {
+    int s = 0;
+    if (O.nseg > 1 && c >= O.sc0[1]) s = 1;
+    const int cc = c - O.sc0[s];
+    if (cc < 0 || cc >= O.K[s]) return;
+    if (O.kind == AO_PLAIN) {
+        reinterpret_cast<float *>(O.dst)[r * O.ld + O.dc0[s] + cc] = v;
+    } else if (O.kind == AO_TRANSPOSE) {
+        reinterpret_cast<float *>(O.dst)[(int64_t)cc * O.ld + r] = v;
+    } else {
+        const int k = O.dc0[s] + cc;
+        const uint32_t h = cvt_pk_bf16(v, 0.f);
+        const float v1 = v - bf_lo(h);
+        const uint32_t m = cvt_pk_bf16(v1, 0.f);
+        const uint32_t l = cvt_pk_bf16(v1 - bf_lo(m), 0.f);
+        uint8_t *d = reinterpret_cast<uint8_t *>(O.dst) + ((r / O.br) * (O.ld >> 5) + (k >> 5)) * (3 * O.br * 64) +
+                     (r % O.br) * 64 + 2 * (k & 31);
+        *reinterpret_cast<uint16_t *>(d) = (uint16_t)h;
+        *reinterpret_cast<uint16_t *>(d + O.br * 64) = (uint16_t)m;
+        *reinterpret_cast<uint16_t *>(d + 2 * O.br * 64) = (uint16_t)l;
+    }
+}
+
+template <bool REPACK>
 __global__ __launch_bounds__(256) void adam_kernel(AdamLaunch A) {
     const int b = blockIdx.x;
     int k = 0;
     while (k + 1 < A.n && b >= A.blk0[k + 1]) ++k;
     const WdAdamTensor &T = A.t[k];
     const int64_t i0 = (int64_t)(b - A.blk0[k]) * ADAM_PER_BLOCK + threadIdx.x;
+    uint32_t mx = 0;
 #pragma unroll
     for (int j = 0; j < ADAM_PER_BLOCK / 256; ++j) {
         const int64_t i = i0 + 256 * j;
@@ -610,7 +676,18 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamLaunch A) {
         T.exp_avg[i] = m;
         T.exp_avg_sq[i] = v;
         const float denom = sqrtf(v) / A.bc2_sqrt + A.eps;
-        T.param[i] = p - A.step_size * m / denom;
+        const float pn = p - A.step_size * m / denom;
+        T.param[i] = pn;
+        if (REPACK) {
+            const int64_t r = i / A.cols[k];
+            const int c = (int)(i % A.cols[k]);
+            for (int o = A.o0[k]; o < A.o0[k + 1]; ++o) adam_out(A.out[o], r, c, pn);
+            mx = max(mx, absbits(pn));
+        }
+    }
+    if (REPACK && A.amax[k]) {  // (uniform per workgroup)
+        __shared__ uint32_t red[4];
+        publish_max(mx, A.amax[k] + (b - A.blk0[k]), red);
     }
 }
 }  // namespace wd

@@ -482,6 +482,41 @@ int gemm_tn(const Src &dZ, const Src &X, int n_out, int m_rows, const TnPlan &tp
 }
 
 // dW[n][w0 + kk] = sum_z slab[z][n][c0 + kk] per mapping {c0, w0, K}; db[n] = slab bias column
+SlabReduce slab_job(const TnPlan &tp, const float *slab, int n_rows, std::initializer_list<std::array<int, 3>> map,
+                    float *dW, int ldw, float *db, int bias_col) {
+    SlabReduce R{};
+    R.slab = slab; R.nsplit = tp.nsplit; R.slab_stride = tp.slab_stride; R.ld_slab = tp.ld_slab; R.rows = n_rows;
+    for (const auto &m : map) {
+        R.c0[R.nseg] = m[0]; R.w0[R.nseg] = m[1]; R.K[R.nseg] = m[2];
+        ++R.nseg;
+    }
+    R.dW = dW; R.ldw = ldw; R.db = db; R.bias_col = bias_col;
+    return R;
+}
+// the reductions of several gradients in one launch (jobs without dW and db skipped)
+int slab_reduce_multi(const SlabReduce *jobs, int n, hipStream_t st) {
+    SlabReduceJobs J{};
+    int blocks = 0;
+    for (int k = 0; k < n; ++k) {
+        const SlabReduce &R = jobs[k];
+        if (!R.dW && !R.db) continue;
+        if (J.n == SLAB_MAX) return fail(WD_ERR_ARG, "slab_reduce_multi: more than %d jobs", SLAB_MAX);
+        int cols = 0;
+        if (R.dW)
+            for (int q = 0; q < R.nseg; ++q) cols += R.K[q];
+        if (R.db) cols += 1;
+        J.j[J.n] = R;
+        J.cgroups[J.n] = (cols + 63) / 64;
+        J.blk0[J.n] = blocks;
+        blocks += J.cgroups[J.n] * ((R.rows + 3) / 4);
+        ++J.n;
+    }
+    if (!J.n) return 0;
+    J.blk0[J.n] = blocks;
+    hipLaunchKernelGGL(slab_reduce_multi_kernel, dim3(blocks), dim3(256), 0, st, J);
+    WD_CHECK_LAUNCH("slab_reduce_multi");
+    return 0;
+}
 int slab_reduce(const TnPlan &tp, const float *slab, int n_rows, std::initializer_list<std::array<int, 3>> map,
                 float *dW, int ldw, float *db, int bias_col, hipStream_t st) {
     if (!dW && !db) return 0;
@@ -571,7 +606,7 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
 
 struct BwdLayout {
     size_t dH = 0, dZd = 0, dHo = 0, dZo = 0, dA = 0, dZ0 = 0, dZ1 = 0, dRes = 0, dX = 0, dMs = 0, slab = 0,
-           prelu = 0, total = 0;
+           slab_h = 0, slab_i = 0, prelu = 0, total = 0;  // slab: W_o's (and W_d's) split-K slabs; W_h's, W_i's
     size_t prelu_floats = 0;
 };
 
@@ -601,16 +636,17 @@ BwdLayout bwd_layout(const WdGraph *g, const Dims &D) {
     L.dRes = take(msg);
     L.dX = take(msg);
     if (D.undirected) L.dMs = take(msg);
-    size_t slab = 0;
-    auto upd = [&](int n_out, const Src &X, int m_rows) {
+    // split-K slabs: W_o's (shared with the descriptor layer's, reduced before W_o's GEMM), W_h's and W_i's
+    // apart, so that one launch at the end reduces all three (slab_reduce_multi)
+    auto slab_of = [&](int n_out, const Src &X, int m_rows) {
         TnPlan tp = tn_plan(n_out, X, m_rows);
-        slab = std::max<size_t>(slab, (size_t)tp.nsplit * (size_t)tp.slab_stride);
+        return (size_t)tp.nsplit * (size_t)tp.slab_stride;
     };
-    upd(D.Hk, x_in(g, D), D.R);
-    upd(D.Hk, x_h(D, nullptr), D.R);
-    upd(D.Hk, x_o(g, D, nullptr), D.Va);
-    if (D.desc) upd(D.Hdk, x_d(g, D, nullptr), D.Va);
-    L.slab = take(slab);
+    size_t so = slab_of(D.Hk, x_o(g, D, nullptr), D.Va);
+    if (D.desc) so = std::max(so, slab_of(D.Hdk, x_d(g, D, nullptr), D.Va));
+    L.slab = take(so);
+    L.slab_h = take(slab_of(D.Hk, x_h(D, nullptr), D.R));
+    L.slab_i = take(slab_of(D.Hk, x_in(g, D), D.R));
     L.prelu_floats = (size_t)(D.T + 2) * std::max(4096, (D.Rp / 128) * (D.Hk / 64));
     L.prelu = take(L.prelu_floats);
     L.total = off;
@@ -1200,6 +1236,9 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
                        epi_store(S(Bl.dHo), Hk), st, true));
         dh = S(Bl.dHo);
     }
+    // the weight-gradient reductions, launched together at the end (slab_reduce_multi)
+    SlabReduce red[SLAB_MAX];
+    int nred = 0;
     // W_o layer
     {
         if (!ro_fused) {
@@ -1211,8 +1250,8 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
         Src X = x_o(g, D, F(L.A));
         TnPlan tp = tn_plan(Hk, X, D.Va);
         WD_TRY(gemm_tn(dZ, X, Hk, D.Va, tp, S(Bl.slab), 0, st));
-        WD_TRY(slab_reduce(tp, S(Bl.slab), H, {{0, 0, D.Fa}, {D.Fak, D.Fa, H}}, grads->W_o, D.Fa + H, grads->b_o,
-                           X.s[2].kp0, st));
+        red[nred++] = slab_job(tp, S(Bl.slab), H, {{0, 0, D.Fa}, {D.Fak, D.Fa, H}}, grads->W_o, D.Fa + H, grads->b_o,
+                               X.s[2].kp0);
         // dA = dZo W_o[:, Fa:] (dZo as plane tiles from the readout backward and this GEMM on LDS-DMA
         // staging measured no faster: 0.3734-0.3761 against 0.3729-0.3756 ms per training step, same box)
         WD_TRY(gemm_nt(S(Bl.dZo), Hk, Hk, nullptr, 0, 0, W(PL.WoT), Hk, D.Vap, Hk, epi_store(S(Bl.dA), Hk), st, true));
@@ -1253,7 +1292,7 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
         m.kind = SEG_ACT; m.act = c->activation; m.slope = p->prelu; m.p_drop = t - 1 == 0 ? 0.f : c->dropout;
         m.seed = c->seed; m.layer = t - 1;
         WD_TRY(gemm_tn(make_src(D.R, {seg_dense(Y, Hk, Hk)}), make_src(D.R, {m, seg_ones()}), Hk, D.R, tph,
-                       S(Bl.slab), t != D.T - 1, st, dZt));
+                       S(Bl.slab_h), t != D.T - 1, st, dZt));
         // dZ_{t-1} = (Y_t W_h) * dropout * act'(Z_{t-1}), the residual sum of mpn.py:123 accumulated, in
         // the GEMM's epilogue (EPI_ACTBWD)
         Epi e{};
@@ -1277,7 +1316,7 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
         float *dZt = dZbuf[cur];
         // dW_h, db_h (+)= dZ_t^T [X_t | 1]
         Src dZ = make_src(D.R, {seg_dense(dZt, Hk, Hk)});
-        WD_TRY(gemm_tn(dZ, x_h(D, F(L.X[t - 1])), Hk, D.R, tph, S(Bl.slab), t != D.T - 1, st));
+        WD_TRY(gemm_tn(dZ, x_h(D, F(L.X[t - 1])), Hk, D.R, tph, S(Bl.slab_h), t != D.T - 1, st));
         // dX = dZ_t W_h[:, :H]
         WD_TRY(gemm_nt(dZt, Hk, Hk, nullptr, 0, 0, W(PL.WhT), Hk, D.Rp, Hk, epi_store(S(Bl.dX), Hk), st, true));
         // dM_{t-1} = gather^T(dX) (+ symmetrize), then through the activation of layer t-1
@@ -1301,19 +1340,21 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
     }
     if (D.T > 1) {
         if (D.atom)
-            WD_TRY(slab_reduce(tph, S(Bl.slab), H, {{0, 0, H}, {Hk, H, D.Fb}}, grads->W_h, H + D.Fb, grads->b_h,
-                               Xh0.s[1].kp0, st));
+            red[nred++] = slab_job(tph, S(Bl.slab_h), H, {{0, 0, H}, {Hk, H, D.Fb}}, grads->W_h, H + D.Fb, grads->b_h,
+                                   Xh0.s[1].kp0);
         else
-            WD_TRY(slab_reduce(tph, S(Bl.slab), H, {{0, 0, H}}, grads->W_h, H, grads->b_h, Xh0.s[1].kp0, st));
+            red[nred++] = slab_job(tph, S(Bl.slab_h), H, {{0, 0, H}}, grads->W_h, H, grads->b_h, Xh0.s[1].kp0);
     }
     // input layer: dW_i, db_i = dZ_0^T [f | 1]
     {
         Src dZ = make_src(D.R, {seg_dense(dZbuf[cur], Hk, Hk)});
         Src X = x_in(g, D);
         TnPlan tp = tn_plan(Hk, X, D.R);
-        WD_TRY(gemm_tn(dZ, X, Hk, D.R, tp, S(Bl.slab), 0, st));
-        WD_TRY(slab_reduce(tp, S(Bl.slab), H, {{0, 0, D.Kin}}, grads->W_i, D.Kin, grads->b_i, X.s[1].kp0, st));
+        WD_TRY(gemm_tn(dZ, X, Hk, D.R, tp, S(Bl.slab_i), 0, st));
+        red[nred++] = slab_job(tp, S(Bl.slab_i), H, {{0, 0, D.Kin}}, grads->W_i, D.Kin, grads->b_i, X.s[1].kp0);
     }
+    // every weight gradient's split-K sum in one launch (three launches of ~4.8 us each before)
+    WD_TRY(slab_reduce_multi(red, nred, st));
     if (prelu && grads->prelu) {
         hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(256), 0, st, prelu_part, prelu_used, grads->prelu);
         WD_CHECK_LAUNCH("prelu sum");
@@ -1765,7 +1806,7 @@ int wdmpnn_adam_step(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *
         }
         if (!A.n) continue;
         A.blk0[A.n] = blocks;
-        hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, A);
+        hipLaunchKernelGGL(adam_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, A);
         WD_CHECK_LAUNCH("adam");
     }
     return 0;
