@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define WDMPNN_ABI_VERSION 9
+#define WDMPNN_ABI_VERSION 10
 #define WDMPNN_ELL_WIDTH 8
 
 enum WdActivation {     /* nn_utils.py:70-99 get_activation_function */
@@ -358,6 +358,16 @@ typedef struct WdAdamHyper {
     int32_t decoupled;    /* 1 = AdamW */
 } WdAdamHyper;
 int wdmpnn_adam_step(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *h, void *stream);
+/* The same step, also rewriting the encoder's packed weights (wdmpnn_pack_params layout for g, p, c) from
+ * the updated values: the copies the next training forward and backward read (padded plain, transposed,
+ * bf16x3 plane tiles, W_h's fp16-pair tiles and scale) come out of the optimizer's own pass instead of a
+ * pack before every forward (train.py:84 then mpn.py:66's next call).  tensors must hold p's W_i, b_i,
+ * W_h, b_h, W_o and b_o (matched by param pointer, with their full sizes) and `packed` must hold a pack of
+ * their previous values (its zero padding is kept); bond messages without descriptors only
+ * (WD_ERR_UNSUPPORTED otherwise: pack after the plain step).  Afterwards `packed` is bytewise the
+ * wdmpnn_pack_params of the updated weights. */
+int wdmpnn_adam_step_repack(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *h, const WdGraph *g,
+                            const WdParams *p, const WdConfig *c, void *packed, size_t packed_bytes, void *stream);
 
 /* The training step's FFN head + masked MSE loss and their gradients in two launches (model.py:57-121
  * with ffn_num_layers = 2 and no dropout, train.py:55-74 with MSELoss): replaces the ~25 small torch ops

@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get('WDMPNN_LIB', os.path.join(HERE, 'libwdmpnn.so'))
 ACTIVATIONS = {'ReLU': 0, 'LeakyReLU': 1, 'PReLU': 2, 'tanh': 3, 'SELU': 4, 'ELU': 5}
 ACT_IDENTITY = 6
 AGGREGATIONS = {'mean': 0, 'sum': 1, 'norm': 2}
-ABI_VERSION = 9
+ABI_VERSION = 10
 GRAPH_LEAN = 1  # WDMPNN_GRAPH_LEAN
 GRAPH_NO_PLANES = 2  # WDMPNN_GRAPH_NO_PLANES
 ERR_UNSUPPORTED = -1003  # WD_ERR_UNSUPPORTED
@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace
                     'wdmpnn_saved_layout', 'wdmpnn_graph_bytes', 'wdmpnn_build_graph', 'wdmpnn_adam_step', 'wdmpnn_head_mse', 'wdmpnn_scale', 'wdmpnn_build_graph_ex',
                     'wdmpnn_forward_many', 'wdmpnn_feed_slot_bytes', 'wdmpnn_feed_create', 'wdmpnn_feed_next',
                     'wdmpnn_feed_release', 'wdmpnn_feed_forward_workspace_bytes', 'wdmpnn_feed_forward',
-                    'wdmpnn_feed_destroy')
+                    'wdmpnn_feed_destroy', 'wdmpnn_adam_step_repack')
 
 
 class WdCsr(Structure):
@@ -173,6 +173,8 @@ def lib() -> ctypes.CDLL:
     L.wdmpnn_feed_destroy.argtypes = [c_void_p]
     L.wdmpnn_scale.argtypes = [POINTER(c_void_p), POINTER(c_int64), c_int32, c_void_p, c_void_p]
     L.wdmpnn_adam_step.argtypes = [POINTER(WdAdamTensor), c_int32, POINTER(WdAdamHyper), c_void_p]
+    L.wdmpnn_adam_step_repack.argtypes = [POINTER(WdAdamTensor), c_int32, POINTER(WdAdamHyper), POINTER(WdGraph),
+                                          POINTER(WdParams), POINTER(WdConfig), c_void_p, c_size_t, c_void_p]
     L.wdmpnn_event_pool_create.argtypes = [c_int32, POINTER(c_void_p)]
     L.wdmpnn_event_pool_destroy.argtypes = [c_void_p]
     L.wdmpnn_event_pool_elapsed_ms.argtypes = [c_void_p, c_int32, c_int32, POINTER(c_float)]
@@ -182,7 +184,7 @@ def lib() -> ctypes.CDLL:
                'wdmpnn_build_bond_features', 'wdmpnn_adam_step', 'wdmpnn_head_mse', 'wdmpnn_scale', 'wdmpnn_build_graph_ex') + \
             ('wdmpnn_forward_many', 'wdmpnn_feed_slot_bytes', 'wdmpnn_feed_create', 'wdmpnn_feed_next',
              'wdmpnn_feed_release', 'wdmpnn_feed_forward_workspace_bytes', 'wdmpnn_feed_forward',
-             'wdmpnn_feed_destroy'):
+             'wdmpnn_feed_destroy', 'wdmpnn_adam_step_repack'):
         getattr(L, fn).restype = c_int
     v = L.wdmpnn_abi_version()
     if v != ABI_VERSION:

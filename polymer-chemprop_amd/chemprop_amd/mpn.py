@@ -187,7 +187,7 @@ class MPNEncoder(nn.Module):
         state = self.__dict__.copy()
         for k in ('_ws_by_stream', '_many_plan'):
             state.pop(k, None)
-        state.update(_pack_cache=None, _infer_configs={}, _plan_token=object())
+        state.update(_pack_cache=None, _train_pack=None, _infer_configs={}, _plan_token=object())
         return state
 
     def _config(self, save: bool) -> _native.WdConfig:
@@ -289,9 +289,35 @@ class MPNEncoder(nn.Module):
         gs = self._graph_struct(dg)
         params = [_f32(t) for t in base[:6]] + [None, None, _f32(base[8])]
         cfg = self._config(True)
-        pstruct, packed, pack = self._packed_params(gs, cfg, params, device, cache=False, defer=True)
+        pstruct, packed, pack = self._train_pack_for(gs, cfg, params, device)
         out, ws, ws_bytes = _forward_call(gs, cfg, pstruct, self.hidden_size, device, pre_launch=pack)
         return out, (gs, cfg, pstruct, ws, ws_bytes, packed, dg)
+
+    def _train_pack_for(self, gs, cfg, params, device):
+        """The direct training step's packed weights: one persistent buffer, rewritten by the optimizer's
+        own pass when it is a :class:`train.HipAdam` step through ``wdmpnn_adam_step_repack`` (which then
+        re-keys it to the parameters' post-step state); packed afresh (the returned launch, enqueued before
+        the forward) whenever the key differs -- the first step, a parameter written any other way (version
+        counters, another optimizer's step), other feature sizes or another stream."""
+        sid = _native.current_stream(device)
+        key = (tuple((t.data_ptr(), t._version) if t is not None else None for t in params), _OPT_STEPS[0],
+               self._parameters['cached_zero_vector'].data_ptr(), gs.atom_fdim, gs.bond_fdim, gs.desc_dim,
+               gs.atom_messages, device, sid)
+        tp = self.__dict__.get('_train_pack')
+        if tp is not None and tp['key'] == key:
+            tp['gs'], tp['cfg'] = gs, cfg
+            return tp['p'], tp['buf'], None
+        pstruct, buf, launch = self._packed_params(gs, cfg, params, device, cache=False, defer=True)
+        buf.zero_()  # (the layout's alignment gaps too: a repacked buffer is bytewise a fresh pack)
+        self._train_pack = {'key': key, 'p': pstruct, 'buf': buf, 'gs': gs, 'cfg': cfg,
+                            'ptrs': frozenset(t.data_ptr() for t in params[:6] if t is not None)}
+        return pstruct, buf, launch
+
+    def _repacked_by_optimizer(self, tp) -> None:
+        """Called by HipAdam after ``wdmpnn_adam_step_repack`` rewrote ``tp['buf']`` from the updated
+        weights: valid at the optimizer-step count the step's post hook is about to set."""
+        k = tp['key']
+        tp['key'] = k[:1] + (_OPT_STEPS[0] + 1,) + k[2:]
 
     def _train_backward(self, state, dout, grads) -> None:
         """wdmpnn_backward of a :meth:`_train_forward` into ``grads`` (name -> tensor, WdGrads names)."""
@@ -441,6 +467,7 @@ class MPNEncoder(nn.Module):
         """Drop the cached padded weights.  Needed only after writing the parameters in a way that
         bypasses both their version counters and ``torch.optim`` (e.g. ``p.data.copy_(...)``)."""
         self._pack_cache = None
+        self._train_pack = None
 
     def _packed_params(self, gs, cfg, params, device, cache=True, stream=None, defer=False, sid=None):
         """WdParams + the padded weight copies (wdmpnn_pack_params).  Inference caches them per

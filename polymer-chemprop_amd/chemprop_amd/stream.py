@@ -284,6 +284,7 @@ class NativeFeed:
                 stream = torch.cuda.current_stream(self.device)
                 if prev is not None:
                     prev.expired = True
+                    prev._streams = set()  # (so the inference path's stream check reaches use_on, which raises)
                 check(L.wdmpnn_feed_release(self.handle, stream.cuda_stream), 'feed release')
                 g = self._native.WdGraph()
                 info = self._native.WdFeedBatch()

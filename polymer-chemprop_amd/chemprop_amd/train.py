@@ -72,6 +72,11 @@ def get_loss_func(dataset_type: str) -> nn.Module:
     raise ValueError(f'Dataset type "{dataset_type}" not supported.')
 
 
+# the direct training step's packed weights rewritten by HipAdam's own pass (wdmpnn_adam_step_repack);
+# False: a pack launch before every training forward (the A/B and test switch)
+ADAM_REPACK = True
+
+
 class HipAdam(Optimizer):
     """torch.optim.Adam / AdamW (no amsgrad, no maximize) whose update is ONE HIP launch per 16
     parameters (``wdmpnn_adam_step``): torch's fused Adam kernel took 40 us per training step for the
@@ -87,6 +92,15 @@ class HipAdam(Optimizer):
         super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
         self.decoupled = bool(decoupled)
         self._tables = {}  # parameter pointers of one launch -> its ctypes tensor table
+        self._repack = None  # (encoder, its training pack) for the next step (train_step's direct path)
+
+    def repack_next(self, encoder) -> None:
+        """Have the next :meth:`step` also rewrite ``encoder``'s training pack (the packed weight copies its
+        direct training forward reads) from the updated weights, instead of a pack launch before the next
+        forward (``wdmpnn_adam_step_repack``).  No effect unless the encoder's six weights are updated in
+        one call of that step."""
+        tp = encoder.__dict__.get('_train_pack')
+        self._repack = (encoder, tp) if tp is not None and ADAM_REPACK else None
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -97,6 +111,7 @@ class HipAdam(Optimizer):
                 loss = closure()
         L = _native.lib()
         state = self.state
+        rp, self._repack = self._repack, None
         for group in self.param_groups:
             ps = [(p, state[p]) for p in group['params'] if p.grad is not None]
             if not ps:
@@ -130,8 +145,18 @@ class HipAdam(Optimizer):
                     st['step'] = step
                 h = _native.WdAdamHyper(float(group['lr']), float(group['betas'][0]), float(group['betas'][1]),
                                         float(group['eps']), float(group['weight_decay']), step, int(self.decoupled))
-                _native.check(L.wdmpnn_adam_step(tab, len(sub), ctypes.byref(h), _native.current_stream(sub[0][0].device)),
-                              'adam step')
+                sid = _native.current_stream(sub[0][0].device)
+                if rp is not None and rp[1]['ptrs'] <= frozenset(key) and rp[1]['key'][-1] == sid:
+                    enc, tp = rp
+                    rp = None
+                    rc = L.wdmpnn_adam_step_repack(tab, len(sub), ctypes.byref(h), ctypes.byref(tp['gs']),
+                                                   ctypes.byref(tp['p']), ctypes.byref(tp['cfg']), tp['buf'].data_ptr(),
+                                                   tp['buf'].numel(), sid)
+                    if rc != _native.ERR_UNSUPPORTED:
+                        _native.check(rc, 'adam step + repack')
+                        enc._repacked_by_optimizer(tp)
+                        continue
+                _native.check(L.wdmpnn_adam_step(tab, len(sub), ctypes.byref(h), sid), 'adam step')
         return loss
 
     def load_state_dict(self, state_dict) -> None:
@@ -493,6 +518,8 @@ def train_step(model: nn.Module, mol_batch, target_batch, loss_func: Callable, o
         bucket.finish_allreduce()
     if grad_clip:
         nn.utils.clip_grad_norm_(model.parameters(), grad_clip)
+    if enc is not None and isinstance(optimizer, HipAdam):
+        optimizer.repack_next(enc)
     optimizer.step()
     if scheduler is not None and isinstance(scheduler, (NoamLR, torch.optim.lr_scheduler.CosineAnnealingLR,
                                                         torch.optim.lr_scheduler.CyclicLR)):

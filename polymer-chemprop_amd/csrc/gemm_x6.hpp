@@ -26,6 +26,11 @@
 
 namespace wd {
 
+// experiment builds: per-chunk stamps of gemm_x6_kernel (1) or gemm_tn_x6_kernel (2), with WD_STAMPS
+#ifndef WD_STAMP_GEMM
+#define WD_STAMP_GEMM 0
+#endif
+
 struct X6Params {
     const float *a0; int lda0; int ka0;   // A segment 0 [Mp][lda0], K extent ka0 (multiple of BK)
     const float *a1; int lda1; int ka1;   // A segment 1 (ka1 = 0: absent)
@@ -133,11 +138,15 @@ __global__ __launch_bounds__(4 * BM) void gemm_x6_kernel(X6Params P) {
     store_chunk(R0, lds);
     __syncthreads();
     auto step = [&](int kc, Regs &Rnext, Regs &Rfree) {
+        if (WD_STAMP_GEMM == 1 && wave == 0) wd_lstamp(kc, 0);
         load_chunk(Rfree, min(kc + 2, nchunks - 1));
         __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this chunk's MFMAs
         compute(lds + (kc & 1) * STAGE);
+        if (WD_STAMP_GEMM == 1 && wave == 0) wd_lstamp(kc, 1);
         if (kc + 1 < nchunks) store_chunk(Rnext, lds + ((kc + 1) & 1) * STAGE);
+        if (WD_STAMP_GEMM == 1 && wave == 0) wd_lstamp(kc, 2);
         __syncthreads();
+        if (WD_STAMP_GEMM == 1 && wave == 0) wd_lstamp(kc, 3);
     };
     int kc = 0;
     for (; kc + 1 < nchunks; kc += 2) {
@@ -209,12 +218,28 @@ struct TnX6Params {
 // a runtime switch over all of them in the staging path bloated the kernel past the instruction cache),
 // -1 when no operand is SEG_ACT.  BEXT: the bias sums come from P.bias_src (a compile-time switch: a runtime
 // branch around those loads left the compiler's vmcnt waits unable to skip the prefetched chunk's loads)
-template <int SACT, bool BEXT>
+#ifndef WD_TN_DEPTH
+#define WD_TN_DEPTH 2
+#endif
+#ifndef WD_TN_H2
+#define WD_TN_H2 0
+#endif
+constexpr bool TN_H2 = WD_TN_H2;
+constexpr int TN_DEPTH = WD_TN_DEPTH;
+// H2: the operands as fp16 hi/lo pairs (planes.hpp split_h2) instead of bf16x3 planes -- two planes per
+// operand, three f16 products (hh hl lh) instead of six.  fp16 needs a scale: each of the tile's 128
+// operand columns gets its own power-of-two scale from its max |value| over this split's rows (a max pass
+// over the split's rows before the GEMM: the values staged are exactly the values maxed, so nothing can
+// overflow), and the epilogue multiplies each output by the inverse scales of its row and column (exact:
+// powers of two).  Error per product <= 2^-22 of the column maxima (planes.hpp); deterministic.
+template <int SACT, bool BEXT, bool H2>
 __global__ __launch_bounds__(256) void gemm_tn_x6_kernel(TnX6Params P) {
     constexpr int BM = 64, BN = 64, NT = 256, BKC = 32;
     constexpr int PL = 32 * 128;           // one plane image: 32 rows (m) x 64 columns x 2 B
-    constexpr int STAGE = 6 * PL;          // A planes, then B planes (24 KB)
+    constexpr int NPL = H2 ? 2 : 3;        // planes per operand
+    constexpr int STAGE = 2 * NPL * PL;    // A planes, then B planes (24 KB; 16 KB with H2)
     __shared__ __attribute__((aligned(16))) uint8_t lds[2 * STAGE];
+    __shared__ float inv_scale[H2 ? 128 : 1];  // H2: A columns (output rows), then B columns
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wi = wave >> 1, wj = wave & 1, g = lane >> 4, i16 = lane & 15;
     // 1-D grid of tiles x splits, XCD-aware (common.hpp xcd_tile): the tiles of one split (same rows of
@@ -249,7 +274,7 @@ __global__ __launch_bounds__(256) void gemm_tn_x6_kernel(TnX6Params P) {
     // LDS byte offsets of this thread's 8-byte pieces (rows 4 h4 + s, columns 4q .. 4q+3) in plane 0
     int dst[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) dst[r] = (isA ? 0 : 3 * PL) + tn_unit(4 * h4 + r, q);
+    for (int r = 0; r < 4; ++r) dst[r] = (isA ? 0 : NPL * PL) + tn_unit(4 * h4 + r, q);
     // branch-free loads: every lane loads (rows past kend clamped to the last row, dead columns from a valid
     // dummy address) and the values are masked when staged, so the loads pipeline ahead of the MFMAs
     const float *abase = live ? sg.src + kk : P.A.s[0].src;
@@ -297,18 +322,27 @@ __global__ __launch_bounds__(256) void gemm_tn_x6_kernel(TnX6Params P) {
             }
         }
     };
+    float csc[4] = {1.f, 1.f, 1.f, 1.f};  // H2: this thread's column scales
     auto store_chunk = [&](Regs &R, int kc, uint8_t *stg) {
         mask_rows(R, kc);
         act_rows(R, kc);
-        // row s of the 4x4 block: columns 4q .. 4q+3 -> three packed pairs per plane
+        // row s of the 4x4 block: columns 4q .. 4q+3 -> packed pairs per plane
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            uint32_t h0, md0, l0, h1, md1, l1;
-            split_pair(R.v[r].x, R.v[r].y, h0, md0, l0);
-            split_pair(R.v[r].z, R.v[r].w, h1, md1, l1);
-            *reinterpret_cast<uint2 *>(stg + dst[r]) = make_uint2(h0, h1);
-            *reinterpret_cast<uint2 *>(stg + dst[r] + PL) = make_uint2(md0, md1);
-            *reinterpret_cast<uint2 *>(stg + dst[r] + 2 * PL) = make_uint2(l0, l1);
+            if constexpr (H2) {
+                uint32_t h0, l0, h1, l1;
+                split_h2(R.v[r].x, R.v[r].y, csc[0], csc[1], h0, l0);
+                split_h2(R.v[r].z, R.v[r].w, csc[2], csc[3], h1, l1);
+                *reinterpret_cast<uint2 *>(stg + dst[r]) = make_uint2(h0, h1);
+                *reinterpret_cast<uint2 *>(stg + dst[r] + PL) = make_uint2(l0, l1);
+            } else {
+                uint32_t h0, md0, l0, h1, md1, l1;
+                split_pair(R.v[r].x, R.v[r].y, h0, md0, l0);
+                split_pair(R.v[r].z, R.v[r].w, h1, md1, l1);
+                *reinterpret_cast<uint2 *>(stg + dst[r]) = make_uint2(h0, h1);
+                *reinterpret_cast<uint2 *>(stg + dst[r] + PL) = make_uint2(md0, md1);
+                *reinterpret_cast<uint2 *>(stg + dst[r] + 2 * PL) = make_uint2(l0, l1);
+            }
         }
         if (bias) {
 #pragma unroll
@@ -324,44 +358,115 @@ __global__ __launch_bounds__(256) void gemm_tn_x6_kernel(TnX6Params P) {
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
     auto compute = [&](const uint8_t *stg) {
-        bf16x8 af[2][3], bfr[2][3];
+        bf16x8 af[2][NPL], bfr[2][NPL];
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
+        for (int p = 0; p < NPL; ++p) {
 #pragma unroll
             for (int a = 0; a < 2; ++a) af[a][p] = tn_frag(stg + p * PL, wi * 32 + a * 16, lane);
 #pragma unroll
-            for (int b = 0; b < 2; ++b) bfr[b][p] = tn_frag(stg + 3 * PL + p * PL, wj * 32 + b * 16, lane);
+            for (int b = 0; b < 2; ++b) bfr[b][p] = tn_frag(stg + NPL * PL + p * PL, wj * 32 + b * 16, lane);
         }
-        constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};
+        if constexpr (H2) {  // hh, hl, lh on fp16 (the same bits read as f16x8)
+            constexpr int PA[3] = {0, 0, 1}, PB[3] = {0, 1, 0};
 #pragma unroll
-        for (int t = 0; t < 6; ++t)
+            for (int t = 0; t < 3; ++t)
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+                for (int a = 0; a < 2; ++a)
 #pragma unroll
-                for (int b = 0; b < 2; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][PA[t]], bfr[b][PB[t]], acc[a][b], 0, 0, 0);
+                    for (int b = 0; b < 2; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[a][PA[t]]),
+                                                                           __builtin_bit_cast(f16x8, bfr[b][PB[t]]),
+                                                                           acc[a][b], 0, 0, 0);
+        } else {
+            constexpr int PA[6] = {0, 0, 1, 0, 2, 1}, PB[6] = {0, 1, 0, 2, 0, 1};
+#pragma unroll
+            for (int t = 0; t < 6; ++t)
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+                        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a][PA[t]], bfr[b][PB[t]], acc[a][b], 0, 0, 0);
+        }
     };
+    if constexpr (H2) {
+        // max pass: |value| per column over the split's rows (as staged: masked, activated), two chunks of
+        // loads in flight; then per column over the 8 row groups through LDS -> scale and inverse scale
+        uint32_t cm[4] = {0u, 0u, 0u, 0u};
+        auto maxv = [&](Regs &R, int kc) {
+            mask_rows(R, kc);
+            act_rows(R, kc);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                cm[0] = max(cm[0], absbits(R.v[r].x)); cm[1] = max(cm[1], absbits(R.v[r].y));
+                cm[2] = max(cm[2], absbits(R.v[r].z)); cm[3] = max(cm[3], absbits(R.v[r].w));
+            }
+        };
+        auto load_v = [&](Regs &R, int kc) {
+            const int r0 = kbeg + kc * BKC + 4 * h4;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) R.v[s] = ld4(abase + (size_t)min(r0 + s, rlast) * ald);
+        };
+#ifndef WD_TN_NOMAX
+        if (nchunks > 0) {
+#else
+        if (false) {
+#endif
+            Regs M0, M1;
+            load_v(M0, 0);
+            load_v(M1, min(1, nchunks - 1));
+            int kc = 0;
+            for (; kc + 1 < nchunks; kc += 2) {
+                maxv(M0, kc);
+                load_v(M0, min(kc + 2, nchunks - 1));
+                maxv(M1, kc + 1);
+                load_v(M1, min(kc + 3, nchunks - 1));
+            }
+            if (kc < nchunks) maxv(M0, kc);
+        }
+        uint32_t *cw = reinterpret_cast<uint32_t *>(lds);  // [2 operands][8 row groups][64 columns]
+#pragma unroll
+        for (int c = 0; c < 4; ++c) cw[(isA ? 0 : 512) + h4 * 64 + 4 * q + c] = cm[c];
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int h = 0; h < 8; ++h) m = max(m, cw[(isA ? 0 : 512) + h * 64 + 4 * q + c]);
+            csc[c] = h2_scale(m);
+            if (h4 == 0) inv_scale[(isA ? 0 : 64) + 4 * q + c] = h2_inv_scale(m);
+        }
+        __syncthreads();  // (the words are overwritten by the first chunk's staging)
+    }
     if (nchunks > 0) {
-        Regs R0, R1;
-        load_chunk(R0, 0);
-        load_chunk(R1, min(1, nchunks - 1));
-        store_chunk(R0, 0, lds);
+        // TN_DEPTH chunks in flight in registers: at step kc chunk kc is in LDS, kc+1 .. kc+D-1 are loading
+        // (or landed) in the ring, and kc+D is issued into the set chunk kc left
+        constexpr int D = TN_DEPTH;
+        Regs R[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) load_chunk(R[i], min(i, nchunks - 1));
+        store_chunk(R[0], 0, lds);
         __syncthreads();
         auto step = [&](int kc, Regs &Rnext, Regs &Rfree) {
+            if (WD_STAMP_GEMM == 2 && BEXT && wave == 0) wd_lstamp(kc, 0);
             // unconditional (the last chunk is reloaded past the end): a skipped load on some path made
             // the compiler's waits for the older chunk drain the fresh prefetch too
-            load_chunk(Rfree, min(kc + 2, nchunks - 1));
+            load_chunk(Rfree, min(kc + D, nchunks - 1));
             __builtin_amdgcn_sched_barrier(0);
             compute(lds + (kc & 1) * STAGE);
+            if (WD_STAMP_GEMM == 2 && BEXT && wave == 0) wd_lstamp(kc, 1);
             if (kc + 1 < nchunks) store_chunk(Rnext, kc + 1, lds + ((kc + 1) & 1) * STAGE);
+            if (WD_STAMP_GEMM == 2 && BEXT && wave == 0) wd_lstamp(kc, 2);
             __syncthreads();
+            if (WD_STAMP_GEMM == 2 && BEXT && wave == 0) wd_lstamp(kc, 3);
         };
         int kc = 0;
-        for (; kc + 1 < nchunks; kc += 2) {
-            step(kc, R1, R0);
-            step(kc + 1, R0, R1);
+        for (; kc + D - 1 < nchunks; kc += D) {
+#pragma unroll
+            for (int i = 0; i < D; ++i) step(kc + i, R[(i + 1) % D], R[i]);
         }
-        if (kc < nchunks) step(kc, R1, R0);
+#pragma unroll
+        for (int i = 0; i < D - 1; ++i)
+            if (kc + i < nchunks) step(kc + i, R[(i + 1) % D], R[i]);
     }
     // epilogue: C tile through LDS, coalesced float4 stores into this split's slab (accumulating over
     // the layers of W_h when asked); the bias sums through LDS in row-group order
@@ -372,7 +477,10 @@ __global__ __launch_bounds__(256) void gemm_tn_x6_kernel(TnX6Params P) {
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) cl[(wi * 32 + a * 16 + 4 * g + r) * LDC + wj * 32 + b * 16 + i16] = acc[a][b][r];
+            for (int r = 0; r < 4; ++r) {
+                const int i = wi * 32 + a * 16 + 4 * g + r, j = wj * 32 + b * 16 + i16;
+                cl[i * LDC + j] = H2 ? acc[a][b][r] * inv_scale[i] * inv_scale[64 + j] : acc[a][b][r];
+            }
     float *bl = cl + BM * LDC;  // [8 row groups][64 columns]
     if (bias) {
 #pragma unroll

@@ -603,91 +603,156 @@ __global__ __launch_bounds__(256) void build_bond_features_kernel(const float *_
 // Adam: L2 weight decay folded into the gradient (AdamW: decoupled, on the parameter), moments as
 // beta * m + (1 - beta) * g, denom = sqrt(v) / sqrt(bc2) + eps, p -= (lr / bc1) * m / denom.
 namespace wd {
-constexpr int ADAM_MAX = 16, ADAM_PER_BLOCK = 1024, ADAM_OUTS = 20;
-// An extra destination of a tensor's updated values (wdmpnn_adam_step_repack: the training step's packed
+constexpr int ADAM_MAX = 16, ADAM_PER_BLOCK = 1024, ADAM_OUTS = 16, ADAM_TJ = 6, ADAM_TILE = 32;
+// An extra destination of a weight's updated values (wdmpnn_adam_step_repack: the training step's packed
 // weight copies written by the optimizer itself instead of a repack before the next forward).  Source
-// element (r, c) of a [rows][cols] tensor, for the column segment s holding c (c in [sc0[s], sc0[s] + K[s])):
+// element (r, c) of a [rows][cols] weight, for the column segment s holding c (c in [sc0[s], sc0[s] + K[s])):
 //   AO_PLAIN      dst[r * ld + dc0[s] + c - sc0[s]]            (pack_kernel's plain jobs)
 //   AO_TRANSPOSE  dst[(c - sc0[s]) * ld + r]                   (its transposes)
-//   AO_PLANES     bf16x3 plane tiles of the padded plain matrix (row blocks of br, kp padded columns), the
-//                 value split exactly as split_pair / x6_store8 split it
+//   AO_PLANES     bf16x3 plane tiles of the padded plain matrix (row blocks of br, kp = ld padded columns),
+//                 the value split exactly as split_pair / x6_store8 split it
 enum { AO_PLAIN = 0, AO_TRANSPOSE = 1, AO_PLANES = 2 };
 struct AdamOut {
     void *dst;
     int kind, ld, nseg, br;
     int sc0[2], dc0[2], K[2];
 };
+// a repacked weight, updated in 32 x 32 tiles (one workgroup each): the transposed copies leave through
+// LDS as whole 128-byte rows, and each tile publishes max |w| (W_h's fp16-pair scale) as one word
+struct AdamTileJob {
+    int t;                  // its tensor in AdamLaunch::t
+    int rows, cols, tiles_c, blk0;
+    int o0, o1;             // its outputs out[o0 .. o1)
+    uint32_t *amax;         // one word per tile, or null
+};
 struct AdamLaunch {
     WdAdamTensor t[ADAM_MAX];
-    int blk0[ADAM_MAX + 1];
+    int blk0[ADAM_MAX + 1];  // element-wise blocks per tensor (none for a tile job's tensor)
     int n;
     float beta1, beta2, eps, wd, lr, step_size, bc2_sqrt;
     int decoupled;
-    // repack (optional): tensor k's outputs out[o0[k] .. o0[k + 1]), its column count, and where its
-    // workgroups publish max |p| (one word per workgroup, or null)
+    AdamTileJob tj[ADAM_TJ];
+    int ntj, tile_blocks;    // tile blocks first, then the element-wise blocks
     AdamOut out[ADAM_OUTS];
-    int o0[ADAM_MAX + 1];
-    int cols[ADAM_MAX];
-    uint32_t *amax[ADAM_MAX];
 };
 
-__device__ __forceinline__ void adam_out(const AdamOut &O, int64_t r, int c, float v) {
-    int s = 0;
-    if (O.nseg > 1 && c >= O.sc0[1]) s = 1;
-    const int cc = c - O.sc0[s];
-    if (cc < 0 || cc >= O.K[s]) return;
-    if (O.kind == AO_PLAIN) {
-        reinterpret_cast<float *>(O.dst)[r * O.ld + O.dc0[s] + cc] = v;
-    } else if (O.kind == AO_TRANSPOSE) {
-        reinterpret_cast<float *>(O.dst)[(int64_t)cc * O.ld + r] = v;
-    } else {
-        const int k = O.dc0[s] + cc;
-        const uint32_t h = cvt_pk_bf16(v, 0.f);
-        const float v1 = v - bf_lo(h);
-        const uint32_t m = cvt_pk_bf16(v1, 0.f);
-        const uint32_t l = cvt_pk_bf16(v1 - bf_lo(m), 0.f);
-        uint8_t *d = reinterpret_cast<uint8_t *>(O.dst) + ((r / O.br) * (O.ld >> 5) + (k >> 5)) * (3 * O.br * 64) +
-                     (r % O.br) * 64 + 2 * (k & 31);
-        *reinterpret_cast<uint16_t *>(d) = (uint16_t)h;
-        *reinterpret_cast<uint16_t *>(d + O.br * 64) = (uint16_t)m;
-        *reinterpret_cast<uint16_t *>(d + 2 * O.br * 64) = (uint16_t)l;
+// one element's update (torch.optim.Adam / AdamW): p, m, v in place from p, g, m, v
+__device__ __forceinline__ void adam_math(const AdamLaunch &A, float &p, float g, float &m, float &v) {
+#pragma clang fp contract(off)
+    if (A.wd != 0.f) {
+        if (A.decoupled) p -= A.lr * A.wd * p;
+        else g += p * A.wd;
     }
+    m = A.beta1 * m + (1.f - A.beta1) * g;
+    v = A.beta2 * v + (1.f - A.beta2) * g * g;
+    const float denom = sqrtf(v) / A.bc2_sqrt + A.eps;
+    p = p - A.step_size * m / denom;
+}
+
+__device__ __forceinline__ int ao_seg(const AdamOut &O, int c) { return O.nseg > 1 && c >= O.sc0[1] ? 1 : 0; }
+
+__device__ void adam_tile(const AdamLaunch &A, int b) {
+    __shared__ float tl[ADAM_TILE][ADAM_TILE + 1];  // [source column][source row]
+    __shared__ uint32_t red[4];
+    int j = 0;
+    while (j + 1 < A.ntj && b >= A.tj[j + 1].blk0) ++j;
+    const AdamTileJob &J = A.tj[j];
+    const WdAdamTensor &T = A.t[J.t];
+    const int tile = b - J.blk0, tr = tile / J.tiles_c, tc = tile % J.tiles_c;
+    const int lr = threadIdx.x >> 3, lc = 4 * (threadIdx.x & 7);
+    const int r = tr * ADAM_TILE + lr;
+    uint32_t mx = 0;
+    bool transposes = false;
+    // all four elements' operands loaded before any store (the stores could alias the loads of the next
+    // element as far as the compiler knows: interleaved, each element paid a memory latency)
+    float pv[4], gv[4], mv[4], vv[4];
+    const int64_t i0 = (int64_t)r * J.cols + tc * ADAM_TILE + lc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const bool ok = r < J.rows && tc * ADAM_TILE + lc + q < J.cols;
+        const int64_t i = ok ? i0 + q : 0;
+        pv[q] = T.param[i]; gv[q] = T.grad[i]; mv[q] = T.exp_avg[i]; vv[q] = T.exp_avg_sq[i];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) adam_math(A, pv[q], gv[q], mv[q], vv[q]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int c = tc * ADAM_TILE + lc + q;
+        float pn = 0.f;
+        if (r < J.rows && c < J.cols) {
+            pn = pv[q];
+            T.param[i0 + q] = pn;
+            T.exp_avg[i0 + q] = mv[q];
+            T.exp_avg_sq[i0 + q] = vv[q];
+            mx = max(mx, absbits(pn));
+            for (int o = J.o0; o < J.o1; ++o) {
+                const AdamOut &O = A.out[o];
+                const int s = ao_seg(O, c), cc = c - O.sc0[s];
+                if (O.kind == AO_TRANSPOSE || cc < 0 || cc >= O.K[s]) continue;
+                if (O.kind == AO_PLAIN) {
+                    reinterpret_cast<float *>(O.dst)[(int64_t)r * O.ld + O.dc0[s] + cc] = pn;
+                } else {
+                    const int k = O.dc0[s] + cc;
+                    const uint32_t h = cvt_pk_bf16(pn, 0.f);
+                    const float v1 = pn - bf_lo(h);
+                    const uint32_t m = cvt_pk_bf16(v1, 0.f);
+                    const uint32_t l = cvt_pk_bf16(v1 - bf_lo(m), 0.f);
+                    uint8_t *d = reinterpret_cast<uint8_t *>(O.dst) +
+                                 ((int64_t)(r / O.br) * (O.ld >> 5) + (k >> 5)) * (3 * O.br * 64) + (r % O.br) * 64 +
+                                 2 * (k & 31);
+                    *reinterpret_cast<uint16_t *>(d) = (uint16_t)h;
+                    *reinterpret_cast<uint16_t *>(d + O.br * 64) = (uint16_t)m;
+                    *reinterpret_cast<uint16_t *>(d + 2 * O.br * 64) = (uint16_t)l;
+                }
+            }
+        }
+        tl[lc + q][lr] = pn;
+    }
+    for (int o = J.o0; o < J.o1; ++o) transposes |= A.out[o].kind == AO_TRANSPOSE;
+    if (transposes) {  // (uniform) column lc8 of the tile as 4 consecutive rows of the transposed copy
+        __syncthreads();
+        const int cl = threadIdx.x >> 3, rl = 4 * (threadIdx.x & 7);
+        const int c = tc * ADAM_TILE + cl;
+        for (int o = J.o0; o < J.o1; ++o) {
+            const AdamOut &O = A.out[o];
+            if (O.kind != AO_TRANSPOSE) continue;
+            const int s = ao_seg(O, c), cc = c - O.sc0[s];
+            if (c >= J.cols || cc < 0 || cc >= O.K[s]) continue;
+            float *d = reinterpret_cast<float *>(O.dst) + (int64_t)cc * O.ld + tr * ADAM_TILE + rl;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (tr * ADAM_TILE + rl + q < J.rows) d[q] = tl[cl][rl + q];
+        }
+    }
+    if (J.amax) publish_max(mx, J.amax + tile, red);  // (uniform per workgroup)
 }
 
 template <bool REPACK>
 __global__ __launch_bounds__(256) void adam_kernel(AdamLaunch A) {
-    const int b = blockIdx.x;
+    int b = blockIdx.x;
+    if (REPACK) {
+        if (b < A.tile_blocks) {
+            adam_tile(A, b);
+            return;
+        }
+        b -= A.tile_blocks;
+    }
     int k = 0;
     while (k + 1 < A.n && b >= A.blk0[k + 1]) ++k;
     const WdAdamTensor &T = A.t[k];
     const int64_t i0 = (int64_t)(b - A.blk0[k]) * ADAM_PER_BLOCK + threadIdx.x;
-    uint32_t mx = 0;
+    constexpr int PT = ADAM_PER_BLOCK / 256;
+    float pv[PT], gv[PT], mv[PT], vv[PT];
 #pragma unroll
-    for (int j = 0; j < ADAM_PER_BLOCK / 256; ++j) {
-        const int64_t i = i0 + 256 * j;
-        if (i >= T.numel) break;
-        float p = T.param[i], g = T.grad[i];
-        if (A.wd != 0.f) {
-            if (A.decoupled) p -= A.lr * A.wd * p;
-            else g += p * A.wd;
-        }
-        const float m = A.beta1 * T.exp_avg[i] + (1.f - A.beta1) * g;
-        const float v = A.beta2 * T.exp_avg_sq[i] + (1.f - A.beta2) * g * g;
-        T.exp_avg[i] = m;
-        T.exp_avg_sq[i] = v;
-        const float denom = sqrtf(v) / A.bc2_sqrt + A.eps;
-        const float pn = p - A.step_size * m / denom;
-        T.param[i] = pn;
-        if (REPACK) {
-            const int64_t r = i / A.cols[k];
-            const int c = (int)(i % A.cols[k]);
-            for (int o = A.o0[k]; o < A.o0[k + 1]; ++o) adam_out(A.out[o], r, c, pn);
-            mx = max(mx, absbits(pn));
-        }
+    for (int j = 0; j < PT; ++j) {  // (loads first: see adam_tile)
+        const int64_t i = min(i0 + 256 * j, T.numel - 1);
+        pv[j] = T.param[i]; gv[j] = T.grad[i]; mv[j] = T.exp_avg[i]; vv[j] = T.exp_avg_sq[i];
     }
-    if (REPACK && A.amax[k]) {  // (uniform per workgroup)
-        __shared__ uint32_t red[4];
-        publish_max(mx, A.amax[k] + (b - A.blk0[k]), red);
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+        const int64_t i = i0 + 256 * j;
+        adam_math(A, pv[j], gv[j], mv[j], vv[j]);
+        if (i < T.numel) { T.param[i] = pv[j]; T.exp_avg[i] = mv[j]; T.exp_avg_sq[i] = vv[j]; }
     }
 }
 }  // namespace wd

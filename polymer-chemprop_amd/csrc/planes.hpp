@@ -228,6 +228,13 @@ __device__ __forceinline__ void split_h2(float a, float b, float s, uint32_t &hi
     hi = __builtin_bit_cast(uint32_t, h);
     lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){ra, rb}, f16x2v));
 }
+// the same with a scale per element (per-column scales of gemm_tn_x6_kernel<H2>)
+__device__ __forceinline__ void split_h2(float a, float b, float sa, float sb, uint32_t &hi, uint32_t &lo) {
+    const f16x2v h = __builtin_convertvector((f32x2v){a * sa, b * sb}, f16x2v);
+    const float ra = fmaf(a, sa, -(float)h[0]), rb = fmaf(b, sb, -(float)h[1]);
+    hi = __builtin_bit_cast(uint32_t, h);
+    lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){ra, rb}, f16x2v));
+}
 
 // workgroup max of a u32 -> one plain store by thread 0 (red: >= blockDim.x / 64 words of LDS; every
 // thread of the workgroup must call it)
@@ -245,12 +252,13 @@ __device__ __forceinline__ void publish_max(uint32_t m, uint32_t *slot, uint32_t
 // fp32 [rows][ld] (first kp columns) -> h2 plane tiles with BR-row blocks: block (r / BR, k / 32) of 2 x
 // BR x 64 bytes (hi plane, then lo), row r % BR, columns k % 32 at 64 (r % BR) + 2 (k % 32) -- the bf16
 // plane-tile layout with two planes.  Scaled by the max of the nw words of `words` (pack_kernel's
-// per-workgroup maxima, nw <= 64), which workgroup 0 also folds into words[nw] for the consumers.
+// per-workgroup maxima, or adam_kernel's), which workgroup 0 also folds into *fold for the consumers.
 __global__ __launch_bounds__(256) void split_h2_kernel(const float *__restrict__ src, int ld, int rows, int kp, int br,
-                                                       uint8_t *__restrict__ dst, uint32_t *words, int nw) {
+                                                       uint8_t *__restrict__ dst, const uint32_t *words, int nw,
+                                                       uint32_t *fold) {
     const uint32_t m = max_words(words, nw);
     const float s = h2_scale(m);
-    if (blockIdx.x == 0 && threadIdx.x == 0) words[nw] = m;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *fold = m;
     const int q8 = kp >> 3;
     const size_t total = (size_t)rows * q8;
     for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {

@@ -195,7 +195,9 @@ PackLayout pack_layout(const Dims &D) {
         L.WoX80 = take((size_t)D.Hk * D.Ko * 3 / 2);
     }
     L.WhH = take((size_t)D.Hk * D.Hk);  // 2 fp16 per value
-    L.amax = take(65);
+    // W_h's h2 scale words: pack_kernel's 64 per-workgroup maxima, their max (word 64, read by the fused
+    // layers), then one word per 32 x 32 tile of W_h from adam_kernel (wdmpnn_adam_step_repack)
+    L.amax = take(65 + (size_t)((D.H + ADAM_TILE - 1) / ADAM_TILE) * ((D.H + (D.atom ? D.Fb : 0) + ADAM_TILE - 1) / ADAM_TILE));
     if (D.atom) {
         L.WiA = take((size_t)3 * D.Hk * (D.Fak + D.Fbk));
         L.WiAX = take((size_t)3 * D.Hk * (D.Fak + D.Fbk) * 3 / 2);
@@ -290,7 +292,7 @@ int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
     WD_CHECK_LAUNCH("pack_params planes");
     // fp16 hi / lo tiles of W_h[:, :Hk] for the fused layers, scaled by its published maximum
     hipLaunchKernelGGL(split_h2_kernel, dim3(ew_blocks((size_t)D.Hk * D.Hk / 8)), dim3(256), 0, st, (const float *)F(L.Wh),
-                       D.ldx, D.Hk, D.Hk, fused_bn(D.Hk), (uint8_t *)(base + L.WhH), wh_amax, 64);
+                       D.ldx, D.Hk, D.Hk, fused_bn(D.Hk), (uint8_t *)(base + L.WhH), wh_amax, 64, wh_amax + 64);
     WD_CHECK_LAUNCH("pack_params h2");
     return 0;
 }
@@ -467,15 +469,16 @@ int gemm_tn(const Src &dZ, const Src &X, int n_out, int m_rows, const TnPlan &tp
         if (X.s[q].kind == SEG_ACT) sact = X.s[q].act;
     if (sact >= 0 && !bias_src) return fail(WD_ERR_ARG, "gemm_tn: a SEG_ACT operand needs its bias source");
     if (bias_src && sact < 0) return fail(WD_ERR_ARG, "gemm_tn: an external bias source goes with a SEG_ACT operand");
+    constexpr bool H2 = TN_H2;
     switch (sact) {
-    case -1: hipLaunchKernelGGL((gemm_tn_x6_kernel<-1, false>), grid, dim3(256), 0, st, P); break;
-    case ACT_RELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_RELU, true>), grid, dim3(256), 0, st, P); break;
-    case ACT_LEAKY: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_LEAKY, true>), grid, dim3(256), 0, st, P); break;
-    case ACT_PRELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_PRELU, true>), grid, dim3(256), 0, st, P); break;
-    case ACT_TANH: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_TANH, true>), grid, dim3(256), 0, st, P); break;
-    case ACT_SELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_SELU, true>), grid, dim3(256), 0, st, P); break;
-    case ACT_ELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_ELU, true>), grid, dim3(256), 0, st, P); break;
-    default: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_IDENTITY, true>), grid, dim3(256), 0, st, P); break;
+    case -1: hipLaunchKernelGGL((gemm_tn_x6_kernel<-1, false, H2>), grid, dim3(256), 0, st, P); break;
+    case ACT_RELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_RELU, true, H2>), grid, dim3(256), 0, st, P); break;
+    case ACT_LEAKY: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_LEAKY, true, H2>), grid, dim3(256), 0, st, P); break;
+    case ACT_PRELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_PRELU, true, H2>), grid, dim3(256), 0, st, P); break;
+    case ACT_TANH: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_TANH, true, H2>), grid, dim3(256), 0, st, P); break;
+    case ACT_SELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_SELU, true, H2>), grid, dim3(256), 0, st, P); break;
+    case ACT_ELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_ELU, true, H2>), grid, dim3(256), 0, st, P); break;
+    default: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_IDENTITY, true, H2>), grid, dim3(256), 0, st, P); break;
     }
     WD_CHECK_LAUNCH("gemm_tn");
     return 0;
@@ -1782,7 +1785,24 @@ int wdmpnn_index_select_rows_backward(const float *grad, int64_t n_index, int64_
     return 0;
 }
 
-int wdmpnn_adam_step(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *h, void *stream) {
+// the encoder weights' packed copies as adam_kernel outputs (wdmpnn_adam_step_repack): the same
+// destinations pack_params writes, element by element
+struct RepackTarget {
+    const float *param;
+    int rows, cols;
+    AdamOut out[6];
+    int nout;
+    uint32_t *amax;  // one word per 32 x 32 tile, or null
+};
+static AdamOut ao(void *dst, int kind, int ld, std::initializer_list<std::array<int, 3>> segs, int br = 0) {
+    AdamOut o{};  // segs: {dst_col0, src_col0, K}
+    o.dst = dst; o.kind = kind; o.ld = ld; o.br = br;
+    for (const auto &g : segs) { o.dc0[o.nseg] = g[0]; o.sc0[o.nseg] = g[1]; o.K[o.nseg] = g[2]; ++o.nseg; }
+    return o;
+}
+
+static int adam_launches(const WdAdamTensor *tensors, int n, const WdAdamHyper *h, hipStream_t st,
+                         const RepackTarget *rt, int nrt, bool *found) {
     if (n < 0 || !h || (n && !tensors)) return fail(WD_ERR_ARG, "null or negative argument");
     if (h->step < 1) return fail(WD_ERR_ARG, "adam step must be >= 1");
     const double bc1 = 1.0 - std::pow((double)h->beta1, (double)h->step);
@@ -1791,14 +1811,30 @@ int wdmpnn_adam_step(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *
         AdamLaunch A{};
         A.beta1 = h->beta1; A.beta2 = h->beta2; A.eps = h->eps; A.wd = h->weight_decay; A.lr = h->lr;
         A.step_size = (float)(h->lr / bc1); A.bc2_sqrt = (float)std::sqrt(bc2); A.decoupled = h->decoupled;
-        int blocks = 0;
+        int blocks = 0, nout = 0;
         for (int i = s; i < n && i < s + ADAM_MAX; ++i) {
             const WdAdamTensor &T = tensors[i];
             if (T.numel < 0) return fail(WD_ERR_ARG, "negative numel");
             if (T.numel == 0) continue;
             if (!T.param || !T.grad || !T.exp_avg || !T.exp_avg_sq) return fail(WD_ERR_ARG, "null tensor pointer");
-            const int64_t nb = (T.numel + ADAM_PER_BLOCK - 1) / ADAM_PER_BLOCK;
-            if (blocks + nb > INT32_MAX / 2) return fail(WD_ERR_SHAPE, "adam launch too large");
+            int64_t nb = (T.numel + ADAM_PER_BLOCK - 1) / ADAM_PER_BLOCK;
+            for (int r = 0; r < nrt; ++r) {  // a repacked weight: tiles instead of element-wise blocks
+                if (!rt[r].param || rt[r].param != T.param) continue;
+                if (found[r]) return fail(WD_ERR_ARG, "adam_step_repack: a weight appears twice");
+                if ((int64_t)rt[r].rows * rt[r].cols != T.numel)
+                    return fail(WD_ERR_SHAPE, "adam_step_repack: weight size %lld, expected %d x %d", (long long)T.numel,
+                                rt[r].rows, rt[r].cols);
+                found[r] = true;
+                AdamTileJob &J = A.tj[A.ntj++];
+                J.t = A.n; J.rows = rt[r].rows; J.cols = rt[r].cols; J.tiles_c = (J.cols + ADAM_TILE - 1) / ADAM_TILE;
+                J.blk0 = A.tile_blocks; J.amax = rt[r].amax;
+                A.tile_blocks += ((J.rows + ADAM_TILE - 1) / ADAM_TILE) * J.tiles_c;
+                J.o0 = nout;
+                for (int o = 0; o < rt[r].nout; ++o) A.out[nout++] = rt[r].out[o];
+                J.o1 = nout;
+                nb = 0;
+            }
+            if (blocks + nb + A.tile_blocks > INT32_MAX / 2) return fail(WD_ERR_SHAPE, "adam launch too large");
             A.t[A.n] = T;
             A.blk0[A.n] = blocks;
             blocks += (int)nb;
@@ -1806,9 +1842,64 @@ int wdmpnn_adam_step(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *
         }
         if (!A.n) continue;
         A.blk0[A.n] = blocks;
-        hipLaunchKernelGGL(adam_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, A);
+        if (A.ntj) hipLaunchKernelGGL(adam_kernel<true>, dim3(A.tile_blocks + blocks), dim3(256), 0, st, A);
+        else hipLaunchKernelGGL(adam_kernel<false>, dim3(blocks), dim3(256), 0, st, A);
         WD_CHECK_LAUNCH("adam");
     }
+    return 0;
+}
+
+int wdmpnn_adam_step(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *h, void *stream) {
+    return adam_launches(tensors, n, h, (hipStream_t)stream, nullptr, 0, nullptr);
+}
+
+int wdmpnn_adam_step_repack(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *h, const WdGraph *g,
+                            const WdParams *p, const WdConfig *c, void *packed, size_t packed_bytes, void *stream) {
+    Dims D;
+    WD_TRY(get_dims(g, p, c, D));
+    if (D.atom || D.desc) return fail(WD_ERR_UNSUPPORTED, "adam_step_repack: bond messages without descriptors only");
+    const PackLayout L = pack_layout(D);
+    if (!packed || packed_bytes < L.total) return fail(WD_ERR_WORKSPACE, "adam_step_repack: packed buffer too small");
+    char *base = (char *)packed;
+    auto F = [&](size_t off) { return (void *)(base + off); };
+    const int H = D.H;
+    const bool b80 = D.Hk % 80 == 0;
+    uint32_t *wh_amax = (uint32_t *)(base + L.amax);
+    RepackTarget rt[6] = {};
+    // (pack_params' jobs, in its order: plain copy, transposes, plane tiles)
+    rt[0] = {p->W_i, H, D.Kin, {}, 0, nullptr};
+    rt[0].out[rt[0].nout++] = ao(F(L.Wi), AO_PLAIN, D.Kink, {{0, 0, D.Kin}});
+    rt[0].out[rt[0].nout++] = ao(F(L.WiT), AO_TRANSPOSE, D.Hk, {{0, 0, D.Kin}});
+    rt[0].out[rt[0].nout++] = ao(F(L.WiX), AO_PLANES, D.Kink, {{0, 0, D.Kin}}, 64);
+    rt[1] = {p->b_i, 1, H, {}, 0, nullptr};
+    rt[1].out[rt[1].nout++] = ao(F(L.bi), AO_PLAIN, D.Hk, {{0, 0, H}});
+    rt[2] = {p->W_h, H, H, {}, 0, wh_amax + 65};
+    rt[2].out[rt[2].nout++] = ao(F(L.Wh), AO_PLAIN, D.ldx, {{0, 0, H}});
+    rt[2].out[rt[2].nout++] = ao(F(L.WhT), AO_TRANSPOSE, D.Hk, {{0, 0, H}});
+    rt[2].out[rt[2].nout++] = ao(F(L.WhX), AO_PLANES, D.ldx, {{0, 0, H}}, 64);
+    if (b80) rt[2].out[rt[2].nout++] = ao(F(L.WhX80), AO_PLANES, D.ldx, {{0, 0, H}}, 80);
+    rt[3] = {p->b_h, 1, H, {}, 0, nullptr};
+    rt[3].out[rt[3].nout++] = ao(F(L.bh), AO_PLAIN, D.Hk, {{0, 0, H}});
+    rt[4] = {p->W_o, H, D.Fa + H, {}, 0, nullptr};
+    rt[4].out[rt[4].nout++] = ao(F(L.Wo), AO_PLAIN, D.Ko, {{0, 0, D.Fa}, {D.Fak, D.Fa, H}});
+    rt[4].out[rt[4].nout++] = ao(F(L.WoT), AO_TRANSPOSE, D.Hk, {{0, D.Fa, H}});
+    rt[4].out[rt[4].nout++] = ao(F(L.WoaT), AO_TRANSPOSE, D.Hk, {{0, 0, D.Fa}});
+    rt[4].out[rt[4].nout++] = ao(F(L.WoX), AO_PLANES, D.Ko, {{0, 0, D.Fa}, {D.Fak, D.Fa, H}}, 64);
+    if (b80) rt[4].out[rt[4].nout++] = ao(F(L.WoX80), AO_PLANES, D.Ko, {{0, 0, D.Fa}, {D.Fak, D.Fa, H}}, 80);
+    rt[5] = {p->b_o, 1, H, {}, 0, nullptr};
+    rt[5].out[rt[5].nout++] = ao(F(L.bo), AO_PLAIN, D.Hk, {{0, 0, H}});
+    bool found[6] = {};
+    for (int r = 0; r < 6; ++r) found[r] = rt[r].param == nullptr;  // (bias-free layers: their packed zeros stay)
+    hipStream_t st = (hipStream_t)stream;
+    WD_TRY(adam_launches(tensors, n, h, st, rt, 6, found));
+    for (int r = 0; r < 6; ++r)
+        if (!found[r]) return fail(WD_ERR_ARG, "adam_step_repack: encoder weight %d is not among the tensors (its packed "
+                                               "copies are stale now: pack before the next forward)", r);
+    // W_h's fp16-pair tiles from the fresh plain copy, scaled by the max over adam_kernel's tile words
+    const int nw = ((H + ADAM_TILE - 1) / ADAM_TILE) * ((H + ADAM_TILE - 1) / ADAM_TILE);
+    hipLaunchKernelGGL(split_h2_kernel, dim3(ew_blocks((size_t)D.Hk * D.Hk / 8)), dim3(256), 0, st, (const float *)F(L.Wh),
+                       D.ldx, D.Hk, D.Hk, fused_bn(D.Hk), (uint8_t *)F(L.WhH), wh_amax + 65, nw, wh_amax + 64);
+    WD_CHECK_LAUNCH("adam_step_repack h2");
     return 0;
 }
 

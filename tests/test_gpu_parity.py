@@ -567,6 +567,64 @@ def test_direct_steps_without_host_sync_read_each_steps_targets():
     assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
 
 
+@pytest.mark.parametrize('hidden', [48, 300])
+def test_adam_repack_rewrites_the_training_pack_bytewise(hidden):
+    """The direct step's packed weights are rewritten by HipAdam's own pass (wdmpnn_adam_step_repack): after
+    every step the persistent training pack is bytewise a fresh wdmpnn_pack_params of the updated weights
+    (plain, transposed, bf16x3 tiles of 64 and 80 rows, W_h's fp16 pairs and scale word), only the first
+    forward packs, and the losses and parameters are bitwise those of steps that pack before every forward."""
+    import ctypes
+    from chemprop_amd import _native
+    from chemprop_amd import train as T
+    from chemprop_amd.nn_utils import initialize_weights
+    from chemprop_amd.train import build_optimizer, get_loss_func, train_step
+    args = TrainArgs(hidden_size=hidden, depth=3, device=DEV)
+    graphs = [BatchMolGraph(synthetic.make_batch('polymer', 12, 50 + i), device_bond_features=True) for i in range(2)]
+    targets = [[[0.3 * j - 1.0 + i] for j in range(12)] for i in range(2)]
+    res = []
+    try:
+        for repack in (True, False):
+            T.ADAM_REPACK = repack
+            torch.manual_seed(0)
+            m = MoleculeModel(args)
+            initialize_weights(m)
+            m = m.to(DEV)
+            enc = m.encoder.encoder[0]
+            opt = build_optimizer(m, 1e-3)
+            packs = []
+            real = enc._packed_params
+            enc._packed_params = lambda *a, **k: (packs.append(1), real(*a, **k))[1]
+            losses = []
+            for step in range(4):
+                g, t = graphs[step % 2], targets[step % 2]
+                losses.append(float(train_step(m, [g], t, get_loss_func('regression'), opt)))
+                if repack:
+                    tp = enc._train_pack
+                    gs, cfg, p = tp['gs'], tp['cfg'], tp['p']
+                    fresh = torch.zeros_like(tp['buf'])
+                    _native.check(_native.lib().wdmpnn_pack_params(ctypes.byref(gs), ctypes.byref(p), ctypes.byref(cfg),
+                                                                   fresh.data_ptr(), fresh.numel(),
+                                                                   _native.current_stream(DEV)), 'pack')
+                    torch.cuda.synchronize()
+                    # bytewise equal except W_h's partial scale words (pack_kernel's 64 per-workgroup maxima
+                    # in a fresh pack, adam_kernel's per-workgroup maxima after a repack): one 256-byte aligned
+                    # run of 65 + nw words whose word 64, the folded scale the layers read, is equal
+                    diff = (fresh != tp['buf']).nonzero().flatten().cpu()
+                    if diff.numel():
+                        start = int(diff[0]) // 256 * 256
+                        nw = (-(-hidden // 32)) ** 2
+                        assert int(diff[-1]) < start + 4 * (65 + nw), (step, fresh.numel(), diff[:16].tolist(),
+                                                                       diff[-16:].tolist(), diff.numel())
+                        assert torch.equal(fresh[start + 256:start + 260], tp['buf'][start + 256:start + 260])
+            del enc._packed_params
+            res.append((losses, [q.detach().clone() for q in m.parameters()], len(packs)))
+    finally:
+        T.ADAM_REPACK = True
+    assert res[0][2] == 1 and res[1][2] == 4
+    assert res[0][0] == res[1][0]
+    assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+
+
 @pytest.mark.parametrize('kind', ['adam', 'adamw'])
 def test_hip_adam_matches_torch_adam(kind):
     """HipAdam (one wdmpnn_adam_step launch) vs torch's single-tensor Adam / AdamW over 6 steps: weight

@@ -9,4 +9,7 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
+if os.environ.get('NO_REPACK'):  # A/B: pack before every training forward instead of HipAdam's repack
+    from chemprop_amd import train
+    train.ADAM_REPACK = False
 print(json.dumps(bench.training_workload(torch.device('cuda:0'), steps=int(os.environ.get('STEPS', '100')))))

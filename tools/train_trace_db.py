@@ -1,6 +1,6 @@
 """One training step's kernel sequence from a rocprofv3 --kernel-trace database (results.db) of
-tools/train_bench.py: the kernels from the last weight pack (pack_kernel, the first launch of a training
-forward) to the end.  Usage: python tools/train_trace_db.py gpurun_out/rocprof_train/run_results.db"""
+tools/train_bench.py: the last step's kernels (its weight pack when the optimizer did not repack, the
+training forward, backward and the optimizer).  Usage: python tools/train_trace_db.py gpurun_out/rocprof_train/run_results.db"""
 import re
 import sqlite3
 import sys
@@ -8,7 +8,12 @@ import sys
 con = sqlite3.connect(sys.argv[1])
 rows = con.execute('select d.start, d.end, s.kernel_name from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s '
                    'on d.kernel_id = s.id order by d.start').fetchall()
-first = max(i for i, r in enumerate(rows) if 'pack_kernel' in r[2])
+# the last step: from the last embed_kernel (the training forward's first layer), back over the weight pack
+# launches that precede it when the optimizer did not repack
+first = max(i for i, r in enumerate(rows) if 'embed_kernel' in r[2])
+while first > 0 and any(k in rows[first - 1][2] for k in ('pack_kernel', 'split_tiles_batch', 'split_h2_kernel')) and \
+        'adam_kernel' not in rows[first - 1][2]:
+    first -= 1
 t0 = rows[first][0]
 print('One training step (B=128 polymer, depth 3, hidden 300, MoleculeModel + MSE + fused Adam), '
       'rocprofv3 --kernel-trace of tools/train_bench.py')
