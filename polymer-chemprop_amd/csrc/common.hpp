@@ -136,15 +136,17 @@ __device__ __forceinline__ int xcd_tile(int b, int ntiles) {
 
 // Several independent batches in one launch (wdmpnn_forward_many, the stream feed's graph builds): per batch its parameter struct and
 // its first tile in the grid; a workgroup finds its batch by a short uniform scan (the structs stay in
-// the kernel-argument segment: scalar loads).  One batch: n = 1.
+// the kernel-argument segment: scalar loads).  One batch: n = 1, launched through the NJ = 1 form (the
+// kernel arguments of eight slots are 0.9-2.2 KB, and a launch's host cost grows with its argument bytes:
+// 2.5-4.3 us at 2.5 KB against 0.9-2.4 us at 64 B, tools/launch_cost.hip).
 constexpr int WD_MULTI = 8;
-template <typename T> struct Multi {
-    T p[WD_MULTI];
-    int t0[WD_MULTI + 1];  // tile ranges: batch j owns grid tiles [t0[j], t0[j + 1])
+template <typename T, int NJ = WD_MULTI> struct Multi {
+    T p[NJ];
+    int t0[NJ + 1];  // tile ranges: batch j owns grid tiles [t0[j], t0[j + 1])
     int n;
 };
-template <typename T>
-__device__ __forceinline__ const T &multi_pick(const Multi<T> &M, int g, int &tile) {
+template <typename T, int NJ>
+__device__ __forceinline__ const T &multi_pick(const Multi<T, NJ> &M, int g, int &tile) {
     int j = 0;
     while (j + 1 < M.n && g >= M.t0[j + 1]) ++j;
     tile = g - M.t0[j];

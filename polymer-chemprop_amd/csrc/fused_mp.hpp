@@ -481,10 +481,10 @@ struct MpEpilogue {
 // then overwrites P with M_t (held in registers across a barrier) for the atom aggregate.
 // ACT: the activation (one instantiation each: the staging of M_{t-1} and the epilogue fold it to
 // straight-line code).
-template <int BN, bool LAST, int ACT, bool ATOM = false>
+template <int BN, bool LAST, int ACT, bool ATOM = false, int NJ = WD_MULTI>
 // (__launch_bounds__ min 4 waves per SIMD: <= 128 VGPRs, so that two layer workgroups -- batches in flight
 // on two streams -- co-reside on a CU)
-__global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpLayerP> MP) {
+__global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpLayerP, NJ> MP) {
     constexpr int BM = BLK_BONDS;
     constexpr int EPI_BYTES = MpEpilogue<BN, MP_THREADS, LAST, ATOM>::LDS_FLOATS * 4;  // P tile + the atom sums
     constexpr int STG_BYTES = h2_lds_bytes<BM, BN>();
@@ -590,8 +590,8 @@ __device__ __forceinline__ float4 code_sum(const WdAtomCode &cd, const float *T,
     return s;
 }
 
-template <int BN, int ACT>
-__global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP> MP) {
+template <int BN, int ACT, int NJ = WD_MULTI>
+__global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP, NJ> MP) {
     constexpr int NT = 512, LDC = BN + 4, C4 = BN / 4, U8 = BN / 8, MAXK = 160, PER = (MAXK * C4 + NT - 1) / NT;
     constexpr int BU = (BLK_BONDS * U8 + NT - 1) / NT;  // bond units (8 columns of a row) per thread
     __shared__ __attribute__((aligned(16))) float wt[MAXK * BN];        // the staged W_i^T tile
@@ -716,8 +716,8 @@ template <> struct WoWaves<80> { static constexpr int WM = 2, WN = 5; };
 // workgroups queue per CU; CPS 1 (55 KB of LDS) for one batch, whose 256 workgroups then co-reside
 // with the layer kernels of batches in flight on other streams (+5 % with two streams, same-box A/B,
 // profiles/round3_*).  64-column tiles: CPS 1.
-template <int BN, int CPS>
-__global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_readout_kernel(const Multi<WoReadoutP> MP) {
+template <int BN, int CPS, int NJ = WD_MULTI>
+__global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_readout_kernel(const Multi<WoReadoutP, NJ> MP) {
     constexpr int BM = BLK_ATOMS, LDC = BN + 4, WM = WoWaves<BN>::WM, WN = WoWaves<BN>::WN;
     constexpr int NT = 64 * WM * WN;
     // (deeper single-chunk pipelines, with the mainloop hook's loads ordered ahead of the partial vmcnt

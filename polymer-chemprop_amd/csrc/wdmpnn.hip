@@ -755,11 +755,20 @@ int launch_multi(const FusedJob *jobs, int n, int tiles_per_blk, Fill &&fill, Mu
     grid = t;
     return 0;
 }
+// the one-batch form of a filled Multi (a launch's host cost grows with its kernel-argument bytes)
+template <typename T>
+Multi<T, 1> one_job(const Multi<T> &M) {
+    Multi<T, 1> o{};
+    o.p[0] = M.p[0]; o.t0[0] = M.t0[0]; o.t0[1] = M.t0[1]; o.n = 1;
+    return o;
+}
 
 int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig *c, const PackLayout &PL,
                   const char *pk, hipStream_t st) {
     if (n < 1 || n > WD_MULTI) return fail(WD_ERR_ARG, "fused forward: %d jobs per launch (1..%d)", n, WD_MULTI);
     const Dims &D0 = jobs[0].D;
+    if (D0.atom && n > 1)  // (the atom-row layer kernel is instantiated for one batch per launch only)
+        return fail(WD_ERR_UNSUPPORTED, "fused forward: atom messages run one batch per launch");
     auto W = [&](size_t off) { return (const float *)(pk + off); };
     auto F = [](const FusedJob &J, size_t off) { return (float *)(J.ws + off); };
     const int Hk = D0.Hk;
@@ -799,7 +808,12 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
         }, M, grid);
         host_with_act(c->activation, [&](auto act_c) {
             constexpr int A = decltype(act_c)::value;
-            if (bn40) hipLaunchKernelGGL((embed_kernel<40, A>), dim3(grid), dim3(512), 0, st, M);
+            if (n == 1) {
+                const Multi<EmbedP, 1> M1 = one_job(M);
+                if (bn40) hipLaunchKernelGGL((embed_kernel<40, A, 1>), dim3(grid), dim3(512), 0, st, M1);
+                else if (bn80) hipLaunchKernelGGL((embed_kernel<80, A, 1>), dim3(grid), dim3(512), 0, st, M1);
+                else hipLaunchKernelGGL((embed_kernel<64, A, 1>), dim3(grid), dim3(512), 0, st, M1);
+            } else if (bn40) hipLaunchKernelGGL((embed_kernel<40, A>), dim3(grid), dim3(512), 0, st, M);
             else if (bn80) hipLaunchKernelGGL((embed_kernel<80, A>), dim3(grid), dim3(512), 0, st, M);
             else hipLaunchKernelGGL((embed_kernel<64, A>), dim3(grid), dim3(512), 0, st, M);
         });
@@ -883,8 +897,10 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
             constexpr bool LAST = decltype(last_c)::value;
             host_with_act(c->activation, [&](auto act_c) {
                 constexpr int A = decltype(act_c)::value;
-                if (D0.atom)
-                    hipLaunchKernelGGL((mp_layer_kernel<BN, LAST, A, true>), dim3(grid), dim3(MP_THREADS), 0, st, M);
+                if (n == 1 && D0.atom)
+                    hipLaunchKernelGGL((mp_layer_kernel<BN, LAST, A, true, 1>), dim3(grid), dim3(MP_THREADS), 0, st, one_job(M));
+                else if (n == 1)
+                    hipLaunchKernelGGL((mp_layer_kernel<BN, LAST, A, false, 1>), dim3(grid), dim3(MP_THREADS), 0, st, one_job(M));
                 else
                     hipLaunchKernelGGL((mp_layer_kernel<BN, LAST, A, false>), dim3(grid), dim3(MP_THREADS), 0, st, M);
             });
@@ -922,7 +938,9 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
         if (bn80 && n > 1)
             hipLaunchKernelGGL((wo_readout_kernel<80, 2>), dim3(grid), dim3(64 * WoWaves<80>::WM * WoWaves<80>::WN), 0, st, M);
         else if (bn80)
-            hipLaunchKernelGGL((wo_readout_kernel<80, 1>), dim3(grid), dim3(64 * WoWaves<80>::WM * WoWaves<80>::WN), 0, st, M);
+            hipLaunchKernelGGL((wo_readout_kernel<80, 1, 1>), dim3(grid), dim3(64 * WoWaves<80>::WM * WoWaves<80>::WN), 0, st, one_job(M));
+        else if (n == 1)
+            hipLaunchKernelGGL((wo_readout_kernel<64, 1, 1>), dim3(grid), dim3(64 * WoWaves<64>::WM * WoWaves<64>::WN), 0, st, one_job(M));
         else
             hipLaunchKernelGGL((wo_readout_kernel<64, 1>), dim3(grid), dim3(64 * WoWaves<64>::WM * WoWaves<64>::WN), 0, st, M);
         WD_CHECK_LAUNCH("wo_readout");
