@@ -384,6 +384,9 @@ typedef struct WdHead {
     float *dx;                             /* [B][ld_x]: d loss / d x                               */
     float *dW1, *db1, *dW2, *db2;          /* parameter gradients (db1 / db2 NULL = skip)           */
     float *loss;                           /* [1]                                                   */
+    int32_t loss_kind;                     /* 0: MSELoss (regression), 1: BCEWithLogitsLoss         */
+                                           /* (classification: the FFN's logits, train.py:55-74 with */
+                                           /* utils.py get_loss_func; sigmoid only at eval)           */
 } WdHead;
 int wdmpnn_head_mse(const WdHead *h, void *stream);
 /* p_i[0 .. n_i) *= *s (device scalar) for k <= 8 buffers: the head's gradients times the loss's

@@ -113,7 +113,8 @@ class WdHead(Structure):
                 ('W1', c_void_p), ('b1', c_void_p), ('W2', c_void_p), ('b2', c_void_p),
                 ('table', c_void_p), ('ld_table', c_int32), ('inv_n', c_float), ('act', c_int32),
                 ('a', c_void_p), ('dh', c_void_p), ('dout', c_void_p), ('lossrow', c_void_p), ('dx', c_void_p),
-                ('dW1', c_void_p), ('db1', c_void_p), ('dW2', c_void_p), ('db2', c_void_p), ('loss', c_void_p)]
+                ('dW1', c_void_p), ('db1', c_void_p), ('dW2', c_void_p), ('db2', c_void_p), ('loss', c_void_p),
+                ('loss_kind', c_int32)]
 
 
 class NativeError(RuntimeError):

@@ -281,8 +281,8 @@ def batch_loss(preds: torch.Tensor, target_batch: Sequence[Sequence[Optional[flo
 # Fused FFN head + masked MSE loss (wdmpnn_head_mse).  The reference's step evaluates ffn(emb) (model.py:
 # 57-121), loss_func(preds, targets) * weights and .sum() / mask.sum() (train.py:55-74) and autograd runs
 # their backward: ~25 small torch ops whose host time left the GPU idle for most of the step
-# (profiles/round2_train_kernel_trace_v3.txt).  For the default regression head (two Linear layers, an
-# activation, no active dropout, MSELoss) the loss and every gradient of the head come from two HIP
+# (profiles/round2_train_kernel_trace_v3.txt).  For the default head (two Linear layers, an activation, no
+# active dropout; MSELoss for regression, BCEWithLogitsLoss for classification) the loss and every gradient of the head come from two HIP
 # launches in the forward; the backward scales them by the loss's incoming gradient (one launch).
 # ------------------------------------------------------------------------------------------------
 def _head_act(m: nn.Module) -> Optional[int]:
@@ -303,7 +303,12 @@ def _head_act(m: nn.Module) -> Optional[int]:
 def _fusable_head(model: nn.Module, loss_func: Callable, dataset_type: str):
     """(Linear 1, Linear 2, activation code) when the step's head + loss can run fused, else None."""
     from .model import MoleculeModel
-    if dataset_type != 'regression' or type(loss_func) is not nn.MSELoss or loss_func.reduction != 'none':
+    if dataset_type == 'regression' and type(loss_func) is nn.MSELoss and loss_func.reduction == 'none':
+        kind = 0
+    elif dataset_type == 'classification' and type(loss_func) is nn.BCEWithLogitsLoss and \
+            loss_func.reduction == 'none' and loss_func.weight is None and loss_func.pos_weight is None:
+        kind = 1  # (the FFN's logits: MoleculeModel applies the sigmoid only outside training, model.py:186-188)
+    else:
         return None
     if not isinstance(model, MoleculeModel) or type(model).forward is not MoleculeModel.forward:
         return None
@@ -324,14 +329,14 @@ def _fusable_head(model: nn.Module, loss_func: Callable, dataset_type: str):
             return None
     if l1.in_features > 4096 or l1.out_features > 4096 or l2.out_features > 64:
         return None
-    return l1, l2, code
+    return l1, l2, code, kind
 
 
 class _HeadMSE(torch.autograd.Function):
     """loss = sum(w (W2 act(W1 x + b1) + b2 - y)^2) / n, with every gradient computed in the forward."""
 
     @staticmethod
-    def forward(ctx, x, W1, b1, W2, b2, table, inv_n, act):
+    def forward(ctx, x, W1, b1, W2, b2, table, inv_n, act, kind):
         from . import _native
         x = x.contiguous()
         dev = x.device
@@ -347,7 +352,7 @@ class _HeadMSE(torch.autograd.Function):
         sp = scratch.data_ptr()
         h = _native.WdHead(ptr(x), F, B, F, Hf, T, ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(table), table.shape[1],
                            float(inv_n), act, sp, sp + 4 * B * Hf, sp + 8 * B * Hf, sp + 4 * B * (2 * Hf + T),
-                           ptr(dx), ptr(dW1), ptr(db1), ptr(dW2), ptr(db2), ptr(loss))
+                           ptr(dx), ptr(dW1), ptr(db1), ptr(dW2), ptr(db2), ptr(loss), kind)
         _native.check(_native.lib().wdmpnn_head_mse(ctypes.byref(h), _native.current_stream(dev)), 'FFN head + loss')
         ctx.grads = (dx, dW1, db1, dW2, db2)
         return loss
@@ -362,12 +367,13 @@ class _HeadMSE(torch.autograd.Function):
         ns = (ctypes.c_int64 * len(live))(*[g.numel() for g in live])
         _native.check(_native.lib().wdmpnn_scale(ptrs, ns, len(live), gl.data_ptr(),
                                                  _native.current_stream(gl.device)), 'scale')
-        return grads + (None, None, None)
+        return grads + (None, None, None, None)
 
 
 def head_loss(emb: torch.Tensor, head, target_batch, target_weights=None, data_weights=None) -> torch.Tensor:
-    """``batch_loss(model.ffn(emb), ...)`` for a head accepted by ``_fusable_head`` (regression, MSE)."""
-    l1, l2, act = head
+    """``batch_loss(model.ffn(emb), ...)`` for a head accepted by ``_fusable_head`` (regression with MSE,
+    classification with BCE on logits)."""
+    l1, l2, act, kind = head
     table, n_t, n_mask = _loss_table(target_batch, target_weights, data_weights, emb.device)
     if n_t != l2.out_features:
         raise ValueError(f'{n_t} targets per row for {l2.out_features} outputs')
@@ -375,7 +381,7 @@ def head_loss(emb: torch.Tensor, head, target_batch, target_weights=None, data_w
         raise ValueError(f'{table.shape[0]} target rows for encodings of shape {tuple(emb.shape)} '
                          f'(FFN input {l1.in_features})')
     inv_n = 1.0 / n_mask if n_mask else float('inf')
-    return _HeadMSE.apply(emb, l1.weight, l1.bias, l2.weight, l2.bias, table, inv_n, act)
+    return _HeadMSE.apply(emb, l1.weight, l1.bias, l2.weight, l2.bias, table, inv_n, act, kind)
 
 
 def _grad_buffer(p: torch.Tensor) -> torch.Tensor:
@@ -410,7 +416,7 @@ def _direct_encoder(model: nn.Module, mol_batch, features_batch, head):
         return None
     # the direct step skips zero_grad and overwrites only the gradients it computes: any other trainable
     # parameter (a future addition to the model) would keep a stale gradient, so it must not exist
-    l1, l2, _ = head
+    l1, l2 = head[:2]
     written = {id(t) for _, t in enc._direct_names()} | {id(t) for t in (l1.weight, l1.bias, l2.weight, l2.bias)
                                                           if t is not None}
     if len(ids) != len(written) or not written.issuperset(ids):
@@ -440,7 +446,7 @@ def _direct_step(model, enc, graph, head, target_batch, target_weights, data_wei
     parameters' .grad buffers.  The same launches as the autograd path minus its host gaps (the engine
     hand-off, the gradient-seed fill and the scale by 1; profiles/round3_*)."""
     from . import _native
-    l1, l2, act = head
+    l1, l2, act, kind = head
     out, state = enc._train_forward(graph)
     # the loss table read by the head kernel straight from its pinned host buffer (no copy launch in the
     # step: the copy kernel and its gap were ~10 us, profiles/round4_train_kernel_trace_v1.txt)
@@ -469,7 +475,7 @@ def _direct_step(model, enc, graph, head, target_batch, target_weights, data_wei
     sp = scratch.data_ptr()
     h = _native.WdHead(ptr(out), F, B, F, Hf, T, ptr(l1.weight), ptr(l1.bias), ptr(l2.weight), ptr(l2.bias), tab_ptr,
                        tshape[1], float(inv_n), act, sp, sp + 4 * B * Hf, sp + 8 * B * Hf, sp + 4 * B * (2 * Hf + T),
-                       ptr(dx), ptr(dW1), ptr(db1), ptr(dW2), ptr(db2), ptr(loss))
+                       ptr(dx), ptr(dW1), ptr(db1), ptr(dW2), ptr(db2), ptr(loss), kind)
     _native.check(_native.lib().wdmpnn_head_mse(ctypes.byref(h), _native.current_stream(dev)), 'FFN head + loss')
     if zc is not None:
         zc[1].record(torch.cuda.current_stream(dev))  # (the pinned buffer's last reader)
@@ -485,7 +491,7 @@ def train_step(model: nn.Module, mol_batch, target_batch, loss_func: Callable, o
                bucket: GradBucket = None, fused_head: bool = True, direct: bool = True) -> torch.Tensor:
     """One optimisation step (train.py:55-86).  With ``bucket`` the gradients are averaged over the
     data-parallel ranks (one all-reduce) before clipping and the optimizer step.  ``fused_head``: the
-    default regression head + loss run as ``wdmpnn_head_mse`` (same loss and gradients within fp32
+    default regression / classification head + loss run as ``wdmpnn_head_mse`` (same loss and gradients within fp32
     summation order; ``False`` = the torch ops of the reference).  ``direct``: with the fused head and a
     plain one-molecule encoder, skip the autograd engine (``_direct_step``: the same launches and results,
     bitwise, without the engine's host gaps)."""

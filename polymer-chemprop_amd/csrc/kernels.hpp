@@ -911,9 +911,15 @@ __global__ __launch_bounds__(256) void head_rows_kernel(WdHead P) {
             for (int j = lane; j < Hf; j += 64) s = fmaf(w2[j], act_fwd(ACT, h[j], 0.f), s);
             s = wave_sum(s) + (P.b2 ? P.b2[t] : 0.f);
             const float y = tlane ? __shfl(tv, t, 64) : tab[t], w = tlane ? __shfl(tv, T + t, 64) : tab[T + t];
-            const float r = s - y;
-            l = fmaf(w * r, r, l);
-            const float d = 2.f * w * r * P.inv_n;
+            float d;
+            if (P.loss_kind == 0) {  // MSE: w (s - y)^2, d/ds = 2 w (s - y)
+                const float r = s - y;
+                l = fmaf(w * r, r, l);
+                d = 2.f * w * r * P.inv_n;
+            } else {  // BCE with logits: w (max(s, 0) - s y + log(1 + e^-|s|)), d/ds = w (sigmoid(s) - y)
+                l = fmaf(w, fmaxf(s, 0.f) - s * y + log1pf(expf(-fabsf(s))), l);
+                d = w * (1.f / (1.f + expf(-s)) - y) * P.inv_n;
+            }
             dsh[wave][t] = d;
             if (lane == 0) P.dout[(size_t)row * T + t] = d;
         }

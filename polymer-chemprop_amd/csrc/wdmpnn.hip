@@ -1928,6 +1928,7 @@ int wdmpnn_head_mse(const WdHead *h, void *stream) {
     if (h->F > HEAD_MAX_F || h->Hf > HEAD_MAX_H || h->T > HEAD_MAX_T)
         return fail(WD_ERR_UNSUPPORTED, "head: F, Hf <= 4096 and T <= 64");
     if (h->act < 0 || h->act > WD_ACT_ELU || h->act == WD_ACT_PRELU) return fail(WD_ERR_UNSUPPORTED, "head activation");
+    if (h->loss_kind != 0 && h->loss_kind != 1) return fail(WD_ERR_UNSUPPORTED, "head loss kind %d", h->loss_kind);
     if (!h->W1 || !h->W2 || !h->a || !h->dh || !h->dout || !h->lossrow || !h->dW1 || !h->dW2 || !h->loss ||
         (h->B && (!h->x || !h->table || !h->dx)))
         return fail(WD_ERR_ARG, "head: null pointer");

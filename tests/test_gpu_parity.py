@@ -542,6 +542,39 @@ def test_direct_training_step_equals_autograd_step(act, bias):
         assert all(torch.equal(a, b) for a, b in zip(res[0][2], res[1][2]))
 
 
+def test_classification_steps_take_the_fused_direct_path():
+    """A classification MoleculeModel (BCEWithLogitsLoss on the FFN's logits, train.py:55-74) trains
+    through the fused head and the direct step: the same losses and parameters bitwise as the fused head
+    under autograd, and within 1e-5 of the torch ops (fused_head=False) over four steps."""
+    from chemprop_amd.nn_utils import initialize_weights
+    from chemprop_amd.train import _fusable_head, build_optimizer, get_loss_func, train_step
+    args = TrainArgs(hidden_size=48, depth=3, device=DEV, dataset_type='classification')
+    args.num_tasks = 2
+    graphs = [BatchMolGraph(synthetic.make_batch('polymer', 12, 60 + i), device_bond_features=True) for i in range(2)]
+    rng = np.random.default_rng(3)
+    targets = [[[None if rng.random() < 0.15 else float(rng.random() < 0.5) for _ in range(2)] for _ in range(12)]
+               for _ in range(2)]
+    lf = get_loss_func('classification')
+    res = []
+    for mode in ('direct', 'autograd', 'torch'):
+        torch.manual_seed(0)
+        m = MoleculeModel(args)
+        initialize_weights(m)
+        m = m.to(DEV)
+        assert _fusable_head(m, lf, 'classification') is not None
+        opt = build_optimizer(m, 1e-3)
+        losses = [float(train_step(m, [g], t, lf, opt, dataset_type='classification', direct=mode == 'direct',
+                                   fused_head=mode != 'torch'))
+                  for _ in range(2) for g, t in zip(graphs, targets)]
+        res.append((losses, [q.detach().clone() for q in m.parameters()]))
+    assert res[0][0] == res[1][0]
+    assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+    for a, b in zip(res[0][0], res[2][0]):
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(b)), (a, b)
+    for a, b in zip(res[0][1], res[2][1]):
+        assert golden_io.normwise(a.cpu().numpy(), b.cpu().numpy()) <= 1e-4
+
+
 def test_direct_steps_without_host_sync_read_each_steps_targets():
     """The direct step's head kernel reads its loss table in place from a ring of 4 coherent mapped host
     buffers.  Ten steps with ten different target sets and NO host sync between them (the losses stay on
@@ -690,21 +723,29 @@ def test_hip_adam_parameter_without_gradient_on_some_steps():
             assert float((x - y).abs().max()) <= 1e-6 * max(1.0, float(x.abs().max()))
 
 
-@pytest.mark.parametrize('b,tasks,act,features', [(128, 1, 'ReLU', 0), (16, 2, 'tanh', 0), (33, 3, 'ELU', 5),
-                                                   (8, 1, 'LeakyReLU', 0), (20, 2, 'SELU', 0)])
-def test_fused_head_loss_matches_torch(b, tasks, act, features):
-    """The fused FFN head + masked MSE (wdmpnn_head_mse: the train step's default regression path) gives
-    the torch head's loss and every gradient (head, encoder) within 1e-5; missing targets, target and
-    data weights, several tasks, extra molecule features, and a scaled incoming gradient."""
+@pytest.mark.parametrize('b,tasks,act,features,dataset', [(128, 1, 'ReLU', 0, 'regression'),
+                                                           (16, 2, 'tanh', 0, 'regression'),
+                                                           (33, 3, 'ELU', 5, 'regression'),
+                                                           (8, 1, 'LeakyReLU', 0, 'regression'),
+                                                           (20, 2, 'SELU', 0, 'regression'),
+                                                           (128, 1, 'ReLU', 0, 'classification'),
+                                                           (33, 3, 'tanh', 5, 'classification')])
+def test_fused_head_loss_matches_torch(b, tasks, act, features, dataset):
+    """The fused FFN head + masked loss (wdmpnn_head_mse: the train step's default path; MSE for regression,
+    BCE on the logits for classification) gives the torch head's loss and every gradient (head, encoder)
+    within 1e-5; missing targets, target and data weights, several tasks, extra molecule features, and a
+    scaled incoming gradient."""
     from chemprop_amd.nn_utils import initialize_weights
     from chemprop_amd.train import _fusable_head, batch_loss, get_loss_func, head_loss
-    args = TrainArgs(hidden_size=96, depth=3, activation=act, ffn_hidden_size=80, device=DEV)
+    args = TrainArgs(hidden_size=96, depth=3, activation=act, ffn_hidden_size=80, device=DEV,
+                     dataset_type=dataset)
     args.num_tasks = tasks
     if features:
         args.use_input_features, args.features_size = True, features
     g = BatchMolGraph(synthetic.make_batch('polymer', b, 31 + b), device_bond_features=True)
     rng = np.random.default_rng(b)
-    targets = [[None if rng.random() < 0.2 else float(rng.normal()) for _ in range(tasks)] for _ in range(b)]
+    value = (lambda: float(rng.normal())) if dataset == 'regression' else (lambda: float(rng.random() < 0.4))
+    targets = [[None if rng.random() < 0.2 else value() for _ in range(tasks)] for _ in range(b)]
     tw = list(rng.uniform(0.5, 1.5, tasks))
     dw = list(rng.uniform(0.5, 1.5, b))
     feats = [rng.normal(size=features).astype(np.float32) for _ in range(b)] if features else None
@@ -712,8 +753,8 @@ def test_fused_head_loss_matches_torch(b, tasks, act, features):
     m = MoleculeModel(args)
     initialize_weights(m)
     m = m.to(DEV).train()
-    lf = get_loss_func('regression')
-    head = _fusable_head(m, lf, 'regression')
+    lf = get_loss_func(dataset)
+    head = _fusable_head(m, lf, dataset)
     assert head is not None
     res = []
     for fused in (True, False):
@@ -721,7 +762,7 @@ def test_fused_head_loss_matches_torch(b, tasks, act, features):
         if fused:
             loss = head_loss(m.encoder([g], feats), head, targets, tw, dw)
         else:
-            loss = batch_loss(m([g], feats), targets, lf, 'regression', tw, dw)
+            loss = batch_loss(m([g], feats), targets, lf, dataset, tw, dw)
         (loss * 0.75).backward()
         res.append((float(loss), {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}))
     (l0, g0), (l1, g1) = res
