@@ -242,23 +242,29 @@ class MPNEncoder(nn.Module):
                 d['activation'], d['aggregation'], d['aggregation_norm'], d['_gemm_variant'])
         plan = dg.encoder_plans.get(ckey)
         if plan is None:
-            gs = self._graph_struct(dg)
-            cfg = self._infer_configs.get(ckey)
-            if cfg is None:
-                cfg = self._infer_configs[ckey] = self._config(False)
-            pstruct, _ = self._packed_params(gs, cfg, params, device, sid=sid)
-            nbytes = ctypes.c_size_t()
-            _native.check(_native.lib().wdmpnn_workspace_bytes(ctypes.byref(gs), ctypes.byref(pstruct),
-                                                               ctypes.byref(cfg), ctypes.byref(nbytes)),
-                          'MPNEncoder workspace')
-            plan = (ctypes.byref(gs), ctypes.byref(cfg), max(nbytes.value, 256), gs.n_mols, gs, cfg)
-            dg.encoder_plans[ckey] = plan
+            plan = self._new_infer_plan(dg, ckey, params, device, sid)
         pstruct, _ = self._packed_params(plan[4], plan[5], params, device, sid=sid)
         ws = self._stream_workspace(sid, plan[2], device)
         out = torch.empty((plan[3], d['hidden_size']), dtype=torch.float32, device=device)
         _native.check(_native.lib().wdmpnn_forward(plan[0], ctypes.byref(pstruct), plan[1], ws.data_ptr(), plan[2],
                                                    out.data_ptr(), sid), 'MPNEncoder forward')
         return out
+
+    def _new_infer_plan(self, dg, ckey, params, device, sid):
+        """(graph struct ref, config ref, workspace bytes, molecules, graph struct, config) of an inference
+        call on ``dg``, stored on it under ``ckey`` (shared by ``_infer`` and ``forward_many``)."""
+        gs = self._graph_struct(dg)
+        cfg = self._infer_configs.get(ckey)
+        if cfg is None:
+            cfg = self._infer_configs[ckey] = self._config(False)
+        pstruct, _ = self._packed_params(gs, cfg, params, device, sid=sid)
+        nbytes = ctypes.c_size_t()
+        _native.check(_native.lib().wdmpnn_workspace_bytes(ctypes.byref(gs), ctypes.byref(pstruct),
+                                                           ctypes.byref(cfg), ctypes.byref(nbytes)),
+                      'MPNEncoder workspace')
+        plan = (ctypes.byref(gs), ctypes.byref(cfg), max(nbytes.value, 256), gs.n_mols, gs, cfg)
+        dg.encoder_plans[ckey] = plan
+        return plan
 
     def _stream_workspace(self, sid: int, nbytes: int, device) -> torch.Tensor:
         """This encoder's inference workspace for the stream ``sid`` (current at the call), grown to the
@@ -355,28 +361,30 @@ class MPNEncoder(nn.Module):
         last = d.get('_many_plan')
         plan = last[1] if last is not None and last[0] == key else None
         if plan is None or any(a is not b for a, b in zip(plan[0], dgs)):
-            cfg = self._config(False)
+            # a new set of graphs: each graph's struct and workspace size come from its inference plan
+            # (built once per graph and encoder configuration, shared with _infer), so a set costs a copy
+            # of its structs, not a workspace query per graph
+            sid = stream.cuda_stream
+            fparams = tuple(_f32(t) for t in params)
             structs = (_native.WdGraph * len(dgs))()
+            sz = ctypes.sizeof(_native.WdGraph)
             sizes, offs, rows, total = [], [], [], 0
             for k, dg in enumerate(dgs):
-                gs = self._graph_struct(dg)
-                ctypes.memmove(ctypes.byref(structs, k * ctypes.sizeof(_native.WdGraph)), ctypes.byref(gs),
-                               ctypes.sizeof(_native.WdGraph))
-                pstruct, _ = self._packed_params(gs, cfg, tuple(_f32(t) for t in params), device, stream=stream)
-                nbytes = ctypes.c_size_t()
-                _native.check(_native.lib().wdmpnn_workspace_bytes(ctypes.byref(gs), ctypes.byref(pstruct),
-                                                                   ctypes.byref(cfg), ctypes.byref(nbytes)),
-                              'MPNEncoder workspace')
+                gp = dg.encoder_plans.get(ckey)
+                if gp is None:
+                    gp = self._new_infer_plan(dg, ckey, fparams, device, sid)
+                ctypes.memmove(ctypes.byref(structs, k * sz), gp[0], sz)
                 offs.append(total)
-                sizes.append(nbytes.value)
-                total += (nbytes.value + 255) & ~255
-                rows.append(gs.n_mols)
+                sizes.append(gp[2])
+                total += (gp[2] + 255) & ~255
+                rows.append(gp[3])
+            cfg = gp[5]
             plan = (dgs, structs, cfg, (ctypes.c_size_t * len(dgs))(*sizes), offs, max(total, 256), rows,
                     np.cumsum([0] + rows).tolist())
             d['_many_plan'] = (key, plan)
         dgs_, structs, cfg, sizes, offs, total, rows, row0 = plan
         pstruct, _ = self._packed_params(structs[0], cfg, params, device, stream=stream)
-        ws = torch.empty(total, dtype=torch.uint8, device=device)
+        ws = self._stream_workspace(stream.cuda_stream, total, device)  # (the encoder's buffer for this stream)
         out = torch.empty((row0[-1], d['hidden_size']), dtype=torch.float32, device=device)
         base, obase, H = ws.data_ptr(), out.data_ptr(), d['hidden_size']
         n = len(dgs_)
