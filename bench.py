@@ -37,7 +37,7 @@ from chemprop_amd.nn_utils import initialize_weights  # noqa: E402
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 / fp16 (the layer issues 3 fp16 products per fp32 product, W_o 6 bf16)
 HBM_PEAK_GBS = 8000.0
-PMC_TRAFFIC = "round4_pmc_traffic.json"  # per-kernel HBM bytes per launch (tools/pmc_summary.py)
+PMC_TRAFFIC = "round5_pmc_traffic.json"  # per-kernel HBM bytes per launch (tools/pmc_summary.py)
 
 
 def log(*a):
