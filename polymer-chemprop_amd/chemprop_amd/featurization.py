@@ -153,12 +153,21 @@ class DeviceGraph:
             return
         if self.ready is not None and not self.ready.query():  # (a finished build needs no wait)
             stream.wait_event(self.ready)
-        seen = set()
-        for t in [self.buffer] + list(self.views.values()):
-            base = t.untyped_storage().data_ptr()
-            if base not in seen:
-                seen.add(base)
-                t.record_stream(stream)
+        cached = self.__dict__.get('_owners')
+        if cached is None or cached[0] != len(self.views):
+            # one tensor per distinct allocation (the views share a few), found once: the per-view storage
+            # walk cost a first use on a stream tens of us of host time
+            seen, owners = set(), []
+            for t in [self.buffer] + list(self.views.values()):
+                if t is None:
+                    continue
+                base = t.untyped_storage().data_ptr()
+                if base not in seen:
+                    seen.add(base)
+                    owners.append(t)
+            cached = self._owners = (len(self.views), owners)
+        for t in cached[1]:
+            t.record_stream(stream)
         self._streams.add(sid)
 
 
