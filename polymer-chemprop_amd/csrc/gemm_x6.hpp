@@ -38,18 +38,29 @@ struct X6Params {
     int M, N;                             // rows / cols written
     int tiles_m, tiles_n;
     Epi epi;
+    // H2 (fp16 pairs): A's scale from the max words its producer published, one per 256 consecutive
+    // float4 of A (act_bwd_kernel's `words`: word (r * a_cv + c / 4) / 256, a_cv = float4 per A row);
+    // B's from one word (W_h's folded max)
+    const uint32_t *a_words; int a_cv;
+    const uint32_t *b_word;
 };
 
 // BM x 64 tile, 4 BM threads = (BM/32) x 2 waves of 32x32 (2x2 16x16x32 accumulators).  BK = 32 or 64
 // wide K chunks, two LDS stages, two register sets (prefetch distance 2).  Operand rows are loaded as
 // whole 128-byte lines (BK/4 consecutive lanes per row chunk: 8 lanes x 16 B at BK = 32) and each
 // float4 is split into three 8-byte plane pieces (ds_write_b64).
-template <int BM, int BK>
+//
+// H2: the same kernel on fp16 hi / lo pairs (planes.hpp "h2"): two planes per operand and three MFMAs
+// (hh, hl, lh) per 16 x 16 x 32 step instead of three planes and six; A scaled by the max of its tile's
+// rows (the words its producer published), B by one word; the accumulators are unscaled before the
+// epilogue (powers of two: exact).  The data-gradient GEMM dM = Y_t W_h of the fused backward.
+template <int BM, int BK, bool H2 = false>
 __global__ __launch_bounds__(4 * BM) void gemm_x6_kernel(X6Params P) {
     constexpr int NT = 4 * BM, BN = X6_BN;
+    constexpr int NPL = H2 ? 2 : 3;                         // planes per operand
     constexpr int ROWB = 2 * BK;                            // bytes per plane row
     constexpr int APL = BM * ROWB, BPL = BN * ROWB;         // plane bytes
-    constexpr int STAGE = 3 * APL + 3 * BPL;
+    constexpr int STAGE = NPL * APL + NPL * BPL;
     constexpr int QR = BK / 4;                              // float4 per row chunk
     constexpr int AQ = BM * QR / NT, BQ = BN * QR / NT;     // float4 per thread per chunk
     static_assert((BN * QR) % NT == 0 && BQ >= 1, "B staging split");
@@ -64,6 +75,13 @@ __global__ __launch_bounds__(4 * BM) void gemm_x6_kernel(X6Params P) {
     const int K = P.ka0 + P.ka1, nchunks = K / BK;
     EpiPrefetch<BM, BN, NT> ep;
     ep.load(P.epi, m0, n0, P.M, P.N);
+    float sa = 1.f, sb = 1.f, inv_sa = 1.f, inv_sb = 1.f;
+    if constexpr (H2) {
+        const int w0 = (m0 * P.a_cv) >> 8, w1 = ((m0 + BM) * P.a_cv - 1) >> 8;
+        const uint32_t ma = max_words(P.a_words + w0, w1 - w0 + 1), mb = P.b_word[0];
+        sa = h2_scale(ma); inv_sa = h2_inv_scale(ma);
+        sb = h2_scale(mb); inv_sb = h2_inv_scale(mb);
+    }
 
     // staging: float4 q = tid + NT j of a chunk -> row q / QR, column quad q % QR
     const int qr = tid / QR, qc = tid % QR;
@@ -85,19 +103,27 @@ __global__ __launch_bounds__(4 * BM) void gemm_x6_kernel(X6Params P) {
 #pragma unroll
         for (int j = 0; j < BQ; ++j) R.b[j] = ld4(brow + (size_t)j * RSTEP * P.ldb + k0);
     };
-    auto put = [&](uint8_t *base, int plane_bytes, int off, const float4 &v) {
-        uint32_t h0, m0_, l0, h1, m1, l1;
-        split_pair(v.x, v.y, h0, m0_, l0);
-        split_pair(v.z, v.w, h1, m1, l1);
-        *reinterpret_cast<uint2 *>(base + off) = make_uint2(h0, h1);
-        *reinterpret_cast<uint2 *>(base + plane_bytes + off) = make_uint2(m0_, m1);
-        *reinterpret_cast<uint2 *>(base + 2 * plane_bytes + off) = make_uint2(l0, l1);
+    auto put = [&](uint8_t *base, int plane_bytes, int off, const float4 &v, float s) {
+        if constexpr (H2) {
+            uint32_t h0, l0, h1, l1;
+            split_h2(v.x, v.y, s, h0, l0);
+            split_h2(v.z, v.w, s, h1, l1);
+            *reinterpret_cast<uint2 *>(base + off) = make_uint2(h0, h1);
+            *reinterpret_cast<uint2 *>(base + plane_bytes + off) = make_uint2(l0, l1);
+        } else {
+            uint32_t h0, m0_, l0, h1, m1, l1;
+            split_pair(v.x, v.y, h0, m0_, l0);
+            split_pair(v.z, v.w, h1, m1, l1);
+            *reinterpret_cast<uint2 *>(base + off) = make_uint2(h0, h1);
+            *reinterpret_cast<uint2 *>(base + plane_bytes + off) = make_uint2(m0_, m1);
+            *reinterpret_cast<uint2 *>(base + 2 * plane_bytes + off) = make_uint2(l0, l1);
+        }
     };
     auto store_chunk = [&](const Regs &R, uint8_t *st) {
 #pragma unroll
-        for (int j = 0; j < AQ; ++j) put(st, APL, dst[j], R.a[j]);
+        for (int j = 0; j < AQ; ++j) put(st, APL, dst[j], R.a[j], sa);
 #pragma unroll
-        for (int j = 0; j < BQ; ++j) put(st + 3 * APL, BPL, dst[j], R.b[j]);
+        for (int j = 0; j < BQ; ++j) put(st + NPL * APL, BPL, dst[j], R.b[j], sb);
     };
 
     floatx4 acc[2][2];
@@ -107,6 +133,32 @@ __global__ __launch_bounds__(4 * BM) void gemm_x6_kernel(X6Params P) {
         for (int b = 0; b < 2; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     auto compute = [&](const uint8_t *st) {
+        if constexpr (H2) {
+#pragma unroll
+            for (int s = 0; s < BK / 32; ++s) {
+                f16x8 af[2][2], bfr[2][2];
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+#pragma unroll
+                    for (int a = 0; a < 2; ++a)
+                        af[a][p] = *reinterpret_cast<const f16x8 *>(st + p * APL + x6_off<BK>(wi * 32 + a * 16 + i16, 4 * s + g));
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+                        bfr[b][p] = *reinterpret_cast<const f16x8 *>(st + 2 * APL + p * BPL +
+                                                                     x6_off<BK>(wj * 32 + b * 16 + i16, 4 * s + g));
+                }
+                // hi hi, hi lo, lo hi
+                constexpr int PA[3] = {0, 0, 1}, PB[3] = {0, 1, 0};
+#pragma unroll
+                for (int t = 0; t < 3; ++t)
+#pragma unroll
+                    for (int a = 0; a < 2; ++a)
+#pragma unroll
+                        for (int b = 0; b < 2; ++b)
+                            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][PA[t]], bfr[b][PB[t]], acc[a][b], 0, 0, 0);
+            }
+            return;
+        }
 #pragma unroll
         for (int s = 0; s < BK / 32; ++s) {
             bf16x8 af[2][3], bfr[2][3];
@@ -165,7 +217,9 @@ __global__ __launch_bounds__(4 * BM) void gemm_x6_kernel(X6Params P) {
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) cl[(wi * 32 + a * 16 + 4 * g + r) * LDC + wj * 32 + b * 16 + i16] = acc[a][b][r];
+            for (int r = 0; r < 4; ++r)
+                cl[(wi * 32 + a * 16 + 4 * g + r) * LDC + wj * 32 + b * 16 + i16] = H2 ? acc[a][b][r] * inv_sa * inv_sb
+                                                                                      : acc[a][b][r];
     __syncthreads();
     epilogue_v4<BM, BN, NT>(P.epi, cl, LDC, m0, n0, P.M, P.N, ep);
 }

@@ -319,6 +319,10 @@ struct ActBwd {
     float *out;
     float *prelu_part;
     int rows, rows_p, cols, ld;  // cols: padded width (zero columns stay zero)
+    // max |dz| of every 256 consecutive vectors (t / 256) as u32 bits: the scale words of the fp16-pair
+    // GEMM that consumes `out` (gemm_x6_kernel<H2>); needs V = 4 and rows_p * cols / 4 % 256 == 0 (every
+    // workgroup's trip count uniform)
+    uint32_t *words;
 };
 
 // V consecutive columns per thread (V = 4 when cols, ld, ldg are multiples of 4: 16-byte loads and
@@ -328,11 +332,13 @@ template <int V>
 __global__ __launch_bounds__(256) void act_bwd_kernel(ActBwd P) {
     typedef float __attribute__((ext_vector_type(V))) fv;
     __shared__ float red[256];
+    __shared__ uint32_t wred[2][4];
     const float slope = (P.Z && P.act == ACT_PRELU) ? P.slope[0] : 0.f;
     float ppart = 0.f;
     const int cv = P.cols / V;
     const int total = P.rows_p * cv;
-    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    int it = 0;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x, ++it) {
         const int r = t / cv, c = (t - r * cv) * V;
         const size_t o = (size_t)r * P.ld + c;
         fv dz = (fv)0.f;
@@ -385,6 +391,17 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(ActBwd P) {
         }
         if (P.res_out) *(fv *)(P.res_out + o) = P.res_init ? dz : *(const fv *)(P.res_out + o) + dz;
         *(fv *)(P.out + o) = dz;
+        if (P.words) {
+            // (two LDS slots alternating: the next iteration's writes cannot pass thread 0's read, which
+            // precedes its barrier)
+            uint32_t m = 0u;
+            for (int q = 0; q < V; ++q) m = max(m, absbits(dz[q]));
+            m = wave_max_u32(m);
+            if ((threadIdx.x & 63) == 0) wred[it & 1][threadIdx.x >> 6] = m;
+            __syncthreads();
+            if (threadIdx.x == 0)
+                P.words[t >> 8] = max(max(wred[it & 1][0], wred[it & 1][1]), max(wred[it & 1][2], wred[it & 1][3]));
+        }
     }
     if (P.prelu_part) {
         red[threadIdx.x] = ppart;

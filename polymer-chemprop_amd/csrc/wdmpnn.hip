@@ -63,6 +63,11 @@ int fail(int code, const char *fmt, ...) {
         if (rc_) return rc_;  \
     } while (0)
 
+// the fused backward's data-gradient GEMMs dM = Y_t W_h on fp16 pairs (1) or bf16x3 planes (0)
+#ifndef WD_BWD_H2
+#define WD_BWD_H2 1
+#endif
+
 inline int rup(int x, int m) { return (x + m - 1) / m * m; }
 
 
@@ -327,8 +332,11 @@ bool epi_aligned(const Epi &epi) {
 // C[Mp][Np] = epi([A0 | A1] B^T) on fp32 operands; A segments [Mp][lda], K extents multiples of 32, B
 // [Np][ldb].  split: bf16x6 GEMM with the operands split into planes in the kernel (gemm_x6_kernel,
 // 128- or 64-row tiles; fp32-accurate), else f32 MFMA (gemm_nt16_kernel, 64x64 tiles).
+// a_words / b_word (split only): fp16 pairs instead of bf16x3 planes (gemm_x6_kernel<H2>), A scaled by the
+// max words act_bwd_kernel published for it (a_cv float4 per A row), B by one word.
 int gemm_nt(const float *a0, int lda0, int ka0, const float *a1, int lda1, int ka1, const float *b, int ldb, int Mp,
-            int Np, const Epi &epi, hipStream_t st, bool split = false) {
+            int Np, const Epi &epi, hipStream_t st, bool split = false, const uint32_t *a_words = nullptr,
+            int a_cv = 0, const uint32_t *b_word = nullptr) {
     if (Mp <= 0 || Np <= 0) return 0;
     if (Mp % NBM || Np % NBN || ka0 % BK || ka1 % BK || ka0 <= 0 || lda0 % 4 || (ka1 && lda1 % 4) || ldb % 4 ||
         !epi_aligned(epi))
@@ -341,8 +349,20 @@ int gemm_nt(const float *a0, int lda0, int ka0, const float *a1, int lda1, int k
         const int bm = Mp % 128 == 0 ? 128 : 64;
         X.tiles_m = Mp / bm;
         const dim3 grid(X.tiles_m * X.tiles_n), blk(4 * bm);
-        if (bm == 128) hipLaunchKernelGGL((gemm_x6_kernel<128, 32>), grid, blk, 0, st, X);
-        else hipLaunchKernelGGL((gemm_x6_kernel<64, 32>), grid, blk, 0, st, X);
+        const bool h2 = a_words != nullptr;
+        if (h2) {
+            if (!b_word || a1 || a_cv <= 0 || ((size_t)Mp * a_cv) % 256)
+                return fail(WD_ERR_SHAPE, "gemm_nt: fp16-pair operands need A's words (Mp %d, %d float4 per row)", Mp,
+                            a_cv);
+            X.a_words = a_words; X.a_cv = a_cv; X.b_word = b_word;
+        }
+        if (bm == 128) {
+            if (h2) hipLaunchKernelGGL((gemm_x6_kernel<128, 32, true>), grid, blk, 0, st, X);
+            else hipLaunchKernelGGL((gemm_x6_kernel<128, 32>), grid, blk, 0, st, X);
+        } else {
+            if (h2) hipLaunchKernelGGL((gemm_x6_kernel<64, 32, true>), grid, blk, 0, st, X);
+            else hipLaunchKernelGGL((gemm_x6_kernel<64, 32>), grid, blk, 0, st, X);
+        }
         WD_CHECK_LAUNCH("gemm_x6");
         return 0;
     }
@@ -609,7 +629,7 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
 
 struct BwdLayout {
     size_t dH = 0, dZd = 0, dHo = 0, dZo = 0, dA = 0, dZ0 = 0, dZ1 = 0, dRes = 0, dX = 0, dMs = 0, slab = 0,
-           slab_h = 0, slab_i = 0, prelu = 0, total = 0;  // slab: W_o's (and W_d's) split-K slabs; W_h's, W_i's
+           slab_h = 0, slab_i = 0, prelu = 0, words = 0, total = 0;  // slab: W_o's (and W_d's) split-K slabs; W_h's, W_i's
     size_t prelu_floats = 0;
 };
 
@@ -652,6 +672,7 @@ BwdLayout bwd_layout(const WdGraph *g, const Dims &D) {
     L.slab_i = take(slab_of(D.Hk, x_in(g, D), D.R));
     L.prelu_floats = (size_t)(D.T + 2) * std::max(4096, (D.Rp / 128) * (D.Hk / 64));
     L.prelu = take(L.prelu_floats);
+    L.words = take((msg / 4 + 255) / 256);  // Y_t's scale words (act_bwd_kernel -> gemm_x6_kernel<H2>)
     L.total = off;
     return L;
 }
@@ -1205,6 +1226,8 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
         const bool v4 = P.cols % 4 == 0 && P.ld % 4 == 0 && P.ldg % 4 == 0 && al(P.G) && al(P.out) &&
                         (!P.Z || al(P.Z)) && (!P.add_in || al(P.add_in)) && (!P.res_out || al(P.res_out));
         const int nb = ew_blocks(v4 ? total / 4 : total);
+        if (P.words && (!v4 || (total / 4) % 256))
+            return fail(WD_ERR_SHAPE, "act_bwd: scale words need 256-vector multiples (%zu elements)", total);
         if (prelu && P.Z) { P.prelu_part = prelu_part + prelu_used; prelu_used += nb; }
         if (v4) hipLaunchKernelGGL(act_bwd_kernel<4>, dim3(nb), dim3(256), 0, st, P);
         else hipLaunchKernelGGL(act_bwd_kernel<1>, dim3(nb), dim3(256), 0, st, P);
@@ -1289,6 +1312,7 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
     }
     const Src Xh0 = x_h(D, nullptr);
     const TnPlan tph = tn_plan(Hk, Xh0, D.R);
+    uint32_t *y_words = (uint32_t *)S(Bl.words);
     for (int t = D.T - 1; t >= 1 && D.blocked; --t) {
         // fused training forward: X_t = G M_{t-1} was never formed (the layer kernel computes G (M W_h^T)),
         // so the adjoint of the gather goes first: Y_t = S G^T dZ_t, dW_h (+)= Y_t^T M_{t-1} (M recomputed
@@ -1301,11 +1325,13 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
             Q.G = dZt; Q.ldg = Hk;
             Q.ptr = g->msg_gather_t.ptr; Q.idx = g->msg_gather_t.idx; Q.coef = g->msg_gather_t.coef;
             Q.rows = D.R; Q.rows_p = D.Rp; Q.cols = Hk; Q.ld = Hk; Q.out = D.undirected ? S(Bl.dMs) : Y;
+            if (WD_BWD_H2 && !D.undirected) Q.words = y_words;
             WD_TRY(act_bwd(Q));
             if (D.undirected) {
                 ActBwd U{};
                 U.G = S(Bl.dMs); U.ldg = Hk; U.sym_rev = g->b2revb;
                 U.rows = D.R; U.rows_p = D.Rp; U.cols = Hk; U.ld = Hk; U.out = Y;
+                if (WD_BWD_H2) U.words = y_words;
                 WD_TRY(act_bwd(U));
             }
         }
@@ -1330,7 +1356,8 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
         }
         // (with Y_t as plane tiles written by the gather above and this GEMM on LDS-DMA staging, gemm_x6g: the
         // plane stores cost the gather 4-8 us, the GEMM gained 0-4.5 us; the in-kernel split is kept)
-        WD_TRY(gemm_nt(Y, Hk, Hk, nullptr, 0, 0, W(PL.WhT), Hk, D.Rp, Hk, e, st, true));
+        WD_TRY(gemm_nt(Y, Hk, Hk, nullptr, 0, 0, W(PL.WhT), Hk, D.Rp, Hk, e, st, true, WD_BWD_H2 ? y_words : nullptr,
+                       Hk / 4, (const uint32_t *)W(PL.amax) + 64));
         cur = nxt;
     }
     for (int t = D.T - 1; t >= 1 && !D.blocked; --t) {
