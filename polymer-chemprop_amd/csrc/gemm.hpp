@@ -51,7 +51,8 @@ struct Epi {
     float *prelu_part;     // per-workgroup PReLU slope partial (indexed by blockIdx.x) or null
     // EPI_ACT, gemm_x6g only: per (64-row tile, 64-column tile) the max |amax_act(z)| of the output columns
     // < amax_cols -> amax[row tile * amax_cols / 64 + column tile] (the h2 scale words of a fused layer's
-    // first operand, planes.hpp; slope: PReLU's)
+    // first operand, planes.hpp; slope: PReLU's).  EPI_ACTBWD, gemm_x6_kernel: per output tile the max
+    // |dropout(act(Z))| -> amax[row tile * tiles_n + column tile]
     uint32_t *amax;
     int amax_cols, amax_act;
 };
@@ -190,12 +191,16 @@ __device__ __forceinline__ uint32_t epilogue_v4_act(const Epi &E, const float *C
 }
 
 
+// returns this thread's max |dropout(act(Z))| when E.amax is set (the layer input M the weight-gradient
+// GEMM restages from Z: its fp16-pair scale words), else 0
 template <int ACT, int BM, int BN, int NT>
-__device__ __forceinline__ void epilogue_v4_actbwd(const Epi &E, const float *C, int ldc, int m0, int n0, int M, int N) {
+__device__ __forceinline__ uint32_t epilogue_v4_actbwd(const Epi &E, const float *C, int ldc, int m0, int n0, int M,
+                                                       int N) {
     using EP = EpiPrefetch<BM, BN, NT>;
     const int t = threadIdx.x, cl = (t % EP::C4) * 4, j = n0 + cl;
     const float slope = ACT == ACT_PRELU ? E.slope[0] : 0.f;
     float pp = 0.f;
+    uint32_t mx = 0;
     if (j < N) {  // (N % 4 == 0: checked by the launcher)
 #pragma unroll
         for (int p = 0; p < EP::NP; ++p) {
@@ -213,6 +218,7 @@ __device__ __forceinline__ void epilogue_v4_actbwd(const Epi &E, const float *C,
                     const float sd = E.p_drop > 0.f ? dropout_scale(E.seed, E.layer, i, j + q, E.p_drop) : 1.f;
                     d[q] = gg[q] * sd * act_grad(ACT, zz[q], slope);
                     if (ACT == ACT_PRELU && !(zz[q] > 0.f)) pp += zz[q] * gg[q] * sd;
+                    if (E.amax) mx = max(mx, absbits(act_fwd(ACT, zz[q], slope) * sd));
                 }
                 dz = make_float4(d[0], d[1], d[2], d[3]);
                 if (E.add_in) {
@@ -241,6 +247,7 @@ __device__ __forceinline__ void epilogue_v4_actbwd(const Epi &E, const float *C,
         }
         if (t == 0) E.prelu_part[blockIdx.x] = red[0];
     }
+    return mx;
 }
 
 // the epilogues with the activation dispatched once per call (common.hpp with_act)
@@ -259,7 +266,7 @@ __device__ __forceinline__ uint32_t epilogue_v4(const Epi &E, const float *C, in
     if (E.kind == EPI_ACT)
         with_act(E.act, [&](auto a) { mx = epilogue_v4_act<decltype(a)::value>(E, C, ldc, m0, n0, M, N, ep); });
     else if (E.kind == EPI_ACTBWD)
-        with_act(E.act, [&](auto a) { epilogue_v4_actbwd<decltype(a)::value, BM, BN, NT>(E, C, ldc, m0, n0, M, N); });
+        with_act(E.act, [&](auto a) { mx = epilogue_v4_actbwd<decltype(a)::value, BM, BN, NT>(E, C, ldc, m0, n0, M, N); });
     else
         mx = epilogue_v4_act<ACT_IDENTITY>(E, C, ldc, m0, n0, M, N, ep);
     return mx;

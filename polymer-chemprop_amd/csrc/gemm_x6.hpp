@@ -221,7 +221,11 @@ __global__ __launch_bounds__(4 * BM) void gemm_x6_kernel(X6Params P) {
                 cl[(wi * 32 + a * 16 + 4 * g + r) * LDC + wj * 32 + b * 16 + i16] = H2 ? acc[a][b][r] * inv_sa * inv_sb
                                                                                       : acc[a][b][r];
     __syncthreads();
-    epilogue_v4<BM, BN, NT>(P.epi, cl, LDC, m0, n0, P.M, P.N, ep);
+    const uint32_t mx = epilogue_v4<BM, BN, NT>(P.epi, cl, LDC, m0, n0, P.M, P.N, ep);
+    if (P.epi.kind == EPI_ACTBWD && P.epi.amax) {
+        __shared__ uint32_t red[NT / 64];
+        publish_max(mx, P.epi.amax + mt * P.tiles_n + nt, red);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -266,6 +270,11 @@ struct TnX6Params {
     float *slab; int ld_slab; long long slab_stride; int accumulate;
     int bias_col;          // slab column of the bias gradient, -1 = none
     const float *bias_src; int bias_ld;  // the bias as column sums of this matrix [K][bias_ld] instead of A (or null)
+    // H2 with published scale words instead of the max pass: one scale per operand over the split's rows.
+    // A: act_bwd_kernel's words (one per 256 float4, a_cv float4 per row); B: the data-gradient GEMM's
+    // (one per b_bm-row x 64-column tile, b_tn column tiles)
+    const uint32_t *a_words; int a_cv;
+    const uint32_t *b_words; int b_bm, b_tn;
 };
 
 // SACT: the activation of a SEG_ACT operand as a compile-time constant (one instantiation per activation:
@@ -443,53 +452,68 @@ __global__ __launch_bounds__(256) void gemm_tn_x6_kernel(TnX6Params P) {
         }
     };
     if constexpr (H2) {
-        // max pass: |value| per column over the split's rows (as staged: masked, activated), two chunks of
-        // loads in flight; then per column over the 8 row groups through LDS -> scale and inverse scale
-        uint32_t cm[4] = {0u, 0u, 0u, 0u};
-        auto maxv = [&](Regs &R, int kc) {
-            mask_rows(R, kc);
-            act_rows(R, kc);
+        if (P.a_words) {
+            // the split's rows' words: one scale per operand (error per product <= 2^-22 of the split maxima,
+            // values below 2^-18 of them keep an absolute error <= 2^-39 of the maxima: planes.hpp)
+            const int ke = max(kend, kbeg + 1);
+            const int wa0 = (kbeg * P.a_cv) >> 8, wa1 = (ke * P.a_cv - 1) >> 8;
+            const int rb0 = kbeg / P.b_bm, rb1 = (ke - 1) / P.b_bm;
+            const uint32_t ma = max_words(P.a_words + wa0, wa1 - wa0 + 1);
+            const uint32_t mb = max_words(P.b_words + rb0 * P.b_tn, (rb1 - rb0 + 1) * P.b_tn);
+            const float s = h2_scale(isA ? ma : mb);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                cm[0] = max(cm[0], absbits(R.v[r].x)); cm[1] = max(cm[1], absbits(R.v[r].y));
-                cm[2] = max(cm[2], absbits(R.v[r].z)); cm[3] = max(cm[3], absbits(R.v[r].w));
-            }
-        };
-        auto load_v = [&](Regs &R, int kc) {
-            const int r0 = kbeg + kc * BKC + 4 * h4;
+            for (int c = 0; c < 4; ++c) csc[c] = s;
+            if (tid < 128) inv_scale[tid] = h2_inv_scale(tid < 64 ? ma : mb);
+            __syncthreads();
+        } else {
+            // max pass: |value| per column over the split's rows (as staged: masked, activated), two chunks of
+            // loads in flight; then per column over the 8 row groups through LDS -> scale and inverse scale
+            uint32_t cm[4] = {0u, 0u, 0u, 0u};
+            auto maxv = [&](Regs &R, int kc) {
+                mask_rows(R, kc);
+                act_rows(R, kc);
 #pragma unroll
-            for (int s = 0; s < 4; ++s) R.v[s] = ld4(abase + (size_t)min(r0 + s, rlast) * ald);
-        };
+                for (int r = 0; r < 4; ++r) {
+                    cm[0] = max(cm[0], absbits(R.v[r].x)); cm[1] = max(cm[1], absbits(R.v[r].y));
+                    cm[2] = max(cm[2], absbits(R.v[r].z)); cm[3] = max(cm[3], absbits(R.v[r].w));
+                }
+            };
+            auto load_v = [&](Regs &R, int kc) {
+                const int r0 = kbeg + kc * BKC + 4 * h4;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) R.v[s] = ld4(abase + (size_t)min(r0 + s, rlast) * ald);
+            };
 #ifndef WD_TN_NOMAX
-        if (nchunks > 0) {
+            if (nchunks > 0) {
 #else
-        if (false) {
+            if (false) {
 #endif
-            Regs M0, M1;
-            load_v(M0, 0);
-            load_v(M1, min(1, nchunks - 1));
-            int kc = 0;
-            for (; kc + 1 < nchunks; kc += 2) {
-                maxv(M0, kc);
-                load_v(M0, min(kc + 2, nchunks - 1));
-                maxv(M1, kc + 1);
-                load_v(M1, min(kc + 3, nchunks - 1));
+                Regs M0, M1;
+                load_v(M0, 0);
+                load_v(M1, min(1, nchunks - 1));
+                int kc = 0;
+                for (; kc + 1 < nchunks; kc += 2) {
+                    maxv(M0, kc);
+                    load_v(M0, min(kc + 2, nchunks - 1));
+                    maxv(M1, kc + 1);
+                    load_v(M1, min(kc + 3, nchunks - 1));
+                }
+                if (kc < nchunks) maxv(M0, kc);
             }
-            if (kc < nchunks) maxv(M0, kc);
+            uint32_t *cw = reinterpret_cast<uint32_t *>(lds);  // [2 operands][8 row groups][64 columns]
+#pragma unroll
+            for (int c = 0; c < 4; ++c) cw[(isA ? 0 : 512) + h4 * 64 + 4 * q + c] = cm[c];
+            __syncthreads();
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                uint32_t m = 0;
+#pragma unroll
+                for (int h = 0; h < 8; ++h) m = max(m, cw[(isA ? 0 : 512) + h * 64 + 4 * q + c]);
+                csc[c] = h2_scale(m);
+                if (h4 == 0) inv_scale[(isA ? 0 : 64) + 4 * q + c] = h2_inv_scale(m);
+            }
+            __syncthreads();  // (the words are overwritten by the first chunk's staging)
         }
-        uint32_t *cw = reinterpret_cast<uint32_t *>(lds);  // [2 operands][8 row groups][64 columns]
-#pragma unroll
-        for (int c = 0; c < 4; ++c) cw[(isA ? 0 : 512) + h4 * 64 + 4 * q + c] = cm[c];
-        __syncthreads();
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            uint32_t m = 0;
-#pragma unroll
-            for (int h = 0; h < 8; ++h) m = max(m, cw[(isA ? 0 : 512) + h * 64 + 4 * q + c]);
-            csc[c] = h2_scale(m);
-            if (h4 == 0) inv_scale[(isA ? 0 : 64) + 4 * q + c] = h2_inv_scale(m);
-        }
-        __syncthreads();  // (the words are overwritten by the first chunk's staging)
     }
     if (nchunks > 0) {
         // TN_DEPTH chunks in flight in registers: at step kc chunk kc is in LDS, kc+1 .. kc+D-1 are loading

@@ -472,8 +472,11 @@ TnPlan tn_plan(int n_out, const Src &X, int m_rows) {
 
 // slab[z][n][j] (+)= sum_{m in split z} dZ[m][n] * X[m][j]  (bias column: sum_m dZ[m][n], or of bias_src
 // [m_rows][dZ's ld] when given)
+// a_words / b_words: fp16 pairs scaled by those published words (gemm_tn_x6_kernel<..., true>; SEG_ACT operands
+// only), else bf16x3 planes (or TN_H2's max-pass pairs)
 int gemm_tn(const Src &dZ, const Src &X, int n_out, int m_rows, const TnPlan &tp, float *slab, int accumulate,
-            hipStream_t st, const float *bias_src = nullptr) {
+            hipStream_t st, const float *bias_src = nullptr, const uint32_t *a_words = nullptr, int a_cv = 0,
+            const uint32_t *b_words = nullptr, int b_bm = 0, int b_tn = 0) {
     if (n_out <= 0 || m_rows <= 0) return 0;
     TnX6Params P{};
     P.A = dZ; P.B = X; P.M = n_out; P.N = tp.n_dense; P.K = m_rows; P.k_per_split = tp.k_per_split;
@@ -489,6 +492,22 @@ int gemm_tn(const Src &dZ, const Src &X, int n_out, int m_rows, const TnPlan &tp
         if (X.s[q].kind == SEG_ACT) sact = X.s[q].act;
     if (sact >= 0 && !bias_src) return fail(WD_ERR_ARG, "gemm_tn: a SEG_ACT operand needs its bias source");
     if (bias_src && sact < 0) return fail(WD_ERR_ARG, "gemm_tn: an external bias source goes with a SEG_ACT operand");
+    if (a_words) {
+        if (sact < 0 || !b_words || a_cv <= 0 || b_bm <= 0 || b_tn <= 0)
+            return fail(WD_ERR_ARG, "gemm_tn: fp16-pair words need a SEG_ACT operand and both word arrays");
+        P.a_words = a_words; P.a_cv = a_cv; P.b_words = b_words; P.b_bm = b_bm; P.b_tn = b_tn;
+        switch (sact) {
+        case ACT_RELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_RELU, true, true>), grid, dim3(256), 0, st, P); break;
+        case ACT_LEAKY: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_LEAKY, true, true>), grid, dim3(256), 0, st, P); break;
+        case ACT_PRELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_PRELU, true, true>), grid, dim3(256), 0, st, P); break;
+        case ACT_TANH: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_TANH, true, true>), grid, dim3(256), 0, st, P); break;
+        case ACT_SELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_SELU, true, true>), grid, dim3(256), 0, st, P); break;
+        case ACT_ELU: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_ELU, true, true>), grid, dim3(256), 0, st, P); break;
+        default: hipLaunchKernelGGL((gemm_tn_x6_kernel<ACT_IDENTITY, true, true>), grid, dim3(256), 0, st, P); break;
+        }
+        WD_CHECK_LAUNCH("gemm_tn");
+        return 0;
+    }
     constexpr bool H2 = TN_H2;
     switch (sact) {
     case -1: hipLaunchKernelGGL((gemm_tn_x6_kernel<-1, false, H2>), grid, dim3(256), 0, st, P); break;
@@ -629,7 +648,7 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
 
 struct BwdLayout {
     size_t dH = 0, dZd = 0, dHo = 0, dZo = 0, dA = 0, dZ0 = 0, dZ1 = 0, dRes = 0, dX = 0, dMs = 0, slab = 0,
-           slab_h = 0, slab_i = 0, prelu = 0, words = 0, total = 0;  // slab: W_o's (and W_d's) split-K slabs; W_h's, W_i's
+           slab_h = 0, slab_i = 0, prelu = 0, words = 0, mwords = 0, total = 0;  // slab: W_o's (and W_d's) split-K slabs; W_h's, W_i's
     size_t prelu_floats = 0;
 };
 
@@ -672,7 +691,8 @@ BwdLayout bwd_layout(const WdGraph *g, const Dims &D) {
     L.slab_i = take(slab_of(D.Hk, x_in(g, D), D.R));
     L.prelu_floats = (size_t)(D.T + 2) * std::max(4096, (D.Rp / 128) * (D.Hk / 64));
     L.prelu = take(L.prelu_floats);
-    L.words = take((msg / 4 + 255) / 256);  // Y_t's scale words (act_bwd_kernel -> gemm_x6_kernel<H2>)
+    L.words = take((msg / 4 + 255) / 256);  // Y_t's scale words (act_bwd_kernel -> gemm_x6_kernel<H2>, gemm_tn)
+    L.mwords = take((size_t)(D.Rp / 64) * (D.Hk / 64));  // M_{t-1}'s (the data-gradient GEMM -> gemm_tn)
     L.total = off;
     return L;
 }
@@ -1312,7 +1332,7 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
     }
     const Src Xh0 = x_h(D, nullptr);
     const TnPlan tph = tn_plan(Hk, Xh0, D.R);
-    uint32_t *y_words = (uint32_t *)S(Bl.words);
+    uint32_t *y_words = (uint32_t *)S(Bl.words), *m_words = (uint32_t *)S(Bl.mwords);
     for (int t = D.T - 1; t >= 1 && D.blocked; --t) {
         // fused training forward: X_t = G M_{t-1} was never formed (the layer kernel computes G (M W_h^T)),
         // so the adjoint of the gather goes first: Y_t = S G^T dZ_t, dW_h (+)= Y_t^T M_{t-1} (M recomputed
@@ -1335,13 +1355,9 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
                 WD_TRY(act_bwd(U));
             }
         }
-        Seg m = seg_dense(F(L.Z[t - 1]), Hk, Hk);
-        m.kind = SEG_ACT; m.act = c->activation; m.slope = p->prelu; m.p_drop = t - 1 == 0 ? 0.f : c->dropout;
-        m.seed = c->seed; m.layer = t - 1;
-        WD_TRY(gemm_tn(make_src(D.R, {seg_dense(Y, Hk, Hk)}), make_src(D.R, {m, seg_ones()}), Hk, D.R, tph,
-                       S(Bl.slab_h), t != D.T - 1, st, dZt));
         // dZ_{t-1} = (Y_t W_h) * dropout * act'(Z_{t-1}), the residual sum of mpn.py:123 accumulated, in
-        // the GEMM's epilogue (EPI_ACTBWD)
+        // the GEMM's epilogue (EPI_ACTBWD), which also publishes max |M_{t-1}| per tile for the weight
+        // gradient below (so this GEMM goes first: neither reads what the other writes)
         Epi e{};
         e.kind = EPI_ACTBWD; e.Y = dZbuf[nxt]; e.ld = Hk; e.Z = F(L.Z[t - 1]); e.act = c->activation;
         e.slope = p->prelu; e.p_drop = t - 1 == 0 ? 0.f : c->dropout; e.seed = c->seed; e.layer = t - 1;
@@ -1356,8 +1372,16 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
         }
         // (with Y_t as plane tiles written by the gather above and this GEMM on LDS-DMA staging, gemm_x6g: the
         // plane stores cost the gather 4-8 us, the GEMM gained 0-4.5 us; the in-kernel split is kept)
+        if (WD_BWD_H2) e.amax = m_words;
         WD_TRY(gemm_nt(Y, Hk, Hk, nullptr, 0, 0, W(PL.WhT), Hk, D.Rp, Hk, e, st, true, WD_BWD_H2 ? y_words : nullptr,
                        Hk / 4, (const uint32_t *)W(PL.amax) + 64));
+        // dW_h (+)= Y_t^T [M_{t-1} | 1], db_h (+)= sum dZ_t
+        Seg m = seg_dense(F(L.Z[t - 1]), Hk, Hk);
+        m.kind = SEG_ACT; m.act = c->activation; m.slope = p->prelu; m.p_drop = t - 1 == 0 ? 0.f : c->dropout;
+        m.seed = c->seed; m.layer = t - 1;
+        WD_TRY(gemm_tn(make_src(D.R, {seg_dense(Y, Hk, Hk)}), make_src(D.R, {m, seg_ones()}), Hk, D.R, tph,
+                       S(Bl.slab_h), t != D.T - 1, st, dZt, WD_BWD_H2 ? y_words : nullptr, Hk / 4, m_words,
+                       D.Rp % 128 == 0 ? 128 : 64, Hk / 64));
         cur = nxt;
     }
     for (int t = D.T - 1; t >= 1 && !D.blocked; --t) {
