@@ -16,8 +16,9 @@
 //   gemm_x6g_kernel  operands arrive as plane tiles (written by their producers: the gathers, the
 //                    weight packer, the graph upload); staging is LDS-DMA (global_load_lds_dwordx4),
 //                    no staging registers, no arithmetic.  The forward's default.
-//   gemm_x6_kernel   fp32 operands split in registers while staging (fallback for operands that
-//                    have no plane copy: atom-message mode, descriptors).
+//   gemm_x6_kernel   fp32 operands split in registers while staging (operands that have no plane copy:
+//                    the backward's data gradients, atom-message mode, descriptors); its H2 form splits
+//                    into fp16 pairs instead (the message layers' data gradients).
 #pragma once
 #include "gemm.hpp"
 #include "planes.hpp"
