@@ -804,27 +804,37 @@ struct SmallGemm {
     float *C; long long ldc;
     int M, N, K;
 };
-// 32 x 32 output tile per workgroup of 4 waves: both operands' K-slices of SG_KC staged k-major in LDS
+// TS x TS output tile per workgroup of 4 waves: both operands' K-slices of SG_KC staged k-major in LDS
 // (every load of the stage in flight at once: these GEMMs are load-latency-bound, 128 x 300 x 300), wave w
-// multiplies the w-th quarter of the stage's K (lane: 4 x 4 outputs from two float4 reads per k), and the
-// four partial tiles are added in wave order (deterministic).
-constexpr int SG_KC = 320, SG_LD = 36;  // (row stride 36: float4-aligned, 4-way bank spread for the staging)
-struct SmallGemmLds { float as[SG_KC][SG_LD]; float bs[SG_KC][SG_LD]; };
+// multiplies the w-th quarter of the stage's K (lane: R x R outputs, R = TS / 8, from two R-float reads per
+// k), and the four partial tiles are added in wave order (deterministic; every output's arithmetic is
+// the same for either tile size).  TS = 16: 4x the workgroups of 32 x 32 tiles, each loading
+// half the operand rows: head_h_kernel's 128 x 300 output as 40 tiles of 32 x 32 took 12.8 us, as 152 of
+// 16 x 16 6.9 us; head_grads_kernel's two GEMMs stay on 32 x 32 (16 x 16: 13.0 against 11.0 us).
+constexpr int SG_KC = 320;
+template <int TS>
+struct alignas(16) SmallGemmLds {
+    static constexpr int LD = TS + 4;  // (row stride TS + 4: R-float aligned, bank spread for the staging)
+    float as[SG_KC][LD];
+    float bs[SG_KC][LD];
+};
 // AK: A's k index contiguous (sak == 1, else sai == 1); BJ: B's j index contiguous (sbj == 1, else sbk == 1)
-template <bool AK, bool BJ>
-__device__ __forceinline__ void small_gemm_tile_t(const SmallGemm &G, int tile, SmallGemmLds &L) {
-    const int tn = (G.N + 31) / 32, i0 = (tile / tn) * 32, j0 = (tile % tn) * 32;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, ri = 4 * (lane >> 3), cj = 4 * (lane & 7);
-    constexpr int PER = 32 * SG_KC / 256;
-    float c[4][4] = {};
+template <int TS, bool AK, bool BJ>
+__device__ __forceinline__ void small_gemm_tile_t(const SmallGemm &G, int tile, SmallGemmLds<TS> &L) {
+    constexpr int R = TS / 8;
+    typedef float fR __attribute__((ext_vector_type(R)));
+    const int tn = (G.N + TS - 1) / TS, i0 = (tile / tn) * TS, j0 = (tile % tn) * TS;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, ri = R * (lane >> 3), cj = R * (lane & 7);
+    constexpr int PER = TS * SG_KC / 256;
+    float c[R][R] = {};
     float ra[PER], rb[PER];
     auto load = [&](int k0) {  // consecutive lanes along each operand's contiguous index (coalesced)
 #pragma unroll
         for (int q = 0; q < PER; ++q) {
             const int e = tid + 256 * q;
-            const int ia = i0 + (AK ? e / SG_KC : e % 32), ka = k0 + (AK ? e % SG_KC : e / 32);
+            const int ia = i0 + (AK ? e / SG_KC : e % TS), ka = k0 + (AK ? e % SG_KC : e / TS);
             ra[q] = ia < G.M && ka < G.K ? G.A[ia * G.sai + ka * G.sak] : 0.f;
-            const int kb = k0 + (BJ ? e / 32 : e % SG_KC), jb = j0 + (BJ ? e % 32 : e / SG_KC);
+            const int kb = k0 + (BJ ? e / TS : e % SG_KC), jb = j0 + (BJ ? e % TS : e / SG_KC);
             rb[q] = kb < G.K && jb < G.N ? G.B[kb * G.sbk + jb * G.sbj] : 0.f;
         }
     };
@@ -833,8 +843,8 @@ __device__ __forceinline__ void small_gemm_tile_t(const SmallGemm &G, int tile, 
         for (int q = 0; q < PER; ++q) {
             const int e = tid + 256 * q;
             if (AK) L.as[e % SG_KC][e / SG_KC] = ra[q];
-            else L.as[e / 32][e % 32] = ra[q];
-            if (BJ) L.bs[e / 32][e % 32] = rb[q];
+            else L.as[e / TS][e % TS] = ra[q];
+            if (BJ) L.bs[e / TS][e % TS] = rb[q];
             else L.bs[e % SG_KC][e / SG_KC] = rb[q];
         }
     };
@@ -846,36 +856,41 @@ __device__ __forceinline__ void small_gemm_tile_t(const SmallGemm &G, int tile, 
         const int kn = min(SG_KC, G.K - k0), kq = (kn + 3) / 4, kb = wave * kq, ke = min(kn, kb + kq);
 #pragma unroll 4
         for (int k = kb; k < ke; ++k) {
-            const float4 a = *reinterpret_cast<const float4 *>(&L.as[k][ri]);
-            const float4 b = *reinterpret_cast<const float4 *>(&L.bs[k][cj]);
-            const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+            const fR a = *reinterpret_cast<const fR *>(&L.as[k][ri]);
+            const fR b = *reinterpret_cast<const fR *>(&L.bs[k][cj]);
 #pragma unroll
-            for (int x = 0; x < 4; ++x)
+            for (int x = 0; x < R; ++x)
 #pragma unroll
-                for (int y = 0; y < 4; ++y) c[x][y] = fmaf(av[x], bv[y], c[x][y]);
+                for (int y = 0; y < R; ++y) c[x][y] = fmaf(a[x], b[y], c[x][y]);
         }
         __syncthreads();
     }
     // the four waves' partial tiles (in as, free after the last barrier), added in wave order
     float *part = &L.as[0][0];
+    static_assert(4 * TS * TS <= SG_KC * SmallGemmLds<TS>::LD, "partial tiles must fit in the A stage");
 #pragma unroll
-    for (int x = 0; x < 4; ++x)
-        *reinterpret_cast<float4 *>(part + wave * 1024 + (ri + x) * 32 + cj) = make_float4(c[x][0], c[x][1], c[x][2], c[x][3]);
+    for (int x = 0; x < R; ++x) {
+        fR v;
+#pragma unroll
+        for (int y = 0; y < R; ++y) v[y] = c[x][y];
+        *reinterpret_cast<fR *>(part + wave * TS * TS + (ri + x) * TS + cj) = v;
+    }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int o = tid + 256 * q, i = i0 + o / 32, j = j0 + o % 32;
-        const float v = ((part[o] + part[1024 + o]) + part[2048 + o]) + part[3072 + o];
+    for (int q = 0; q < TS * TS / 256; ++q) {
+        const int o = tid + 256 * q, i = i0 + o / TS, j = j0 + o % TS;
+        const float v = ((part[o] + part[TS * TS + o]) + part[2 * TS * TS + o]) + part[3 * TS * TS + o];
         if (i < G.M && j < G.N) G.C[i * G.ldc + j] = v + (G.bias ? G.bias[j] : 0.f);
     }
 }
-__device__ __forceinline__ void small_gemm_tile(const SmallGemm &G, int tile, SmallGemmLds &L) {
+template <int TS>
+__device__ __forceinline__ void small_gemm_tile(const SmallGemm &G, int tile, SmallGemmLds<TS> &L) {
     if (G.sak == 1) {
-        if (G.sbj == 1) small_gemm_tile_t<true, true>(G, tile, L);
-        else small_gemm_tile_t<true, false>(G, tile, L);
+        if (G.sbj == 1) small_gemm_tile_t<TS, true, true>(G, tile, L);
+        else small_gemm_tile_t<TS, true, false>(G, tile, L);
     } else {
-        if (G.sbj == 1) small_gemm_tile_t<false, true>(G, tile, L);
-        else small_gemm_tile_t<false, false>(G, tile, L);
+        if (G.sbj == 1) small_gemm_tile_t<TS, false, true>(G, tile, L);
+        else small_gemm_tile_t<TS, false, false>(G, tile, L);
     }
 }
 
@@ -897,11 +912,13 @@ __device__ __forceinline__ float row_sum(const float *x, long long ld, const flo
     for (; r < B; ++r) s = y ? fmaf(x[r * ld], y[r * ldy], s) : s + x[r * ld];
     return s;
 }
-__device__ __forceinline__ int small_gemm_tiles(const SmallGemm &G) { return ((G.M + 31) / 32) * ((G.N + 31) / 32); }
+// tile sizes of the head's GEMMs and the launch sizes they give
+constexpr int HEAD_H_TS = 16, HEAD_G_TS = 32;
+__host__ __device__ inline int head_tiles(int M, int N, int ts) { return ((M + ts - 1) / ts) * ((N + ts - 1) / ts); }
 
 // head step 1: H = X W1^T + b1 -> P.a (pre-activation, [B][Hf])
 __global__ __launch_bounds__(256) void head_h_kernel(WdHead P) {
-    __shared__ SmallGemmLds L;
+    __shared__ SmallGemmLds<HEAD_H_TS> L;
     SmallGemm G{P.x, P.ld_x, 1, P.W1, 1, P.F, P.b1, P.a, P.Hf, P.B, P.Hf, P.F};
     small_gemm_tile(G, blockIdx.x, L);
 }
@@ -954,10 +971,10 @@ __global__ __launch_bounds__(256) void head_rows_kernel(WdHead P) {
 // head step 3: dX = dH W1 (tiles 0 .. n1), dW1 = dH^T X (next n2 tiles), then db1, dW2, db2 and the loss
 // (one thread per element, rows summed in order)
 __global__ __launch_bounds__(256) void head_grads_kernel(WdHead P) {
-    __shared__ SmallGemmLds L;
+    __shared__ SmallGemmLds<HEAD_G_TS> L;
     const SmallGemm GX{P.dh, P.Hf, 1, P.W1, P.F, 1, nullptr, P.dx, P.ld_x, P.B, P.F, P.Hf};
     const SmallGemm GW{P.dh, 1, P.Hf, P.x, P.ld_x, 1, nullptr, P.dW1, P.F, P.Hf, P.F, P.B};
-    const int n1 = small_gemm_tiles(GX), n2 = small_gemm_tiles(GW);
+    const int n1 = head_tiles(GX.M, GX.N, HEAD_G_TS), n2 = head_tiles(GW.M, GW.N, HEAD_G_TS);
     const int b = blockIdx.x;
     if (b < n1) { small_gemm_tile(GX, b, L); return; }
     if (b < n1 + n2) { small_gemm_tile(GW, b - n1, L); return; }
@@ -978,8 +995,6 @@ __global__ __launch_bounds__(256) void head_grads_kernel(WdHead P) {
     }
 }
 
-// launch sizes of the head steps
-__host__ __device__ inline int head_tiles(int M, int N) { return ((M + 31) / 32) * ((N + 31) / 32); }
 
 // y_i *= s[0] for up to 8 buffers (the head's gradients times the incoming gradient of the loss)
 struct ScaleJobs {

@@ -1985,13 +1985,13 @@ int wdmpnn_head_mse(const WdHead *h, void *stream) {
         return fail(WD_ERR_ARG, "head: null pointer");
     hipStream_t st = (hipStream_t)stream;
     if (h->B > 0) {
-        hipLaunchKernelGGL(head_h_kernel, dim3(head_tiles(h->B, h->Hf)), dim3(256), 0, st, *h);
+        hipLaunchKernelGGL(head_h_kernel, dim3(head_tiles(h->B, h->Hf, HEAD_H_TS)), dim3(256), 0, st, *h);
         WD_CHECK_LAUNCH("head_h");
         hipLaunchKernelGGL(head_rows_kernel, dim3((h->B + 3) / 4), dim3(256), 0, st, *h);
         WD_CHECK_LAUNCH("head_rows");
     }
     const long long rest = h->Hf + (long long)h->T * h->Hf + h->T + 1;
-    const long long blocks = head_tiles(h->B, h->F) + head_tiles(h->Hf, h->F) + (rest + 255) / 256;
+    const long long blocks = head_tiles(h->B, h->F, HEAD_G_TS) + head_tiles(h->Hf, h->F, HEAD_G_TS) + (rest + 255) / 256;
     hipLaunchKernelGGL(head_grads_kernel, dim3((unsigned)blocks), dim3(256), 0, st, *h);
     WD_CHECK_LAUNCH("head_grads");
     return 0;
