@@ -810,7 +810,8 @@ struct SmallGemm {
 // k), and the four partial tiles are added in wave order (deterministic; every output's arithmetic is
 // the same for either tile size).  TS = 16: 4x the workgroups of 32 x 32 tiles, each loading
 // half the operand rows: head_h_kernel's 128 x 300 output as 40 tiles of 32 x 32 took 12.8 us, as 152 of
-// 16 x 16 6.9 us; head_grads_kernel's two GEMMs stay on 32 x 32 (16 x 16: 13.0 against 11.0 us).
+// 16 x 16 6.9 us; head_grads_kernel's dX = dH W1 (K = 300) on 16 x 16 too, its dW1 = dH^T X (K = B = 128,
+// half of a 320-deep stage) on 32 x 32 (all of it on 16 x 16: 13.0 against 11.0 us).
 constexpr int SG_KC = 320;
 template <int TS>
 struct alignas(16) SmallGemmLds {
@@ -818,6 +819,7 @@ struct alignas(16) SmallGemmLds {
     float as[SG_KC][LD];
     float bs[SG_KC][LD];
 };
+static_assert(sizeof(SmallGemmLds<16>) <= sizeof(SmallGemmLds<32>), "head_grads_kernel shares one LDS area");
 // AK: A's k index contiguous (sak == 1, else sai == 1); BJ: B's j index contiguous (sbj == 1, else sbk == 1)
 template <int TS, bool AK, bool BJ>
 __device__ __forceinline__ void small_gemm_tile_t(const SmallGemm &G, int tile, SmallGemmLds<TS> &L) {
@@ -974,9 +976,9 @@ __global__ __launch_bounds__(256) void head_grads_kernel(WdHead P) {
     __shared__ SmallGemmLds<HEAD_G_TS> L;
     const SmallGemm GX{P.dh, P.Hf, 1, P.W1, P.F, 1, nullptr, P.dx, P.ld_x, P.B, P.F, P.Hf};
     const SmallGemm GW{P.dh, 1, P.Hf, P.x, P.ld_x, 1, nullptr, P.dW1, P.F, P.Hf, P.F, P.B};
-    const int n1 = head_tiles(GX.M, GX.N, HEAD_G_TS), n2 = head_tiles(GW.M, GW.N, HEAD_G_TS);
+    const int n1 = head_tiles(GX.M, GX.N, HEAD_H_TS), n2 = head_tiles(GW.M, GW.N, HEAD_G_TS);
     const int b = blockIdx.x;
-    if (b < n1) { small_gemm_tile(GX, b, L); return; }
+    if (b < n1) { small_gemm_tile(GX, b, *reinterpret_cast<SmallGemmLds<HEAD_H_TS> *>(&L)); return; }
     if (b < n1 + n2) { small_gemm_tile(GW, b - n1, L); return; }
     const int Hf = P.Hf, T = P.T, B = P.B;
     const long long q = (long long)(b - n1 - n2) * 256 + threadIdx.x;

@@ -1991,7 +1991,7 @@ int wdmpnn_head_mse(const WdHead *h, void *stream) {
         WD_CHECK_LAUNCH("head_rows");
     }
     const long long rest = h->Hf + (long long)h->T * h->Hf + h->T + 1;
-    const long long blocks = head_tiles(h->B, h->F, HEAD_G_TS) + head_tiles(h->Hf, h->F, HEAD_G_TS) + (rest + 255) / 256;
+    const long long blocks = head_tiles(h->B, h->F, HEAD_H_TS) + head_tiles(h->Hf, h->F, HEAD_G_TS) + (rest + 255) / 256;
     hipLaunchKernelGGL(head_grads_kernel, dim3((unsigned)blocks), dim3(256), 0, st, *h);
     WD_CHECK_LAUNCH("head_grads");
     return 0;
