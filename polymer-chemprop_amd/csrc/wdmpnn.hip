@@ -332,6 +332,10 @@ bool epi_aligned(const Epi &epi) {
 // C[Mp][Np] = epi([A0 | A1] B^T) on fp32 operands; A segments [Mp][lda], K extents multiples of 32, B
 // [Np][ldb].  split: bf16x6 GEMM with the operands split into planes in the kernel (gemm_x6_kernel,
 // 128- or 64-row tiles; fp32-accurate), else f32 MFMA (gemm_nt16_kernel, 64x64 tiles).
+// gemm_x6_kernel's row tile (its grid, PReLU partials and TN scale-word rows follow it).  (64-row tiles for
+// grids under 256 workgroups, the training batch's atom-row GEMM: 12.80 vs 12.76 us, not taken)
+inline int x6_bm(int Mp) { return Mp % 128 == 0 ? 128 : 64; }
+
 // a_words / b_word (split only): fp16 pairs instead of bf16x3 planes (gemm_x6_kernel<H2>), A scaled by the
 // max words act_bwd_kernel published for it (a_cv float4 per A row), B by one word.
 int gemm_nt(const float *a0, int lda0, int ka0, const float *a1, int lda1, int ka1, const float *b, int ldb, int Mp,
@@ -346,7 +350,7 @@ int gemm_nt(const float *a0, int lda0, int ka0, const float *a1, int lda1, int k
         X.a0 = a0; X.lda0 = lda0; X.ka0 = ka0; X.a1 = a1; X.lda1 = lda1; X.ka1 = ka1;
         X.bf = b; X.ldb = ldb;
         X.M = Mp; X.N = Np; X.epi = epi; X.tiles_n = Np / X6_BN;
-        const int bm = Mp % 128 == 0 ? 128 : 64;
+        const int bm = x6_bm(Mp);
         X.tiles_m = Mp / bm;
         const dim3 grid(X.tiles_m * X.tiles_n), blk(4 * bm);
         const bool h2 = a_words != nullptr;
@@ -689,7 +693,7 @@ BwdLayout bwd_layout(const WdGraph *g, const Dims &D) {
     L.slab = take(so);
     L.slab_h = take(slab_of(D.Hk, x_h(D, nullptr), D.R));
     L.slab_i = take(slab_of(D.Hk, x_in(g, D), D.R));
-    L.prelu_floats = (size_t)(D.T + 2) * std::max(4096, (D.Rp / 128) * (D.Hk / 64));
+    L.prelu_floats = (size_t)(D.T + 2) * std::max(4096, (D.Rp / 64) * (D.Hk / 64));  // (64-row tiles at most)
     L.prelu = take(L.prelu_floats);
     L.words = take((msg / 4 + 255) / 256);  // Y_t's scale words (act_bwd_kernel -> gemm_x6_kernel<H2>, gemm_tn)
     L.mwords = take((size_t)(D.Rp / 64) * (D.Hk / 64));  // M_{t-1}'s (the data-gradient GEMM -> gemm_tn)
@@ -1365,7 +1369,7 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
         if (t - 1 == 0) e.add_in = S(Bl.dRes);
         else { e.res_out = S(Bl.dRes); e.res_init = 0; }
         if (prelu) {
-            const int tiles = (D.Rp / 128) * (Hk / 64);  // (gemm_x6_kernel<128>'s grid)
+            const int tiles = (D.Rp / x6_bm(D.Rp)) * (Hk / 64);  // (gemm_x6_kernel's grid)
             if (prelu_used + tiles > (int)Bl.prelu_floats) return fail(WD_ERR_SHAPE, "PReLU partials overflow");
             e.prelu_part = prelu_part + prelu_used;
             prelu_used += tiles;
@@ -1381,7 +1385,7 @@ int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, cons
         m.seed = c->seed; m.layer = t - 1;
         WD_TRY(gemm_tn(make_src(D.R, {seg_dense(Y, Hk, Hk)}), make_src(D.R, {m, seg_ones()}), Hk, D.R, tph,
                        S(Bl.slab_h), t != D.T - 1, st, dZt, WD_BWD_H2 ? y_words : nullptr, Hk / 4, m_words,
-                       D.Rp % 128 == 0 ? 128 : 64, Hk / 64));
+                       x6_bm(D.Rp), Hk / 64));
         cur = nxt;
     }
     for (int t = D.T - 1; t >= 1 && !D.blocked; --t) {
