@@ -221,7 +221,10 @@ struct RoActBwd {
     int rows, rows_p;
     float *prelu_part;                      // [gridDim.x * gridDim.y] or null
 };
-constexpr int RO_ACT_MAXLD = 2560, RO_ACT_Y = 4, RO_ACT_U = 4;
+#ifndef WD_RO_ACT_Y
+#define WD_RO_ACT_Y 16  // (workgroups per molecule: 4 / 8 / 16 took 7.5 / 6.5 / 6.4 us at B = 128)
+#endif
+constexpr int RO_ACT_MAXLD = 2560, RO_ACT_Y = WD_RO_ACT_Y, RO_ACT_U = 4;
 
 __global__ __launch_bounds__(256) void readout_act_bwd_kernel(ReadoutP P, const float *__restrict__ dout, RoActBwd A) {
     constexpr int NT = 256, U = RO_ACT_U;
