@@ -26,6 +26,33 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, 'polymer-chemprop_amd'))
 sys.path.insert(0, ROOT)
 
+
+def _pin_cpus(argv):
+    """--cpus N: restrict this process to N CPUs of its affinity set (rank r of a node takes the r-th
+    disjoint slice) before torch or the HIP runtime start any thread, so that one GPU can measure what a
+    rank gets when eight ranks share a 16-CPU quota (N = 2).  Every later thread (torch's, the HIP
+    runtime's, the native feed's producers and feeder) inherits the set, and the producer cap
+    (chemprop_amd.stream.producer_cap) reads it.  Returns the CPU list, or None without the option."""
+    n = 0
+    for i, x in enumerate(argv):
+        if x == '--cpus' and i + 1 < len(argv):
+            n = int(argv[i + 1])
+        elif x.startswith('--cpus='):
+            n = int(x.split('=', 1)[1])
+    if n <= 0:
+        return None
+    allowed = sorted(os.sched_getaffinity(0))
+    r = int(os.environ.get('LOCAL_RANK', '0'))
+    pick = allowed[(r * n) % len(allowed):][:n]
+    if len(pick) < n:
+        pick = allowed[:n]
+    os.sched_setaffinity(0, pick)
+    os.environ['OMP_NUM_THREADS'] = str(n)
+    return pick
+
+
+PINNED_CPUS = _pin_cpus(sys.argv)
+
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -124,6 +151,30 @@ def pmc_traffic(prefix):
     return sum(v) / len(v), f'profiles/{PMC_TRAFFIC}: {d.get("_note", "")}'
 
 
+ROCPROF_STATS = "round5_bench_b64_kernel_stats.csv"  # rocprofv3 --kernel-trace --stats of the headline, one stream
+
+
+def rocprof_alone(prefix):
+    """(mean launch us of the kernels named ``prefix``* -- their variants weighted by calls --, source) from the
+    committed rocprofv3 kernel-stats summary of the headline workload with one batch in flight: the
+    dominant kernel's time alone on the GPU, next to the events' in-flight figure the bench measures."""
+    import csv
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', ROCPROF_STATS)
+    try:
+        rows = list(csv.DictReader(open(path)))
+    except OSError:
+        return None, None
+    calls = tot = 0
+    for r in rows:
+        name = r['Name'].replace('void ', '').replace('wd::', '')
+        if name.startswith(prefix):
+            calls += int(r['Calls'])
+            tot += float(r['TotalDurationNs'])
+    if not calls:
+        return None, None
+    return tot / calls / 1e3, f'profiles/{ROCPROF_STATS} ({calls} launches)'
+
+
 def forward_roofline(graphs, a, t_fwd):
     """Whole-forward fractions per SURVEY §8(d): algorithmic bytes (fp32, each logical tensor read or
     written once, gathers at unique size, int32 indices) and FLOPs of mpn.py:92-171 for the average
@@ -197,6 +248,8 @@ def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_b
         streams = default_streams(sum(g.n_bonds - 1 for g in graphs) / len(graphs))
     ss = bench_streams(device, streams)
 
+    prev_stream = torch.cuda.current_stream(device)
+
     def timed(n_streams):
         def fwd(i):
             if n_streams == 1:
@@ -205,12 +258,12 @@ def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_b
             return enc(graphs[i % len(graphs)])
         for i in range(warmup):
             fwd(i)
-        torch.cuda.set_stream(ss[0])
+        torch.cuda.set_stream(prev_stream)
         torch.cuda.synchronize(device)
         t0 = time.perf_counter()
         for i in range(steps):
             fwd(i)
-        torch.cuda.set_stream(ss[0])
+        torch.cuda.set_stream(prev_stream)
         torch.cuda.synchronize(device)
         return time.perf_counter() - t0
 
@@ -438,6 +491,9 @@ def main():
     ap.add_argument('--producers', type=int, default=0,
                     help='native generator threads per rank of the streamed workloads (0 = the cap: max(2, usable '
                          'cores // ranks per node - 2), chemprop_amd.stream.producer_cap; larger requests are capped)')
+    ap.add_argument('--cpus', type=int, default=0,
+                    help='run this rank on N CPUs only (sched_setaffinity before torch starts; 0 = all): the '
+                         'per-rank host budget of an 8-rank node, e.g. 2 on a 16-CPU quota')
     ap.add_argument('--stream-train-graphs', type=int, default=131_072,
                     help='configs[4] as DP training: streamed graphs per rank (batches of 128); 0 = skip')
     a = ap.parse_args()
@@ -482,8 +538,10 @@ def main():
         torch.cuda.set_stream(streams[i % len(streams)])
         return enc(graphs[i % len(graphs)])
 
+    prev_stream = torch.cuda.current_stream(device)  # (torch's default stream: every loop returns to it)
+
     def restore():
-        torch.cuda.set_stream(streams[0])
+        torch.cuda.set_stream(prev_stream)
 
     def barrier():
         torch.cuda.synchronize(device)
@@ -607,6 +665,7 @@ def main():
         bytes_launch = 4.0 * (3 * E_avg * H + H * H + H) + 8.0 * E_avg * d_avg + 4.0 * E_avg
         avg_launch_s = (kernel_ms.value / 1e3 / n_launch) if n_launch else float('nan')
         traffic, traffic_src = pmc_traffic('mp_layer_kernel<80')
+        alone_us, alone_src = rocprof_alone('mp_layer_kernel<80')
         achieved = flops_launch / avg_launch_s / 1e12 if n_launch else None
         hbm = bytes_launch / avg_launch_s / 1e9 if n_launch else None
         line = {
@@ -624,9 +683,9 @@ def main():
             'scaling': 'weak',
             'vs_baseline': None,
             'dtype': 'fp32',
-            'arith': 'fp32-accurate GEMMs: message-passing layers as fp16 hi/lo operand pairs with per-block '
-                     'power-of-two scales on fp16 MFMA (3 products, fp32 accumulate), W_o as exact bf16x3 '
-                     'splits (6 products); gathers, residual, activations and readout in fp32',
+            'arith': 'fp32-accurate GEMMs: the message-passing layers and W_o on fp16 hi/lo operand pairs (power-of-two '
+                     'scales per producer tile, written by the producing kernel and copied by LDS-DMA) on fp16 MFMA '
+                     '(3 products per fp32 product, fp32 accumulate); gathers, residual, activations and readout in fp32',
             'data': 'synthetic',
             'config': {'workload': f'MPNEncoder.forward on synthetic {a.kind} batches of {a.batch} graphs '
                                    f'(avg E={E_avg:.0f} directed edges), depth={a.depth}, hidden={H}, '
@@ -655,7 +714,16 @@ def main():
                          'avg_launch_us': avg_launch_s * 1e6, 'flops_per_launch': flops_launch,
                          'bytes_per_launch': bytes_launch, 'hbm_gbs': hbm,
                          'hbm_frac': hbm / HBM_PEAK_GBS if hbm else None,
-                         'launches_timed': n_launch},
+                         'launches_timed': n_launch,
+                         'in_flight': {'avg_launch_us': avg_launch_s * 1e6,
+                                       'frac': achieved / FP32_MFMA_PEAK_TFLOPS if achieved else None,
+                                       'source': f'HIP events around the layer launches, {a.streams} batches in '
+                                                 'flight (a second pass of the timed loop)'},
+                         'alone': ({'avg_launch_us': alone_us,
+                                    'frac': flops_launch / (alone_us * 1e-6) / 1e12 / FP32_MFMA_PEAK_TFLOPS,
+                                    'source': alone_src + ', one batch in flight'}
+                                   if alone_us else None)},
+            'host_cpus': {'pinned': PINNED_CPUS, 'usable': _usable_cores(1)[0]},
         }
         line['forward'] = forward_roofline(graphs, a, elapsed / a.steps)
         if st_dt > 0:

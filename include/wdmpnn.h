@@ -20,7 +20,11 @@
  *    PyTorch caching allocator).  The library never allocates device memory.
  *  - Row 0 of every atom / bond array is the reference's zero pad row (featurization.py:767-781);
  *    n_atoms / n_bonds INCLUDE it, exactly like BatchMolGraph.n_atoms / n_bonds.
- *  - fp32 storage and fp32 arithmetic (MFMA f32 in/out), int32 indices.
+ *  - fp32 storage and fp32-accurate arithmetic, int32 indices.  The GEMMs run on MFMA with fp32
+ *    accumulation over exact splits of the fp32 operands: fp16 hi / lo pairs with a power-of-two scale
+ *    (three products per fp32 product, the message layers and the backward's W_h GEMMs) or three bf16
+ *    planes (six products: W_o, W_i and the unblocked path).  Error against fp64 stays that of an fp32
+ *    GEMM; WdConfig.gemm_variant 9 selects plain f32-in MFMA on the unblocked path.
  *  - Padding: f_atoms / f_bonds / atom_desc rows are allocated up to a multiple of 128 and their row
  *    stride covers the feature width rounded up to 32; padding is zero.  (The host packer,
  *    BatchMolGraph.device_graph, lays them out this way.)  Weights are the unpadded nn.Linear
@@ -40,7 +44,7 @@
 extern "C" {
 #endif
 
-#define WDMPNN_ABI_VERSION 10
+#define WDMPNN_ABI_VERSION 11
 #define WDMPNN_ELL_WIDTH 8
 
 enum WdActivation {     /* nn_utils.py:70-99 get_activation_function */
@@ -191,8 +195,11 @@ typedef struct WdConfig {
                                forward: before the first, after the last                          */
     int32_t gemm_variant;   /* 0 (default): bf16x6 split-plane GEMMs (fp32-accurate), with the
                                molecule-blocked fused inference forward when WdGraph.blocks allow it;
-                               9: f32-MFMA GEMMs on the unblocked path (precision A/B).  The backward
-                               always runs the deterministic f32-MFMA kernels.                       */
+                               9: f32-MFMA GEMMs on the unblocked path (precision A/B); 11: the fused
+                               four-launch forward also for QM9-sized blocks (no one-launch forward);
+                               12: as 11, with the message layers staging M_{t-1} from fp32 Z_t rows
+                               through registers (the round-5 layer) instead of reading the fp16 pair
+                               tiles their producer wrote (A/B and the one-launch bitwise test).    */
 } WdConfig;
 
 /* Gradients (device, caller-zeroed NOT required: every pointer is fully overwritten). NULL = skip. */
@@ -202,6 +209,13 @@ typedef struct WdGrads {
 
 int wdmpnn_abi_version(void);
 const char *wdmpnn_last_error(void);
+/* Load-time kernel check (ABI 11): 0 when the library's gfx950 code object holds every kernel its host
+ * code launches (a mismatched build would otherwise abort the process inside a HIP launch), else
+ * WD_ERR_UNSUPPORTED with the missing kernel in wdmpnn_last_error().  Reads only the library file (no HIP
+ * call, runs without a GPU); every compute entry point runs it once per process and fails the same way.
+ * The counts (either pointer may be NULL): kernels the host registers, kernel descriptors in the code
+ * object. */
+int wdmpnn_self_check(int32_t *n_host_kernels, int32_t *n_device_kernels);
 
 /* Padded / transposed copies of the weights for the GEMMs; depends only on the parameter values and
  * the encoder dimensions, so callers cache it per parameter version (chemprop_amd does). */
@@ -364,8 +378,10 @@ int wdmpnn_adam_step(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *
  * pack before every forward (train.py:84 then mpn.py:66's next call).  tensors must hold p's W_i, b_i,
  * W_h, b_h, W_o and b_o (matched by param pointer, with their full sizes) and `packed` must hold a pack of
  * their previous values (its zero padding is kept); bond messages without descriptors only
- * (WD_ERR_UNSUPPORTED otherwise: pack after the plain step).  Afterwards `packed` is bytewise the
- * wdmpnn_pack_params of the updated weights. */
+ * (WD_ERR_UNSUPPORTED otherwise: pack after the plain step).  Afterwards `packed` equals a fresh
+ * wdmpnn_pack_params of the updated weights bytewise except W_h's partial scale words (the per-workgroup
+ * maxima before word 64, and the per-tile words after it, are the optimizer's, not pack_kernel's); the
+ * folded word 64, the one every consumer reads, is equal. */
 int wdmpnn_adam_step_repack(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *h, const WdGraph *g,
                             const WdParams *p, const WdConfig *c, void *packed, size_t packed_bytes, void *stream);
 

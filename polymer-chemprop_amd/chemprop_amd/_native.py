@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get('WDMPNN_LIB', os.path.join(HERE, 'libwdmpnn.so'))
 ACTIVATIONS = {'ReLU': 0, 'LeakyReLU': 1, 'PReLU': 2, 'tanh': 3, 'SELU': 4, 'ELU': 5}
 ACT_IDENTITY = 6
 AGGREGATIONS = {'mean': 0, 'sum': 1, 'norm': 2}
-ABI_VERSION = 10
+ABI_VERSION = 11
 GRAPH_LEAN = 1  # WDMPNN_GRAPH_LEAN
 GRAPH_NO_PLANES = 2  # WDMPNN_GRAPH_NO_PLANES
 ERR_UNSUPPORTED = -1003  # WD_ERR_UNSUPPORTED
@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = ('wdmpnn_abi_version', 'wdmpnn_last_error', 'wdmpnn_workspace
                     'wdmpnn_saved_layout', 'wdmpnn_graph_bytes', 'wdmpnn_build_graph', 'wdmpnn_adam_step', 'wdmpnn_head_mse', 'wdmpnn_scale', 'wdmpnn_build_graph_ex',
                     'wdmpnn_forward_many', 'wdmpnn_feed_slot_bytes', 'wdmpnn_feed_create', 'wdmpnn_feed_next',
                     'wdmpnn_feed_release', 'wdmpnn_feed_forward_workspace_bytes', 'wdmpnn_feed_forward',
-                    'wdmpnn_feed_destroy', 'wdmpnn_adam_step_repack')
+                    'wdmpnn_feed_destroy', 'wdmpnn_adam_step_repack', 'wdmpnn_self_check')
 
 
 class WdCsr(Structure):
@@ -190,6 +190,13 @@ def lib() -> ctypes.CDLL:
     v = L.wdmpnn_abi_version()
     if v != ABI_VERSION:
         raise NativeError(f'libwdmpnn ABI {v} != expected {ABI_VERSION}; rebuild the library')
+    # the load-time kernel check (wdmpnn.h, ABI 11): a library whose gfx950 code object lacks a kernel its
+    # host code launches would abort the process at that launch; refuse it here instead
+    L.wdmpnn_self_check.argtypes = [POINTER(c_int32), POINTER(c_int32)]
+    L.wdmpnn_self_check.restype = c_int
+    n_host, n_dev = c_int32(0), c_int32(0)
+    if L.wdmpnn_self_check(ctypes.byref(n_host), ctypes.byref(n_dev)) != 0:
+        raise NativeError(f'{LIB_PATH}: ' + L.wdmpnn_last_error().decode(errors='replace'))
     _LIB = L
     return L
 

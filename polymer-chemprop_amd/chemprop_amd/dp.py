@@ -88,7 +88,9 @@ class GradBucket:
     then the rest.  :meth:`start_early` all-reduces the early segment while the encoder backward still
     runs on the compute stream (RCCL runs the collective on its own stream, ordered after the work
     enqueued so far); :meth:`start_allreduce` then launches the rest and :meth:`finish_allreduce` waits
-    for both."""
+    for both.  Every rank issues the same two collectives in the same order (the early one from
+    :meth:`start_allreduce` when :meth:`start_early` was not called), so ranks on different step paths
+    stay matched."""
 
     def __init__(self, module: nn.Module, early: Sequence[nn.Parameter] = None):
         params = [p for p in module.parameters() if p.requires_grad]
@@ -162,7 +164,13 @@ class GradBucket:
                 v.copy_(p.grad)  # autograd created a fresh tensor: fold it into the bucket
                 p.grad = v
         if self._multi_rank():
-            self._launch(self.buffer[self.n_early:] if self._early_started else self.buffer)
+            # the same collectives on every rank whichever step path it took (the direct step calls
+            # start_early, the autograd path does not): with an early segment always two, early then rest,
+            # so ranks never disagree on the count or sizes of their all-reduces
+            if self.n_early and not self._early_started:
+                self._launch(self.buffer[:self.n_early])
+            if self.n_early < self.buffer.numel():
+                self._launch(self.buffer[self.n_early:])
 
     def finish_allreduce(self) -> None:
         works, self._works, self._early_started = self._works, [], False

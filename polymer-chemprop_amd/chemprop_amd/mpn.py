@@ -9,6 +9,7 @@ The encoder's whole forward (mpn.py:66-173) is one ``wdmpnn_forward`` call; its 
 from __future__ import annotations
 
 import ctypes
+import weakref
 from functools import reduce
 from typing import List, Union
 
@@ -306,16 +307,20 @@ class MPNEncoder(nn.Module):
         the forward) whenever the key differs -- the first step, a parameter written any other way (version
         counters, another optimizer's step), other feature sizes or another stream."""
         sid = _native.current_stream(device)
-        key = (tuple((t.data_ptr(), t._version) if t is not None else None for t in params), _OPT_STEPS[0],
+        key = (tuple((t.data_ptr(), t._version, id(t)) if t is not None else None for t in params), _OPT_STEPS[0],
                self._parameters['cached_zero_vector'].data_ptr(), gs.atom_fdim, gs.bond_fdim, gs.desc_dim,
                gs.atom_messages, device, sid)
         tp = self.__dict__.get('_train_pack')
-        if tp is not None and tp['key'] == key:
+        # (the weak references: a Parameter that replaced a freed one at the same address, object id and
+        # version still forces a repack)
+        if tp is not None and tp['key'] == key and all(r is None if t is None else r() is t
+                                                        for r, t in zip(tp['refs'], params)):
             tp['gs'], tp['cfg'] = gs, cfg
             return tp['p'], tp['buf'], None
         pstruct, buf, launch = self._packed_params(gs, cfg, params, device, cache=False, defer=True)
         buf.zero_()  # (the layout's alignment gaps too: a repacked buffer is bytewise a fresh pack)
         self._train_pack = {'key': key, 'p': pstruct, 'buf': buf, 'gs': gs, 'cfg': cfg,
+                            'refs': tuple(None if t is None else weakref.ref(t) for t in params),
                             'ptrs': frozenset(t.data_ptr() for t in params[:6] if t is not None)}
         return pstruct, buf, launch
 
@@ -472,18 +477,27 @@ class MPNEncoder(nn.Module):
         return _EncoderFunction.apply(self, gs, cfg, pstruct, (packed, desc, dg, pack), hidden_out, device, *params)
 
     def invalidate_packed_params(self) -> None:
-        """Drop the cached padded weights.  Needed only after writing the parameters in a way that
-        bypasses both their version counters and ``torch.optim`` (e.g. ``p.data.copy_(...)``)."""
+        """Drop the cached padded weights (the inference cache and the direct training step's persistent
+        pack).  Needed only after writing the parameters in a way that bypasses both their version counters
+        and ``torch.optim`` / :class:`train.HipAdam` -- ``p.data.copy_(...)``, ``p.data[...] = ...``: writes
+        through ``.data`` do not bump ``p._version``.  Reassigned parameters and ``load_state_dict`` are
+        handled without it (object identity in the key; the caches are dropped on load)."""
         self._pack_cache = None
         self._train_pack = None
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        """nn.Module hook of ``load_state_dict``: the loaded values invalidate every packed copy."""
+        self.invalidate_packed_params()
+        return super()._load_from_state_dict(*args, **kwargs)
 
     def _packed_params(self, gs, cfg, params, device, cache=True, stream=None, defer=False, sid=None):
         """WdParams + the padded weight copies (wdmpnn_pack_params).  Inference caches them per
         (parameter pointer, version counter, optimizer-step generation): fused optimizers update the
         weights without bumping version counters, so every ``Optimizer.step`` also bumps
-        ``_OPT_STEPS``.  A training forward always repacks and leaves no cache behind.  ``sid``: the raw
+        ``_OPT_STEPS``.  A training forward through autograd repacks and leaves no cache behind (the direct
+        step keeps its own persistent pack, :meth:`_train_pack_for`).  ``sid``: the raw
         id of the current stream (the inference path's cheaper alternative to ``stream``)."""
-        key = (tuple((t.data_ptr(), t._version) if t is not None else None for t in params), _OPT_STEPS[0],
+        key = (tuple((t.data_ptr(), t._version, id(t)) if t is not None else None for t in params), _OPT_STEPS[0],
                self._parameters['cached_zero_vector'].data_ptr(), gs.atom_fdim, gs.bond_fdim, gs.desc_dim,
                gs.atom_messages, device) if cache else None
         cached = self._pack_cache if cache else None

@@ -83,7 +83,10 @@ class HipAdam(Optimizer):
     355 k parameters of the default model (profiles/round2_train_kernel_trace_v2.txt), this one a few.
     Same per-element arithmetic as torch's fused Adam; lr / weight_decay / betas / eps are read from the
     param groups at every step, so schedulers (NoamLR) work unchanged.  State per parameter:
-    ``step`` (int), ``exp_avg``, ``exp_avg_sq`` (as torch's Adam)."""
+    ``step`` (int), ``exp_avg``, ``exp_avg_sq`` (as torch's Adam).  Writes its parameters through raw
+    pointers (no version-counter bump): the encoders' packed-weight caches are keyed on the optimizer-step
+    count instead.  A write of an encoder parameter through ``.data`` between steps needs
+    ``MPNEncoder.invalidate_packed_params()``."""
 
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
                  decoupled: bool = False):
@@ -494,7 +497,9 @@ def train_step(model: nn.Module, mol_batch, target_batch, loss_func: Callable, o
     default regression / classification head + loss run as ``wdmpnn_head_mse`` (same loss and gradients within fp32
     summation order; ``False`` = the torch ops of the reference).  ``direct``: with the fused head and a
     plain one-molecule encoder, skip the autograd engine (``_direct_step``: the same launches and results,
-    bitwise, without the engine's host gaps)."""
+    bitwise, without the engine's host gaps).  The direct step keeps one packed copy of the encoder weights
+    across steps (rewritten by :class:`HipAdam`); after writing an encoder parameter through ``.data`` call
+    ``MPNEncoder.invalidate_packed_params()`` (reassigned parameters and ``load_state_dict`` are detected)."""
     if not model.training:  # (module.train() walks every submodule: the reference sets it once per epoch)
         model.train()
     head = _fusable_head(model, loss_func, dataset_type) if fused_head else None

@@ -114,6 +114,16 @@ struct MpLayerP {
     // entry (atom 0, outside every block) is skipped
     const uint8_t *mell_idx; const float *mell_coef;
     const int32_t *mptr, *midx; const float *mcoef;
+    // pair-operand layers (the template's PAIRS, round 6): M_{t-1} comes as fp16 hi / lo pair tiles of the
+    // molecule blocks ([nblk][Hk / 32 chunks][2 planes][128 rows][64 B]), scaled per group of ain_g columns
+    // by the words amax_in [nblk][amax_in_n] (the embed: 32-column groups; a layer: its BN-column tiles),
+    // and the layer writes M_t the same way into aout (not the last layer), scaled by its tile's max
+    const uint8_t *ain; int ain_g;
+    uint8_t *aout;
+    // ... and the last layer writes the atom aggregate A as pair tiles of the blocks' atom rows ([nblk][Hk / 32]
+    // [2][64][64 B], W_o's A operand: wo_readout_kernel<..., PAIRS>), scaled by its tile's max, published in
+    // amax_out [nblk][n_tiles]
+    uint8_t *apairs;
 };
 
 // The GEMM operand M_{t-1} = dropout(act(Z_{t-1})), formed while staging from the fp32 Z rows (the
@@ -223,7 +233,7 @@ constexpr int MP_THREADS = 512;
 // registers: with <= 128 VGPRs two layer workgroups co-reside on a CU -- one's epilogue beside the
 // other's GEMM when batches are in flight on two streams); the residual rows are loaded when the
 // epilogue starts and land behind the atom sums.
-template <int BN, int NT, bool LAST, bool ATOM = false>
+template <int BN, int NT, bool LAST, bool ATOM = false, bool POUT = false>
 struct MpEpilogue {
     static constexpr int BM = BLK_BONDS, LDC = BN + 4;
     static constexpr int UPR = BN / 8, UNITS = BM * UPR, UPT = (UNITS + NT - 1) / NT;  // 8-column units
@@ -382,7 +392,7 @@ struct MpEpilogue {
             wd_stamp(5 + 8 * LAST);
         }
         const float slope = ACT == ACT_PRELU ? P.slope[0] : 0.f;
-        float4 ym[LAST ? YPT : 1][2];  // LAST: this thread's M_t units until P is dead
+        float4 ym[LAST || POUT ? YPT : 1][2];  // LAST: this thread's M_t units until P is dead; POUT: until the scale is known
         // Z_t rows of this block (the training forward's save in the last layer)
         float *zr = LAST ? P.zsave : P.zout;
         const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc(zr ? (void *)(zr + (size_t)rs * P.kp) : (void *)P.inp, 0,
@@ -435,12 +445,26 @@ struct MpEpilogue {
                 y0 = make_float4(z[0], z[1], z[2], z[3]);
                 y1 = make_float4(z[4], z[5], z[6], z[7]);
             }
-            if constexpr (LAST) {
+            if constexpr (LAST || POUT) {
                 ym[i][0] = y0;
                 ym[i][1] = y1;
             }
         }
-        if constexpr (!LAST) {
+        if constexpr (!LAST && POUT) {
+            // M_t as fp16 pairs scaled by this tile's max (the next layer's A operand, copied by LDS-DMA)
+            __shared__ uint32_t red[MP_THREADS / 64];
+            const float s = h2_scale(publish_max_all(mx, P.amax_out + (size_t)blk * P.n_tiles + n0 / BN, red));
+            constexpr int CH = 2 * BM * 64;
+            const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+                P.aout + (size_t)blk * (P.kp >> 5) * CH, 0, (P.kp >> 5) * CH, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < PT; ++i) {
+                const int v = tid + NT * i, lr = v / UPR, c = 8 * (v % UPR);
+                // (rows up to the end of the last 16-row group the consumers multiply: zeros past the block)
+                if (v >= NU || lr >= ((rn + 15) & ~15)) break;
+                h2_store8(prs, h2_blk_off<BM>(lr, n0 + c), BM * 64, ym[i][0], ym[i][1], s);
+            }
+        } else if constexpr (!LAST) {
             __shared__ uint32_t red[MP_THREADS / 64];
             publish_max(mx, P.amax_out + (size_t)blk * P.n_tiles + n0 / BN, red);
         }
@@ -457,6 +481,34 @@ struct MpEpilogue {
             __syncthreads();
             // atom aggregate of this column tile: A[a] = sum_{x into a} w M_t[x] (mpn.py:126-131; x: the
             // atom's in-bonds, or its a2a neighbours in atom-message mode)
+            if constexpr (POUT) {
+                // A as fp16 pairs scaled by this tile's max (rows to the end of the last 16-row group: zeros)
+                float4 as[AUPT][2];
+                uint32_t amx = 0;
+#pragma unroll
+                for (int i = 0; i < AUPT; ++i) {
+                    const int v = tid + NT * i, la = v / UPR, c = 8 * (v % UPR);
+                    as[i][0] = as[i][1] = f4zero();
+                    if (v < AUNITS && la < B.an) {
+                        atom_sum(P, B, aell[i], la, c, Mt, as[i][0], as[i][1]);
+                        const float q[8] = {as[i][0].x, as[i][0].y, as[i][0].z, as[i][0].w,
+                                            as[i][1].x, as[i][1].y, as[i][1].z, as[i][1].w};
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) amx = max(amx, absbits(q[k]));
+                    }
+                }
+                __shared__ uint32_t red[MP_THREADS / 64];
+                const float s = h2_scale(publish_max_all(amx, P.amax_out + (size_t)blk * P.n_tiles + n0 / BN, red));
+                constexpr int CHA = 2 * BLK_ATOMS * 64;
+                const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+                    P.apairs + (size_t)blk * (P.kp >> 5) * CHA, 0, (P.kp >> 5) * CHA, 0x00020000);
+#pragma unroll
+                for (int i = 0; i < AUPT; ++i) {
+                    const int v = tid + NT * i, la = v / UPR, c = 8 * (v % UPR);
+                    if (v >= AUNITS || la >= ((B.an + 15) & ~15)) break;
+                    h2_store8(prs, h2_blk_off<BLK_ATOMS>(la, n0 + c), BLK_ATOMS * 64, as[i][0], as[i][1], s);
+                }
+            } else {
             const __amdgpu_buffer_rsrc_t ars = x6_block_rsrc<BLK_ATOMS>(P.aplanes, P.kp, blk);
 #pragma unroll
             for (int i = 0; i < AUPT; ++i) {
@@ -472,6 +524,7 @@ struct MpEpilogue {
                     st4(ar + 4, s1);
                 }
             }
+            }
         }
     }
 };
@@ -481,13 +534,14 @@ struct MpEpilogue {
 // then overwrites P with M_t (held in registers across a barrier) for the atom aggregate.
 // ACT: the activation (one instantiation each: the staging of M_{t-1} and the epilogue fold it to
 // straight-line code).
-template <int BN, bool LAST, int ACT, bool ATOM = false, int NJ = WD_MULTI>
+template <int BN, bool LAST, int ACT, bool ATOM = false, int NJ = WD_MULTI, bool PAIRS = false>
 // (__launch_bounds__ min 4 waves per SIMD: <= 128 VGPRs, so that two layer workgroups -- batches in flight
 // on two streams -- co-reside on a CU)
 __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpLayerP, NJ> MP) {
     constexpr int BM = BLK_BONDS;
-    constexpr int EPI_BYTES = MpEpilogue<BN, MP_THREADS, LAST, ATOM>::LDS_FLOATS * 4;  // P tile + the atom sums
-    constexpr int STG_BYTES = h2_lds_bytes<BM, BN>();
+    using Epi_ = MpEpilogue<BN, MP_THREADS, LAST, ATOM, PAIRS>;
+    constexpr int EPI_BYTES = Epi_::LDS_FLOATS * 4;  // P tile + the atom sums
+    constexpr int STG_BYTES = PAIRS ? h2p_lds_bytes<BM, BN>() : h2_lds_bytes<BM, BN>();
     constexpr int LDS_BYTES = EPI_BYTES > STG_BYTES ? EPI_BYTES : STG_BYTES;
     static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU");
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
@@ -496,9 +550,42 @@ __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpL
     const MpLayerP &P = multi_pick(MP, xcd_tile(blockIdx.x, gridDim.x), tile);
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
-    MpEpilogue<BN, MP_THREADS, LAST, ATOM> E;
+    Epi_ E;
     float *Pt = reinterpret_cast<float *>(lds);
     const int rs = ATOM ? B.as : B.bs, rn = ATOM ? B.an : B.bn;  // the block's message rows
+    if constexpr (PAIRS) {
+        static_assert(!ATOM, "pair operands: bond messages");
+        // the epilogue's gather lists and ids, staged by the loader waves while the consumers multiply the
+        // last chunk, in the tail of ring stage 2 (the last chunk lands in stage 0): clear of the P tile and
+        // the atom sums the epilogue writes
+        static_assert(EPI_BYTES + Epi_::PRE_BYTES <= STG_BYTES, "epilogue lists beside the P tile");
+        uint8_t *pre = lds + STG_BYTES - Epi_::PRE_BYTES;
+        const uint32_t wv = lane_word(P.amax_in + (size_t)blk * P.amax_in_n, P.amax_in_n);
+        const uint32_t whm = *P.wh_amax;
+        wd_stamp(1 + 8 * LAST);
+        floatx4 acc[BM / 64][BN / 16];
+        int se;
+        constexpr int CH = 2 * BM * 64;
+        h2_mainloop_pairs<BM, BN>(P.ain + (size_t)blk * (P.kp >> 5) * CH, P.wh + (size_t)nt * (P.kp >> 5) * (2 * BN * 64),
+                                  P.kp >> 5, rn, wv, P.ain_g, lds, acc, se);
+        wd_stamp(2 + 8 * LAST);
+        if (threadIdx.x >= MP_THREADS / 2) E.fill_pre(P, B, pre);
+        __syncthreads();
+        E.take_pre(B, pre);
+        wd_stamp(3 + 8 * LAST);
+        if (threadIdx.x < 256) {  // (the consumer waves hold the tile)
+            const float ia = se >= 0 ? __uint_as_float((uint32_t)(254 - se) << 23) : 1.f;
+            x6_acc_to_lds_scaled<BM, BN, 4, 1>(acc, Pt, ia, h2_inv_scale(whm));
+        }
+        __syncthreads();
+        E.template run<ACT>(P, B, blk, n0, Pt);
+        wd_stamp(6 + 8 * LAST);
+        if (blk == 0 && threadIdx.x < BN / 4) {  // (pad rows, as below)
+            float *zr = LAST ? P.zsave : P.zout;
+            if (zr) st4(zr + n0 + 4 * threadIdx.x, f4zero());
+            if (LAST && P.asave) st4(P.asave + n0 + 4 * threadIdx.x, f4zero());
+        }
+    } else {
     // the block's scale words of M_{t-1} (<= 64, one per lane) and W_h's: loaded before the GEMM's first
     // loads, reduced by the producers before their first stage and by the consumers after the GEMM
     int w0 = blk * P.amax_in_n, wn = P.amax_in_n;
@@ -520,7 +607,6 @@ __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpL
 #ifndef WD_EPI_PRE
 #define WD_EPI_PRE 1
 #endif
-    using Epi_ = MpEpilogue<BN, MP_THREADS, LAST, ATOM>;
     __shared__ __attribute__((aligned(16))) uint8_t pre[WD_EPI_PRE ? Epi_::PRE_BYTES : 16];
     static_assert(LDS_BYTES + (WD_EPI_PRE ? Epi_::PRE_BYTES : 0) + 64 <= 80 * 1024, "two workgroups per CU");
     if (WD_EPI_PRE) {
@@ -544,6 +630,7 @@ __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpL
         if (zr) st4(zr + n0 + 4 * threadIdx.x, f4zero());
         if (LAST && P.asave) st4(P.asave + n0 + 4 * threadIdx.x, f4zero());
     }
+    }  // (register-staged path)
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -573,6 +660,9 @@ struct EmbedP {
     float *inp;                  // [Rp][Hk]
     const float *slope;          // PReLU slope (or null)
     uint32_t *amax;              // [nblk][n_tiles]: max |act(inp)| per workgroup (the first layer's scale, planes.hpp h2)
+    uint8_t *m0;                 // the template's PAIRS: M_0 = act(inp) as fp16 pair tiles of the molecule blocks
+                                 // ([nblk][Hk / 32][2][128][64 B]), scaled by this workgroup's word (the first
+                                 // layer's A operand, copied by LDS-DMA: mp_layer_kernel<..., PAIRS>)
 };
 
 // s = sum_{c in code} T[c][c4 .. c4+3] + last * T[Fa - 1][c4 ..] (ascending columns, then the mass column:
@@ -590,8 +680,9 @@ __device__ __forceinline__ float4 code_sum(const WdAtomCode &cd, const float *T,
     return s;
 }
 
-template <int BN, int ACT, int NJ = WD_MULTI>
+template <int BN, int ACT, int NJ = WD_MULTI, bool PAIRS = false>
 __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP, NJ> MP) {
+    static_assert(!PAIRS || BN % 16 == 0, "pair groups of whole 16-column halves");
     constexpr int NT = 512, LDC = BN + 4, C4 = BN / 4, U8 = BN / 8, MAXK = 160, PER = (MAXK * C4 + NT - 1) / NT;
     constexpr int BU = (BLK_BONDS * U8 + NT - 1) / NT;  // bond units (8 columns of a row) per thread
     __shared__ __attribute__((aligned(16))) float wt[MAXK * BN];        // the staged W_i^T tile
@@ -657,6 +748,9 @@ __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP, NJ> MP) 
     __syncthreads();
     const float slope = ACT == ACT_PRELU ? P.slope[0] : 0.f;
     uint32_t mx = 0;
+    float4 ym[PAIRS ? BU : 1][2];  // PAIRS: this thread's act(inp) units until the scale is known
+#pragma unroll
+    for (int u = 0; u < (PAIRS ? BU : 1); ++u) ym[u][0] = ym[u][1] = f4zero();
 #pragma unroll
     for (int u = 0; u < BU; ++u) {
         const int v = tid + NT * u, lb = v / U8, c = 8 * (v % U8), b = B.bs + lb;
@@ -675,13 +769,35 @@ __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP, NJ> MP) 
         float *zr = P.inp + (size_t)b * P.Hk + n0 + c;
         st4(zr, z0);
         st4(zr + 4, z1);
-        const float zz[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+        float zz[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
 #pragma unroll
-        for (int q = 0; q < 8; ++q) mx = max(mx, absbits(act_fwd(ACT, zz[q], slope)));
+        for (int q = 0; q < 8; ++q) {
+            zz[q] = act_fwd(ACT, zz[q], slope);
+            mx = max(mx, absbits(zz[q]));
+        }
+        if constexpr (PAIRS) {
+            ym[u][0] = make_float4(zz[0], zz[1], zz[2], zz[3]);
+            ym[u][1] = make_float4(zz[4], zz[5], zz[6], zz[7]);
+        }
     }
     if (blk == 0 && tid < C4) st4(P.inp + n0 + 4 * tid, f4zero());  // pad row 0 (Z_0 of the backward)
     __shared__ uint32_t red[NT / 64];
-    publish_max(mx, P.amax + (size_t)blk * P.n_tiles + nt, red);
+    if constexpr (PAIRS) {
+        // M_0 = act(inp) as fp16 pairs scaled by this tile's max (rows up to the end of the last 16-row group
+        // the layer multiplies: zeros past the block)
+        const float s = h2_scale(publish_max_all(mx, P.amax + (size_t)blk * P.n_tiles + nt, red));
+        constexpr int CH = 2 * BLK_BONDS * 64;
+        const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+            P.m0 + (size_t)blk * (P.Hk >> 5) * CH, 0, (P.Hk >> 5) * CH, 0x00020000);
+#pragma unroll
+        for (int u = 0; u < BU; ++u) {
+            const int v = tid + NT * u, lb = v / U8, c = 8 * (v % U8);
+            if (lb >= ((B.bn + 15) & ~15)) break;
+            h2_store8(prs, h2_blk_off<BLK_BONDS>(lb, n0 + c), BLK_BONDS * 64, ym[u][0], ym[u][1], s);
+        }
+    } else {
+        publish_max(mx, P.amax + (size_t)blk * P.n_tiles + nt, red);
+    }
 }
 
 constexpr int WO_MAXK = 160;  // f_atoms / f_bonds columns embed_kernel stages (Fa, Fb <= 160)
@@ -704,6 +820,11 @@ struct WoReadoutP {
     const float *eo;
     int Hk, ldeo;
     float *zosave;  // training forward or null: the W_o pre-activation (mpn.py:133) as fp32 natural atom rows [Vap][Hk]
+    // the template's PAIRS (round 6): A as fp16 pair tiles of the blocks' atom rows ([nblk][Hk / 32][2][64][64 B],
+    // written by the last layer) with its words [nblk][a_nw] (groups of a_g columns), and W_o[:, Fa:] as fp16
+    // pair tiles with BN-row blocks scaled by the word wo_amax (wdmpnn_pack_params)
+    const uint8_t *apairs; const uint32_t *a_amax; int a_nw, a_g;
+    const uint8_t *woh; const uint32_t *wo_amax;
 };
 
 template <int BN> struct WoWaves;
@@ -716,15 +837,21 @@ template <> struct WoWaves<80> { static constexpr int WM = 2, WN = 5; };
 // workgroups queue per CU; CPS 1 (55 KB of LDS) for one batch, whose 256 workgroups then co-reside
 // with the layer kernels of batches in flight on other streams (+5 % with two streams, same-box A/B,
 // profiles/round3_*).  64-column tiles: CPS 1.
-template <int BN, int CPS, int NJ = WD_MULTI>
-__global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_readout_kernel(const Multi<WoReadoutP, NJ> MP) {
-    constexpr int BM = BLK_ATOMS, LDC = BN + 4, WM = WoWaves<BN>::WM, WN = WoWaves<BN>::WN;
-    constexpr int NT = 64 * WM * WN;
+// PAIRS (round 6): the GEMM on fp16 pair tiles of A and W_o (gemm_x6.hpp h2_mainloop_pairs: 4 MFMA waves of
+// 16 atom rows, 4 waves copying A; three products per fp32 product instead of the planes' six), 512 threads.
+template <int BN, int CPS, int NJ = WD_MULTI, bool PAIRS = false>
+// (PAIRS: <= 128 VGPRs, two workgroups per CU beside other streams' layers)
+__global__ __launch_bounds__(PAIRS ? 512 : 64 * WoWaves<BN>::WM * WoWaves<BN>::WN, PAIRS ? 4 : 1) void wo_readout_kernel(const Multi<WoReadoutP, NJ> MP) {
+    // (PAIRS: WM x WN = 4 x 1 MFMA waves, and four more copying A: NT = 512)
+    constexpr int BM = BLK_ATOMS, LDC = BN + 4, WM = PAIRS ? 4 : WoWaves<BN>::WM, WN = PAIRS ? 1 : WoWaves<BN>::WN;
+    constexpr int NT = PAIRS ? 512 : 64 * WM * WN;
     // (deeper single-chunk pipelines, with the mainloop hook's loads ordered ahead of the partial vmcnt
     // waits, measured slower: three / four stages 15.1 / 14.8 us here, 12.8 / 11.8 against 9.7 us on
     // QM9-shaped batches)
     constexpr int WS = 2;  // LDS stages
-    constexpr int LDS_BYTES = WS * CPS * x6_stage_bytes<BM, BN>();
+    constexpr int EPI_BYTES = (BM * LDC + BM + 3 * BLK_MOLS + BN) * 4;  // (+ the bias columns: PAIRS)
+    constexpr int LDS_BYTES = PAIRS ? (h2p_lds_bytes<BM, BN>() > EPI_BYTES ? h2p_lds_bytes<BM, BN>() : EPI_BYTES)
+                                    : WS * CPS * x6_stage_bytes<BM, BN>();
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
     int tile;
     const WoReadoutP &P = multi_pick(MP, xcd_tile(blockIdx.x, gridDim.x), tile);
@@ -742,7 +869,7 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     // prefetched during the GEMM (mainloop hook): this thread's bias columns, the block's atom weights
     // (thread a < an: w_atoms[as + a]) and its molecules' scope / Xn (thread i < nm)
     constexpr int C4 = BN / 4;
-    static_assert(NT % C4 == 0 && BM <= NT, "one bias group per thread, one atom weight per thread");
+    static_assert((PAIRS || NT % C4 == 0) && BM <= NT, "one bias group per thread, one atom weight per thread");
     const int nm = min(B.mh - B.ml, BLK_MOLS);  // (the packer never exceeds BLK_MOLS)
     if (P.zosave && blk == 0 && tid < BN / 4) st4(P.zosave + n0 + 4 * tid, f4zero());  // pad atom row 0
     float4 bb = f4zero();
@@ -753,7 +880,7 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     float4 eo[EPU];
     auto prefetch = [&](int phase) {
         if (phase != 0) return;
-        bb = ld4(P.bias + n0 + 4 * (tid % C4));
+        if (!PAIRS || tid < C4) bb = ld4(P.bias + n0 + 4 * (tid % C4));  // (PAIRS: staged through LDS below)
         if (tid < B.an) watom = P.w_atoms[B.as + tid];
 #pragma unroll
         for (int j = 0; j < EPU; ++j) {
@@ -768,14 +895,28 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
     };
     float *H = reinterpret_cast<float *>(lds);
     floatx4 acc[BM / WM / 16][BN / WN / 16];
-    x6_mainloop<BM, BN, WM, WN, WS, CPS>(O, lds, acc, prefetch);
-    __syncthreads();
-    x6_acc_to_lds<BM, BN, WM, WN>(acc, H);
+    if constexpr (PAIRS) {
+        prefetch(0);  // (registers across the GEMM: 16 rows per MFMA wave leave room)
+        const uint32_t wv = threadIdx.x < 256 ? lane_word(P.a_amax + (size_t)blk * P.a_nw, P.a_nw) : 0u;
+        int se;
+        h2_mainloop_pairs<BM, BN>(P.apairs + (size_t)blk * (P.kp >> 5) * (2 * BM * 64),
+                                  P.woh + (size_t)nt * (P.kp >> 5) * (2 * BN * 64), P.kp >> 5, B.an, wv, P.a_g, lds,
+                                  acc, se);
+        __syncthreads();
+        if (threadIdx.x < 256)
+            x6_acc_to_lds_scaled<BM, BN, 4, 1>(acc, H, se >= 0 ? __uint_as_float((uint32_t)(254 - se) << 23) : 1.f,
+                                               h2_inv_scale(*P.wo_amax));
+    } else {
+        x6_mainloop<BM, BN, WM, WN, WS, CPS>(O, lds, acc, prefetch);
+        __syncthreads();
+        x6_acc_to_lds<BM, BN, WM, WN>(acc, H);
+    }
     float *Wl = H + BM * LDC;           // [BM] atom weights of the block
     float *Ml = Wl + BM;                // [3][BLK_MOLS] per molecule: start (as float bits), size, Xn
-    static_assert((BM * LDC + BM + 3 * BLK_MOLS) * 4 <= LDS_BYTES, "readout staging fits");
+    static_assert(EPI_BYTES <= LDS_BYTES, "readout staging fits");
     static_assert(BLK_MOLS <= NT, "one molecule per thread in the prefetch");
     if (tid < BM) Wl[tid] = watom;
+    if (PAIRS && tid < C4) st4(Ml + 3 * BLK_MOLS + 4 * tid, bb);
     if (tid < nm) {
         Ml[tid] = __int_as_float(mstart);
         Ml[BLK_MOLS + tid] = __int_as_float(msize);
@@ -793,7 +934,9 @@ __global__ __launch_bounds__(64 * WoWaves<BN>::WM * WoWaves<BN>::WN) void wo_rea
             const int la = v / C4, c = 4 * (v % C4);
             float4 hv = ld4(H + la * LDC + c);
             hv.x += eo[j].x; hv.y += eo[j].y; hv.z += eo[j].z; hv.w += eo[j].w;  // (0 without codes)
-            float z[4] = {hv.x + bb.x, hv.y + bb.y, hv.z + bb.z, hv.w + bb.w};
+            // (PAIRS, 512 threads: NT % C4 != 0, each unit its own bias columns, from LDS)
+            const float4 b4 = PAIRS ? ld4(Ml + 3 * BLK_MOLS + c) : bb;
+            float z[4] = {hv.x + b4.x, hv.y + b4.y, hv.z + b4.z, hv.w + b4.w};
             if (P.zosave && la < B.an) st4(P.zosave + (size_t)(B.as + la) * P.Hk + n0 + c, make_float4(z[0], z[1], z[2], z[3]));
 #pragma unroll
             for (int q = 0; q < 4; ++q) z[q] = act_fwd(ACT, z[q], slope);

@@ -249,6 +249,35 @@ __device__ __forceinline__ void publish_max(uint32_t m, uint32_t *slot, uint32_t
     }
 }
 
+// the same, returning the workgroup max to every thread (a producer that scales its own output by it:
+// the pair-writing epilogues); one barrier
+__device__ __forceinline__ uint32_t publish_max_all(uint32_t m, uint32_t *slot, uint32_t *red) {
+    m = wave_max_u32(m);
+    const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[wave] = m;
+    __syncthreads();
+    for (int w = 0; w < nw; ++w) m = red[w] > m ? red[w] : m;
+    if (threadIdx.x == 0) *slot = m;
+    return m;
+}
+
+// 8 values (columns k .. k + 7 of one row, k % 8 == 0) scaled by s -> their fp16 hi and lo units of a
+// pair tile (planes: hi at +0, lo at +plane bytes) by two 16-byte buffer stores, default (write-back) policy
+__device__ __forceinline__ void h2_store8(__amdgpu_buffer_rsrc_t rs, int off, int plane, const float4 &a,
+                                          const float4 &b, float s) {
+    uint32_t h[4], l[4];
+    split_h2(a.x, a.y, s, h[0], l[0]);
+    split_h2(a.z, a.w, s, h[1], l[1]);
+    split_h2(b.x, b.y, s, h[2], l[2]);
+    split_h2(b.z, b.w, s, h[3], l[3]);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{h[0], h[1], h[2], h[3]}, rs, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{l[0], l[1], l[2], l[3]}, rs, off + plane, 0, 0);
+}
+// byte offset of (row r, column k) of a molecule block's pair tiles (BR rows, kp columns): chunk k / 32 of
+// 2 x BR x 64 bytes, row r % BR at 64 r, column k % 32 at 2 (k % 32) (the plane-tile layout with two planes)
+template <int BR>
+__device__ __forceinline__ int h2_blk_off(int r, int k) { return (k >> 5) * (2 * BR * 64) + r * 64 + 2 * (k & 31); }
+
 // fp32 [rows][ld] (first kp columns) -> h2 plane tiles with BR-row blocks: block (r / BR, k / 32) of 2 x
 // BR x 64 bytes (hi plane, then lo), row r % BR, columns k % 32 at 64 (r % BR) + 2 (k % 32) -- the bf16
 // plane-tile layout with two planes.  Scaled by the max of the nw words of `words` (pack_kernel's

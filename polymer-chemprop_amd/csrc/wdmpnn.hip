@@ -33,6 +33,7 @@
 #include "gemm_x6.hpp"
 #include "graph_build.hpp"
 #include "kernels.hpp"
+#include "selfcheck.hpp"
 #include "small_fwd.hpp"
 #include "wdmpnn.h"
 
@@ -52,6 +53,12 @@ int fail(int code, const char *fmt, ...) {
     return code;
 }
 
+// Load-time kernel check (selfcheck.hpp): run once per process, before the first launch of any entry point;
+// a library whose gfx950 code object lacks a kernel its host code launches fails every call with
+// WD_ERR_UNSUPPORTED instead of aborting the process inside the HIP launch.
+int self_check_once();
+#define WD_KERNELS_OK() WD_TRY(self_check_once())
+
 #define WD_CHECK_LAUNCH(what)                                                                  \
     do {                                                                                       \
         hipError_t e_ = hipGetLastError();                                                     \
@@ -62,6 +69,30 @@ int fail(int code, const char *fmt, ...) {
         int rc_ = (x);        \
         if (rc_) return rc_;  \
     } while (0)
+
+struct SelfCheck {
+    int rc;
+    std::string why;
+    int n_host, n_dev;
+};
+const SelfCheck &self_check_result() {
+    static const SelfCheck r = [] {
+        SelfCheck c{};
+        c.rc = code_object_check(reinterpret_cast<const void *>(&self_check_result), c.why, c.n_host, c.n_dev);
+        return c;
+    }();
+    return r;
+}
+int self_check_once() {
+    const SelfCheck &c = self_check_result();
+    return c.rc ? fail(WD_ERR_UNSUPPORTED, "libwdmpnn self-check: %s", c.why.c_str()) : 0;
+}
+
+// feed events that host threads wait for: hipEventBlockingSync (the waiting thread sleeps) or 0 (polls;
+// experiments)
+#ifndef WD_FEED_EVENT_SYNC
+#define WD_FEED_EVENT_SYNC hipEventBlockingSync
+#endif
 
 // the fused backward's data-gradient GEMMs dM = Y_t W_h on fp16 pairs (1) or bf16x3 planes (0)
 #ifndef WD_BWD_H2
@@ -92,6 +123,9 @@ struct Dims {
     bool x6;   // plane-tile pipeline: gathers emit bf16x3 plane tiles, GEMMs run gemm_x6g_kernel
     bool blocked;  // molecule-blocked fused inference forward (fused_mp.hpp)
     bool small;    // ... as ONE launch, a workgroup per block (small_fwd.hpp: blocks <= 32 rows, Hk 320)
+    bool pairs;    // ... with M_t handed between the launches as fp16 pair tiles (LDS-DMA layer operands)
+    bool pack_pairs;  // the packed weights hold W_o's pair tiles (a function of the encoder and config only:
+                      // one inference pack serves every graph)
     int nblk;
 };
 
@@ -136,10 +170,18 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     D.blocked = blk_common && (atom_blk || (D.x6 && g->bond_blk_row && (codes || (g->f_atoms_blk_x6 && g->f_bonds_x6)) &&
                                             g->bond_src_blk && g->b2revb));
     D.nblk = D.blocked ? g->n_blocks : 0;
-    // QM9-sized blocks, inference: the one-launch forward (WdConfig.gemm_variant 11 keeps the four launches)
+    // QM9-sized blocks, inference: the one-launch forward (WdConfig.gemm_variant 11 / 12 keep the four launches)
     D.small = D.blocked && codes && !D.atom && !D.save && c->dropout == 0.f && D.Hk == SF_HK && !D.undirected &&
-              c->gemm_variant != 11 && g->blk_max_bonds > 0 && g->blk_max_bonds <= SF_ROWS &&
+              c->gemm_variant != 11 && c->gemm_variant != 12 && c->gemm_variant < 100 && g->blk_max_bonds > 0 && g->blk_max_bonds <= SF_ROWS &&
               g->blk_max_atoms <= SF_ATOMS && D.Fa <= WO_MAXK && D.Fb <= WO_MAXK && D.Fb - D.Fa <= SF_ROWS;
+    // inference through the embed (codes), bond messages, 80-column layer tiles, <= 64 embed words per block:
+    // the layers read M_{t-1} as fp16 pair tiles written by its producer (fused_mp.hpp PAIRS; WdConfig.gemm_variant
+    // 12 keeps the register-staged layers that read Z_t)
+    D.pack_pairs = !D.atom && !D.save && D.Hk % 80 == 0 && D.Hk / 32 <= 64;
+    // (debug variants 1ab: a = 1 pair layers / 2 register-staged layers, the fused forward stopped after stage
+    // b = 1 embed, 2 first layer, ...: intermediate buffers left for tools/debug_pairs.py)
+    const bool staged_layers = c->gemm_variant == 12 || (c->gemm_variant >= 100 && (c->gemm_variant / 10) % 10 == 2);
+    D.pairs = D.pack_pairs && D.blocked && codes && !staged_layers;
     if (D.atom && D.undirected)
         return fail(WD_ERR_UNSUPPORTED, "undirected with atom_messages (the reference indexes atom messages "
                                         "with b2revb, mpn.py:101-102)");
@@ -172,6 +214,9 @@ struct PackLayout {
     // atom-message mode: the fused forward's input GEMM [f_atoms | Fs] B^T with B [3 Hk][Fak + Fbk] =
     // [[W_i, 0], [W_i, W_h[:, H:]], [W_o[:, :Fa], 0]] -> inp | inp + Fs W_h[:, H:]^T | f_atoms W_o[:, :Fa]^T
     size_t WiA = 0, WiAX = 0;          // fp32, and its bf16x3 plane tiles (64-row blocks)
+    // inference with pair operands (D.pairs; no training pack holds them): W_o[:, Fa:] as fp16 pair tiles with
+    // 80-row blocks (wo_readout_kernel<..., PAIRS>'s B) and its scale: pack_kernel's 64 maxima + their max
+    size_t WoH = 0, wo_amax = 0;
 };
 
 // column tile of the fused kernels: 80 when it divides Hk (Hk = 320: 4 tiles, one workgroup per CU at the
@@ -206,6 +251,10 @@ PackLayout pack_layout(const Dims &D) {
     if (D.atom) {
         L.WiA = take((size_t)3 * D.Hk * (D.Fak + D.Fbk));
         L.WiAX = take((size_t)3 * D.Hk * (D.Fak + D.Fbk) * 3 / 2);
+    }
+    if (D.pack_pairs) {
+        L.WoH = take((size_t)D.Hk * D.Hk);  // 2 fp16 per value
+        L.wo_amax = take(65);
     }
     if (D.desc) {
         L.Wd = take((size_t)D.Hdk * D.Kd);
@@ -255,6 +304,7 @@ int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
     // transposes for dX = dZ W_h[:, :H] and dA = dZo W_o[:, Fa:]
     add(job_transpose(F(L.WhT), D.Hk, D.Hk, p->W_h, D.atom ? H + D.Fb : H, 0, H, H));
     add(job_transpose(F(L.WoT), D.Hk, D.Hk, p->W_o, D.Fa + H, D.Fa, H, H));
+    if (D.pack_pairs) J.j[J.n - 1].amax = (uint32_t *)(base + L.wo_amax);  // (max |W_o[:, Fa:]|: the pair tiles' scale)
     // weight columns as rows for the categorical-code embedding (fused_mp.hpp embed_kernel / wo_readout)
     add(job_transpose(F(L.WiT), D.Kink, D.Hk, p->W_i, D.Kin, 0, D.Kin, H));
     add(job_transpose(F(L.WoaT), D.Fak, D.Hk, p->W_o, D.Fa + H, 0, D.Fa, H));
@@ -299,6 +349,12 @@ int pack_params(const Dims &D, const WdParams *p, char *base, hipStream_t st) {
     hipLaunchKernelGGL(split_h2_kernel, dim3(ew_blocks((size_t)D.Hk * D.Hk / 8)), dim3(256), 0, st, (const float *)F(L.Wh),
                        D.ldx, D.Hk, D.Hk, fused_bn(D.Hk), (uint8_t *)(base + L.WhH), wh_amax, 64, wh_amax + 64);
     WD_CHECK_LAUNCH("pack_params h2");
+    if (D.pack_pairs) {  // W_o[:, Fa:] (columns Fak.. of the padded copy) as fp16 pair tiles, 80-row blocks
+        hipLaunchKernelGGL(split_h2_kernel, dim3(ew_blocks((size_t)D.Hk * D.Hk / 8)), dim3(256), 0, st,
+                           (const float *)F(L.Wo) + D.Fak, D.Ko, D.Hk, D.Hk, 80, (uint8_t *)(base + L.WoH),
+                           (const uint32_t *)(base + L.wo_amax), 64, (uint32_t *)(base + L.wo_amax) + 64);
+        WD_CHECK_LAUNCH("pack_params W_o h2");
+    }
     return 0;
 }
 
@@ -600,6 +656,8 @@ struct FwdLayout {
     size_t Xp = 0, Ap = 0;  // plane tiles of X_t and A (D.x6)
     size_t Zb[2] = {0, 0}, Ab = 0;  // D.blocked inference: Z_t fp32 rows (ping-pong); A as blocked plane tiles
     size_t amax[2] = {0, 0};        // D.blocked: h2 scale words of M_t, ping-pong [nblk][tiles] (planes.hpp)
+    size_t Mp[2] = {0, 0};          // D.pairs: M_t as fp16 pair tiles of the molecule blocks, ping-pong
+                                    // [nblk][Hk / 32][2][128][64 B] (the embed writes M_0)
     size_t Eo = 0;                  // D.blocked: f_atoms W_o[:, :Fa]^T per blocked atom row (compact codes)
     size_t Fs = 0, In3 = 0;         // D.blocked atom-message mode: per atom the sum of its in-bonds' features
                                     // (plane tiles [Vap][Fbk]), and the input GEMM's [Vap][3 Hk] output
@@ -624,12 +682,15 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
     if (D.blocked) {
         // Z_t, ping-pong (layer t writes Zb[t & 1]; the first reads inp, the last writes none; a training
         // forward writes L.Z[t] instead)
-        if (!D.save)
+        if (!D.save && !D.pairs)
             for (int i = 0; i < 2 && i < D.T - 2; ++i) L.Zb[1 - i] = take(msg);
+        if (D.pairs)  // (M_0 .. M_{T-2}: the last layer writes none)
+            for (int i = 0; i < 2 && i < D.T - 1; ++i) L.Mp[i] = take((size_t)D.nblk * BLK_BONDS * D.Hk * 4);
         // (<= 64 tiles per block; the atom-message input GEMM: one word per 64 x 64 tile of inp)
         const size_t words = std::max((size_t)D.nblk * 64, (size_t)(D.Rp / 64) * (D.Hk / 64));
         for (int i = 0; i < 2; ++i) L.amax[i] = take(words * 4);
-        L.Ab = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 6);
+        // A: bf16x3 plane tiles, or fp16 pair tiles (D.pairs), of the blocks' atom rows
+        L.Ab = take((size_t)D.nblk * BLK_ATOMS * D.Hk * (D.pairs ? 4 : 6));
         if (D.atom) {
             L.Fs = take((size_t)D.Vap * D.Fbk * 6);
             L.In3 = take((size_t)D.Rp * 3 * D.Hk * 4);
@@ -836,8 +897,12 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
 #ifndef WD_EMBED40
 #define WD_EMBED40 1
 #endif
-    const bool bn40 = WD_EMBED40 && Hk % 40 == 0;
-    const int embed_tiles = Hk / (bn40 ? 40 : BNf);
+    // (the pair path: 32-column embed tiles, one scale word per chunk of M_0)
+    const bool pairs = D0.pairs;
+    for (int j = 1; j < n; ++j)
+        if (jobs[j].D.pairs != pairs) return fail(WD_ERR_UNSUPPORTED, "fused forward: batches of one launch differ in layout");
+    const bool bn40 = WD_EMBED40 && Hk % 40 == 0 && !pairs;
+    const int embed_tiles = Hk / (pairs ? 32 : (bn40 ? 40 : BNf));
     if (codes) {
         const int nt = embed_tiles;
         Multi<EmbedP> M;
@@ -850,10 +915,14 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
             E.Fa = J.D.Fa; E.Fb = J.D.Fb; E.Hk = Hk; E.n_tiles = nt;
             E.inp = F(J, J.L.Z[0]);
             E.slope = p->prelu; E.amax = slot(J, 0);
+            E.m0 = pairs ? (uint8_t *)(J.ws + J.L.Mp[0]) : nullptr;
         }, M, grid);
         host_with_act(c->activation, [&](auto act_c) {
             constexpr int A = decltype(act_c)::value;
-            if (n == 1) {
+            if (pairs) {
+                if (n == 1) hipLaunchKernelGGL((embed_kernel<32, A, 1, true>), dim3(grid), dim3(512), 0, st, one_job(M));
+                else hipLaunchKernelGGL((embed_kernel<32, A, WD_MULTI, true>), dim3(grid), dim3(512), 0, st, M);
+            } else if (n == 1) {
                 const Multi<EmbedP, 1> M1 = one_job(M);
                 if (bn40) hipLaunchKernelGGL((embed_kernel<40, A, 1>), dim3(grid), dim3(512), 0, st, M1);
                 else if (bn80) hipLaunchKernelGGL((embed_kernel<80, A, 1>), dim3(grid), dim3(512), 0, st, M1);
@@ -863,6 +932,7 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
             else hipLaunchKernelGGL((embed_kernel<64, A>), dim3(grid), dim3(512), 0, st, M);
         });
         WD_CHECK_LAUNCH("embed");
+        if (c->gemm_variant >= 100 && c->gemm_variant % 10 == 1) return 0;
     } else {
         for (int j = 0; j < n; ++j) {
             const FusedJob &J = jobs[j];
@@ -934,6 +1004,17 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
             Q.n_tiles = Hk / BNf;
             Q.zsave = J.D.save && last ? F(J, J.L.Z[t]) : nullptr;
             Q.asave = J.D.save && last ? F(J, J.L.A) : nullptr;
+            if (pairs) {  // M_{t-1} from the pair tiles of its producer (no Z_t in inference)
+                Q.ain = (const uint8_t *)(J.ws + J.L.Mp[(t - 1) & 1]);
+                Q.ain_g = t == 1 ? 32 : BNf;
+                Q.aout = last ? nullptr : (uint8_t *)(J.ws + J.L.Mp[t & 1]);
+                Q.zin = nullptr;
+                Q.zout = nullptr;
+                // the last layer: A as pair tiles, its words in the slot this layer does not read
+                Q.apairs = last ? (uint8_t *)(J.ws + J.L.Ab) : nullptr;
+                Q.amax_out = slot(J, t);
+                Q.aplanes = nullptr;
+            }
         }, M, grid);
         if (t == 1) WD_TRY(record_prof(c, 0, 0, st));  // one pair around all the layers
         // one instantiation per (tile width, last layer, activation)
@@ -942,6 +1023,15 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
             constexpr bool LAST = decltype(last_c)::value;
             host_with_act(c->activation, [&](auto act_c) {
                 constexpr int A = decltype(act_c)::value;
+                if constexpr (BN == 80) {
+                    if (pairs) {
+                        if (n == 1)
+                            hipLaunchKernelGGL((mp_layer_kernel<BN, LAST, A, false, 1, true>), dim3(grid), dim3(MP_THREADS), 0, st, one_job(M));
+                        else
+                            hipLaunchKernelGGL((mp_layer_kernel<BN, LAST, A, false, WD_MULTI, true>), dim3(grid), dim3(MP_THREADS), 0, st, M);
+                        return;
+                    }
+                }
                 if (n == 1 && D0.atom)
                     hipLaunchKernelGGL((mp_layer_kernel<BN, LAST, A, true, 1>), dim3(grid), dim3(MP_THREADS), 0, st, one_job(M));
                 else if (n == 1)
@@ -956,6 +1046,7 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
         else { if (last) go(I64{}, std::true_type{}); else go(I64{}, std::false_type{}); }
         WD_CHECK_LAUNCH("mp_layer");
         if (last) WD_TRY(record_prof(c, 0, 1, st));
+        if (c->gemm_variant >= 100 && c->gemm_variant % 10 == t + 1) return 0;
     }
     // W_o + readout (empty batches -- no molecules -- have no blocks and write nothing)
     Multi<WoReadoutP> M;
@@ -977,10 +1068,21 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
         R.act = c->activation; R.slope = p->prelu; R.p_drop = c->dropout; R.seed = c->seed; R.layer = J.D.T;
         R.out = J.out; R.ncols = J.D.H; R.n_tiles = Hk / BNf;
         R.zosave = J.D.save ? F(J, J.L.Zo) : nullptr;
+        // (debug variants 1a4: the W_o pre-activation into the free second ping-pong buffer, tools/debug_pairs.py)
+        if (c->gemm_variant >= 100 && c->gemm_variant % 10 == 4 && J.D.T == 3)
+            R.zosave = pairs ? F(J, J.L.Mp[1]) : F(J, J.L.Zb[1]);
+        if (pairs) {
+            R.apairs = (const uint8_t *)(J.ws + J.L.Ab); R.a_amax = slot(J, J.D.T - 1); R.a_nw = Hk / BNf; R.a_g = BNf;
+            R.woh = (const uint8_t *)(pk + PL.WoH); R.wo_amax = (const uint32_t *)(pk + PL.wo_amax) + 64;
+        }
     }, M, grid);
     if (grid > 0) {
         // one batch: single-chunk stages (55 KB, co-resident with other streams' layers); several: two
-        if (bn80 && n > 1)
+        if (pairs && n > 1)
+            hipLaunchKernelGGL((wo_readout_kernel<80, 1, WD_MULTI, true>), dim3(grid), dim3(512), 0, st, M);
+        else if (pairs)
+            hipLaunchKernelGGL((wo_readout_kernel<80, 1, 1, true>), dim3(grid), dim3(512), 0, st, one_job(M));
+        else if (bn80 && n > 1)
             hipLaunchKernelGGL((wo_readout_kernel<80, 2>), dim3(grid), dim3(64 * WoWaves<80>::WM * WoWaves<80>::WN), 0, st, M);
         else if (bn80)
             hipLaunchKernelGGL((wo_readout_kernel<80, 1, 1>), dim3(grid), dim3(64 * WoWaves<80>::WM * WoWaves<80>::WN), 0, st, one_job(M));
@@ -1033,6 +1135,26 @@ extern "C" {
 
 int wdmpnn_abi_version(void) { return WDMPNN_ABI_VERSION; }
 
+int wdmpnn_self_check(int32_t *n_host_kernels, int32_t *n_device_kernels) {
+    const SelfCheck &c = self_check_result();
+    if (n_host_kernels) *n_host_kernels = c.n_host;
+    if (n_device_kernels) *n_device_kernels = c.n_dev;
+    return self_check_once();
+}
+
+// debug (tools/debug_pairs.py; not in the header): byte offsets in the forward workspace of inp, M_0 / M_1 pair
+// tiles, A, the two scale-word slots and the two Z_t ping-pong buffers
+int wdmpnn_debug_fwd_offsets(const WdGraph *g, const WdParams *p, const WdConfig *c, size_t *out) {
+    Dims D;
+    WD_TRY(get_dims(g, p, c, D));
+    const FwdLayout L = fwd_layout(D, p->packed == nullptr);
+    const PackLayout PL = pack_layout(D);
+    const size_t v[15] = {L.Z.empty() ? 0 : L.Z[0], L.Mp[0], L.Mp[1], L.Ab, L.amax[0], L.amax[1], L.Zb[0], L.Zb[1],
+                          L.total, (size_t)D.pairs, PL.WoH, PL.wo_amax, PL.WhH, PL.amax, L.Eo};
+    memcpy(out, v, sizeof(v));
+    return 0;
+}
+
 // experiment builds (WD_STAMPS): copy the layer kernel's phase stamps of the last launch to the host
 int wdmpnn_debug_stamps(void *host, size_t bytes) {
 #if WD_STAMPS
@@ -1064,6 +1186,7 @@ int wdmpnn_packed_params_bytes(const WdGraph *g, const WdParams *p, const WdConf
 
 int wdmpnn_pack_params(const WdGraph *g, const WdParams *p, const WdConfig *c, void *packed, size_t bytes,
                        void *stream) {
+    WD_KERNELS_OK();
     Dims D;
     WD_TRY(get_dims(g, p, c, D));
     if (!packed || bytes < pack_layout(D).total) return fail(WD_ERR_WORKSPACE, "packed buffer too small");
@@ -1088,6 +1211,7 @@ int wdmpnn_backward_workspace_bytes(const WdGraph *g, const WdParams *p, const W
 
 int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void *workspace, size_t workspace_bytes,
                    float *out, void *stream) {
+    WD_KERNELS_OK();
     Dims D;
     WD_TRY(get_dims(g, p, c, D));
     const FwdLayout L = fwd_layout(D, p->packed == nullptr);
@@ -1187,6 +1311,7 @@ int wdmpnn_forward(const WdGraph *g, const WdParams *p, const WdConfig *c, void 
 
 int wdmpnn_forward_many(int32_t n, const WdGraph *graphs, const WdParams *p, const WdConfig *c,
                         void *const *workspaces, const size_t *workspace_bytes, float *const *outs, void *stream) {
+    WD_KERNELS_OK();
     if (n < 0 || (n && (!graphs || !workspaces || !workspace_bytes || !outs))) return fail(WD_ERR_ARG, "forward_many: bad arrays");
     if (n == 0) return 0;
     if (!p || !c) return fail(WD_ERR_ARG, "null params/config");
@@ -1219,6 +1344,7 @@ int wdmpnn_forward_many(int32_t n, const WdGraph *graphs, const WdParams *p, con
 int wdmpnn_backward(const WdGraph *g, const WdParams *p, const WdConfig *c, const void *workspace,
                     size_t workspace_bytes, const float *dout, void *scratch, size_t scratch_bytes,
                     const WdGrads *grads, void *stream) {
+    WD_KERNELS_OK();
     Dims D;
     WD_TRY(get_dims(g, p, c, D));
     if (!D.save) return fail(WD_ERR_ARG, "backward needs a forward run with save_for_backward=1");
@@ -1494,6 +1620,7 @@ int wdmpnn_plane_bytes(int32_t rows, int32_t kp, size_t *bytes) {
 
 int wdmpnn_split_planes(const float *src, int32_t ld, int32_t rows, int32_t kp, void *dst, size_t dst_bytes,
                         void *stream) {
+    WD_KERNELS_OK();
     if (rows == 0 || kp == 0) return 0;
     if (!src || !dst) return fail(WD_ERR_ARG, "null pointer");
     if (rows % 64 || kp % 32 || ld < kp || ld % 4 || !aligned16(src) || !aligned16(dst))
@@ -1508,6 +1635,7 @@ int wdmpnn_split_planes(const float *src, int32_t ld, int32_t rows, int32_t kp, 
 
 int wdmpnn_split_planes_rows(const float *src, int32_t ld, int32_t rows, int32_t kp, const int32_t *row_map,
                              int32_t out_rows, void *dst, size_t dst_bytes, void *stream) {
+    WD_KERNELS_OK();
     if (out_rows == 0 || kp == 0) return 0;
     if (!src || !dst || !row_map) return fail(WD_ERR_ARG, "null pointer");
     if (out_rows % 64 || kp % 32 || ld < kp || ld % 4 || !aligned16(src) || !aligned16(dst))
@@ -1527,6 +1655,7 @@ int wdmpnn_split_planes_rows(const float *src, int32_t ld, int32_t rows, int32_t
 int wdmpnn_build_bond_features(const float *f_atoms, int32_t ld_atoms, int32_t atom_fdim, int32_t atom_rows,
                                const int32_t *b2a, const float *bond_tail, int32_t ld_tail, int32_t tail_dim,
                                int32_t rows, float *f_bonds, int32_t ld_bonds, void *stream) {
+    WD_KERNELS_OK();
     if (rows == 0) return 0;
     if (!f_atoms || !b2a || !f_bonds || (tail_dim && !bond_tail)) return fail(WD_ERR_ARG, "null pointer");
     if (rows < 0 || atom_rows <= 0 || atom_fdim < 0 || tail_dim < 0 || atom_fdim > ld_atoms || tail_dim > ld_tail ||
@@ -1543,6 +1672,7 @@ int wdmpnn_build_bond_features(const float *f_atoms, int32_t ld_atoms, int32_t a
 
 int wdmpnn_index_select_rows(const float *src, int64_t n_src_rows, int64_t row_len, const int64_t *index,
                              int64_t n_index, float *out, void *stream) {
+    WD_KERNELS_OK();
     if (n_index < 0 || row_len < 0 || n_src_rows < 0) return fail(WD_ERR_ARG, "negative size");
     if (n_index == 0 || row_len == 0) return 0;
     if (!src || !index || !out) return fail(WD_ERR_ARG, "null pointer");
@@ -1566,6 +1696,7 @@ int wdmpnn_build_graph(const WdCompact *c, void *buffer, size_t bytes, WdGraph *
 }
 
 int wdmpnn_build_graph_ex(const WdCompact *c, void *buffer, size_t bytes, WdGraph *g, int32_t flags, void *stream) {
+    WD_KERNELS_OK();
     Multi<GraphBuildP> M{};
     if (!g) return fail(WD_ERR_ARG, "null graph");
     WD_TRY(graph_build_prepare(c, buffer, bytes, flags, M.p[0], *g));
@@ -1696,6 +1827,7 @@ int wdmpnn_feed_slot_bytes(int32_t kind, int32_t batch, int32_t atom_fdim, int32
 }
 
 int wdmpnn_feed_create(const WdFeedSpec *spec, void **feed) {
+    WD_KERNELS_OK();
     if (!spec || !feed) return fail(WD_ERR_ARG, "feed: null argument");
     const WdFeedSpec &S = *spec;
     if (S.kind < 0 || S.kind > 2 || S.batch < 1 || S.n_batches < 0 || S.producers < 1 || S.slots < 2 ||
@@ -1720,9 +1852,12 @@ int wdmpnn_feed_create(const WdFeedSpec *spec, void **feed) {
     for (int s = 0; s < F->R && ok; ++s) {
         Feed::Slot &Q = F->slot[(size_t)s];
         Q.turn = s;
-        ok = hipEventCreateWithFlags(&Q.copy_done, hipEventDisableTiming) == hipSuccess &&
+        // (the two events host threads wait for are blocking-sync: a default event's hipEventSynchronize polls,
+        // and the feeder, which runs several batches ahead, would hold a CPU busy for the whole stream -- one of
+        // a rank's two CPUs when eight ranks share a 16-CPU quota)
+        ok = hipEventCreateWithFlags(&Q.copy_done, hipEventDisableTiming | WD_FEED_EVENT_SYNC) == hipSuccess &&
              hipEventCreateWithFlags(&Q.ready, hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&Q.released, hipEventDisableTiming) == hipSuccess;
+             hipEventCreateWithFlags(&Q.released, hipEventDisableTiming | WD_FEED_EVENT_SYNC) == hipSuccess;
     }
     if (!ok) {
         delete F;
@@ -1779,8 +1914,10 @@ static int feed_batch_workspace(const Feed *F, const WdParams *p, const WdConfig
     D.Va = F->spec.batch * f.atoms_per_mol + 1; D.Vap = rup(D.Va, 128);
     D.Fa = F->spec.atom_fdim; D.Fak = rup(D.Fa, 32); D.Fb = F->spec.bond_fdim; D.Fbk = rup(D.Fb, 32);
     D.Hd = D.H; D.Hdk = rup(D.Hd, 64); D.Kin = D.Fb; D.Kink = D.Fbk; D.ldx = D.Hk; D.Ko = D.Fak + D.Hk; D.Kd = D.Hk;
-    D.x6 = true; D.blocked = true; D.nblk = F->spec.batch;
-    *bytes = align256(fwd_layout(D, false).total);
+    D.x6 = true; D.blocked = true; D.nblk = F->spec.batch;  // (blocks hold whole molecules: <= batch)
+    const size_t staged = fwd_layout(D, false).total;
+    D.pairs = true;  // (pair tiles instead of Z_t rows: whichever layout get_dims picks is covered)
+    *bytes = align256(std::max(staged, fwd_layout(D, false).total));
     return 0;
 }
 
@@ -1796,6 +1933,7 @@ int wdmpnn_feed_forward_workspace_bytes(void *feed, const WdParams *p, const WdC
 int wdmpnn_feed_forward(void *feed, int32_t k, const WdParams *p, const WdConfig *c, void *workspace,
                         size_t workspace_bytes, float *out, int64_t out_rows, void *stream, int32_t *got,
                         int64_t *rows, int64_t *edges, int64_t *h2d_bytes) {
+    WD_KERNELS_OK();
     Feed *F = (Feed *)feed;
     if (!F || k < 1 || !p || !c || !workspace || !out || !got || !rows || !edges || !h2d_bytes)
         return fail(WD_ERR_ARG, "feed_forward: bad argument");
@@ -1848,6 +1986,7 @@ int wdmpnn_feed_destroy(void *feed) {
 
 int wdmpnn_index_select_rows_backward(const float *grad, int64_t n_index, int64_t row_len, const int64_t *perm,
                                       const int64_t *ptr, int64_t n_src_rows, float *dsrc, void *stream) {
+    WD_KERNELS_OK();
     if (n_index < 0 || row_len < 0 || n_src_rows < 0) return fail(WD_ERR_ARG, "negative size");
     if (n_src_rows == 0 || row_len == 0) return 0;
     if (!dsrc || !ptr || (n_index && (!grad || !perm))) return fail(WD_ERR_ARG, "null pointer");
@@ -1923,11 +2062,13 @@ static int adam_launches(const WdAdamTensor *tensors, int n, const WdAdamHyper *
 }
 
 int wdmpnn_adam_step(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *h, void *stream) {
+    WD_KERNELS_OK();
     return adam_launches(tensors, n, h, (hipStream_t)stream, nullptr, 0, nullptr);
 }
 
 int wdmpnn_adam_step_repack(const WdAdamTensor *tensors, int32_t n, const WdAdamHyper *h, const WdGraph *g,
                             const WdParams *p, const WdConfig *c, void *packed, size_t packed_bytes, void *stream) {
+    WD_KERNELS_OK();
     Dims D;
     WD_TRY(get_dims(g, p, c, D));
     if (D.atom || D.desc) return fail(WD_ERR_UNSUPPORTED, "adam_step_repack: bond messages without descriptors only");
@@ -1977,6 +2118,7 @@ int wdmpnn_adam_step_repack(const WdAdamTensor *tensors, int32_t n, const WdAdam
 }
 
 int wdmpnn_head_mse(const WdHead *h, void *stream) {
+    WD_KERNELS_OK();
     if (!h) return fail(WD_ERR_ARG, "null head");
     if (h->B < 0 || h->F <= 0 || h->Hf <= 0 || h->T <= 0 || h->ld_x < h->F || h->ld_table < 2 * h->T)
         return fail(WD_ERR_SHAPE, "head: bad sizes");
@@ -2002,6 +2144,7 @@ int wdmpnn_head_mse(const WdHead *h, void *stream) {
 }
 
 int wdmpnn_scale(float *const *p, const int64_t *n, int32_t k, const float *s, void *stream) {
+    WD_KERNELS_OK();
     if (k < 0 || k > 8 || !s || (k && (!p || !n))) return fail(WD_ERR_ARG, "scale: bad arguments");
     ScaleJobs J{};
     long long most = 0;

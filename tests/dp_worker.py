@@ -84,6 +84,30 @@ def run_segments(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
+def run_mixed_paths(rank, world, port, out_path):
+    """Rank 0 takes the direct step's order (start_early, then start_allreduce), rank 1 the autograd
+    path's (start_allreduce only): both must issue the same two collectives and average every gradient."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dp.init_distributed('gloo')
+    torch.manual_seed(0)
+    model = HeadModel()
+    bucket = dp.GradBucket(model)
+    for k, p in enumerate(model.parameters()):
+        p.grad.copy_(torch.full_like(p, float(10 * k + rank + 1)))
+    if rank == 0:
+        bucket.start_early()
+    bucket.start_allreduce()
+    n_works = len(bucket._works)
+    bucket.finish_allreduce()
+    res = [None] * world
+    dist.all_gather_object(res, {'works': n_works, 'grads': [p.grad.clone() for p in model.parameters()]})
+    if rank == 0:
+        torch.save(res, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def run_gpu(rank, world, port, out_path):
     """Two ranks on cuda:0 (gloo process group): MoleculeModel with the HIP encoder, DP training with the
     flat GradBucket all-reduce, fused Adam, on disjoint synthetic polymer shards."""

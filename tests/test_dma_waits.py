@@ -3,7 +3,8 @@
 ``s_waitcnt vmcnt`` before the barrier that publishes the stage.  That protocol is sound only if no
 compiler-issued vector-memory instruction is in flight between a DMA and the wait that covers it: an
 extra load or store there would change what the hand-written count means (and a store may complete out of
-order with the DMA).  This test disassembles every ``mp_layer_kernel`` instantiation in the built
+order with the DMA).  This test disassembles every ``mp_layer_kernel`` instantiation (and the pair-operand
+``wo_readout_kernel``) in the built
 libwdmpnn.so (gfx950 code object) and walks the control-flow graph from each DMA: every path must reach an
 ``s_waitcnt`` with a vmcnt field before it meets any other vector-memory instruction."""
 import os
@@ -38,8 +39,10 @@ def layer_kernels(tmp_path_factory):
     subprocess.run([bundler, '--type=o', f'--input={fat}', '--targets=hipv4-amdgcn-amd-amdhsa--gfx950',
                     f'--output={co}', '--unbundle'], check=True)
     table = subprocess.run([objdump, '-t', co], check=True, capture_output=True, text=True).stdout
-    syms = sorted({ln.split()[-1] for ln in table.split('\n') if 'mp_layer_kernel' in ln and ' F ' in ln
-                   and not ln.split()[-1].endswith('.kd')})
+    # (and the W_o kernel's pair instantiations, PAIRS = true: the same untracked copies, gemm_x6.hpp
+    # h2_mainloop_pairs)
+    syms = sorted({ln.split()[-1] for ln in table.split('\n') if ' F ' in ln and not ln.split()[-1].endswith('.kd')
+                   and ('mp_layer_kernel' in ln or ('wo_readout_kernel' in ln and 'Lb1EEEv' in ln))})
     assert syms, 'no mp_layer_kernel in the code object'
     text = subprocess.run([objdump, '-d', '--mcpu=gfx950', '--disassemble-symbols=' + ','.join(syms), co],
                           check=True, capture_output=True, text=True).stdout

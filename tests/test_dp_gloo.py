@@ -68,6 +68,18 @@ def test_two_segment_allreduce_averages_every_gradient(tmp_path):
         assert torch.equal(g, torch.full_like(g, 10 * k + 1.5)), k
 
 
+def test_ranks_on_different_step_paths_issue_the_same_collectives(tmp_path):
+    """One rank calls start_early (direct step), the other does not (autograd path): each still issues two
+    all-reduces (head segment, then the rest) and every gradient is the mean (no count / size mismatch)."""
+    out = str(tmp_path / 'mixed.pt')
+    mp.spawn(dp_worker.run_mixed_paths, args=(2, free_port(), out), nprocs=2, join=True)
+    res = torch.load(out, weights_only=False)
+    assert [r['works'] for r in res] == [2, 2]
+    for r in res:
+        for k, g in enumerate(r['grads']):
+            assert torch.equal(g, torch.full_like(g, 10 * k + 1.5)), k
+
+
 @pytest.mark.gpu
 def test_two_rank_molecule_model_on_gpu_matches_single_process(tmp_path):
     """World size 2 on cuda:0 (gloo): the real MoleculeModel with the HIP encoder (its autograd.Function

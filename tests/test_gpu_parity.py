@@ -72,7 +72,7 @@ def test_golden_forward_and_gradients(name):
     assert err <= TOL, ('no-grad path', err)
 
 
-def _oracle_vs_hip(graphs, args, seed, desc=None):
+def _oracle_vs_hip(graphs, args, seed, desc=None, row_scale=None):
     """Errors of the HIP training path (forward + backward) against the oracle.  The output must meet
     1e-5 normwise vs the fp32 oracle (the reference's own arithmetic).  Parameter gradients must meet
     1e-5 normwise vs an fp64 evaluation of the same op sequence that takes the branch of every kinked
@@ -85,6 +85,8 @@ def _oracle_vs_hip(graphs, args, seed, desc=None):
     synthetic.fill_parameters(enc, seed)
     R = torch.randn((len(graphs.a_scope), args.hidden_size + (args.atom_descriptors_size if desc else 0)),
                     generator=torch.Generator().manual_seed(seed))
+    if row_scale is not None:  # per-molecule magnitudes of the output gradient
+        R = R * row_scale[:, None]
     cpu_params = {n: t.detach().clone() for n, t in enc.named_parameters()}
     trainable = {n for n, t in enc.named_parameters() if t.requires_grad}
     enc = enc.to(DEV)
@@ -168,6 +170,24 @@ def test_per_molecule_accuracy_in_mixed_magnitude_blocks(activation):
     assert float(mx.max() / mx.min()) > 100  # the magnitudes really are mixed
     err = (out - ref).abs().max(dim=1).values / mx
     assert float(err.max()) <= TOL, err.tolist()
+
+
+@pytest.mark.parametrize('activation,depth', [('ReLU', 5), ('LeakyReLU', 4)])
+def test_gradients_with_wide_dynamic_range(activation, depth):
+    """The backward's W_h GEMMs run on fp16 pairs scaled per group of Y_t (256 float4) and per 128 x 64 tile
+    of M_{t-1} (gemm_x6.hpp): entries far below their group's max keep an absolute error near 2^-22 of it.
+    Output gradients spanning 10^-4 .. 10^4 across molecules, messages 10^2 - 10^3 x larger in three
+    molecules, deep T: every weight gradient must still meet 1e-5 normwise against the fp64 evaluation
+    (the weight gradients are sums over all rows, where those absolute errors stay below the sum's own
+    fp32 rounding)."""
+    mols = synthetic.make_batch('polymer', 24, 71)
+    for i, f in ((3, 1e2), (11, 1e3), (19, 3e2)):
+        _scale_mass(mols[i], f)
+    g = BatchMolGraph(mols)
+    scale = torch.tensor([10.0 ** ((7 * i) % 9 - 4) for i in range(24)])
+    assert float(scale.max() / scale.min()) >= 1e8
+    args = TrainArgs(hidden_size=300, depth=depth, activation=activation, bias=True)
+    _check(_oracle_vs_hip(g, args, seed=71, row_scale=scale))
 
 
 def test_edge_cases_hub_degree_empty_single_atom():
@@ -338,6 +358,41 @@ def test_blocked_fused_forward(kind, b, hidden, depth, extra):
     with torch.no_grad():
         out = enc(g)
     assert golden_io.normwise(out.cpu().numpy(), ref.numpy()) <= TOL
+
+
+@pytest.mark.parametrize('kind,b,hidden,depth,extra', [
+    ('polymer', 64, 300, 3, {}),                                         # the benchmark: Hk 320, 80-column tiles
+    ('polymer', 64, 300, 4, dict(activation='LeakyReLU', bias=True)),   # two pair hand-offs between layers
+    ('polymer', 32, 300, 3, dict(undirected=True, activation='tanh')),
+    ('polymer', 24, 600, 3, dict(activation='SELU', aggregation='sum')),  # Hk 640: 8 layer tiles, 20 embed words
+    ('polymer', 16, 300, 2, dict(activation='PReLU', bias=True)),       # T = 2: the embed's pairs feed the last layer
+    ('qm9', 96, 300, 3, dict(activation='ELU')),                        # many molecules per block
+])
+def test_pair_operand_layers_vs_register_staged(kind, b, hidden, depth, extra):
+    """The message layers reading M_{t-1} as fp16 pair tiles written by their producer (the embed, the
+    previous layer; per-tile scales, gemm_x6.hpp h2_mainloop_pairs) meet the fp32 oracle at 1e-5 and agree
+    with the register-staged layers (WdConfig.gemm_variant 12) to fp32 rounding; both runs bitwise
+    reproducible."""
+    args = TrainArgs(hidden_size=hidden, depth=depth, **extra)
+    kw = dict(block_target=1) if kind == 'qm9' else {}  # (QM9: full blocks, past the one-launch forward's 32 rows)
+    g = BatchMolGraph(synthetic.make_batch(kind, b, 500 + b), device_bond_features=True, **kw)
+    enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim())
+    synthetic.fill_parameters(enc, 14)
+    p = {n: t.detach().clone() for n, t in enc.named_parameters()}
+    ref = mpn_ref.encoder_forward(p, g, args)
+    enc = enc.to(DEV).eval()
+    with torch.no_grad():
+        enc._gemm_variant = 11
+        pairs = enc(g)
+        pairs2 = enc(g)
+        enc._gemm_variant = 12
+        staged = enc(g)
+        enc._gemm_variant = 0
+    torch.cuda.synchronize()
+    assert torch.equal(pairs, pairs2)
+    assert golden_io.normwise(pairs.cpu().numpy(), ref.numpy()) <= TOL
+    assert golden_io.normwise(staged.cpu().numpy(), ref.numpy()) <= TOL
+    assert golden_io.normwise(pairs.cpu().numpy(), staged.cpu().numpy()) <= 2e-6
 
 
 def _runs_blocked(enc, g):
@@ -837,10 +892,11 @@ def _small_batch(seed):
                                           ('tanh', False, 'mean'), ('SELU', True, 'mean'), ('ELU', False, 'sum')])
 def test_one_launch_small_block_forward_is_bitwise_the_four_launch_forward(act, bias, agg):
     """QM9-sized blocks run the whole inference forward as ONE launch (small_fwd.hpp).  It must give
-    torch.equal outputs to the four-launch fused forward (WdConfig.gemm_variant 11 keeps that path) for
-    every activation, with and without biases, every aggregation, on the default block plan (about one
-    molecule per block) and on blocks of two to three molecules (block_target=20: <= 32 rows), and match the
-    fp32 oracle at 1e-5."""
+    torch.equal outputs to the four-launch fused forward with register-staged layers (WdConfig.gemm_variant
+    12: the same arithmetic in the same order) for every activation, with and without biases, every
+    aggregation, on the default block plan (about one molecule per block) and on blocks of two to three
+    molecules (block_target=20: <= 32 rows), and match the fp32 oracle at 1e-5, as must the four-launch
+    forward on fp16 pair tiles (variant 11: per-tile scales, a different but fp32-accurate rounding)."""
     args = TrainArgs(hidden_size=300, depth=3, activation=act, bias=bias, aggregation=agg)
     enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim())
     synthetic.fill_parameters(enc, 13)
@@ -855,11 +911,14 @@ def test_one_launch_small_block_forward_is_bitwise_the_four_launch_forward(act, 
         assert target is None or dg.struct.n_blocks <= 24  # several molecules per block
         with torch.no_grad():
             one = enc(g)
-            enc._gemm_variant = 11
+            enc._gemm_variant = 12
             four = enc(g)
+            enc._gemm_variant = 11
+            four_pairs = enc(g)
             enc._gemm_variant = 0
         torch.cuda.synchronize()
         assert torch.equal(one, four), (target, float((one - four).abs().max()))
         with torch.no_grad():
             ref = mpn_ref.encoder_forward(p, g, args)
         assert golden_io.normwise(one.cpu().numpy(), ref.numpy()) <= TOL
+        assert golden_io.normwise(four_pairs.cpu().numpy(), ref.numpy()) <= TOL
