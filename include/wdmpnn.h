@@ -197,9 +197,10 @@ typedef struct WdConfig {
                                molecule-blocked fused inference forward when WdGraph.blocks allow it;
                                9: f32-MFMA GEMMs on the unblocked path (precision A/B); 11: the fused
                                four-launch forward also for QM9-sized blocks (no one-launch forward);
-                               12: as 11, with the message layers staging M_{t-1} from fp32 Z_t rows
-                               through registers (the round-5 layer) instead of reading the fp16 pair
-                               tiles their producer wrote (A/B and the one-launch bitwise test).    */
+                               12: as 11, the message layers always staging M_{t-1} from fp32 Z_t rows
+                               through registers (the one-batch default); 13: as 11, the layers and W_o
+                               always on the fp16 pair tiles their producer wrote (the default for
+                               launches of several batches: wdmpnn_forward_many, the feed).          */
 } WdConfig;
 
 /* Gradients (device, caller-zeroed NOT required: every pointer is fully overwritten). NULL = skip. */

@@ -210,6 +210,11 @@ struct H2Prod {
     }
 };
 
+// K-chunk order rotated per molecule block (experiment; gemm_x6.hpp h2_mainloop_ws)
+#ifndef WD_KROT
+#define WD_KROT 0
+#endif
+
 // cache policy of the Z_t row stores: default write-back.  Write-through, as the planes use, measured
 // slower on the first polymer layer (17.46 us against 16.50, same box)
 #ifndef WD_ZWT
@@ -481,7 +486,7 @@ struct MpEpilogue {
             __syncthreads();
             // atom aggregate of this column tile: A[a] = sum_{x into a} w M_t[x] (mpn.py:126-131; x: the
             // atom's in-bonds, or its a2a neighbours in atom-message mode)
-            if constexpr (POUT) {
+            if (POUT && P.apairs) {
                 // A as fp16 pairs scaled by this tile's max (rows to the end of the last 16-row group: zeros)
                 float4 as[AUPT][2];
                 uint32_t amx = 0;
@@ -599,7 +604,8 @@ __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpL
     H2Prod<BM, ACT> ap(P, rs, rn, wv);
     wd_stamp(1 + 8 * LAST);
     floatx4 acc[BM / 64][BN / 16];
-    h2_mainloop_ws<BM, BN>(P.wh + (size_t)nt * (P.kp >> 5) * (2 * BN * 64), P.kp >> 5, rn, lds, acc, ap);
+    h2_mainloop_ws<BM, BN>(P.wh + (size_t)nt * (P.kp >> 5) * (2 * BN * 64), P.kp >> 5, rn, lds, acc, ap,
+                           WD_KROT ? blk % (P.kp >> 5) : 0);
     // the epilogue's gather lists and ids: not during the GEMM (live across the GEMM loop they pushed the
     // consumers' accumulators and fragments past 128 VGPRs); the staging waves load them into LDS while the
     // MFMA waves finish the last chunk

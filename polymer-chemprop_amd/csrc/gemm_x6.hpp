@@ -863,9 +863,12 @@ constexpr int H2_B_AHEAD = WD_H2_B_AHEAD, H2_A_STAGES = 2;
 template <int BM, int BN>
 constexpr int h2_lds_bytes() { return H2_A_STAGES * (2 * BM * 64) + (H2_B_AHEAD + 1) * (2 * BN * 64); }
 
+// rot: the workgroup multiplies the K chunks in the order rot, rot + 1, ..., nchunks - 1, 0, ..., rot - 1
+// (WD_KROT: rotated per molecule block, so that the blocks of an XCD do not all read the same W_h chunk at once)
 template <int BM, int BN, typename AProd>
 __device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nchunks, int a_rows, uint8_t *lds,
-                                               floatx4 (&acc)[BM / 64][BN / 16], AProd &ap) {
+                                               floatx4 (&acc)[BM / 64][BN / 16], AProd &ap, int rot = 0) {
+    auto K = [&](int c) { return c + rot < nchunks ? c + rot : c + rot - nchunks; };
     static_assert(BM == 128, "four consumer waves of 32 rows");
     constexpr int TM = BM / 64, TN = BN / 16;
     constexpr int APL = BM * 64, BPL = BN * 64;
@@ -879,20 +882,20 @@ __device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nch
         // compiler's own vmcnt waits before each store are exact: all but the NS - 1 younger sets)
         constexpr int NS = AProd::SETS;
         static_assert(NA - 1 <= NS, "the stages filled ahead come from distinct register sets");
-        static_for<NS>([&](auto i) { ap.load(i, min((int)decltype(i)::value, nchunks - 1)); });
+        static_for<NS>([&](auto i) { ap.load(i, K(min((int)decltype(i)::value, nchunks - 1))); });
         ap.init();  // (after the first loads are out: the scale's words are not on the rows' critical path)
         static_for<NA - 1>([&](auto c) {  // chunks 0 .. NA - 2 before the first barrier
             constexpr int C = decltype(c)::value;
-            ap.store(c, C, lds + C * ASTAGE);
-            ap.load(c, min(C + NS, nchunks - 1));
+            ap.store(c, K(C), lds + C * ASTAGE);
+            ap.load(c, K(min(C + NS, nchunks - 1)));
         });
         auto produce = [&](int kc, auto set) {  // set = (kc + NA - 1) % NS holds chunk kc + NA - 1
             const int cs = kc + NA - 1;
             if (cs >= nchunks) return;
             if (WD_STAMPS && wave == 4) wd_lstamp(kc, 4);
-            ap.store(set, cs, lds + (cs % NA) * ASTAGE);
+            ap.store(set, K(cs), lds + (cs % NA) * ASTAGE);
             if (WD_STAMPS && wave == 4) { __builtin_amdgcn_s_waitcnt(0xc07f); wd_lstamp(kc, 5); }
-            ap.load(set, min(cs + NS, nchunks - 1));
+            ap.load(set, K(min(cs + NS, nchunks - 1)));
         };
         int kc = 0;
         for (; kc + NS <= nchunks; kc += NS)
@@ -920,7 +923,7 @@ __device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nch
         bsrc[j] = p * BPL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
     }
     auto issue_b = [&](int kc) {
-        const uint8_t *bblk = bsrc_base + (size_t)kc * (2 * BPL);
+        const uint8_t *bblk = bsrc_base + (size_t)K(kc) * (2 * BPL);
         uint8_t *st = lds + NA * ASTAGE + (kc % NB) * BSTAGE;
 #pragma unroll
         for (int j = 0; j < BPW; ++j)
@@ -1018,6 +1021,10 @@ __device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nch
 // c = c / G; nchunks <= 64.
 // ---------------------------------------------------------------------------------------------
 constexpr int H2P_STAGES = 3;  // (2 chunks in flight + the one multiplied)
+#ifndef WD_H2P_BLOAD
+#define WD_H2P_BLOAD 1
+#endif
+constexpr bool H2P_BLOAD = WD_H2P_BLOAD;
 template <int BM, int BN>
 constexpr int h2p_stage_bytes() { return 2 * BM * 64 + 2 * BN * 64; }
 template <int BM, int BN>
@@ -1043,9 +1050,19 @@ __device__ __forceinline__ void h2_mainloop_pairs(const uint8_t *a_src, const ui
     const bool loader = wave >= 4;
     // this wave's pieces: source offsets in a chunk block (the DMA writes LDS lane-linearly, so the bank
     // swizzle of x6_slot is applied on the source side) and whether each is copied
-    int src[APW > BPW ? APW : BPW], dst[APW > BPW ? APW : BPW];
-    bool on[APW > BPW ? APW : BPW];
+    // (H2P_BLOAD: the loader waves copy B too, the MFMA waves issue no copy: a consumer issuing its B copies
+    // stalled ~350 cycles per chunk at the copy instructions, per-chunk stamps)
+    constexpr int XW = H2P_BLOAD ? BPW : 0;  // loader B pieces
+    int src[(APW > BPW ? APW : BPW) + XW], dst[(APW > BPW ? APW : BPW) + XW];
+    bool on[(APW > BPW ? APW : BPW) + XW];
     int mine = 0;
+    auto b_piece = [&](int j, int k) {
+        const int c = 4 * j + w4, q = 64 * c + lane, p = (q / (BN * 4)) % 2, r = (q >> 2) % BN, sl = q & 3;
+        src[k] = p * BPL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
+        dst[k] = 2 * APL + 1024 * c;
+        on[k] = BP % 4 == 0 || c < BP;
+        mine += on[k];
+    };
     if (loader) {
 #pragma unroll
         for (int j = 0; j < APW; ++j) {
@@ -1055,15 +1072,11 @@ __device__ __forceinline__ void h2_mainloop_pairs(const uint8_t *a_src, const ui
             on[j] = 16 * (c % (BM / 16)) < a_rows;  // 16-row groups past the block's rows: not copied
             mine += on[j];
         }
-    } else {
 #pragma unroll
-        for (int j = 0; j < BPW; ++j) {
-            const int c = 4 * j + w4, q = 64 * c + lane, p = (q / (BN * 4)) % 2, r = (q >> 2) % BN, sl = q & 3;
-            src[j] = p * BPL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
-            dst[j] = 2 * APL + 1024 * c;
-            on[j] = BP % 4 == 0 || c < BP;
-            mine += on[j];
-        }
+        for (int j = 0; j < XW; ++j) b_piece(j, APW + j);
+    } else if (!H2P_BLOAD) {
+#pragma unroll
+        for (int j = 0; j < BPW; ++j) b_piece(j, j);
     }
     // chunk kc in stage (kc + roff) % NS, so that the LAST chunk lands in stage 0: the caller may use the
     // tail of stage NS - 1 while the consumers multiply that chunk (mp_layer_kernel's epilogue lists)
@@ -1075,7 +1088,11 @@ __device__ __forceinline__ void h2_mainloop_pairs(const uint8_t *a_src, const ui
 #pragma unroll
             for (int j = 0; j < APW; ++j)
                 if (on[j]) glds16_untracked(blk + src[j], st + dst[j]);
-        } else {
+            const uint8_t *bblk = b_src + (size_t)kc * (2 * BPL);
+#pragma unroll
+            for (int j = 0; j < XW; ++j)
+                if (on[APW + j]) glds16_untracked(bblk + src[APW + j], st + dst[APW + j]);
+        } else if (!H2P_BLOAD) {
             const uint8_t *blk = b_src + (size_t)kc * (2 * BPL);
 #pragma unroll
             for (int j = 0; j < BPW; ++j)

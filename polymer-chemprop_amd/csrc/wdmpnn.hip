@@ -88,6 +88,12 @@ int self_check_once() {
     return c.rc ? fail(WD_ERR_UNSUPPORTED, "libwdmpnn self-check: %s", c.why.c_str()) : 0;
 }
 
+// W_o + readout on fp16 pair tiles (1; the last pair layer writes A as pairs) or on bf16x3 planes (0) in the
+// pair-operand forward
+#ifndef WD_WO_PAIRS
+#define WD_WO_PAIRS 1
+#endif
+
 // feed events that host threads wait for: hipEventBlockingSync (the waiting thread sleeps) or 0 (polls;
 // experiments)
 #ifndef WD_FEED_EVENT_SYNC
@@ -123,7 +129,8 @@ struct Dims {
     bool x6;   // plane-tile pipeline: gathers emit bf16x3 plane tiles, GEMMs run gemm_x6g_kernel
     bool blocked;  // molecule-blocked fused inference forward (fused_mp.hpp)
     bool small;    // ... as ONE launch, a workgroup per block (small_fwd.hpp: blocks <= 32 rows, Hk 320)
-    bool pairs;    // ... with M_t handed between the launches as fp16 pair tiles (LDS-DMA layer operands)
+    bool pairs;    // ... may hand M_t between the launches as fp16 pair tiles (LDS-DMA layer operands): the
+                   // workspace holds them; fused_forward uses them for launches of several batches
     bool pack_pairs;  // the packed weights hold W_o's pair tiles (a function of the encoder and config only:
                       // one inference pack serves every graph)
     int nblk;
@@ -170,18 +177,18 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     D.blocked = blk_common && (atom_blk || (D.x6 && g->bond_blk_row && (codes || (g->f_atoms_blk_x6 && g->f_bonds_x6)) &&
                                             g->bond_src_blk && g->b2revb));
     D.nblk = D.blocked ? g->n_blocks : 0;
-    // QM9-sized blocks, inference: the one-launch forward (WdConfig.gemm_variant 11 / 12 keep the four launches)
+    // QM9-sized blocks, inference: the one-launch forward (WdConfig.gemm_variant 11 / 12 / 13 keep the four launches)
     D.small = D.blocked && codes && !D.atom && !D.save && c->dropout == 0.f && D.Hk == SF_HK && !D.undirected &&
-              c->gemm_variant != 11 && c->gemm_variant != 12 && c->gemm_variant < 100 && g->blk_max_bonds > 0 && g->blk_max_bonds <= SF_ROWS &&
+              c->gemm_variant != 11 && c->gemm_variant != 12 && c->gemm_variant != 13 && c->gemm_variant < 100 &&
+              g->blk_max_bonds > 0 && g->blk_max_bonds <= SF_ROWS &&
               g->blk_max_atoms <= SF_ATOMS && D.Fa <= WO_MAXK && D.Fb <= WO_MAXK && D.Fb - D.Fa <= SF_ROWS;
     // inference through the embed (codes), bond messages, 80-column layer tiles, <= 64 embed words per block:
     // the layers read M_{t-1} as fp16 pair tiles written by its producer (fused_mp.hpp PAIRS; WdConfig.gemm_variant
     // 12 keeps the register-staged layers that read Z_t)
-    D.pack_pairs = !D.atom && !D.save && D.Hk % 80 == 0 && D.Hk / 32 <= 64;
+    D.pack_pairs = !D.atom && !D.save && D.Hk % 80 == 0 && D.Hk / 32 <= 64 && c->gemm_variant >= 13;
     // (debug variants 1ab: a = 1 pair layers / 2 register-staged layers, the fused forward stopped after stage
     // b = 1 embed, 2 first layer, ...: intermediate buffers left for tools/debug_pairs.py)
-    const bool staged_layers = c->gemm_variant == 12 || (c->gemm_variant >= 100 && (c->gemm_variant / 10) % 10 == 2);
-    D.pairs = D.pack_pairs && D.blocked && codes && !staged_layers;
+    D.pairs = D.pack_pairs && D.blocked && codes;
     if (D.atom && D.undirected)
         return fail(WD_ERR_UNSUPPORTED, "undirected with atom_messages (the reference indexes atom messages "
                                         "with b2revb, mpn.py:101-102)");
@@ -682,7 +689,7 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
     if (D.blocked) {
         // Z_t, ping-pong (layer t writes Zb[t & 1]; the first reads inp, the last writes none; a training
         // forward writes L.Z[t] instead)
-        if (!D.save && !D.pairs)
+        if (!D.save)
             for (int i = 0; i < 2 && i < D.T - 2; ++i) L.Zb[1 - i] = take(msg);
         if (D.pairs)  // (M_0 .. M_{T-2}: the last layer writes none)
             for (int i = 0; i < 2 && i < D.T - 1; ++i) L.Mp[i] = take((size_t)D.nblk * BLK_BONDS * D.Hk * 4);
@@ -690,7 +697,7 @@ FwdLayout fwd_layout(const Dims &D, bool own_pack) {
         const size_t words = std::max((size_t)D.nblk * 64, (size_t)(D.Rp / 64) * (D.Hk / 64));
         for (int i = 0; i < 2; ++i) L.amax[i] = take(words * 4);
         // A: bf16x3 plane tiles, or fp16 pair tiles (D.pairs), of the blocks' atom rows
-        L.Ab = take((size_t)D.nblk * BLK_ATOMS * D.Hk * (D.pairs ? 4 : 6));
+        L.Ab = take((size_t)D.nblk * BLK_ATOMS * D.Hk * 6);  // (6 bytes per value: also room for pairs)
         if (D.atom) {
             L.Fs = take((size_t)D.Vap * D.Fbk * 6);
             L.In3 = take((size_t)D.Rp * 3 * D.Hk * 4);
@@ -898,9 +905,16 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
 #define WD_EMBED40 1
 #endif
     // (the pair path: 32-column embed tiles, one scale word per chunk of M_0)
-    const bool pairs = D0.pairs;
+    // The pair-operand layers (M_t as fp16 pair tiles, written by its producer and copied by LDS-DMA; DESIGN.md
+    // §4 "Pair operands") only on request (gemm_variant 13): measured on one box against the register-staged
+    // layers, with W_o on pairs 108.5-108.8 vs 114.1 M edges/s one batch in flight, 172.8-173.6 vs 177.7 M three
+    // in flight, 181.6-182.3 vs 174.6 M forward_many(4); with W_o on planes (WD_WO_PAIRS 0) 112.6 / 175.3 /
+    // 173.0 M: the layer workgroup's chunk loop is bound by the bytes it keeps in flight per CU, which moving
+    // the split to the producer does not raise (round-6 stamps: ~2,000 cycles per chunk either way)
+    bool pairs = D0.pairs && c->gemm_variant == 13;
+    if (c->gemm_variant >= 100) pairs = D0.pairs && (c->gemm_variant / 10) % 10 == 1;  // (debug stops)
     for (int j = 1; j < n; ++j)
-        if (jobs[j].D.pairs != pairs) return fail(WD_ERR_UNSUPPORTED, "fused forward: batches of one launch differ in layout");
+        if (jobs[j].D.pairs != D0.pairs) return fail(WD_ERR_UNSUPPORTED, "fused forward: batches of one launch differ in layout");
     const bool bn40 = WD_EMBED40 && Hk % 40 == 0 && !pairs;
     const int embed_tiles = Hk / (pairs ? 32 : (bn40 ? 40 : BNf));
     if (codes) {
@@ -1010,10 +1024,10 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
                 Q.aout = last ? nullptr : (uint8_t *)(J.ws + J.L.Mp[t & 1]);
                 Q.zin = nullptr;
                 Q.zout = nullptr;
-                // the last layer: A as pair tiles, its words in the slot this layer does not read
-                Q.apairs = last ? (uint8_t *)(J.ws + J.L.Ab) : nullptr;
+                // the last layer: A as pair tiles (W_o on pairs, WD_WO_PAIRS), its words in the slot this layer
+                // does not read; else bf16x3 plane tiles
+                Q.apairs = last && WD_WO_PAIRS ? (uint8_t *)(J.ws + J.L.Ab) : nullptr;
                 Q.amax_out = slot(J, t);
-                Q.aplanes = nullptr;
             }
         }, M, grid);
         if (t == 1) WD_TRY(record_prof(c, 0, 0, st));  // one pair around all the layers
@@ -1071,16 +1085,16 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
         // (debug variants 1a4: the W_o pre-activation into the free second ping-pong buffer, tools/debug_pairs.py)
         if (c->gemm_variant >= 100 && c->gemm_variant % 10 == 4 && J.D.T == 3)
             R.zosave = pairs ? F(J, J.L.Mp[1]) : F(J, J.L.Zb[1]);
-        if (pairs) {
+        if (pairs && WD_WO_PAIRS) {
             R.apairs = (const uint8_t *)(J.ws + J.L.Ab); R.a_amax = slot(J, J.D.T - 1); R.a_nw = Hk / BNf; R.a_g = BNf;
             R.woh = (const uint8_t *)(pk + PL.WoH); R.wo_amax = (const uint32_t *)(pk + PL.wo_amax) + 64;
         }
     }, M, grid);
     if (grid > 0) {
         // one batch: single-chunk stages (55 KB, co-resident with other streams' layers); several: two
-        if (pairs && n > 1)
+        if (pairs && WD_WO_PAIRS && n > 1)
             hipLaunchKernelGGL((wo_readout_kernel<80, 1, WD_MULTI, true>), dim3(grid), dim3(512), 0, st, M);
-        else if (pairs)
+        else if (pairs && WD_WO_PAIRS)
             hipLaunchKernelGGL((wo_readout_kernel<80, 1, 1, true>), dim3(grid), dim3(512), 0, st, one_job(M));
         else if (bn80 && n > 1)
             hipLaunchKernelGGL((wo_readout_kernel<80, 2>), dim3(grid), dim3(64 * WoWaves<80>::WM * WoWaves<80>::WN), 0, st, M);
@@ -1916,7 +1930,7 @@ static int feed_batch_workspace(const Feed *F, const WdParams *p, const WdConfig
     D.Hd = D.H; D.Hdk = rup(D.Hd, 64); D.Kin = D.Fb; D.Kink = D.Fbk; D.ldx = D.Hk; D.Ko = D.Fak + D.Hk; D.Kd = D.Hk;
     D.x6 = true; D.blocked = true; D.nblk = F->spec.batch;  // (blocks hold whole molecules: <= batch)
     const size_t staged = fwd_layout(D, false).total;
-    D.pairs = true;  // (pair tiles instead of Z_t rows: whichever layout get_dims picks is covered)
+    D.pairs = true;  // (the pair tiles too: whichever layout get_dims picks is covered)
     *bytes = align256(std::max(staged, fwd_layout(D, false).total));
     return 0;
 }

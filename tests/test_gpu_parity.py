@@ -370,9 +370,9 @@ def test_blocked_fused_forward(kind, b, hidden, depth, extra):
 ])
 def test_pair_operand_layers_vs_register_staged(kind, b, hidden, depth, extra):
     """The message layers reading M_{t-1} as fp16 pair tiles written by their producer (the embed, the
-    previous layer; per-tile scales, gemm_x6.hpp h2_mainloop_pairs) meet the fp32 oracle at 1e-5 and agree
-    with the register-staged layers (WdConfig.gemm_variant 12) to fp32 rounding; both runs bitwise
-    reproducible."""
+    previous layer; per-tile scales, gemm_x6.hpp h2_mainloop_pairs; WdConfig.gemm_variant 13 forces them for
+    one batch, forward_many uses them by default) meet the fp32 oracle at 1e-5 and agree with the
+    register-staged layers (variant 12) to fp32 rounding; both runs bitwise reproducible."""
     args = TrainArgs(hidden_size=hidden, depth=depth, **extra)
     kw = dict(block_target=1) if kind == 'qm9' else {}  # (QM9: full blocks, past the one-launch forward's 32 rows)
     g = BatchMolGraph(synthetic.make_batch(kind, b, 500 + b), device_bond_features=True, **kw)
@@ -382,7 +382,7 @@ def test_pair_operand_layers_vs_register_staged(kind, b, hidden, depth, extra):
     ref = mpn_ref.encoder_forward(p, g, args)
     enc = enc.to(DEV).eval()
     with torch.no_grad():
-        enc._gemm_variant = 11
+        enc._gemm_variant = 13
         pairs = enc(g)
         pairs2 = enc(g)
         enc._gemm_variant = 12
@@ -896,7 +896,7 @@ def test_one_launch_small_block_forward_is_bitwise_the_four_launch_forward(act, 
     12: the same arithmetic in the same order) for every activation, with and without biases, every
     aggregation, on the default block plan (about one molecule per block) and on blocks of two to three
     molecules (block_target=20: <= 32 rows), and match the fp32 oracle at 1e-5, as must the four-launch
-    forward on fp16 pair tiles (variant 11: per-tile scales, a different but fp32-accurate rounding)."""
+    forward on fp16 pair tiles (variant 13: per-tile scales, a different but fp32-accurate rounding)."""
     args = TrainArgs(hidden_size=300, depth=3, activation=act, bias=bias, aggregation=agg)
     enc = MPNEncoder(args, get_atom_fdim(), get_bond_fdim())
     synthetic.fill_parameters(enc, 13)
@@ -913,7 +913,7 @@ def test_one_launch_small_block_forward_is_bitwise_the_four_launch_forward(act, 
             one = enc(g)
             enc._gemm_variant = 12
             four = enc(g)
-            enc._gemm_variant = 11
+            enc._gemm_variant = 13
             four_pairs = enc(g)
             enc._gemm_variant = 0
         torch.cuda.synchronize()
