@@ -210,11 +210,6 @@ struct H2Prod {
     }
 };
 
-// K-chunk order rotated per molecule block (experiment; gemm_x6.hpp h2_mainloop_ws)
-#ifndef WD_KROT
-#define WD_KROT 0
-#endif
-
 // cache policy of the Z_t row stores: default write-back.  Write-through, as the planes use, measured
 // slower on the first polymer layer (17.46 us against 16.50, same box)
 #ifndef WD_ZWT
@@ -548,7 +543,7 @@ __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpL
     constexpr int EPI_BYTES = Epi_::LDS_FLOATS * 4;  // P tile + the atom sums
     constexpr int STG_BYTES = PAIRS ? h2p_lds_bytes<BM, BN>() : h2_lds_bytes<BM, BN>();
     constexpr int LDS_BYTES = EPI_BYTES > STG_BYTES ? EPI_BYTES : STG_BYTES;
-    static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU");
+    static_assert(LDS_BYTES <= (PAIRS && H2P_STAGES > 3 ? 160 : 80) * 1024, "two workgroups per CU");
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
     int tile;
     wd_stamp(0 + 8 * LAST);
@@ -604,8 +599,7 @@ __global__ __launch_bounds__(MP_THREADS, 4) void mp_layer_kernel(const Multi<MpL
     H2Prod<BM, ACT> ap(P, rs, rn, wv);
     wd_stamp(1 + 8 * LAST);
     floatx4 acc[BM / 64][BN / 16];
-    h2_mainloop_ws<BM, BN>(P.wh + (size_t)nt * (P.kp >> 5) * (2 * BN * 64), P.kp >> 5, rn, lds, acc, ap,
-                           WD_KROT ? blk % (P.kp >> 5) : 0);
+    h2_mainloop_ws<BM, BN>(P.wh + (size_t)nt * (P.kp >> 5) * (2 * BN * 64), P.kp >> 5, rn, lds, acc, ap);
     // the epilogue's gather lists and ids: not during the GEMM (live across the GEMM loop they pushed the
     // consumers' accumulators and fragments past 128 VGPRs); the staging waves load them into LDS while the
     // MFMA waves finish the last chunk

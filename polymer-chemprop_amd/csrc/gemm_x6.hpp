@@ -640,6 +640,15 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
     case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
     case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
     case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
+    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 21: asm volatile("s_waitcnt vmcnt(21)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
     }
 }
@@ -863,12 +872,11 @@ constexpr int H2_B_AHEAD = WD_H2_B_AHEAD, H2_A_STAGES = 2;
 template <int BM, int BN>
 constexpr int h2_lds_bytes() { return H2_A_STAGES * (2 * BM * 64) + (H2_B_AHEAD + 1) * (2 * BN * 64); }
 
-// rot: the workgroup multiplies the K chunks in the order rot, rot + 1, ..., nchunks - 1, 0, ..., rot - 1
-// (WD_KROT: rotated per molecule block, so that the blocks of an XCD do not all read the same W_h chunk at once)
+// (Measured, round 6: the K chunks multiplied in an order rotated per molecule block, so that the blocks of an
+// XCD do not all read the same W_h chunk at once: 15.9 / 15.5 vs 15.6 / 15.1 us, same box -- no gain.)
 template <int BM, int BN, typename AProd>
 __device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nchunks, int a_rows, uint8_t *lds,
-                                               floatx4 (&acc)[BM / 64][BN / 16], AProd &ap, int rot = 0) {
-    auto K = [&](int c) { return c + rot < nchunks ? c + rot : c + rot - nchunks; };
+                                               floatx4 (&acc)[BM / 64][BN / 16], AProd &ap) {
     static_assert(BM == 128, "four consumer waves of 32 rows");
     constexpr int TM = BM / 64, TN = BN / 16;
     constexpr int APL = BM * 64, BPL = BN * 64;
@@ -882,20 +890,20 @@ __device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nch
         // compiler's own vmcnt waits before each store are exact: all but the NS - 1 younger sets)
         constexpr int NS = AProd::SETS;
         static_assert(NA - 1 <= NS, "the stages filled ahead come from distinct register sets");
-        static_for<NS>([&](auto i) { ap.load(i, K(min((int)decltype(i)::value, nchunks - 1))); });
+        static_for<NS>([&](auto i) { ap.load(i, min((int)decltype(i)::value, nchunks - 1)); });
         ap.init();  // (after the first loads are out: the scale's words are not on the rows' critical path)
         static_for<NA - 1>([&](auto c) {  // chunks 0 .. NA - 2 before the first barrier
             constexpr int C = decltype(c)::value;
-            ap.store(c, K(C), lds + C * ASTAGE);
-            ap.load(c, K(min(C + NS, nchunks - 1)));
+            ap.store(c, C, lds + C * ASTAGE);
+            ap.load(c, min(C + NS, nchunks - 1));
         });
         auto produce = [&](int kc, auto set) {  // set = (kc + NA - 1) % NS holds chunk kc + NA - 1
             const int cs = kc + NA - 1;
             if (cs >= nchunks) return;
             if (WD_STAMPS && wave == 4) wd_lstamp(kc, 4);
-            ap.store(set, K(cs), lds + (cs % NA) * ASTAGE);
+            ap.store(set, cs, lds + (cs % NA) * ASTAGE);
             if (WD_STAMPS && wave == 4) { __builtin_amdgcn_s_waitcnt(0xc07f); wd_lstamp(kc, 5); }
-            ap.load(set, K(min(cs + NS, nchunks - 1)));
+            ap.load(set, min(cs + NS, nchunks - 1));
         };
         int kc = 0;
         for (; kc + NS <= nchunks; kc += NS)
@@ -923,7 +931,7 @@ __device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nch
         bsrc[j] = p * BPL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
     }
     auto issue_b = [&](int kc) {
-        const uint8_t *bblk = bsrc_base + (size_t)K(kc) * (2 * BPL);
+        const uint8_t *bblk = bsrc_base + (size_t)kc * (2 * BPL);
         uint8_t *st = lds + NA * ASTAGE + (kc % NB) * BSTAGE;
 #pragma unroll
         for (int j = 0; j < BPW; ++j)
@@ -1020,7 +1028,11 @@ __device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nch
 // Words: lane l of every consumer wave holds word l of the block (nw <= 64, lane_word), group of column
 // c = c / G; nchunks <= 64.
 // ---------------------------------------------------------------------------------------------
-constexpr int H2P_STAGES = 3;  // (2 chunks in flight + the one multiplied)
+// (2 chunks in flight + the one multiplied; WD_H2P_STAGES 4: 104 KB of LDS, one layer workgroup per CU, measured)
+#ifndef WD_H2P_STAGES
+#define WD_H2P_STAGES 3
+#endif
+constexpr int H2P_STAGES = WD_H2P_STAGES;
 #ifndef WD_H2P_BLOAD
 #define WD_H2P_BLOAD 1
 #endif
@@ -1174,7 +1186,7 @@ __device__ __forceinline__ void h2_mainloop_pairs(const uint8_t *a_src, const ui
         // chunk kc landed for this wave (chunk kc + 1 may stay in flight), this wave's LDS reads done; then
         // for every wave: chunk kc complete, stage (kc + NS - 1) % NS read by all (at kc - 1)
         if (WD_STAMPS && (wave == 0 || wave == 4)) wd_lstamp(kc, wave == 0 ? 0 : 4);
-        wait_vmcnt(kc + 1 < nchunks ? mine : 0);
+        wait_vmcnt(min(NS - 2, nchunks - 1 - kc) * mine);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (WD_STAMPS && (wave == 0 || wave == 4)) wd_lstamp(kc, wave == 0 ? 1 : 5);
         __builtin_amdgcn_s_barrier();
