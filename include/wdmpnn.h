@@ -193,14 +193,14 @@ typedef struct WdConfig {
     void   *prof_pool;      /* optional WdEventPool: one event pair (pair prof_slot) is recorded around
                                the depth - 1 message-passing launches (the dominant kernel) of this
                                forward: before the first, after the last                          */
-    int32_t gemm_variant;   /* 0 (default): bf16x6 split-plane GEMMs (fp32-accurate), with the
-                               molecule-blocked fused inference forward when WdGraph.blocks allow it;
+    int32_t gemm_variant;   /* 0 (default): fp32-accurate split GEMMs with the molecule-blocked
+                               fused inference forward when WdGraph.blocks allow it: its message layers and
+                               W_o read fp16 pair tiles their producers wrote (bond messages, hidden rounded
+                               to 64 a multiple of 80), QM9-sized blocks take the one-launch forward;
                                9: f32-MFMA GEMMs on the unblocked path (precision A/B); 11: the fused
                                four-launch forward also for QM9-sized blocks (no one-launch forward);
-                               12: as 11, the message layers always staging M_{t-1} from fp32 Z_t rows
-                               through registers (the one-batch default); 13: as 11, the layers and W_o
-                               always on the fp16 pair tiles their producer wrote (the default for
-                               launches of several batches: wdmpnn_forward_many, the feed).          */
+                               12: as 11, the message layers staging M_{t-1} from fp32 Z_t rows through
+                               registers (the round-5 default); 13: as 11, on pair tiles.            */
 } WdConfig;
 
 /* Gradients (device, caller-zeroed NOT required: every pointer is fully overwritten). NULL = skip. */

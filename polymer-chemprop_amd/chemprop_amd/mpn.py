@@ -499,7 +499,7 @@ class MPNEncoder(nn.Module):
         id of the current stream (the inference path's cheaper alternative to ``stream``)."""
         key = (tuple((t.data_ptr(), t._version, id(t)) if t is not None else None for t in params), _OPT_STEPS[0],
                self._parameters['cached_zero_vector'].data_ptr(), gs.atom_fdim, gs.bond_fdim, gs.desc_dim,
-               gs.atom_messages, device, cfg.gemm_variant >= 13) if cache else None  # (13: + W_o's pair tiles)
+               gs.atom_messages, device, cfg.gemm_variant not in (9, 12)) if cache else None  # (+ W_o's pair tiles)
         cached = self._pack_cache if cache else None
         if cached is not None and cached[0] == key:
             if sid is None:

@@ -1010,21 +1010,22 @@ __device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nch
 // operands are pre-split fp16 hi / lo pair tiles in HBM -- A = the block's M_{t-1}, written as pairs by
 // its producer (the embed, or the previous layer's epilogue) with a power-of-two scale per group of G
 // columns (the producer's column tile), B = W_h (wdmpnn_pack_params).  No register staging: waves 4-7
-// ("loaders") copy A, waves 0-3 (MFMA "consumers", as in h2_mainloop_ws) copy B, both by LDS-DMA two
-// chunks ahead into a ring of H2P_STAGES stages, one s_barrier per chunk.
+// ("loaders") copy A and B by LDS-DMA NS - 1 chunks ahead into a ring of H2P_STAGES stages, waves 0-3
+// (MFMA "consumers", one per SIMD, BM / 4 rows x BN columns each) multiply; one s_barrier per chunk.  The
+// two roles run separate loops with the same barrier count, and the consumers' loop is instantiated per
+// count of live 16-row tiles: no control flow inside a consumer's chunk, so its accumulators stay in
+// place and its MFMAs run on across the barrier into the next chunk (a loop shared by both roles, with
+// per-chunk scale steps, made the register allocator copy all 40 accumulators after every chunk -- each
+// copy waiting for its MFMA -- 2,200 against 1,200 cycles per chunk, tools/ring_probe.hip).
 //
 // Scales.  The A groups carry different scales s_g = 2^(se_g - 127) (se = h2_sexp of the group's word).
-// The accumulator holds its sum in the units of the scale of the group last multiplied; moving to a
-// chunk of another scale multiplies it by 2^(se_new - se_cur) first (v_ldexp_f32: exact).  A chunk whose
-// two 16-column halves lie in different groups of different scales (BN = 80 producer tiles: chunks 2 and 7
-// of Hk = 320) is multiplied at the scale of its larger half: the A fragments of the other half (lanes
-// 32-63 hold k 16..31 of a v_mfma_f32_16x16x32_f16 operand, lanes 0-31 k 0..15) are multiplied by
-// 2^-d in fp16 (v_pk_mul_f16; d = their exponent difference, zero past d = 24), rounding at 2^-24 of the
-// scaled unit: the precision of one shared scale, as the register-staged layer's per-block scale.  A group
-// whose word is 0 (all zero) is skipped; so is a group more than 2^60 below the accumulator's scale
-// (|acc| <= K 2^30 < 2^39 keeps every upward rescale finite; the skipped products lie below the
-// per-block-scale error bound, planes.hpp h2).  The accumulator's final exponent comes back in se_out
-// (-1: no group had data; acc is zero).
+// Every chunk is multiplied at ONE scale, the block's largest-magnitude group (smallest se, `cur`): each
+// lane multiplies its A fragments by 2^-(se_g - cur) in fp16 (v_pk_mul_f16; lanes 32-63 hold k 16..31 of
+// a v_mfma_f32_16x16x32_f16 operand, lanes 0-31 k 0..15, so the two 16-column halves of a chunk that
+// straddles two producer tiles take their own factors; zero past a difference of 24), rounding at 2^-24
+// of the shared scaled unit: the precision of one scale per block, as the register-staged layer's.  An
+// all-zero group (word 0) multiplies zeros.  The accumulator's exponent comes back in se_out (-1: no group
+// had data; acc is zero).
 // Words: lane l of every consumer wave holds word l of the block (nw <= 64, lane_word), group of column
 // c = c / G; nchunks <= 64.
 // ---------------------------------------------------------------------------------------------
@@ -1033,21 +1034,18 @@ __device__ __forceinline__ void h2_mainloop_ws(const uint8_t *bsrc_base, int nch
 #define WD_H2P_STAGES 3
 #endif
 constexpr int H2P_STAGES = WD_H2P_STAGES;
-#ifndef WD_H2P_BLOAD
-#define WD_H2P_BLOAD 1
-#endif
-constexpr bool H2P_BLOAD = WD_H2P_BLOAD;
 template <int BM, int BN>
 constexpr int h2p_stage_bytes() { return 2 * BM * 64 + 2 * BN * 64; }
 template <int BM, int BN>
 constexpr int h2p_lds_bytes() { return H2P_STAGES * h2p_stage_bytes<BM, BN>(); }
 
-__device__ __forceinline__ void acc_ldexp(floatx4 &a, int d) {
-    a[0] = __builtin_amdgcn_ldexpf(a[0], d); a[1] = __builtin_amdgcn_ldexpf(a[1], d);
-    a[2] = __builtin_amdgcn_ldexpf(a[2], d); a[3] = __builtin_amdgcn_ldexpf(a[3], d);
-}
-
-template <int BM, int BN>
+// FRAG (fragment schedule; tools/ring_probe.hip measures the variants): 0: each column tile's next B
+// fragments read after its first MFMAs; 1: read before them; 2: every B fragment of the chunk read before
+// the first MFMA
+#ifndef WD_H2P_FRAG
+#define WD_H2P_FRAG 0
+#endif
+template <int BM, int BN, int FRAG = WD_H2P_FRAG>
 __device__ __forceinline__ void h2_mainloop_pairs(const uint8_t *a_src, const uint8_t *b_src, int nchunks, int a_rows,
                                                   uint32_t wv, int G, uint8_t *lds, floatx4 (&acc)[BM / 64][BN / 16],
                                                   int &se_out) {
@@ -1056,26 +1054,22 @@ __device__ __forceinline__ void h2_mainloop_pairs(const uint8_t *a_src, const ui
     constexpr int RW = BM / 4, TM = RW / 16, TN = BN / 16;  // rows per consumer wave, its 16-row tiles
     constexpr int APL = BM * 64, BPL = BN * 64, STAGE = h2p_stage_bytes<BM, BN>(), NS = H2P_STAGES;
     constexpr int AP = 2 * BM / 16, APW = AP / 4;        // A: 16 pieces of 1 KB per chunk, 4 per loader wave
-    constexpr int BP = 2 * BN / 16, BPW = (BP + 3) / 4;  // B: 10 pieces, <= 3 per consumer wave
+    constexpr int BP = 2 * BN / 16, BPW = (BP + 3) / 4;  // B: 10 pieces, <= 3 per loader wave
     static_assert(AP % 4 == 0, "A pieces split evenly over the loader waves");
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, w4 = wave & 3, g = lane >> 4, i16 = lane & 15;
-    const bool loader = wave >= 4;
-    // this wave's pieces: source offsets in a chunk block (the DMA writes LDS lane-linearly, so the bank
-    // swizzle of x6_slot is applied on the source side) and whether each is copied
-    // (H2P_BLOAD: the loader waves copy B too, the MFMA waves issue no copy: a consumer issuing its B copies
-    // stalled ~350 cycles per chunk at the copy instructions, per-chunk stamps)
-    constexpr int XW = H2P_BLOAD ? BPW : 0;  // loader B pieces
-    int src[(APW > BPW ? APW : BPW) + XW], dst[(APW > BPW ? APW : BPW) + XW];
-    bool on[(APW > BPW ? APW : BPW) + XW];
-    int mine = 0;
-    auto b_piece = [&](int j, int k) {
-        const int c = 4 * j + w4, q = 64 * c + lane, p = (q / (BN * 4)) % 2, r = (q >> 2) % BN, sl = q & 3;
-        src[k] = p * BPL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
-        dst[k] = 2 * APL + 1024 * c;
-        on[k] = BP % 4 == 0 || c < BP;
-        mine += on[k];
-    };
-    if (loader) {
+    // chunk kc in stage (kc + roff) % NS, so that the LAST chunk lands in stage 0: the caller may use the
+    // tail of stage NS - 1 while the consumers multiply that chunk (mp_layer_kernel's epilogue lists)
+    const int roff = (NS - (nchunks - 1) % NS) % NS;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (wave >= 4) {  // ---- loaders
+        // this wave's pieces: source offsets in a chunk block (the DMA writes LDS lane-linearly, so the bank
+        // swizzle of x6_slot is applied on the source side) and whether each is copied
+        int src[APW + BPW], dst[APW + BPW];
+        bool on[APW + BPW];
+        int mine = 0;
 #pragma unroll
         for (int j = 0; j < APW; ++j) {
             const int c = 4 * j + w4, q = 64 * c + lane, p = q / (BM * 4), r = (q >> 2) % BM, sl = q & 3;
@@ -1085,132 +1079,120 @@ __device__ __forceinline__ void h2_mainloop_pairs(const uint8_t *a_src, const ui
             mine += on[j];
         }
 #pragma unroll
-        for (int j = 0; j < XW; ++j) b_piece(j, APW + j);
-    } else if (!H2P_BLOAD) {
-#pragma unroll
-        for (int j = 0; j < BPW; ++j) b_piece(j, j);
-    }
-    // chunk kc in stage (kc + roff) % NS, so that the LAST chunk lands in stage 0: the caller may use the
-    // tail of stage NS - 1 while the consumers multiply that chunk (mp_layer_kernel's epilogue lists)
-    const int roff = (NS - (nchunks - 1) % NS) % NS;
-    auto issue = [&](int kc) {
-        uint8_t *st = lds + ((kc + roff) % NS) * STAGE;
-        if (loader) {
-            const uint8_t *blk = a_src + (size_t)kc * (2 * APL);
+        for (int j = 0; j < BPW; ++j) {
+            const int c = 4 * j + w4, q = 64 * c + lane, p = (q / (BN * 4)) % 2, r = (q >> 2) % BN, sl = q & 3;
+            src[APW + j] = p * BPL + r * 64 + 16 * (sl ^ ((r >> 1) & 3));
+            dst[APW + j] = 2 * APL + 1024 * c;
+            on[APW + j] = BP % 4 == 0 || c < BP;
+            mine += on[APW + j];
+        }
+        mine = __builtin_amdgcn_readfirstlane(mine);  // (wave-uniform: a scalar wait below)
+        auto issue = [&](int kc) {
+            uint8_t *st = lds + ((kc + roff) % NS) * STAGE;
+            const uint8_t *ablk = a_src + (size_t)kc * (2 * APL), *bblk = b_src + (size_t)kc * (2 * BPL);
 #pragma unroll
             for (int j = 0; j < APW; ++j)
-                if (on[j]) glds16_untracked(blk + src[j], st + dst[j]);
-            const uint8_t *bblk = b_src + (size_t)kc * (2 * BPL);
-#pragma unroll
-            for (int j = 0; j < XW; ++j)
-                if (on[APW + j]) glds16_untracked(bblk + src[APW + j], st + dst[APW + j]);
-        } else if (!H2P_BLOAD) {
-            const uint8_t *blk = b_src + (size_t)kc * (2 * BPL);
+                if (on[j]) glds16_untracked(ablk + src[j], st + dst[j]);
 #pragma unroll
             for (int j = 0; j < BPW; ++j)
-                if (on[j]) glds16_untracked(blk + src[j], st + dst[j]);
+                if (on[APW + j]) glds16_untracked(bblk + src[APW + j], st + dst[APW + j]);
+        };
+#pragma unroll
+        for (int c = 0; c < NS - 1; ++c)
+            if (c < nchunks) issue(c);
+        for (int kc = 0; kc < nchunks; ++kc) {
+            // chunk kc landed (chunks kc + 1 .. kc + NS - 2 may stay in flight); after the barrier every
+            // consumer is done reading stage (kc + NS - 1 + roff) % NS (chunk kc - 1's)
+            if (WD_STAMPS && wave == 4) wd_lstamp(kc, 4);
+            wait_vmcnt(min(NS - 2, nchunks - 1 - kc) * mine);
+            if (WD_STAMPS && wave == 4) wd_lstamp(kc, 5);
+            __builtin_amdgcn_s_barrier();
+            if (kc + NS - 1 < nchunks) issue(kc + NS - 1);
         }
-    };
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+        __builtin_amdgcn_s_waitcnt(0x0070);  // (vmcnt(0): every copy of this wave landed)
+        se_out = -1;
+        return;
+    }
+    // ---- consumers
     int ao[TM], bo[TN];
 #pragma unroll
     for (int a = 0; a < TM; ++a) ao[a] = x6_slot(RW * w4 + 16 * a + i16, g);
 #pragma unroll
     for (int b = 0; b < TN; ++b) bo[b] = x6_slot(16 * b + i16, g);
     const int na = min(TM, max(0, (a_rows - RW * w4 + 15) >> 4));
-    // MODE 1: the A fragments multiplied by this lane's factor fl (2^-d for the half at the smaller scale)
-    auto compute_n = [&](const uint8_t *st, const uint8_t *sb, auto na_c, auto mode_c, _Float16 fl) {
-        constexpr int NA = decltype(na_c)::value, MODE = decltype(mode_c)::value;
-        f16x8 af[TM][2], bq[2][2];
+    // the scale exponents of chunk `lane`'s two halves (all-zero group: BIG), the shared one (the smallest
+    // over the chunks multiplied) and per chunk (lane) the two halves' fp16 factors 2^-(se - cur), packed
+    constexpr int BIG = 1 << 20;
+    const int k0 = min((32 * lane) / G, 63), k1 = min((32 * lane + 16) / G, 63);
+    const uint32_t lw0 = (uint32_t)__shfl((int)wv, k0, 64), lw1 = (uint32_t)__shfl((int)wv, k1, 64);
+    const int s0 = lw0 ? h2_sexp(lw0) : BIG, s1 = lw1 ? h2_sexp(lw1) : BIG;
+    const int cur = BIG - (int)wave_max_u32((uint32_t)(BIG - (lane < nchunks ? min(s0, s1) : BIG)));
+    auto f16code = [&](int se) -> uint32_t {
+        const int d = se - cur;
+        return d > 24 ? 0u : (uint32_t)__builtin_bit_cast(unsigned short, (_Float16)__builtin_amdgcn_ldexpf(1.0f, -d));
+    };
+    const uint32_t fcode = f16code(s0) | (f16code(s1) << 16);
+    const int fsh = lane < 32 ? 0 : 16;
+    auto compute_n = [&](const uint8_t *st, const uint8_t *sb, auto na_c, _Float16 fl) {
+        constexpr int NA = decltype(na_c)::value;
+        constexpr int SCH = FRAG & 3, NB = SCH == 2 ? TN : 2;
+        f16x8 af[TM][2], bq[NB][2];
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
 #pragma unroll
             for (int a = 0; a < NA; ++a) {
                 af[a][p] = *reinterpret_cast<const f16x8 *>(st + p * APL + ao[a]);
-                if constexpr (MODE != 0) af[a][p] = af[a][p] * fl;
+                af[a][p] = af[a][p] * fl;
             }
-            bq[0][p] = *reinterpret_cast<const f16x8 *>(sb + p * BPL + bo[0]);
+#pragma unroll
+            for (int b = 0; b < (SCH == 2 ? TN : 1); ++b) bq[b][p] = *reinterpret_cast<const f16x8 *>(sb + p * BPL + bo[b]);
         }
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
+            const int cb = SCH == 2 ? b : (b & 1);
+            if constexpr (SCH == 1) {
+                if (b + 1 < TN)
+#pragma unroll
+                    for (int p = 0; p < 2; ++p) bq[(b + 1) & 1][p] = *reinterpret_cast<const f16x8 *>(sb + p * BPL + bo[b + 1]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
 #pragma unroll
             for (int a = 0; a < NA; ++a)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][0], bq[b & 1][0], acc[a][b], 0, 0, 0);
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][0], bq[cb][0], acc[a][b], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
-            if (b + 1 < TN)
+            if (SCH == 0 && b + 1 < TN)
 #pragma unroll
                 for (int p = 0; p < 2; ++p) bq[(b + 1) & 1][p] = *reinterpret_cast<const f16x8 *>(sb + p * BPL + bo[b + 1]);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int a = 0; a < NA; ++a) {
-                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][0], bq[b & 1][1], acc[a][b], 0, 0, 0);
-                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][1], bq[b & 1][0], acc[a][b], 0, 0, 0);
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][0], bq[cb][1], acc[a][b], 0, 0, 0);
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][1], bq[cb][0], acc[a][b], 0, 0, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
     };
-    auto rescale = [&](int d) {
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-            for (int b = 0; b < TN; ++b) acc_ldexp(acc[a][b], d);
-    };
-    int cur = -1;  // exponent of the accumulator's scale (-1: nothing accumulated yet)
-    // the scale step in front of a group's products (se: its scale exponent, -1 for an all-zero group):
-    // false = skip them (zero or negligible group)
-    auto enter = [&](int se) {
-        if (se < 0) return false;
-        if (cur < 0) { cur = se; return true; }
-        const int d = se - cur;
-        if (d > 60) return false;
-        if (d != 0) { rescale(d); cur = se; }
-        return true;
-    };
-    // the scale exponents of every chunk's two halves, lane kc describing chunk kc (+1, 0 = all-zero group),
-    // formed before the first copy: in the loop a chunk's pair is one v_readlane of a register no load feeds
-    // (a readlane of the words themselves made the compiler wait for every copy in flight -- vmcnt(0) -- at
-    // each chunk: the words' load, pending on entry, is "pending" at the loop header)
-    uint32_t ecode = 0;
-    if (!loader) {
-        const int k0 = min((32 * lane) / G, 63), k1 = min((32 * lane + 16) / G, 63);
-        const uint32_t lw0 = (uint32_t)__shfl((int)wv, k0, 64), lw1 = (uint32_t)__shfl((int)wv, k1, 64);
-        ecode = (lw0 ? (uint32_t)h2_sexp(lw0) + 1u : 0u) | ((lw1 ? (uint32_t)h2_sexp(lw1) + 1u : 0u) << 16);
-    }
-#pragma unroll
-    for (int c = 0; c < NS - 1; ++c)
-        if (c < nchunks) issue(c);
-    for (int kc = 0; kc < nchunks; ++kc) {
-        // chunk kc landed for this wave (chunk kc + 1 may stay in flight), this wave's LDS reads done; then
-        // for every wave: chunk kc complete, stage (kc + NS - 1) % NS read by all (at kc - 1)
-        if (WD_STAMPS && (wave == 0 || wave == 4)) wd_lstamp(kc, wave == 0 ? 0 : 4);
-        wait_vmcnt(min(NS - 2, nchunks - 1 - kc) * mine);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (WD_STAMPS && (wave == 0 || wave == 4)) wd_lstamp(kc, wave == 0 ? 1 : 5);
-        __builtin_amdgcn_s_barrier();
-        if (WD_STAMPS && wave == 0) wd_lstamp(kc, 2);
-        if (kc + NS - 1 < nchunks) issue(kc + NS - 1);
-        if (loader) continue;
-        const uint8_t *st = lds + ((kc + roff) % NS) * STAGE, *sb = st + 2 * APL;
-        const uint32_t ec = __builtin_amdgcn_readlane(ecode, kc);
-        const int e0 = (int)(ec & 0xffffu) - 1, e1 = (int)(ec >> 16) - 1;
-        // the chunk's scale: its larger half's (an all-zero half -- its products are zero at any scale -- takes
-        // the other's); this lane's half is multiplied by 2^-(its shortfall), 1 in the common case of one scale
-        // (one code path: a second, unscaled instantiation of the MFMA loop pushed the kernel past 128 VGPRs)
-        const int e = e0 < 0 ? e1 : (e1 < 0 ? e0 : min(e0, e1));
-        const int eh = lane < 32 ? e0 : e1, d = eh < 0 ? 0 : eh - e;
-        const _Float16 fl = d > 24 ? (_Float16)0.f : (_Float16)__uint_as_float((uint32_t)(127 - d) << 23);
-        if (enter(e))
-            dispatch_upto<TM>(na, [&](auto c) { compute_n(st, sb, c, std::integral_constant<int, 1>{}, fl); });
-        if (WD_STAMPS && wave == 0) {
+    dispatch_upto<TM>(na, [&](auto na_c) {
+        for (int kc = 0; kc < nchunks; ++kc) {
+            // this wave's fragment reads done (the stage of chunk kc - 1 is refilled after the barrier);
+            // after it chunk kc is in LDS
+            if (WD_STAMPS && wave == 0) wd_lstamp(kc, 0);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            wd_lstamp(kc, 3);
+            if (WD_STAMPS && wave == 0) wd_lstamp(kc, 1);
+            __builtin_amdgcn_s_barrier();
+            if (WD_STAMPS && wave == 0) wd_lstamp(kc, 2);
+            const uint8_t *st = lds + ((kc + roff) % NS) * STAGE, *sb = st + 2 * APL;
+            const uint32_t fc = __builtin_amdgcn_readlane(fcode, kc);
+            const _Float16 fl = __builtin_bit_cast(_Float16, (unsigned short)((fc >> fsh) & 0xffffu));
+            compute_n(st, sb, na_c, fl);
+            if (WD_STAMPS && wave == 0) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                wd_lstamp(kc, 3);
+            }
         }
-    }
-    __builtin_amdgcn_s_waitcnt(0x0070);  // (vmcnt(0): every copy of this wave landed)
-    se_out = cur;
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    se_out = cur >= BIG ? -1 : cur;
 }
 
 // acc tile -> LDS fp32 [BM][BN + 4] (C/D map of 16x16: col = lane & 15, row = 4 (lane >> 4) + reg)

@@ -129,12 +129,16 @@ struct Dims {
     bool x6;   // plane-tile pipeline: gathers emit bf16x3 plane tiles, GEMMs run gemm_x6g_kernel
     bool blocked;  // molecule-blocked fused inference forward (fused_mp.hpp)
     bool small;    // ... as ONE launch, a workgroup per block (small_fwd.hpp: blocks <= 32 rows, Hk 320)
-    bool pairs;    // ... may hand M_t between the launches as fp16 pair tiles (LDS-DMA layer operands): the
-                   // workspace holds them; fused_forward uses them for launches of several batches
+    bool pairs;    // ... hands M_t between the launches as fp16 pair tiles (LDS-DMA layer operands): the
+                   // workspace holds them (fused_forward: unless gemm_variant 12)
     bool pack_pairs;  // the packed weights hold W_o's pair tiles (a function of the encoder and config only:
                       // one inference pack serves every graph)
     int nblk;
 };
+
+// WdConfig.gemm_variant values that run the fused forward's layers on fp16 pair operands where the layout
+// allows (all but 9, the f32-MFMA A/B, and 12, the register-staged layers)
+inline bool pair_variant(int v) { return v != 9 && v != 12; }
 
 int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     if (!g || !p || !c) return fail(WD_ERR_ARG, "null graph/params/config");
@@ -184,8 +188,8 @@ int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
               g->blk_max_atoms <= SF_ATOMS && D.Fa <= WO_MAXK && D.Fb <= WO_MAXK && D.Fb - D.Fa <= SF_ROWS;
     // inference through the embed (codes), bond messages, 80-column layer tiles, <= 64 embed words per block:
     // the layers read M_{t-1} as fp16 pair tiles written by its producer (fused_mp.hpp PAIRS; WdConfig.gemm_variant
-    // 12 keeps the register-staged layers that read Z_t)
-    D.pack_pairs = !D.atom && !D.save && D.Hk % 80 == 0 && D.Hk / 32 <= 64 && c->gemm_variant >= 13;
+    // 12 keeps the register-staged layers that read Z_t, 13 the pair layers also for QM9-sized blocks)
+    D.pack_pairs = !D.atom && !D.save && D.Hk % 80 == 0 && D.Hk / 32 <= 64 && pair_variant(c->gemm_variant);
     // (debug variants 1ab: a = 1 pair layers / 2 register-staged layers, the fused forward stopped after stage
     // b = 1 embed, 2 first layer, ...: intermediate buffers left for tools/debug_pairs.py)
     D.pairs = D.pack_pairs && D.blocked && codes;
@@ -906,12 +910,10 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
 #endif
     // (the pair path: 32-column embed tiles, one scale word per chunk of M_0)
     // The pair-operand layers (M_t as fp16 pair tiles, written by its producer and copied by LDS-DMA; DESIGN.md
-    // §4 "Pair operands") only on request (gemm_variant 13): measured on one box against the register-staged
-    // layers, with W_o on pairs 108.5-108.8 vs 114.1 M edges/s one batch in flight, 172.8-173.6 vs 177.7 M three
-    // in flight, 181.6-182.3 vs 174.6 M forward_many(4); with W_o on planes (WD_WO_PAIRS 0) 112.6 / 175.3 /
-    // 173.0 M: the layer workgroup's chunk loop is bound by the bytes it keeps in flight per CU, which moving
-    // the split to the producer does not raise (round-6 stamps: ~2,000 cycles per chunk either way)
-    bool pairs = D0.pairs && c->gemm_variant == 13;
+    // §4 "Pair operands") wherever the layout allows (D.pairs; gemm_variant 12 keeps the register-staged layers):
+    // round 6, one box, 190.1 vs 178.8 M edges/s three batches in flight, 121.2 vs 118.1 M one, 203.0 vs 175.0 M
+    // forward_many(4) (profiles/round6_pairs_default_ab.txt)
+    bool pairs = D0.pairs;
     if (c->gemm_variant >= 100) pairs = D0.pairs && (c->gemm_variant / 10) % 10 == 1;  // (debug stops)
     for (int j = 1; j < n; ++j)
         if (jobs[j].D.pairs != D0.pairs) return fail(WD_ERR_UNSUPPORTED, "fused forward: batches of one launch differ in layout");

@@ -66,9 +66,10 @@ def test_forward_many_with_gradients_takes_the_one_batch_path():
 
 def test_full_block_plan_gives_the_same_outputs():
     """block_target=1 (forward_many's throughput layout: small batches in full molecule blocks) changes
-    only the block plan: outputs equal the default plan's within fp32 rounding of the same arithmetic
-    (bitwise here: every per-element operation and its order is independent of the blocking), and
-    forward_many on such graphs equals the single calls bitwise."""
+    only the block plan: outputs equal the default plan's within fp32 rounding (the pair-operand layers
+    scale each block's fp16 operands by that block's maxima, so the roundings differ with the blocking;
+    the register-staged layers, gemm_variant 12, are bitwise independent of it), and forward_many on such
+    graphs equals the single calls bitwise."""
     enc, _ = _enc(hidden_size=300, depth=3)
     mols = [synthetic.make_batch('qm9', 64, 900 + i) for i in range(6)]
     sliced = [BatchMolGraph(m, device_bond_features=True) for m in mols]
@@ -78,6 +79,12 @@ def test_full_block_plan_gives_the_same_outputs():
         a = [enc(g) for g in sliced]
         b = [enc(g) for g in full]
         c = enc.forward_many(full)
+        enc._gemm_variant = 12
+        a12 = [enc(g) for g in sliced]
+        b12 = [enc(g) for g in full]
+        enc._gemm_variant = 0
     torch.cuda.synchronize()
     for x, y, z in zip(a, b, c):
-        assert torch.equal(x, y) and torch.equal(y, z)
+        assert golden_io.normwise(x.cpu().numpy(), y.cpu().numpy()) <= 2e-6 and torch.equal(y, z)
+    for x, y in zip(a12, b12):
+        assert torch.equal(x, y)

@@ -370,9 +370,9 @@ def test_blocked_fused_forward(kind, b, hidden, depth, extra):
 ])
 def test_pair_operand_layers_vs_register_staged(kind, b, hidden, depth, extra):
     """The message layers reading M_{t-1} as fp16 pair tiles written by their producer (the embed, the
-    previous layer; per-tile scales, gemm_x6.hpp h2_mainloop_pairs; WdConfig.gemm_variant 13 forces them for
-    one batch, forward_many uses them by default) meet the fp32 oracle at 1e-5 and agree with the
-    register-staged layers (variant 12) to fp32 rounding; both runs bitwise reproducible."""
+    previous layer; per-tile scales, one shared scale per block in the GEMM, gemm_x6.hpp h2_mainloop_pairs; the
+    default path, WdConfig.gemm_variant 13 forces them also for QM9-sized blocks) meet the fp32 oracle at 1e-5
+    and agree with the register-staged layers (variant 12) to fp32 rounding; both runs bitwise reproducible."""
     args = TrainArgs(hidden_size=hidden, depth=depth, **extra)
     kw = dict(block_target=1) if kind == 'qm9' else {}  # (QM9: full blocks, past the one-launch forward's 32 rows)
     g = BatchMolGraph(synthetic.make_batch(kind, b, 500 + b), device_bond_features=True, **kw)

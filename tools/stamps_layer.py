@@ -20,6 +20,7 @@ from chemprop_amd.featurization import BatchMolGraph, get_bond_fdim  # noqa: E40
 dev = torch.device('cuda:0')
 kind = sys.argv[1] if len(sys.argv) > 1 else 'polymer'
 enc = bench.make_encoder(TrainArgs(hidden_size=300, depth=3, device=dev), dev)
+enc._gemm_variant = int(os.environ.get('WD_VARIANT', '0'))  # (13: pair operands)
 g = BatchMolGraph(synthetic.make_batch(kind, 64, 1000), device_bond_features=True)
 g.device_graph(dev, False, get_bond_fdim())
 L = _native.lib()
