@@ -90,6 +90,7 @@ __global__ __launch_bounds__(512, 2) void ring_probe(const uint8_t *A, const uin
     for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 5; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    f16x8 af[2][2], bq[5][2];
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     if (loader)
         for (int c = 0; c < NS - 1 && c < nchunks; ++c) issue(c);
@@ -104,17 +105,19 @@ __global__ __launch_bounds__(512, 2) void ring_probe(const uint8_t *A, const uin
         __builtin_amdgcn_s_barrier();
         if (loader) {
             if (kc + NS - 1 < nchunks) issue(kc + NS - 1);
-        } else if (MODE == 1) {
+        } else if (MODE == 1 || MODE == 4 || MODE == 5) {
+            // (4: the B fragments read at chunk 0 only -- no per-chunk B reads; 5: the A fragments likewise)
             const uint8_t *st = lds + (kc % NS) * STAGE, *sb = st + ACH;
-            f16x8 af[2][2], bq[5][2];
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
+                if (MODE != 5 || kc == 0)
 #pragma unroll
-                for (int a = 0; a < 2; ++a)
-                    af[a][p] = *reinterpret_cast<const f16x8 *>(st + p * 8192 + wd::x6_slot(32 * w4 + 16 * a + (lane & 15), lane >> 4));
+                    for (int a = 0; a < 2; ++a)
+                        af[a][p] = *reinterpret_cast<const f16x8 *>(st + p * 8192 + wd::x6_slot(32 * w4 + 16 * a + (lane & 15), lane >> 4));
+                if (MODE != 4 || kc == 0)
 #pragma unroll
-                for (int b = 0; b < 5; ++b)
-                    bq[b][p] = *reinterpret_cast<const f16x8 *>(sb + p * 5120 + wd::x6_slot(16 * b + (lane & 15), lane >> 4));
+                    for (int b = 0; b < 5; ++b)
+                        bq[b][p] = *reinterpret_cast<const f16x8 *>(sb + p * 5120 + wd::x6_slot(16 * b + (lane & 15), lane >> 4));
             }
 #pragma unroll
             for (int b = 0; b < 5; ++b)
@@ -129,7 +132,7 @@ __global__ __launch_bounds__(512, 2) void ring_probe(const uint8_t *A, const uin
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     if (tid == 0) cyc[blockIdx.x] = t1 - t0;
-    if (MODE == 1 && !loader) {
+    if ((MODE == 1 || MODE == 4 || MODE == 5) && !loader) {
         float s = 0.f;
 #pragma unroll
         for (int a = 0; a < 2; ++a)
@@ -229,14 +232,16 @@ int main() {
     uint4 *fp = reinterpret_cast<uint4 *>(A);
     int rc = 0;
     const size_t fn = (size_t)64 * 10 * ACH / 16;  // the A the 64-block, 10-chunk runs read
-    for (int fresh = 0; fresh < 2; ++fresh) {
+    for (int fresh = 0; fresh < 1; ++fresh) {
         rc |= run<3, 0>("barriers only", A, B, 64, 10, fresh, cyc, sink, fp, fn);
         rc |= run<3, 1>("copies + MFMA (swizzled)", A, B, 64, 10, fresh, cyc, sink, fp, fn);
+        rc |= run<3, 4>("copies + MFMA, B reads once", A, B, 64, 10, fresh, cyc, sink, fp, fn);
+        rc |= run<3, 5>("copies + MFMA, A reads once", A, B, 64, 10, fresh, cyc, sink, fp, fn);
         rc |= run_k(real_pairs<0>, 0, 3, "pairs FRAG 0", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE);
-        rc |= run_k(real_pairs<1>, 0, 3, "pairs FRAG 1", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE);
-        rc |= run_k(real_pairs<2>, 0, 3, "pairs FRAG 2", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE);
-        rc |= run_k(real_pairs<0>, 0, 3, "pairs FRAG 0, 2/CU", A, B, 128, 10, fresh, cyc, sink, fp, 2 * fn, STAGE);
-        rc |= run_k(real_pairs<2>, 0, 3, "pairs FRAG 2, 2/CU", A, B, 128, 10, fresh, cyc, sink, fp, 2 * fn, STAGE);
+        rc |= run_k(real_pairs<4>, 0, 3, "pairs FRAG 4 (skip x1)", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE);
+        rc |= run_k(real_pairs<6>, 0, 3, "pairs FRAG 6", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE);
+        rc |= run<3, 1>("copies + MFMA, 40 chunks", A, B, 64, 40, fresh, cyc, sink, fp, 4 * fn);
+        rc |= run<3, 4>("B reads once, 40 chunks", A, B, 64, 40, fresh, cyc, sink, fp, 4 * fn);
     }
     return rc;
 }
