@@ -238,8 +238,8 @@ int main() {
         rc |= run<3, 4>("copies + MFMA, B reads once", A, B, 64, 10, fresh, cyc, sink, fp, fn);
         rc |= run<3, 5>("copies + MFMA, A reads once", A, B, 64, 10, fresh, cyc, sink, fp, fn);
         rc |= run_k(real_pairs<0>, 0, 3, "pairs FRAG 0", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE);
-        rc |= run_k(real_pairs<4>, 0, 3, "pairs FRAG 4 (skip x1)", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE);
-        rc |= run_k(real_pairs<6>, 0, 3, "pairs FRAG 6", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE);
+        rc |= run_k(real_pairs<1>, 0, 3, "pairs FRAG 1", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE);
+        rc |= run_k(real_pairs<2>, 0, 3, "pairs FRAG 2", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE);
         rc |= run<3, 1>("copies + MFMA, 40 chunks", A, B, 64, 40, fresh, cyc, sink, fp, 4 * fn);
         rc |= run<3, 4>("B reads once, 40 chunks", A, B, 64, 40, fresh, cyc, sink, fp, 4 * fn);
     }
