@@ -64,7 +64,7 @@ from chemprop_amd.nn_utils import initialize_weights  # noqa: E402
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 / fp16 (the layer issues 3 fp16 products per fp32 product, W_o 6 bf16)
 HBM_PEAK_GBS = 8000.0
-PMC_TRAFFIC = "round5_pmc_traffic.json"  # per-kernel HBM bytes per launch (tools/pmc_summary.py)
+PMC_TRAFFIC = "round6_pmc_traffic.json"  # per-kernel HBM bytes per launch (tools/pmc_summary.py)
 
 
 def log(*a):
@@ -151,7 +151,7 @@ def pmc_traffic(prefix):
     return sum(v) / len(v), f'profiles/{PMC_TRAFFIC}: {d.get("_note", "")}'
 
 
-ROCPROF_STATS = "round5_bench_b64_kernel_stats.csv"  # rocprofv3 --kernel-trace --stats of the headline, one stream
+ROCPROF_STATS = "round6_bench_b64_kernel_stats.csv"  # rocprofv3 --kernel-trace --stats of the headline, one stream
 
 
 def rocprof_alone(prefix):
