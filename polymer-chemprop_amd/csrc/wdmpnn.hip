@@ -139,6 +139,10 @@ struct Dims {
 // WdConfig.gemm_variant values that run the fused forward's layers on fp16 pair operands where the layout
 // allows (all but 9, the f32-MFMA A/B, and 12, the register-staged layers)
 inline bool pair_variant(int v) { return v != 9 && v != 12; }
+#ifndef WD_EMBED_PAIR_BN
+#define WD_EMBED_PAIR_BN 32
+#endif
+constexpr int EPB = WD_EMBED_PAIR_BN;  // the pair path's embed tile width (a multiple of 16 dividing every Hk: 32, 64)
 
 int get_dims(const WdGraph *g, const WdParams *p, const WdConfig *c, Dims &D) {
     if (!g || !p || !c) return fail(WD_ERR_ARG, "null graph/params/config");
@@ -908,7 +912,8 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
 #ifndef WD_EMBED40
 #define WD_EMBED40 1
 #endif
-    // (the pair path: 32-column embed tiles, one scale word per chunk of M_0)
+    // (the pair path: EPB-column embed tiles, one scale word per tile of M_0; measured, same box: 64-column
+    // tiles -- 320 workgroups, one round at B = 64 -- 11.29 vs 9.63 us for 32, 186.5 vs 194.0 M edges/s)
     // The pair-operand layers (M_t as fp16 pair tiles, written by its producer and copied by LDS-DMA; DESIGN.md
     // §4 "Pair operands") wherever the layout allows (D.pairs; gemm_variant 12 keeps the register-staged layers):
     // round 6, one box, 190.1 vs 178.8 M edges/s three batches in flight, 121.2 vs 118.1 M one, 203.0 vs 175.0 M
@@ -918,7 +923,7 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
     for (int j = 1; j < n; ++j)
         if (jobs[j].D.pairs != D0.pairs) return fail(WD_ERR_UNSUPPORTED, "fused forward: batches of one launch differ in layout");
     const bool bn40 = WD_EMBED40 && Hk % 40 == 0 && !pairs;
-    const int embed_tiles = Hk / (pairs ? 32 : (bn40 ? 40 : BNf));
+    const int embed_tiles = Hk / (pairs ? EPB : (bn40 ? 40 : BNf));
     if (codes) {
         const int nt = embed_tiles;
         Multi<EmbedP> M;
@@ -936,8 +941,8 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
         host_with_act(c->activation, [&](auto act_c) {
             constexpr int A = decltype(act_c)::value;
             if (pairs) {
-                if (n == 1) hipLaunchKernelGGL((embed_kernel<32, A, 1, true>), dim3(grid), dim3(512), 0, st, one_job(M));
-                else hipLaunchKernelGGL((embed_kernel<32, A, WD_MULTI, true>), dim3(grid), dim3(512), 0, st, M);
+                if (n == 1) hipLaunchKernelGGL((embed_kernel<EPB, A, 1, true>), dim3(grid), dim3(512), 0, st, one_job(M));
+                else hipLaunchKernelGGL((embed_kernel<EPB, A, WD_MULTI, true>), dim3(grid), dim3(512), 0, st, M);
             } else if (n == 1) {
                 const Multi<EmbedP, 1> M1 = one_job(M);
                 if (bn40) hipLaunchKernelGGL((embed_kernel<40, A, 1>), dim3(grid), dim3(512), 0, st, M1);
@@ -1022,7 +1027,7 @@ int fused_forward(const FusedJob *jobs, int n, const WdParams *p, const WdConfig
             Q.asave = J.D.save && last ? F(J, J.L.A) : nullptr;
             if (pairs) {  // M_{t-1} from the pair tiles of its producer (no Z_t in inference)
                 Q.ain = (const uint8_t *)(J.ws + J.L.Mp[(t - 1) & 1]);
-                Q.ain_g = t == 1 ? 32 : BNf;
+                Q.ain_g = t == 1 ? EPB : BNf;
                 Q.aout = last ? nullptr : (uint8_t *)(J.ws + J.L.Mp[t & 1]);
                 Q.zin = nullptr;
                 Q.zout = nullptr;

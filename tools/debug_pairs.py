@@ -36,6 +36,7 @@ L.wdmpnn_debug_fwd_offsets.argtypes = [ctypes.c_void_p] * 4
 blocks = np.array(g.molecule_blocks(), np.int64)
 Hk = -(-H // 64) * 64
 nch = Hk // 32
+EPB = int(os.environ.get('WD_EMBED_PAIR_BN', '32'))  # the embed's pair tile width (wdmpnn.hip EPB)
 
 
 def run(v):
@@ -103,8 +104,8 @@ R = lambda k: blocks[k][1]  # noqa: E731
 inp_blk = np.zeros((len(blocks), 128, Hk))
 for k, (bs, bn, *_) in enumerate(blocks):
     inp_blk[k, :bn] = inp[bs * Hk:(bs + bn) * Hk].reshape(bn, Hk)
-w0 = words(ws, off[4], nch)
-m0 = pairs(ws, off[1], 128, w0, 32)
+w0 = words(ws, off[4], Hk // EPB)
+m0 = pairs(ws, off[1], 128, w0, EPB)
 print('M0 pairs vs act(inp): rel err %.3e (block %d)' % err(m0, relu(inp_blk), R))
 print('   embed words block 0:', [hex(x) for x in w0[0]])
 
