@@ -142,6 +142,78 @@ __global__ __launch_bounds__(512, 2) void ring_probe(const uint8_t *A, const uin
     }
 }
 
+// NL loader waves (waves 4 .. 4 + NL - 1) sharing the 26 pieces of a chunk (A 16, B 10): piece c to loader
+// wave c % NL; consumers as MODE 1 (or none: MODE 0)
+template <int NS, int MODE, int NL>
+__global__ __launch_bounds__(64 * (4 + NL)) void ring_probe_nl(const uint8_t *A, const uint8_t *B, int nchunks,
+                                                              unsigned long long *cyc, float *sink) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, w4 = wave & 3;
+    const int tile = xcd_tile(blockIdx.x, gridDim.x), blk = tile >> 2, nt = tile & 3;
+    const uint8_t *a_src = A + (size_t)blk * nchunks * ACH, *b_src = B + (size_t)nt * nchunks * BCH;
+    const bool loader = wave >= 4;
+    const int lw = wave - 4;
+    constexpr int NP = 26, PMAX = (NP + NL - 1) / NL;
+    const int mine = loader ? (NP - lw + NL - 1) / NL : 0;
+    auto issue = [&](int kc) {
+        uint8_t *st = lds + (kc % NS) * STAGE;
+#pragma unroll
+        for (int j = 0; j < PMAX; ++j) {
+            const int c = lw + NL * j;
+            if (c < 16) glds16(a_src + (size_t)kc * ACH + c * 1024 + lane * 16, st + c * 1024);
+            else if (c < NP) glds16(b_src + (size_t)kc * BCH + (c - 16) * 1024 + lane * 16, st + ACH + (c - 16) * 1024);
+        }
+    };
+    floatx4 acc[2][5];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 5; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    f16x8 af[2][2], bq[5][2];
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    if (loader)
+        for (int c = 0; c < NS - 1 && c < nchunks; ++c) issue(c);
+    const int m_s = __builtin_amdgcn_readfirstlane(mine);
+    for (int kc = 0; kc < nchunks; ++kc) {
+        if (loader) vmwait_n(std::min(NS - 2, nchunks - 1 - kc) * m_s);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (loader) {
+            if (kc + NS - 1 < nchunks) issue(kc + NS - 1);
+        } else if (MODE == 1) {
+            const uint8_t *st = lds + (kc % NS) * STAGE, *sb = st + ACH;
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+                    af[a][p] = *reinterpret_cast<const f16x8 *>(st + p * 8192 + wd::x6_slot(32 * w4 + 16 * a + (lane & 15), lane >> 4));
+#pragma unroll
+                for (int b = 0; b < 5; ++b)
+                    bq[b][p] = *reinterpret_cast<const f16x8 *>(sb + p * 5120 + wd::x6_slot(16 * b + (lane & 15), lane >> 4));
+            }
+#pragma unroll
+            for (int b = 0; b < 5; ++b)
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][0], bq[b][0], acc[a][b], 0, 0, 0);
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][0], bq[b][1], acc[a][b], 0, 0, 0);
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[a][1], bq[b][0], acc[a][b], 0, 0, 0);
+                }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (tid == 0) cyc[blockIdx.x] = t1 - t0;
+    if (MODE == 1 && !loader) {
+        float s = 0.f;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 5; ++b) s += acc[a][b][0] + acc[a][b][1] + acc[a][b][2] + acc[a][b][3];
+        if (s == 12345.f) sink[tid] = s;
+    }
+}
+
 // the layer's own loop (csrc/gemm_x6.hpp h2_mainloop_pairs<128, 80>), one scale for every chunk
 template <int FRAG>
 __global__ __launch_bounds__(512, 2) void real_pairs(const uint8_t *A, const uint8_t *B, int nchunks,
@@ -176,7 +248,7 @@ __global__ void fill(uint4 *p, size_t n, uint32_t v) {
 
 typedef void (*probe_fn)(const uint8_t *, const uint8_t *, int, unsigned long long *, float *);
 int run_k(probe_fn k, int lds, int ns, const char *name, uint8_t *A, uint8_t *B, int nblk, int nchunks, bool fresh,
-          unsigned long long *cyc, float *sink, uint4 *fillp, size_t filln, int bytes) {
+          unsigned long long *cyc, float *sink, uint4 *fillp, size_t filln, int bytes, int nthr = 512) {
     const int grid = nblk * 4;
     if (lds) CK(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     hipEvent_t e0, e1;
@@ -188,7 +260,7 @@ int run_k(probe_fn k, int lds, int ns, const char *name, uint8_t *A, uint8_t *B,
     for (int r = 0; r < reps + 3; ++r) {
         if (fresh) fill<<<1024, 256>>>(fillp, filln, r);
         CK(hipEventRecord(e0));
-        k<<<grid, 512, lds>>>(A, B, nchunks, cyc, sink);
+        k<<<grid, nthr, lds>>>(A, B, nchunks, cyc, sink);
         CK(hipGetLastError());
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
@@ -235,13 +307,16 @@ int main() {
     for (int fresh = 0; fresh < 1; ++fresh) {
         rc |= run<3, 0>("barriers only", A, B, 64, 10, fresh, cyc, sink, fp, fn);
         rc |= run<3, 1>("copies + MFMA (swizzled)", A, B, 64, 10, fresh, cyc, sink, fp, fn);
-        rc |= run<3, 4>("copies + MFMA, B reads once", A, B, 64, 10, fresh, cyc, sink, fp, fn);
-        rc |= run<3, 5>("copies + MFMA, A reads once", A, B, 64, 10, fresh, cyc, sink, fp, fn);
         rc |= run_k(real_pairs<0>, 0, 3, "pairs FRAG 0", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE);
-        rc |= run_k(real_pairs<1>, 0, 3, "pairs FRAG 1", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE);
-        rc |= run_k(real_pairs<2>, 0, 3, "pairs FRAG 2", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE);
-        rc |= run<3, 1>("copies + MFMA, 40 chunks", A, B, 64, 40, fresh, cyc, sink, fp, 4 * fn);
-        rc |= run<3, 4>("B reads once, 40 chunks", A, B, 64, 40, fresh, cyc, sink, fp, 4 * fn);
+        rc |= run_k(ring_probe_nl<3, 0, 4>, 3 * STAGE, 3, "NL 4, barriers only", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE, 512);
+        rc |= run_k(ring_probe_nl<3, 0, 6>, 3 * STAGE, 3, "NL 6, barriers only", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE, 640);
+        rc |= run_k(ring_probe_nl<3, 0, 8>, 3 * STAGE, 3, "NL 8, barriers only", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE, 768);
+        rc |= run_k(ring_probe_nl<3, 1, 4>, 3 * STAGE, 3, "NL 4, copies + MFMA", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE, 512);
+        rc |= run_k(ring_probe_nl<3, 1, 6>, 3 * STAGE, 3, "NL 6, copies + MFMA", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE, 640);
+        rc |= run_k(ring_probe_nl<3, 1, 8>, 3 * STAGE, 3, "NL 8, copies + MFMA", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE, 768);
+        rc |= run_k(ring_probe_nl<3, 1, 12>, 3 * STAGE, 3, "NL 12, copies + MFMA", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE, 1024);
+        rc |= run_k(ring_probe_nl<3, 1, 6>, 3 * STAGE, 3, "NL 6, copies + MFMA, 2/CU", A, B, 128, 10, fresh, cyc, sink, fp, 2 * fn, STAGE, 640);
+        rc |= run_k(ring_probe_nl<4, 1, 8>, 4 * STAGE, 4, "NL 8, NS 4, copies + MFMA", A, B, 64, 10, fresh, cyc, sink, fp, fn, STAGE, 768);
     }
     return rc;
 }
