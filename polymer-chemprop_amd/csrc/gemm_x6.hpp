@@ -1100,15 +1100,21 @@ __device__ __forceinline__ void h2_mainloop_pairs(const uint8_t *a_src, const ui
 #pragma unroll
         for (int c = 0; c < NS - 1; ++c)
             if (c < nchunks) issue(c);
-        for (int kc = 0; kc < nchunks; ++kc) {
-            // chunk kc landed (chunks kc + 1 .. kc + NS - 2 may stay in flight); after the barrier every
-            // consumer is done reading stage (kc + NS - 1 + roff) % NS (chunk kc - 1's)
-            if (WD_STAMPS && wave == 4) wd_lstamp(kc, 4);
-            wait_vmcnt(min(NS - 2, nchunks - 1 - kc) * mine);
-            if (WD_STAMPS && wave == 4) wd_lstamp(kc, 5);
-            __builtin_amdgcn_s_barrier();
-            if (kc + NS - 1 < nchunks) issue(kc + NS - 1);
-        }
+        // the loop instantiated per copy count (its steady-state wait a constant: a wait on a runtime count
+        // is a scalar branch search per chunk, ~300 cycles of the chunk period in tools/ring_probe.hip)
+        dispatch_upto<APW + BPW>(mine, [&](auto m_c) {
+            constexpr int M = decltype(m_c)::value;
+            for (int kc = 0; kc < nchunks; ++kc) {
+                // chunk kc landed (chunks kc + 1 .. kc + NS - 2 may stay in flight); after the barrier every
+                // consumer is done reading stage (kc + NS - 1 + roff) % NS (chunk kc - 1's)
+                if (WD_STAMPS && wave == 4) wd_lstamp(kc, 4);
+                if (nchunks - 1 - kc >= NS - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * M) : "memory");
+                else wait_vmcnt((nchunks - 1 - kc) * M);
+                if (WD_STAMPS && wave == 4) wd_lstamp(kc, 5);
+                __builtin_amdgcn_s_barrier();
+                if (kc + NS - 1 < nchunks) issue(kc + NS - 1);
+            }
+        });
         __builtin_amdgcn_s_waitcnt(0x0070);  // (vmcnt(0): every copy of this wave landed)
         se_out = -1;
         return;
