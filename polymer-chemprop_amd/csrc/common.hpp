@@ -102,6 +102,13 @@ __device__ __forceinline__ void wd_stamp(int slot) {
 // per-chunk loop stamps (shader clock, s_memtime): [WG][chunk < 16][slot < 8], one lane of the calling wave
 constexpr int WD_LSTAMP_WG = 512;
 __device__ uint64_t g_wd_lstamps[WD_LSTAMP_WG * 16 * 8];
+// the embed's phases (tools/stamps_embed.py): [WG][8], after the loop stamps in wdmpnn_debug_stamps' buffer
+__device__ uint64_t g_wd_estamps[WD_STAMP_WG * 8];
+__device__ __forceinline__ void wd_estamp(int slot) {
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0 && blockIdx.x < WD_STAMP_WG)
+        __hip_atomic_store(&g_wd_estamps[blockIdx.x * 8 + slot], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void wd_lstamp(int chunk, int slot) {
     const uint64_t t = __builtin_amdgcn_s_memtime();
     if ((threadIdx.x & 63) == 0 && blockIdx.x < WD_LSTAMP_WG && chunk < 16)
@@ -109,6 +116,7 @@ __device__ __forceinline__ void wd_lstamp(int chunk, int slot) {
 }
 #else
 __device__ __forceinline__ void wd_stamp(int) {}
+__device__ __forceinline__ void wd_estamp(int) {}
 __device__ __forceinline__ void wd_lstamp(int, int) {}
 #endif
 

@@ -680,8 +680,14 @@ __device__ __forceinline__ float4 code_sum(const WdAtomCode &cd, const float *T,
     return s;
 }
 
+// (EO_LAST measured, same box: embed 10.00 vs 10.25 us, the bench's single stream 119.2 vs 125.2 M, headline
+// 202.7 vs 204.8 M -- not kept)
+#ifndef WD_EMBED_EO_LAST
+#define WD_EMBED_EO_LAST 0
+#endif
 template <int BN, int ACT, int NJ = WD_MULTI, bool PAIRS = false>
 __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP, NJ> MP) {
+    constexpr bool EO_LAST = WD_EMBED_EO_LAST;
     static_assert(!PAIRS || BN % 16 == 0, "pair groups of whole 16-column halves");
     constexpr int NT = 512, LDC = BN + 4, C4 = BN / 4, U8 = BN / 8, MAXK = 160, PER = (MAXK * C4 + NT - 1) / NT;
     constexpr int BU = (BLK_BONDS * U8 + NT - 1) / NT;  // bond units (8 columns of a row) per thread
@@ -692,6 +698,7 @@ __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP, NJ> MP) 
     static_assert(sizeof(float) * (MAXK * BN + BLK_ATOMS * LDC + BN) + sizeof(WdAtomCode) * BLK_ATOMS <= 80 * 1024,
                   "LDS of two co-resident workgroups");
     int tile;
+    wd_estamp(0);
     const EmbedP &P = multi_pick(MP, xcd_tile(blockIdx.x, gridDim.x), tile);
     const int blk = tile / P.n_tiles, nt = tile % P.n_tiles, n0 = nt * BN;
     const BlockRow B = load_block(P.blocks, blk);
@@ -722,30 +729,40 @@ __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP, NJ> MP) 
     }
     if (tid < B.an) reinterpret_cast<u32x4 *>(code)[tid] = cd;
     if (tid >= NT - C4) st4(bb + 4 * (tid - (NT - C4)), bq);
+    // (EO_LAST: the W_i tile and the layers' operand first, the f_atoms half of W_o -- for wo_readout, two
+    // launches later -- while the M_0 stores drain)
+    auto eo_half = [&]() {
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        const int v = tid + NT * q, k = v / C4, c = 4 * (v % C4);
-        if (k < P.Fa) st4(wt + k * BN + c, ro[q]);
+        for (int q = 0; q < PER; ++q) {
+            const int v = tid + NT * q, k = v / C4, c = 4 * (v % C4);
+            if (k < P.Fa) st4(wt + k * BN + c, ro[q]);
+        }
+        __syncthreads();
+        // Eo[a] = sum_{c in code(a)} W_o[:, c] + last(a) W_o[:, Fa-1] (the f_atoms half of W_o)
+        for (int v = tid; v < B.an * C4; v += NT) {
+            const int la = v / C4, c = 4 * (v % C4);
+            st4(P.eo + (size_t)(B.as + la) * P.Hk + n0 + c, code_sum<BN>(code[la], wt, P.Fa, c));
+        }
+    };
+    if constexpr (!EO_LAST) {
+        eo_half();
+        __syncthreads();  // every read of the W_o tile done
     }
-    __syncthreads();
-    // Eo[a] = sum_{c in code(a)} W_o[:, c] + last(a) W_o[:, Fa-1] (the f_atoms half of W_o)
-    for (int v = tid; v < B.an * C4; v += NT) {
-        const int la = v / C4, c = 4 * (v % C4);
-        st4(P.eo + (size_t)(B.as + la) * P.Hk + n0 + c, code_sum<BN>(code[la], wt, P.Fa, c));
-    }
-    __syncthreads();  // every read of the W_o tile done
+    wd_estamp(2);
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const int v = tid + NT * q, k = v / C4, c = 4 * (v % C4);
         if (k < P.Fb) st4(wt + k * BN + c, ri[q]);
     }
     __syncthreads();
+    wd_estamp(3);
     // Ea[a] = sum_{c in code(a)} W_i[:, c] + last(a) W_i[:, Fa-1]
     for (int v = tid; v < B.an * C4; v += NT) {
         const int la = v / C4, c = 4 * (v % C4);
         st4(ea + la * LDC + c, code_sum<BN>(code[la], wt, P.Fa, c));
     }
     __syncthreads();
+    wd_estamp(4);
     const float slope = ACT == ACT_PRELU ? P.slope[0] : 0.f;
     uint32_t mx = 0;
     float4 ym[PAIRS ? BU : 1][2];  // PAIRS: this thread's act(inp) units until the scale is known
@@ -781,11 +798,13 @@ __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP, NJ> MP) 
         }
     }
     if (blk == 0 && tid < C4) st4(P.inp + n0 + 4 * tid, f4zero());  // pad row 0 (Z_0 of the backward)
+    wd_estamp(5);
     __shared__ uint32_t red[NT / 64];
     if constexpr (PAIRS) {
         // M_0 = act(inp) as fp16 pairs scaled by this tile's max (rows up to the end of the last 16-row group
         // the layer multiplies: zeros past the block)
         const float s = h2_scale(publish_max_all(mx, P.amax + (size_t)blk * P.n_tiles + nt, red));
+        wd_estamp(6);
         constexpr int CH = 2 * BLK_BONDS * 64;
         const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
             P.m0 + (size_t)blk * (P.Hk >> 5) * CH, 0, (P.Hk >> 5) * CH, 0x00020000);
@@ -795,8 +814,13 @@ __global__ __launch_bounds__(512) void embed_kernel(const Multi<EmbedP, NJ> MP) 
             if (lb >= ((B.bn + 15) & ~15)) break;
             h2_store8(prs, h2_blk_off<BLK_BONDS>(lb, n0 + c), BLK_BONDS * 64, ym[u][0], ym[u][1], s);
         }
+        wd_estamp(7);
     } else {
         publish_max(mx, P.amax + (size_t)blk * P.n_tiles + nt, red);
+    }
+    if constexpr (EO_LAST) {
+        __syncthreads();  // every read of the W_i tile done (the bond units' tail sums)
+        eo_half();
     }
 }
 

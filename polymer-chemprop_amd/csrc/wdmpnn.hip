@@ -1186,6 +1186,10 @@ int wdmpnn_debug_stamps(void *host, size_t bytes) {
         hipMemcpyFromSymbol((char *)host + sizeof(g_wd_stamps), HIP_SYMBOL(g_wd_lstamps),
                             std::min(bytes - sizeof(g_wd_stamps), sizeof(g_wd_lstamps))) != hipSuccess)
         return fail(WD_ERR_ARG, "loop stamps copy");
+    const size_t eo = sizeof(g_wd_stamps) + sizeof(g_wd_lstamps);
+    if (bytes > eo && hipMemcpyFromSymbol((char *)host + eo, HIP_SYMBOL(g_wd_estamps),
+                                          std::min(bytes - eo, sizeof(g_wd_estamps))) != hipSuccess)
+        return fail(WD_ERR_ARG, "embed stamps copy");
     return 0;
 #else
     (void)host; (void)bytes;
