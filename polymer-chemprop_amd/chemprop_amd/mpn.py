@@ -235,7 +235,13 @@ class MPNEncoder(nn.Module):
             return None  # the general path raises
         if params[8] is not None and params[8].numel() != 1:
             return None
-        dg = mol_graph.device_graph(device, d['atom_messages'], d['bond_fdim'], not d['bias'])
+        # (the graph's DeviceGraph for this encoder's mode, memoised in the graph's device cache under a short
+        # key: device_graph's own lookup builds a device string and its key per call, ~0.5 us of host time)
+        cache = mol_graph._device_cache
+        dkey = ('infer', device.index, d['atom_messages'], d['bond_fdim'], d['bias'])
+        dg = cache.get(dkey)
+        if dg is None:
+            dg = cache[dkey] = mol_graph.device_graph(device, d['atom_messages'], d['bond_fdim'], not d['bias'])
         sid = _native.current_stream(device)
         if sid not in dg._streams:
             dg.use_on(torch.cuda.current_stream(device))

@@ -20,7 +20,8 @@ torch.manual_seed(0)
 enc = MPNEncoder(TrainArgs(hidden_size=300, depth=3), 133, 147)
 initialize_weights(enc)
 enc = enc.to(dev).eval()
-g = BatchMolGraph(synthetic.make_batch('polymer', 64, 3), device_bond_features=True)
+KIND = sys.argv[1] if len(sys.argv) > 1 else 'polymer'
+g = BatchMolGraph(synthetic.make_batch(KIND, 64, 3), device_bond_features=True)
 dg = g.device_graph(dev, False, get_bond_fdim())
 L = _native.lib()
 res = {}
@@ -44,6 +45,7 @@ with torch.no_grad():
     stream = torch.cuda.current_stream(dev)
     timeit('enc(g) total', lambda: enc(g))
     timeit('torch.cuda.current_stream', lambda: torch.cuda.current_stream(dev))
+    timeit('_native.current_stream (raw id)', lambda: _native.current_stream(dev))
     timeit('g.device_graph lookup', lambda: g.device_graph(dev, False, 147))
     timeit('dg.use_on (seen stream)', lambda: dg.use_on(stream))
     timeit('enc._param_tuple', enc._param_tuple)
@@ -79,5 +81,6 @@ with torch.no_grad():
     ev = torch.cuda.Event()
     timeit('event.record', lambda: ev.record(stream))
     torch.cuda.synchronize()
+print(f'# {KIND} B=64')
 for k, v in res.items():
     print(f'{k:40s} {v:7.2f} us', flush=True)
