@@ -367,6 +367,7 @@ def test_blocked_fused_forward(kind, b, hidden, depth, extra):
     ('polymer', 24, 600, 3, dict(activation='SELU', aggregation='sum')),  # Hk 640: 8 layer tiles, 20 embed words
     ('polymer', 16, 300, 2, dict(activation='PReLU', bias=True)),       # T = 2: the embed's pairs feed the last layer
     ('qm9', 96, 300, 3, dict(activation='ELU')),                        # many molecules per block
+    ('polymer', 8, 1600, 3, {}),                                         # Hk 1600: 50 chunks, 50 embed words
 ])
 def test_pair_operand_layers_vs_register_staged(kind, b, hidden, depth, extra):
     """The message layers reading M_{t-1} as fp16 pair tiles written by their producer (the embed, the
