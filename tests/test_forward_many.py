@@ -88,3 +88,24 @@ def test_full_block_plan_gives_the_same_outputs():
         assert golden_io.normwise(x.cpu().numpy(), y.cpu().numpy()) <= 2e-6 and torch.equal(y, z)
     for x, y in zip(a12, b12):
         assert torch.equal(x, y)
+
+
+def test_prepare_caches_plans_and_keeps_outputs():
+    """MPNEncoder.prepare (host-side setup: device graphs registered on the given streams, call plans cached)
+    changes no result: forwards after it equal an unprepared encoder's bitwise, on the current stream and on a
+    prepared side stream, and the plans are in place before the first forward."""
+    enc, _ = _enc(hidden_size=300, depth=3)
+    ref, _ = _enc(hidden_size=300, depth=3)
+    graphs = [BatchMolGraph(synthetic.make_batch(kind, b, 70 + i), device_bond_features=True)
+              for i, (kind, b) in enumerate([('polymer', 16), ('qm9', 64), ('polymer', 5)])]
+    side = torch.cuda.Stream(DEV)
+    enc.prepare(graphs, [side])
+    assert all(len(g.device_graph(DEV, False, get_bond_fdim()).encoder_plans) == 1 for g in graphs)
+    with torch.no_grad():
+        a = [enc(g) for g in graphs]
+        with torch.cuda.stream(side):
+            b = [enc(g) for g in graphs]
+        c = [ref(g) for g in graphs]
+    torch.cuda.synchronize()
+    for x, y, z in zip(a, b, c):
+        assert torch.equal(x, y) and torch.equal(x, z)
