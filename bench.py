@@ -247,6 +247,7 @@ def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_b
     if streams is None:
         streams = default_streams(sum(g.n_bonds - 1 for g in graphs) / len(graphs))
     ss = bench_streams(device, streams)
+    enc.prepare(graphs, ss)  # (resident inputs registered on the streams and their plans cached, as main())
 
     prev_stream = torch.cuda.current_stream(device)
 
@@ -752,6 +753,10 @@ def main():
         log('[bench] packing report')
         line['packing'] = packing_report(a, device, elapsed / a.steps)
         if world == 1 and a.kind == 'polymer' and not a.no_secondary:
+            # (after the streamed legs the host-bound QM9 loop below takes 15-19 instead of 10.3-10.9 us per
+            # forward -- four in flight, same box, round 6; run before them it recovers and the streamed leg
+            # loses 60 %: the feed's stream and the bench's streams share the 4 hardware queues, whichever
+            # workload comes second pays; the order stays, the north-star streamed leg first)
             log('[bench] secondary workloads (qm9, zinc, training step)')
             line['secondary'] = [secondary_workload(device, 'qm9', 64, 3, 300, 200),
                                  secondary_workload(device, 'zinc', 512, 5, 512, 30),
