@@ -246,7 +246,7 @@ def secondary_workload(device, kind, batch, depth, hidden, steps, warmup=10, n_b
         g.device_graph(device, False, get_bond_fdim())
     if streams is None:
         streams = default_streams(sum(g.n_bonds - 1 for g in graphs) / len(graphs))
-    ss = bench_streams(device, streams)
+    ss = bench_streams(device, streams)  # (streams created here instead, after the feed's: 23.9 vs 19.5 us, round 6)
     enc.prepare(graphs, ss)  # (resident inputs registered on the streams and their plans cached, as main())
 
     prev_stream = torch.cuda.current_stream(device)
