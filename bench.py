@@ -755,8 +755,8 @@ def main():
         if world == 1 and a.kind == 'polymer' and not a.no_secondary:
             # (after the streamed legs the host-bound QM9 loop below takes 15-19 instead of 10.3-10.9 us per
             # forward -- four in flight, same box, round 6; run before them it recovers and the streamed leg
-            # loses 60 %: the feed's stream and the bench's streams share the 4 hardware queues, whichever
-            # workload comes second pays; the order stays, the north-star streamed leg first)
+            # loses 60 %: whichever workload comes second pays -- not the hardware queues (8 change nothing),
+            # cause not isolated; the order stays, the north-star streamed leg first)
             log('[bench] secondary workloads (qm9, zinc, training step)')
             line['secondary'] = [secondary_workload(device, 'qm9', 64, 3, 300, 200),
                                  secondary_workload(device, 'zinc', 512, 5, 512, 30),
